@@ -1,0 +1,30 @@
+# Builds the gfx950 C-ABI library (product) and the CPU oracle (test infrastructure).
+#   make            -> libvfilter_hip.so + oracle
+#   make tools      -> tools/tune_invert (kernel variant sweep, run on the GPU box)
+HIPCC     ?= /opt/rocm/bin/hipcc
+ARCH      ?= gfx950
+PKG       := distributed-video-filter_amd
+CSRC      := $(PKG)/csrc
+LIB       := $(PKG)/vfilter/libvfilter_hip.so
+HIPFLAGS  := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -fvisibility=hidden -Wall -Iinclude
+LDFLAGS   := -shared -Wl,-rpath,/opt/rocm/lib -Wl,--no-undefined
+
+.PHONY: all lib oracle tools clean
+all: lib oracle
+
+lib: $(LIB)
+
+$(LIB): $(CSRC)/vf_kernels.hip $(CSRC)/vf_api.hip $(CSRC)/vf_internal.h include/vfilter.h
+	$(HIPCC) $(HIPFLAGS) $(LDFLAGS) $(CSRC)/vf_kernels.hip $(CSRC)/vf_api.hip -o $@
+
+oracle:
+	$(MAKE) -C oracle
+
+tools: tools/tune_invert
+
+tools/tune_invert: tools/tune_invert.hip $(CSRC)/vf_kernels.hip $(CSRC)/vf_internal.h
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -Iinclude -I$(CSRC) tools/tune_invert.hip $(CSRC)/vf_kernels.hip -o $@
+
+clean:
+	rm -f $(LIB) tools/tune_invert
+	$(MAKE) -C oracle clean

@@ -1,0 +1,282 @@
+#!/usr/bin/env python3
+"""Benchmark: 1080p RGB invert frames/s on 1..N MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1], kernel-only): batches of 32 frames of 1920x1080x3 uint8,
+resident in HBM.  One *step* = one launch of the invert kernel over one 32-frame batch
+(199,065,600 B read + 199,065,600 B written).  Steps rotate over a ring of distinct
+batches (default 2.4 GB in+out) so the 256 MiB Infinity Cache cannot serve them: the rate is
+an HBM rate.  Each rank (one process per GPU) processes its own frame-index shard (global
+batch b goes to rank b % N); there is no collective on the data path, so scaling is weak.
+
+Launched as  python bench.py --gpus N --steps K --warmup W  (torch.distributed.run for N>1).
+Prints ONE JSON line on rank 0 (contract in the task statement), including
+  roofline      algorithmic bytes per launch / mean per-launch hipEvent duration, vs 8 TB/s;
+                traffic = HBM bytes per launch from rocprofv3 PMC (FETCH_SIZE x 2 per the
+                gfx950 correction in MI355X_MICROARCH.md §HBM, + WRITE_SIZE), rank 0 at N=1
+  cpu_baseline  the oracle's numpy restatement of inverter.py:41 (np.bitwise_not per frame,
+                a new array each call, like cv2.bitwise_not), 1 host core, ~10 s sample
+  end_to_end    host->host rate through vf_invert_batch_host (pageable and pinned): PCIe-bound,
+                reported beside value, never as value.
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import glob
+import json
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "distributed-video-filter_amd"))
+sys.path.insert(0, ROOT)
+
+H, W, C = 1080, 1920, 3
+FRAME_BYTES = H * W * C
+METRIC = "frames/sec (1080p RGB invert) at 1/2/4/8 GPUs; kernel HBM GB/s vs peak"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def log(*a):
+    print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def parse():
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--warmup", type=int, default=30)
+    ap.add_argument("--batch", type=int, default=32, help="frames per step (configs[1]: 32)")
+    ap.add_argument("--ring-gb", type=float, default=2.4, help="in+out bytes the steps rotate over")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="cpu_baseline sample length (0 = skip)")
+    ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC traffic passes")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the host->host end-to-end leg")
+    ap.add_argument("--probe", action="store_true", help=argparse.SUPPRESS)  # child under rocprofv3
+    return ap.parse_args()
+
+
+# ---------------------------------------------------------------------------------------
+# device ring
+# ---------------------------------------------------------------------------------------
+
+def make_ring(ctx, batch, ring_gb, np):
+    batch_bytes = batch * FRAME_BYTES
+    nbuf = max(2, int(ring_gb * 1e9 // (2 * batch_bytes)))
+    from vfilter.synthetic import synthetic_frame
+    host = np.empty(batch_bytes, np.uint8)
+    for f in range(batch):
+        host[f * FRAME_BYTES:(f + 1) * FRAME_BYTES] = synthetic_frame(f, H, W).reshape(-1)
+    srcs, dsts = [], []
+    for _ in range(nbuf):
+        s, d = ctx.alloc_device(batch_bytes), ctx.alloc_device(batch_bytes)
+        ctx.upload(s, host, batch_bytes)
+        srcs.append(s)
+        dsts.append(d)
+    ctx.sync()
+    return srcs, dsts, batch_bytes, host
+
+
+def probe(args):
+    """Child of rocprofv3 --pmc: launch the same kernel on the same ring, nothing else."""
+    import numpy as np
+    from vfilter import Context
+    ctx = Context(0)
+    srcs, dsts, batch_bytes, _ = make_ring(ctx, args.batch, args.ring_gb, np)
+    ctx.bench_device_ring(srcs, dsts, batch_bytes, args.steps)
+    ctx.close()
+
+
+def pmc_traffic(args):
+    """HBM bytes per launch from two separate rocprofv3 --pmc passes (FETCH_SIZE needs 3 TCC
+    slots and WRITE_SIZE 2, so they cannot share a pass).  Returns (bytes, detail) or (None, why)."""
+    rp = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(rp):
+        return None, "rocprofv3 not found"
+    vals = {}
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        out = tempfile.mkdtemp(prefix="vf_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
+        cmd = ["timeout", "-s", "KILL", "90", rp, "--pmc", ctr, "--output-format", "csv", "-d", out,
+               "-o", "pmc", "--", sys.executable, os.path.abspath(__file__), "--probe",
+               "--steps", "20", "--batch", str(args.batch), "--ring-gb", str(args.ring_gb)]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        files = glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True)
+        if r.returncode != 0 or not files:
+            shutil.rmtree(out, ignore_errors=True)
+            return None, f"rocprofv3 --pmc {ctr} failed (rc={r.returncode}): {r.stderr[-300:]}"
+        per = []
+        for fn in files:
+            with open(fn) as f:
+                for row in csv.DictReader(f):
+                    if "invert_stream_kernel" in row.get("Kernel_Name", "") and row.get("Counter_Name") == ctr:
+                        per.append(float(row["Counter_Value"]))
+        shutil.rmtree(out, ignore_errors=True)
+        if not per:
+            return None, f"no {ctr} rows for invert_stream_kernel"
+        per.sort()
+        vals[ctr] = per[len(per) // 2]  # median over dispatches, KB per launch
+    # gfx950: FETCH_SIZE counts 64 B per 128-B wide streaming read request -> x2 (guide §HBM)
+    fetch = vals["FETCH_SIZE"] * 1024.0 * 2.0
+    write = vals["WRITE_SIZE"] * 1024.0
+    return fetch + write, {"fetch_size_kb": vals["FETCH_SIZE"], "write_size_kb": vals["WRITE_SIZE"],
+                           "correction": "bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024"}
+
+
+# ---------------------------------------------------------------------------------------
+# CPU baseline: the oracle's restatement of inverter.py:41 on the host
+# ---------------------------------------------------------------------------------------
+
+def cpu_baseline(host_batch, batch, seconds, np):
+    from oracle import oracle
+    frames = host_batch.reshape(batch, H, W, C)
+    n = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        for f in range(batch):
+            oracle.invert(frames[f])  # new array per call, as cv2.bitwise_not(frame)
+        n += batch
+    dt = time.perf_counter() - t0
+    return {"value": round(n / dt, 2), "unit": "frames/s", "cores": 1, "kind": "port",
+            "sample": f"{n} x 1080p frames ({dt:.1f} s), np.bitwise_not per frame "
+                      f"(oracle restatement of cv2.bitwise_not, inverter.py:41), 1 thread"}
+
+
+def end_to_end(ctx, host_batch, batch, np, reps=5):
+    """Host->host frames/s through vf_invert_batch_host: pageable numpy, and pinned buffers."""
+    import ctypes
+    out = np.empty_like(host_batch)
+    res = {}
+    for label in ("pageable", "pinned"):
+        if label == "pinned":
+            ps, pd = ctx.alloc_host(host_batch.nbytes), ctx.alloc_host(host_batch.nbytes)
+            src = np.ctypeslib.as_array((ctypes.c_uint8 * host_batch.nbytes).from_address(ps))
+            dst = np.ctypeslib.as_array((ctypes.c_uint8 * host_batch.nbytes).from_address(pd))
+            src[:] = host_batch
+        else:
+            src, dst = host_batch, out
+        ctx.invert_batch_host(src, dst, FRAME_BYTES, batch)  # warm
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            ctx.invert_batch_host(src, dst, FRAME_BYTES, batch)
+        dt = time.perf_counter() - t0
+        res[f"{label}_fps"] = round(reps * batch / dt, 1)
+        res[f"{label}_GBps_each_way"] = round(reps * host_batch.nbytes / dt / 1e9, 2)
+        if label == "pinned":
+            ctx.free_host(ps)
+            ctx.free_host(pd)
+    res["pcie_ceiling_fps"] = round(63e9 / FRAME_BYTES, 0)  # Gen5 x16 spec, one direction
+    res["note"] = "host->host incl. PCIe both directions; never the headline value"
+    return res
+
+
+def main():
+    args = parse()
+    if args.probe:
+        return probe(args)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: WORLD_SIZE={world} but --gpus {args.gpus}; using WORLD_SIZE")
+
+    # PMC passes run before this process touches the GPU (the profiler child owns it).
+    traffic, traffic_detail = None, "skipped"
+    if rank == 0 and world == 1 and not args.no_traffic:
+        t0 = time.time()
+        traffic, traffic_detail = pmc_traffic(args)
+        log(f"pmc traffic: {traffic} ({traffic_detail}) in {time.time() - t0:.1f}s")
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from vfilter import Context
+
+    have_gpu = torch.cuda.is_available()
+    if world > 1:
+        backend = "nccl" if have_gpu else "gloo"
+        if have_gpu:
+            torch.cuda.set_device(local_rank)
+        dist.init_process_group(backend, rank=rank, world_size=world)
+
+    def barrier_sync():
+        if have_gpu:
+            torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        if have_gpu:
+            torch.cuda.synchronize()
+
+    ctx = Context(local_rank, max_frame_bytes=FRAME_BYTES, max_batch=args.batch)
+    srcs, dsts, batch_bytes, host_batch = make_ring(ctx, args.batch, args.ring_gb, np)
+    log(f"rank {rank}: ring {len(srcs)} x 2 x {batch_bytes / 1e6:.1f} MB on device {local_rank}")
+
+    if args.warmup:
+        ctx.bench_device_ring(srcs, dsts, batch_bytes, args.warmup)
+    barrier_sync()
+    t0 = time.perf_counter()
+    per_launch = ctx.bench_device_ring(srcs, dsts, batch_bytes, args.steps)
+    ctx.sync()
+    barrier_sync()
+    elapsed = time.perf_counter() - t0
+
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if have_gpu else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    mean_ms = float(np.mean(per_launch)) if args.steps else float("nan")
+    achieved = 2.0 * batch_bytes / (mean_ms * 1e-3) / 1e9
+    e2e = None
+    cpu = None
+    if rank == 0 and not args.no_e2e:
+        e2e = end_to_end(ctx, host_batch, args.batch, np)
+        log(f"end-to-end: {e2e}")
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        cpu = cpu_baseline(host_batch, args.batch, args.cpu_seconds, np)
+        log(f"cpu baseline: {cpu}")
+
+    for s, d in zip(srcs, dsts):
+        ctx.free_device(s)
+        ctx.free_device(d)
+    ctx.close()
+
+    if rank == 0:
+        frames = world * args.steps * args.batch
+        line = {
+            "metric": METRIC,
+            "value": round(frames / elapsed, 1),
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (seeded uniform uint8 frames, resident in HBM)",
+            "config": {"workload": "configs[1]: 1080p RGB invert, batch=32, kernel-only, HBM-resident",
+                       "frame": [H, W, C], "global_batch": world * args.batch,
+                       "frames_per_rank_step": args.batch,
+                       "ring_bytes_in_plus_out": 2 * batch_bytes * len(srcs),
+                       "parallelism": f"frame-index shard x{world} (no collective)",
+                       "kernel": "invert_stream_kernel<4,nt,nt> (vf_kernels.hip)"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": None if traffic is None else round(traffic),
+                         "algorithmic_bytes_per_launch": 2 * batch_bytes,
+                         "mean_launch_ms": round(mean_ms, 5),
+                         "traffic_detail": traffic_detail},
+            "cpu_baseline": cpu,
+            "end_to_end": e2e,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,629 @@
+// vf_api.hip — C ABI of libvfilter_hip.so (declared in include/vfilter.h).
+//
+// Host side of the MI355X frame filter.  What it replaces in the reference:
+//   * InverterWorker per-process state          inverter.py:10-20   -> vf_create / vf_destroy
+//   * cv2.bitwise_not(frame) on one frame       inverter.py:41      -> vf_invert_host
+//   * the one-frame-per-iteration worker loop   worker.py:35-57     -> vf_invert_batch_host,
+//                                                                      vf_invert_frames_host
+// Host->host calls run a slot pipeline: the byte stream (one range, a packed batch, or a
+// gather list of frames) is cut into slot-sized chunks; chunk i uses slot i % S, whose own
+// HIP stream carries H2D -> kernel -> D2H, so DMA in, the kernel and DMA out of different
+// chunks overlap across the slot streams (the copy engines run both directions at once).
+// Pageable caller memory is staged through pinned slot buffers by a small host copy pool;
+// caller memory that is already page-locked (vf_alloc_host / vf_host_register, e.g. a
+// shared-memory frame ring) is DMA'd directly with no host copy.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <mutex>
+#include <new>
+#include <thread>
+#include <vector>
+
+#include "../../include/vfilter.h"
+#include "vf_internal.h"
+
+#define VF_EXPORT extern "C" __attribute__((visibility("default")))
+
+namespace {
+
+constexpr int kMaxSlots = 8;
+
+struct ErrState {
+  int hip = 0;
+  char msg[512] = "no error";
+};
+thread_local ErrState g_thread_err;
+
+// ---- host copy pool -------------------------------------------------------------------
+// memcpy of large staging chunks split over a few persistent threads: one core moves
+// ~10 GB/s, well under one PCIe Gen5 x16 direction, so a single-threaded stage would cap
+// the end-to-end rate.
+class CopyPool {
+ public:
+  explicit CopyPool(int nthreads) : n_(std::max(1, nthreads)) {
+    for (int i = 1; i < n_; ++i) threads_.emplace_back([this, i] { run(i); });
+  }
+  ~CopyPool() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+      ++gen_;
+    }
+    cv_.notify_all();
+    for (auto &t : threads_) t.join();
+  }
+  // Copies each (dst, src, len) job; big jobs are split across the pool.
+  void copy(uint8_t *dst, const uint8_t *src, size_t len) {
+    if (len < kSplitMin || n_ == 1) {
+      std::memcpy(dst, src, len);
+      return;
+    }
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      dst_ = dst;
+      src_ = src;
+      len_ = len;
+      pending_ = n_ - 1;
+      ++gen_;
+    }
+    cv_.notify_all();
+    do_part(0);
+    std::unique_lock<std::mutex> lk(mu_);
+    done_cv_.wait(lk, [this] { return pending_ == 0; });
+  }
+
+ private:
+  static constexpr size_t kSplitMin = 1 << 20;
+  void do_part(int i) {
+    size_t per = (len_ / n_ + 63) & ~size_t(63);
+    size_t b = std::min(len_, per * (size_t)i);
+    size_t e = std::min(len_, b + per);
+    if (i == n_ - 1) e = len_;
+    if (e > b) std::memcpy(dst_ + b, src_ + b, e - b);
+  }
+  void run(int i) {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return gen_ != seen; });
+        seen = gen_;
+        if (stop_) return;
+      }
+      do_part(i);
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        if (--pending_ == 0) done_cv_.notify_one();
+      }
+    }
+  }
+  int n_;
+  std::vector<std::thread> threads_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_cv_;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+  int pending_ = 0;
+  uint8_t *dst_ = nullptr;
+  const uint8_t *src_ = nullptr;
+  size_t len_ = 0;
+};
+
+struct OutPiece {
+  uint8_t *dst;
+  size_t off;  // offset in the slot
+  size_t len;
+};
+
+struct Slot {
+  hipStream_t stream = nullptr;
+  hipEvent_t k0 = nullptr, k1 = nullptr;
+  uint8_t *pin_in = nullptr, *pin_out = nullptr;
+  uint8_t *d_in = nullptr, *d_out = nullptr;
+  bool busy = false;
+  bool staged_out = false;
+  std::vector<OutPiece> out;
+};
+
+// A contiguous run of the logical byte stream: src[0..len) -> dst[0..len).
+struct Seg {
+  const uint8_t *src;
+  uint8_t *dst;
+  size_t len;
+};
+
+size_t env_size(const char *name, size_t dflt) {
+  const char *v = std::getenv(name);
+  if (!v || !*v) return dflt;
+  char *end = nullptr;
+  unsigned long long x = std::strtoull(v, &end, 0);
+  return (end && *end == 0) ? (size_t)x : dflt;
+}
+
+}  // namespace
+
+struct vf_ctx {
+  int device = -1;
+  int num_cus = 256;
+  int nslots = 4;
+  size_t slot_bytes = 0;
+  Slot slots[kMaxSlots];
+  vf::LaunchCfg cfg;
+  CopyPool *pool = nullptr;
+  int hip = 0;
+  char msg[512] = "no error";
+  float last_kernel_ms = 0.f;
+};
+
+namespace {
+
+int set_err(vf_ctx *ctx, int status, int hip, const char *fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  std::vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  ErrState &t = g_thread_err;
+  t.hip = hip;
+  std::snprintf(t.msg, sizeof t.msg, "%s", buf);
+  if (ctx) {
+    ctx->hip = hip;
+    std::snprintf(ctx->msg, sizeof ctx->msg, "%s", buf);
+  }
+  return status;
+}
+
+int fail_hip(vf_ctx *ctx, hipError_t e, const char *what, int line) {
+  return set_err(ctx, VF_E_HIP, (int)e, "%s failed: %s (%s, vf_api.hip:%d)", what,
+                 hipGetErrorString(e), hipGetErrorName(e), line);
+}
+
+#define VF_HIP(ctx, call)                                         \
+  do {                                                            \
+    hipError_t e_ = (call);                                       \
+    if (e_ != hipSuccess) return fail_hip((ctx), e_, #call, __LINE__); \
+  } while (0)
+
+#define VF_CHECK_CTX(ctx)                                                        \
+  do {                                                                           \
+    if (!(ctx)) return set_err(nullptr, VF_E_INVALID, 0, "%s: ctx is NULL", __func__); \
+  } while (0)
+
+bool is_pinned(const void *p) {
+  hipPointerAttribute_t a;
+  std::memset(&a, 0, sizeof a);
+  hipError_t e = hipPointerGetAttributes(&a, p);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();  // pageable pointers report an error on some runtimes
+    return false;
+  }
+  return a.type == hipMemoryTypeHost;
+}
+
+int release_slots(vf_ctx *ctx) {
+  for (int i = 0; i < kMaxSlots; ++i) {
+    Slot &s = ctx->slots[i];
+    if (s.stream) (void)hipStreamSynchronize(s.stream);
+    if (s.k0) (void)hipEventDestroy(s.k0);
+    if (s.k1) (void)hipEventDestroy(s.k1);
+    if (s.pin_in) (void)hipHostFree(s.pin_in);
+    if (s.pin_out) (void)hipHostFree(s.pin_out);
+    if (s.d_in) (void)hipFree(s.d_in);
+    if (s.d_out) (void)hipFree(s.d_out);
+    if (s.stream) (void)hipStreamDestroy(s.stream);
+    s = Slot();
+  }
+  return VF_OK;
+}
+
+// Wait for slot `s`, scatter its staged output, add its kernel time.
+int complete_slot(vf_ctx *ctx, Slot &s) {
+  if (!s.busy) return VF_OK;
+  VF_HIP(ctx, hipStreamSynchronize(s.stream));
+  float ms = 0.f;
+  if (hipEventElapsedTime(&ms, s.k0, s.k1) == hipSuccess) ctx->last_kernel_ms += ms;
+  if (s.staged_out)
+    for (const OutPiece &p : s.out) ctx->pool->copy(p.dst, s.pin_out + p.off, p.len);
+  s.out.clear();
+  s.busy = false;
+  return VF_OK;
+}
+
+// The slot pipeline over a list of segments (see file header).
+int run_pipeline(vf_ctx *ctx, const Seg *segs, size_t nseg) {
+  VF_HIP(ctx, hipSetDevice(ctx->device));
+  ctx->last_kernel_ms = 0.f;
+  bool direct = true;  // every source and destination page-locked?
+  size_t total = 0;
+  for (size_t i = 0; i < nseg; ++i) {
+    total += segs[i].len;
+    if (segs[i].len && direct && !(is_pinned(segs[i].src) && is_pinned(segs[i].dst))) direct = false;
+  }
+  if (total == 0) return VF_OK;
+  size_t seg = 0, seg_off = 0;
+  int next = 0;
+  int rc = VF_OK;
+  while (seg < nseg && rc == VF_OK) {
+    Slot &s = ctx->slots[next];
+    next = (next + 1) % ctx->nslots;
+    if ((rc = complete_slot(ctx, s)) != VF_OK) break;
+    s.out.clear();
+    // Fill the slot from the segment cursor.
+    size_t filled = 0;
+    while (seg < nseg && filled < ctx->slot_bytes) {
+      const Seg &g = segs[seg];
+      size_t take = std::min(g.len - seg_off, ctx->slot_bytes - filled);
+      if (take) {
+        if (direct) {
+          hipError_t e = hipMemcpyAsync(s.d_in + filled, g.src + seg_off, take,
+                                        hipMemcpyHostToDevice, s.stream);
+          if (e != hipSuccess) { rc = fail_hip(ctx, e, "hipMemcpyAsync(H2D)", __LINE__); break; }
+        } else {
+          ctx->pool->copy(s.pin_in + filled, g.src + seg_off, take);
+        }
+        s.out.push_back(OutPiece{g.dst + seg_off, filled, take});
+        filled += take;
+        seg_off += take;
+      }
+      if (seg_off == g.len) { ++seg; seg_off = 0; }
+    }
+    if (rc != VF_OK) break;
+    if (filled == 0) break;
+    hipError_t e = hipSuccess;
+    if (!direct) e = hipMemcpyAsync(s.d_in, s.pin_in, filled, hipMemcpyHostToDevice, s.stream);
+    if (e == hipSuccess) e = hipEventRecord(s.k0, s.stream);
+    if (e == hipSuccess) e = vf::launch_invert(s.d_in, s.d_out, filled, ctx->cfg, s.stream);
+    if (e == hipSuccess) e = hipEventRecord(s.k1, s.stream);
+    if (e == hipSuccess) {
+      if (direct) {
+        for (const OutPiece &p : s.out) {
+          e = hipMemcpyAsync(p.dst, s.d_out + p.off, p.len, hipMemcpyDeviceToHost, s.stream);
+          if (e != hipSuccess) break;
+        }
+      } else {
+        e = hipMemcpyAsync(s.pin_out, s.d_out, filled, hipMemcpyDeviceToHost, s.stream);
+      }
+    }
+    if (e != hipSuccess) { rc = fail_hip(ctx, e, "slot submit", __LINE__); break; }
+    s.staged_out = !direct;
+    s.busy = true;
+  }
+  // Drain in submission order (oldest first).
+  for (int k = 0; k < ctx->nslots; ++k) {
+    Slot &s = ctx->slots[(next + k) % ctx->nslots];
+    int r = complete_slot(ctx, s);
+    if (rc == VF_OK) rc = r;
+  }
+  return rc;
+}
+
+}  // namespace
+
+// ---- library / context ---------------------------------------------------------------
+
+VF_EXPORT int vf_get_abi_version(void) { return VF_ABI_VERSION; }
+
+VF_EXPORT const char *vf_status_string(int status) {
+  switch (status) {
+    case VF_OK: return "VF_OK";
+    case VF_E_INVALID: return "VF_E_INVALID: invalid argument";
+    case VF_E_HIP: return "VF_E_HIP: HIP runtime error";
+    case VF_E_NOMEM: return "VF_E_NOMEM: out of memory";
+    case VF_E_NODEVICE: return "VF_E_NODEVICE: no usable gfx950 device";
+    default: return "unknown vfilter status";
+  }
+}
+
+VF_EXPORT int vf_device_count(int *out_count) {
+  if (!out_count) return set_err(nullptr, VF_E_INVALID, 0, "vf_device_count: out_count is NULL");
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    n = 0;
+  }
+  *out_count = n;
+  return VF_OK;
+}
+
+VF_EXPORT int vf_create(int device, size_t max_frame_bytes, int max_batch, vf_ctx **out) {
+  if (!out) return set_err(nullptr, VF_E_INVALID, 0, "vf_create: out is NULL");
+  *out = nullptr;
+  if (max_batch < 1) max_batch = 1;
+  int ndev = 0;
+  vf_device_count(&ndev);
+  if (device < 0 || device >= ndev)
+    return set_err(nullptr, VF_E_NODEVICE, 0, "vf_create: device %d not available (%d visible)",
+                   device, ndev);
+  hipDeviceProp_t prop;
+  hipError_t e = hipGetDeviceProperties(&prop, device);
+  if (e != hipSuccess) return fail_hip(nullptr, e, "hipGetDeviceProperties", __LINE__);
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return set_err(nullptr, VF_E_NODEVICE, 0,
+                   "vf_create: device %d is %s; libvfilter_hip.so is built for gfx950 only",
+                   device, prop.gcnArchName);
+  vf_ctx *ctx = new (std::nothrow) vf_ctx();
+  if (!ctx) return set_err(nullptr, VF_E_NOMEM, 0, "vf_create: out of host memory");
+  ctx->device = device;
+  ctx->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+  ctx->cfg.variant = (int)env_size("VF_VARIANT", (size_t)vf::kVariantU4NT);
+  if (ctx->cfg.variant < 0 || ctx->cfg.variant >= vf::kVariantCount) ctx->cfg.variant = vf::kVariantU4NT;
+  ctx->cfg.max_blocks = (int)env_size("VF_MAX_BLOCKS", (size_t)ctx->num_cus * 16);
+  if (ctx->cfg.max_blocks < 1) ctx->cfg.max_blocks = ctx->num_cus * 16;
+  ctx->nslots = (int)std::min<size_t>(kMaxSlots, std::max<size_t>(2, env_size("VF_SLOTS", 4)));
+  size_t want = max_frame_bytes ? max_frame_bytes * (size_t)max_batch : (size_t)8 << 20;
+  size_t slot = env_size("VF_SLOT_BYTES", std::min(want, (size_t)8 << 20));
+  slot = std::max<size_t>(slot, (size_t)1 << 20);
+  slot = std::min<size_t>(slot, (size_t)64 << 20);
+  slot = (slot + 4095) & ~(size_t)4095;
+  ctx->slot_bytes = slot;
+  int rc = VF_OK;
+  e = hipSetDevice(device);
+  if (e != hipSuccess) rc = fail_hip(ctx, e, "hipSetDevice", __LINE__);
+  for (int i = 0; i < ctx->nslots && rc == VF_OK; ++i) {
+    Slot &s = ctx->slots[i];
+    if ((e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking)) != hipSuccess ||
+        (e = hipEventCreate(&s.k0)) != hipSuccess || (e = hipEventCreate(&s.k1)) != hipSuccess) {
+      rc = fail_hip(ctx, e, "stream/event create", __LINE__);
+      break;
+    }
+    if ((e = hipHostMalloc((void **)&s.pin_in, slot, hipHostMallocDefault)) != hipSuccess ||
+        (e = hipHostMalloc((void **)&s.pin_out, slot, hipHostMallocDefault)) != hipSuccess ||
+        (e = hipMalloc((void **)&s.d_in, slot)) != hipSuccess ||
+        (e = hipMalloc((void **)&s.d_out, slot)) != hipSuccess) {
+      rc = set_err(ctx, VF_E_NOMEM, (int)e, "vf_create: slot allocation of %zu bytes failed: %s",
+                   slot, hipGetErrorString(e));
+      break;
+    }
+  }
+  if (rc != VF_OK) {
+    g_thread_err.hip = ctx->hip;
+    std::snprintf(g_thread_err.msg, sizeof g_thread_err.msg, "%s", ctx->msg);
+    release_slots(ctx);
+    delete ctx;
+    return rc;
+  }
+  ctx->pool = new CopyPool((int)env_size("VF_HOST_THREADS", 4));
+  *out = ctx;
+  return VF_OK;
+}
+
+VF_EXPORT int vf_destroy(vf_ctx *ctx) {
+  if (!ctx) return VF_OK;
+  (void)hipSetDevice(ctx->device);
+  release_slots(ctx);
+  delete ctx->pool;
+  delete ctx;
+  return VF_OK;
+}
+
+VF_EXPORT const char *vf_last_error(const vf_ctx *ctx) {
+  return ctx ? ctx->msg : g_thread_err.msg;
+}
+
+VF_EXPORT int vf_last_hip_error(const vf_ctx *ctx) { return ctx ? ctx->hip : g_thread_err.hip; }
+
+VF_EXPORT int vf_ctx_device(const vf_ctx *ctx, int *out_device) {
+  if (!ctx || !out_device) return set_err(nullptr, VF_E_INVALID, 0, "vf_ctx_device: NULL argument");
+  *out_device = ctx->device;
+  return VF_OK;
+}
+
+// ---- host -> host ----------------------------------------------------------------------
+
+static bool overlaps_partially(const uint8_t *a, const uint8_t *b, size_t n) {
+  if (a == b || n == 0) return false;
+  return (a < b + n) && (b < a + n);
+}
+
+VF_EXPORT int vf_invert_host(vf_ctx *ctx, const uint8_t *src, uint8_t *dst, size_t nbytes) {
+  VF_CHECK_CTX(ctx);
+  if (nbytes == 0) { ctx->last_kernel_ms = 0.f; return VF_OK; }
+  if (!src || !dst) return set_err(ctx, VF_E_INVALID, 0, "vf_invert_host: NULL buffer");
+  if (overlaps_partially(src, dst, nbytes))
+    return set_err(ctx, VF_E_INVALID, 0, "vf_invert_host: src and dst partially overlap");
+  Seg s{src, dst, nbytes};
+  return run_pipeline(ctx, &s, 1);
+}
+
+VF_EXPORT int vf_invert_batch_host(vf_ctx *ctx, const uint8_t *src, uint8_t *dst,
+                                   size_t frame_bytes, int n) {
+  VF_CHECK_CTX(ctx);
+  if (n < 0) return set_err(ctx, VF_E_INVALID, 0, "vf_invert_batch_host: n < 0");
+  if (n == 0 || frame_bytes == 0) { ctx->last_kernel_ms = 0.f; return VF_OK; }
+  if (frame_bytes > SIZE_MAX / (size_t)n)
+    return set_err(ctx, VF_E_INVALID, 0, "vf_invert_batch_host: size overflow");
+  return vf_invert_host(ctx, src, dst, frame_bytes * (size_t)n);
+}
+
+VF_EXPORT int vf_invert_frames_host(vf_ctx *ctx, const uint8_t *const *srcs, uint8_t *const *dsts,
+                                    const size_t *nbytes, int n) {
+  VF_CHECK_CTX(ctx);
+  if (n < 0) return set_err(ctx, VF_E_INVALID, 0, "vf_invert_frames_host: n < 0");
+  if (n == 0) { ctx->last_kernel_ms = 0.f; return VF_OK; }
+  if (!srcs || !dsts || !nbytes)
+    return set_err(ctx, VF_E_INVALID, 0, "vf_invert_frames_host: NULL array");
+  std::vector<Seg> segs;
+  segs.reserve((size_t)n);
+  for (int i = 0; i < n; ++i) {
+    if (nbytes[i] == 0) continue;
+    if (!srcs[i] || !dsts[i])
+      return set_err(ctx, VF_E_INVALID, 0, "vf_invert_frames_host: frame %d has a NULL buffer", i);
+    if (overlaps_partially(srcs[i], dsts[i], nbytes[i]))
+      return set_err(ctx, VF_E_INVALID, 0, "vf_invert_frames_host: frame %d src/dst partially overlap", i);
+    segs.push_back(Seg{srcs[i], dsts[i], nbytes[i]});
+  }
+  if (segs.empty()) { ctx->last_kernel_ms = 0.f; return VF_OK; }
+  return run_pipeline(ctx, segs.data(), segs.size());
+}
+
+// ---- device-resident ---------------------------------------------------------------------
+
+VF_EXPORT int vf_invert_device(vf_ctx *ctx, const void *dsrc, void *ddst, size_t nbytes,
+                               void *stream) {
+  VF_CHECK_CTX(ctx);
+  if (nbytes == 0) return VF_OK;
+  if (!dsrc || !ddst) return set_err(ctx, VF_E_INVALID, 0, "vf_invert_device: NULL buffer");
+  if (overlaps_partially((const uint8_t *)dsrc, (const uint8_t *)ddst, nbytes))
+    return set_err(ctx, VF_E_INVALID, 0, "vf_invert_device: src and dst partially overlap");
+  VF_HIP(ctx, hipSetDevice(ctx->device));
+  VF_HIP(ctx, vf::launch_invert(dsrc, ddst, nbytes, ctx->cfg, (hipStream_t)stream));
+  return VF_OK;
+}
+
+VF_EXPORT int vf_invert_device_frames(vf_ctx *ctx, const void *const *dsrcs, void *const *ddsts,
+                                      const size_t *nbytes, int n, size_t total_bytes,
+                                      void *stream) {
+  VF_CHECK_CTX(ctx);
+  if (n < 0 || n > 65535)
+    return set_err(ctx, VF_E_INVALID, 0, "vf_invert_device_frames: n=%d outside [0, 65535]", n);
+  if (n == 0) return VF_OK;
+  if (!dsrcs || !ddsts || !nbytes)
+    return set_err(ctx, VF_E_INVALID, 0, "vf_invert_device_frames: NULL descriptor array");
+  VF_HIP(ctx, hipSetDevice(ctx->device));
+  VF_HIP(ctx, vf::launch_invert_frames(dsrcs, ddsts, nbytes, n, total_bytes, ctx->cfg,
+                                       (hipStream_t)stream));
+  return VF_OK;
+}
+
+// ---- memory helpers ------------------------------------------------------------------------
+
+VF_EXPORT int vf_alloc_device(vf_ctx *ctx, size_t nbytes, void **out) {
+  VF_CHECK_CTX(ctx);
+  if (!out) return set_err(ctx, VF_E_INVALID, 0, "vf_alloc_device: out is NULL");
+  *out = nullptr;
+  VF_HIP(ctx, hipSetDevice(ctx->device));
+  hipError_t e = hipMalloc(out, nbytes ? nbytes : 1);
+  if (e != hipSuccess)
+    return set_err(ctx, VF_E_NOMEM, (int)e, "hipMalloc(%zu) failed: %s", nbytes, hipGetErrorString(e));
+  return VF_OK;
+}
+
+VF_EXPORT int vf_free_device(vf_ctx *ctx, void *p) {
+  VF_CHECK_CTX(ctx);
+  if (!p) return VF_OK;
+  VF_HIP(ctx, hipSetDevice(ctx->device));
+  VF_HIP(ctx, hipFree(p));
+  return VF_OK;
+}
+
+VF_EXPORT int vf_alloc_host(vf_ctx *ctx, size_t nbytes, void **out) {
+  VF_CHECK_CTX(ctx);
+  if (!out) return set_err(ctx, VF_E_INVALID, 0, "vf_alloc_host: out is NULL");
+  *out = nullptr;
+  VF_HIP(ctx, hipSetDevice(ctx->device));
+  hipError_t e = hipHostMalloc(out, nbytes ? nbytes : 1, hipHostMallocDefault);
+  if (e != hipSuccess)
+    return set_err(ctx, VF_E_NOMEM, (int)e, "hipHostMalloc(%zu) failed: %s", nbytes, hipGetErrorString(e));
+  return VF_OK;
+}
+
+VF_EXPORT int vf_free_host(vf_ctx *ctx, void *p) {
+  VF_CHECK_CTX(ctx);
+  if (!p) return VF_OK;
+  VF_HIP(ctx, hipHostFree(p));
+  return VF_OK;
+}
+
+VF_EXPORT int vf_host_register(vf_ctx *ctx, void *p, size_t nbytes) {
+  VF_CHECK_CTX(ctx);
+  if (!p || !nbytes) return set_err(ctx, VF_E_INVALID, 0, "vf_host_register: empty range");
+  VF_HIP(ctx, hipSetDevice(ctx->device));
+  VF_HIP(ctx, hipHostRegister(p, nbytes, hipHostRegisterDefault));
+  return VF_OK;
+}
+
+VF_EXPORT int vf_host_unregister(vf_ctx *ctx, void *p) {
+  VF_CHECK_CTX(ctx);
+  if (!p) return VF_OK;
+  VF_HIP(ctx, hipHostUnregister(p));
+  return VF_OK;
+}
+
+VF_EXPORT int vf_upload(vf_ctx *ctx, void *ddst, const void *hsrc, size_t nbytes, void *stream) {
+  VF_CHECK_CTX(ctx);
+  if (!nbytes) return VF_OK;
+  if (!ddst || !hsrc) return set_err(ctx, VF_E_INVALID, 0, "vf_upload: NULL buffer");
+  VF_HIP(ctx, hipSetDevice(ctx->device));
+  VF_HIP(ctx, hipMemcpyAsync(ddst, hsrc, nbytes, hipMemcpyHostToDevice, (hipStream_t)stream));
+  return VF_OK;
+}
+
+VF_EXPORT int vf_download(vf_ctx *ctx, void *hdst, const void *dsrc, size_t nbytes, void *stream) {
+  VF_CHECK_CTX(ctx);
+  if (!nbytes) return VF_OK;
+  if (!hdst || !dsrc) return set_err(ctx, VF_E_INVALID, 0, "vf_download: NULL buffer");
+  VF_HIP(ctx, hipSetDevice(ctx->device));
+  VF_HIP(ctx, hipMemcpyAsync(hdst, dsrc, nbytes, hipMemcpyDeviceToHost, (hipStream_t)stream));
+  return VF_OK;
+}
+
+VF_EXPORT int vf_memset_device(vf_ctx *ctx, void *d, int value, size_t nbytes, void *stream) {
+  VF_CHECK_CTX(ctx);
+  if (!nbytes) return VF_OK;
+  if (!d) return set_err(ctx, VF_E_INVALID, 0, "vf_memset_device: NULL buffer");
+  VF_HIP(ctx, hipSetDevice(ctx->device));
+  VF_HIP(ctx, hipMemsetAsync(d, value, nbytes, (hipStream_t)stream));
+  return VF_OK;
+}
+
+VF_EXPORT int vf_sync(vf_ctx *ctx, void *stream) {
+  VF_CHECK_CTX(ctx);
+  VF_HIP(ctx, hipSetDevice(ctx->device));
+  if (stream) {
+    VF_HIP(ctx, hipStreamSynchronize((hipStream_t)stream));
+  } else {
+    VF_HIP(ctx, hipDeviceSynchronize());
+  }
+  return VF_OK;
+}
+
+// ---- timing ----------------------------------------------------------------------------
+
+VF_EXPORT int vf_elapsed_ms(const vf_ctx *ctx, float *out_ms) {
+  if (!ctx || !out_ms) return set_err(nullptr, VF_E_INVALID, 0, "vf_elapsed_ms: NULL argument");
+  *out_ms = ctx->last_kernel_ms;
+  return VF_OK;
+}
+
+VF_EXPORT int vf_bench_device_ring(vf_ctx *ctx, void *const *srcs, void *const *dsts, int nbuf,
+                                   size_t nbytes, int steps, void *stream, float *per_launch_ms) {
+  VF_CHECK_CTX(ctx);
+  if (!srcs || !dsts || nbuf < 1 || steps < 0)
+    return set_err(ctx, VF_E_INVALID, 0, "vf_bench_device_ring: bad arguments");
+  VF_HIP(ctx, hipSetDevice(ctx->device));
+  hipStream_t st = (hipStream_t)stream;
+  std::vector<hipEvent_t> ev(2 * (size_t)steps, nullptr);
+  int rc = VF_OK;
+  for (auto &e : ev) {
+    hipError_t h = hipEventCreate(&e);
+    if (h != hipSuccess) { rc = fail_hip(ctx, h, "hipEventCreate", __LINE__); break; }
+  }
+  for (int s = 0; s < steps && rc == VF_OK; ++s) {
+    hipError_t h = hipEventRecord(ev[2 * s], st);
+    if (h == hipSuccess) h = vf::launch_invert(srcs[s % nbuf], dsts[s % nbuf], nbytes, ctx->cfg, st);
+    if (h == hipSuccess) h = hipEventRecord(ev[2 * s + 1], st);
+    if (h != hipSuccess) rc = fail_hip(ctx, h, "bench launch", __LINE__);
+  }
+  if (rc == VF_OK) {
+    hipError_t h = hipStreamSynchronize(st);
+    if (h != hipSuccess) rc = fail_hip(ctx, h, "hipStreamSynchronize", __LINE__);
+  }
+  for (int s = 0; s < steps && rc == VF_OK && per_launch_ms; ++s) {
+    float ms = 0.f;
+    hipError_t h = hipEventElapsedTime(&ms, ev[2 * s], ev[2 * s + 1]);
+    if (h != hipSuccess) { rc = fail_hip(ctx, h, "hipEventElapsedTime", __LINE__); break; }
+    per_launch_ms[s] = ms;
+  }
+  for (auto &e : ev)
+    if (e) (void)hipEventDestroy(e);
+  return rc;
+}

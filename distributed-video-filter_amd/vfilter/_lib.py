@@ -1,0 +1,268 @@
+"""ctypes binding to ``libvfilter_hip.so`` (the C ABI declared in ``include/vfilter.h``).
+
+The reference's filter call is ``cv2.bitwise_not(frame)`` (inverter.py:41), a Python call
+into OpenCV's C++ core.  Here the same call goes through ctypes into hand-written gfx950
+HIP kernels.  ctypes releases the GIL for the duration of each foreign call, so a worker's
+transport threads keep running while a batch is on the GPU.
+
+There is no fallback: if the library is missing or no gfx950 device is present, the calls
+raise.  (The CPU oracle under ``oracle/`` is test infrastructure and is never imported here.)
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from typing import Optional, Sequence
+
+import numpy as np
+
+LIB_NAME = "libvfilter_hip.so"
+ABI_VERSION = 1
+
+VF_OK = 0
+VF_E_INVALID = -1
+VF_E_HIP = -2
+VF_E_NOMEM = -3
+VF_E_NODEVICE = -4
+
+_c_int_p = ctypes.POINTER(ctypes.c_int)
+_c_float_p = ctypes.POINTER(ctypes.c_float)
+_vp = ctypes.c_void_p
+_sz = ctypes.c_size_t
+_u8p = ctypes.c_void_p  # passed as raw addresses
+
+# name -> (restype, argtypes); must list every entry point of include/vfilter.h
+SIGNATURES = {
+    "vf_get_abi_version": (ctypes.c_int, []),
+    "vf_status_string": (ctypes.c_char_p, [ctypes.c_int]),
+    "vf_device_count": (ctypes.c_int, [_c_int_p]),
+    "vf_create": (ctypes.c_int, [ctypes.c_int, _sz, ctypes.c_int, ctypes.POINTER(_vp)]),
+    "vf_destroy": (ctypes.c_int, [_vp]),
+    "vf_last_error": (ctypes.c_char_p, [_vp]),
+    "vf_last_hip_error": (ctypes.c_int, [_vp]),
+    "vf_ctx_device": (ctypes.c_int, [_vp, _c_int_p]),
+    "vf_invert_host": (ctypes.c_int, [_vp, _u8p, _u8p, _sz]),
+    "vf_invert_batch_host": (ctypes.c_int, [_vp, _u8p, _u8p, _sz, ctypes.c_int]),
+    "vf_invert_frames_host": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_int]),
+    "vf_invert_device": (ctypes.c_int, [_vp, _vp, _vp, _sz, _vp]),
+    "vf_invert_device_frames": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_int, _sz, _vp]),
+    "vf_alloc_device": (ctypes.c_int, [_vp, _sz, ctypes.POINTER(_vp)]),
+    "vf_free_device": (ctypes.c_int, [_vp, _vp]),
+    "vf_alloc_host": (ctypes.c_int, [_vp, _sz, ctypes.POINTER(_vp)]),
+    "vf_free_host": (ctypes.c_int, [_vp, _vp]),
+    "vf_host_register": (ctypes.c_int, [_vp, _vp, _sz]),
+    "vf_host_unregister": (ctypes.c_int, [_vp, _vp]),
+    "vf_upload": (ctypes.c_int, [_vp, _vp, _vp, _sz, _vp]),
+    "vf_download": (ctypes.c_int, [_vp, _vp, _vp, _sz, _vp]),
+    "vf_memset_device": (ctypes.c_int, [_vp, _vp, ctypes.c_int, _sz, _vp]),
+    "vf_sync": (ctypes.c_int, [_vp, _vp]),
+    "vf_elapsed_ms": (ctypes.c_int, [_vp, _c_float_p]),
+    "vf_bench_device_ring": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_int, _sz, ctypes.c_int, _vp, _c_float_p]),
+}
+
+
+class VFilterError(RuntimeError):
+    """A libvfilter_hip call failed.  ``status`` is the VF_E_* code, ``hip_error`` the hipError_t."""
+
+    def __init__(self, message: str, status: int = VF_E_HIP, hip_error: int = 0):
+        super().__init__(message)
+        self.status = status
+        self.hip_error = hip_error
+
+
+_lib: Optional[ctypes.CDLL] = None
+_lib_lock = threading.Lock()
+
+
+def library_path() -> str:
+    """Path of the in-tree library (override with ``VFILTER_LIB``)."""
+    return os.environ.get("VFILTER_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+
+
+def load_library() -> ctypes.CDLL:
+    """Load libvfilter_hip.so once and declare its signatures.  Raises if it is absent."""
+    global _lib
+    with _lib_lock:
+        if _lib is not None:
+            return _lib
+        path = library_path()
+        if not os.path.exists(path):
+            raise VFilterError(
+                f"{LIB_NAME} not found at {path}; build it with `make` (hipcc --offload-arch=gfx950)",
+                VF_E_NODEVICE)
+        lib = ctypes.CDLL(path)
+        for name, (restype, argtypes) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = restype
+            fn.argtypes = argtypes
+        got = lib.vf_get_abi_version()
+        if got != ABI_VERSION:
+            raise VFilterError(f"{path}: ABI version {got}, binding expects {ABI_VERSION}", VF_E_INVALID)
+        _lib = lib
+        return lib
+
+
+def device_count() -> int:
+    lib = load_library()
+    n = ctypes.c_int(0)
+    lib.vf_device_count(ctypes.byref(n))
+    return n.value
+
+
+def _addr(a) -> int:
+    """Address of a numpy array / writable buffer / int pointer."""
+    if isinstance(a, int):
+        return a
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data
+    if isinstance(a, (bytes, bytearray, memoryview)):
+        return np.frombuffer(a, dtype=np.uint8).ctypes.data
+    raise TypeError(f"cannot take the address of {type(a).__name__}")
+
+
+class Context:
+    """One ``vf_ctx``: a device, its HIP streams and the pinned staging ring.
+
+    Mirrors the per-process filter state of ``InverterWorker.__init__`` (inverter.py:10-20);
+    one per worker process, bound to one GPU.  Not thread-safe.
+    """
+
+    def __init__(self, device: int = 0, max_frame_bytes: int = 0, max_batch: int = 1):
+        self._lib = load_library()
+        self._ctx = _vp()
+        st = self._lib.vf_create(int(device), int(max_frame_bytes), int(max_batch), ctypes.byref(self._ctx))
+        if st != VF_OK:
+            raise VFilterError(self._lib.vf_last_error(None).decode(), st, self._lib.vf_last_hip_error(None))
+        self.device = int(device)
+
+    # -- plumbing -----------------------------------------------------------------------
+    def _check(self, st: int) -> None:
+        if st != VF_OK:
+            raise VFilterError(self._lib.vf_last_error(self._ctx).decode(), st,
+                               self._lib.vf_last_hip_error(self._ctx))
+
+    @property
+    def handle(self) -> int:
+        return self._ctx.value or 0
+
+    def close(self) -> None:
+        if self._ctx:
+            self._lib.vf_destroy(self._ctx)
+            self._ctx = _vp()
+
+    def __enter__(self) -> "Context":
+        return self
+
+    def __exit__(self, *exc) -> None:
+        self.close()
+
+    def __del__(self):  # best effort
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- host -> host -------------------------------------------------------------------
+    def invert_host(self, src, dst, nbytes: Optional[int] = None) -> None:
+        if nbytes is None:
+            nbytes = src.nbytes if isinstance(src, np.ndarray) else len(src)
+        self._check(self._lib.vf_invert_host(self._ctx, _addr(src), _addr(dst), nbytes))
+
+    def invert_batch_host(self, src, dst, frame_bytes: int, n: int) -> None:
+        self._check(self._lib.vf_invert_batch_host(self._ctx, _addr(src), _addr(dst), frame_bytes, n))
+
+    def invert_frames_host(self, srcs: Sequence, dsts: Sequence, nbytes: Sequence[int]) -> None:
+        n = len(srcs)
+        if not (len(dsts) == n == len(nbytes)):
+            raise ValueError("srcs, dsts and nbytes must have the same length")
+        sa = (ctypes.c_void_p * n)(*[_addr(s) for s in srcs])
+        da = (ctypes.c_void_p * n)(*[_addr(d) for d in dsts])
+        na = (ctypes.c_size_t * n)(*[int(b) for b in nbytes])
+        self._check(self._lib.vf_invert_frames_host(self._ctx, sa, da, na, n))
+
+    # -- device-resident ------------------------------------------------------------------
+    def invert_device(self, dsrc: int, ddst: int, nbytes: int, stream: int = 0) -> None:
+        self._check(self._lib.vf_invert_device(self._ctx, dsrc, ddst, nbytes, stream or None))
+
+    def invert_device_frames(self, dsrcs_dev: int, ddsts_dev: int, nbytes_dev: int, n: int,
+                             total_bytes: int, stream: int = 0) -> None:
+        self._check(self._lib.vf_invert_device_frames(self._ctx, dsrcs_dev, ddsts_dev, nbytes_dev, n,
+                                                      total_bytes, stream or None))
+
+    def alloc_device(self, nbytes: int) -> int:
+        p = _vp()
+        self._check(self._lib.vf_alloc_device(self._ctx, nbytes, ctypes.byref(p)))
+        return p.value or 0
+
+    def free_device(self, p: int) -> None:
+        self._check(self._lib.vf_free_device(self._ctx, p))
+
+    def alloc_host(self, nbytes: int) -> int:
+        p = _vp()
+        self._check(self._lib.vf_alloc_host(self._ctx, nbytes, ctypes.byref(p)))
+        return p.value or 0
+
+    def free_host(self, p: int) -> None:
+        self._check(self._lib.vf_free_host(self._ctx, p))
+
+    def host_register(self, buf, nbytes: Optional[int] = None) -> int:
+        addr = _addr(buf)
+        if nbytes is None:
+            nbytes = buf.nbytes if isinstance(buf, np.ndarray) else len(buf)
+        self._check(self._lib.vf_host_register(self._ctx, addr, nbytes))
+        return addr
+
+    def host_unregister(self, addr: int) -> None:
+        self._check(self._lib.vf_host_unregister(self._ctx, addr))
+
+    def upload(self, ddst: int, hsrc, nbytes: int, stream: int = 0) -> None:
+        self._check(self._lib.vf_upload(self._ctx, ddst, _addr(hsrc), nbytes, stream or None))
+
+    def download(self, hdst, dsrc: int, nbytes: int, stream: int = 0) -> None:
+        self._check(self._lib.vf_download(self._ctx, _addr(hdst), dsrc, nbytes, stream or None))
+
+    def memset_device(self, d: int, value: int, nbytes: int, stream: int = 0) -> None:
+        self._check(self._lib.vf_memset_device(self._ctx, d, value, nbytes, stream or None))
+
+    def sync(self, stream: int = 0) -> None:
+        self._check(self._lib.vf_sync(self._ctx, stream or None))
+
+    def elapsed_ms(self) -> float:
+        ms = ctypes.c_float(0.0)
+        self._check(self._lib.vf_elapsed_ms(self._ctx, ctypes.byref(ms)))
+        return ms.value
+
+    def bench_device_ring(self, srcs: Sequence[int], dsts: Sequence[int], nbytes: int, steps: int,
+                          stream: int = 0) -> np.ndarray:
+        nbuf = len(srcs)
+        sa = (ctypes.c_void_p * nbuf)(*srcs)
+        da = (ctypes.c_void_p * nbuf)(*dsts)
+        out = np.zeros(max(steps, 1), dtype=np.float32)
+        self._check(self._lib.vf_bench_device_ring(self._ctx, sa, da, nbuf, nbytes, steps, stream or None,
+                                                   out.ctypes.data_as(_c_float_p)))
+        return out[:steps]
+
+
+_default_ctx: Optional[Context] = None
+
+
+def default_device() -> int:
+    """GPU of this worker process: VF_DEVICE, else LOCAL_RANK, else 0.
+
+    One process owns one GPU; a launcher that sets HIP_VISIBLE_DEVICES per
+    worker leaves the visible ordinal at 0.
+    """
+    for var in ("VF_DEVICE", "LOCAL_RANK"):
+        v = os.environ.get(var)
+        if v not in (None, ""):
+            return int(v)
+    return 0
+
+
+def get_context() -> Context:
+    """Process-wide default context (created on first use)."""
+    global _default_ctx
+    if _default_ctx is None:
+        _default_ctx = Context(default_device())
+    return _default_ctx

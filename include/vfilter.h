@@ -1,0 +1,150 @@
+/*
+ * vfilter.h — C ABI of libvfilter_hip.so, the MI355X (gfx950) frame-filter backend.
+ *
+ * This library replaces the per-frame filter of kylemcdonald/distributed-video-filter:
+ *
+ *     inverted = cv2.bitwise_not(frame)            # inverter.py:41
+ *
+ * called once per frame from Worker.start()         # worker.py:57 -> inverter.py:29-46
+ *
+ * The reference is pure Python; its "FFI" for this path is the Python call into
+ * OpenCV.  The build's Python side binds these entry points with ctypes
+ * (distributed-video-filter_amd/vfilter/_lib.py); INTEGRATION.md shows the binding.
+ *
+ * Conventions
+ *   - every entry point is extern "C", never throws, and returns an int status:
+ *     VF_OK (0) on success, a negative VF_E_* code on failure;
+ *   - the failing hipError_t and a human-readable message are kept per context
+ *     (vf_last_error) and per thread for calls made without a context;
+ *   - buffers are plain pointers and byte counts; any alignment and any byte count
+ *     (including 0 and counts that are not a multiple of 16) are accepted;
+ *   - HIP streams cross the boundary as `void*` (a hipStream_t; NULL = the null stream),
+ *     so no HIP or torch type appears in a signature;
+ *   - a context is bound to one device and is not thread-safe: one per worker process
+ *     (the reference runs one filter per process, worker.py:5-28).
+ *
+ * Semantics of the filter (OpenCV `bitwise_not`, inverter.py:41): dst[i] = ~src[i] for
+ * every byte of a C-contiguous uint8 H x W x 3 frame.  The operation is channel-order
+ * agnostic (BGR vs RGB irrelevant) and shape agnostic, so a batch of frames packed back
+ * to back is filtered as one byte range.
+ */
+#ifndef VFILTER_H
+#define VFILTER_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VF_ABI_VERSION 1
+
+/* status codes */
+#define VF_OK           0
+#define VF_E_INVALID   -1  /* bad argument (NULL pointer, negative count, size > capacity) */
+#define VF_E_HIP       -2  /* a HIP runtime call failed; see vf_last_error / vf_last_hip_error */
+#define VF_E_NOMEM     -3  /* host or device allocation failed */
+#define VF_E_NODEVICE  -4  /* no usable gfx950 device / bad device ordinal */
+
+typedef struct vf_ctx vf_ctx;
+
+/* ---- library / context ------------------------------------------------------------ */
+
+/* ABI version of the loaded library (VF_ABI_VERSION).  Makes no HIP call. */
+int vf_get_abi_version(void);
+
+/* Static string for a VF_* status code.  Makes no HIP call. */
+const char *vf_status_string(int status);
+
+/* Number of visible HIP devices (0 when there is no GPU; never fails for that). */
+int vf_device_count(int *out_count);
+
+/* Create a context on `device`.  Allocates the pinned host staging ring and device slot
+ * buffers used by the host->host entry points (each slot holds `max_frame_bytes` x
+ * `max_batch` bytes, clamped to [1 MiB, 64 MiB]) and creates one HIP stream per slot.
+ * Replaces the per-process filter state of InverterWorker.__init__ (inverter.py:10-20). */
+int vf_create(int device, size_t max_frame_bytes, int max_batch, vf_ctx **out);
+
+/* Destroy a context (NULL is allowed).  Synchronises its streams first. */
+int vf_destroy(vf_ctx *ctx);
+
+/* Last error message of `ctx`, or of the calling thread when ctx is NULL.  Never NULL. */
+const char *vf_last_error(const vf_ctx *ctx);
+
+/* Last hipError_t recorded by `ctx` (0 if none), or by the calling thread when ctx is NULL. */
+int vf_last_hip_error(const vf_ctx *ctx);
+
+/* Device ordinal of the context. */
+int vf_ctx_device(const vf_ctx *ctx, int *out_device);
+
+/* ---- host -> host filtering (synchronous) ------------------------------------------- */
+
+/* Invert `nbytes` bytes of host memory: dst[i] = ~src[i].
+ * Replaces `cv2.bitwise_not(frame)` (inverter.py:41) for one frame.  `src` and `dst` may
+ * be pageable or pinned, any alignment; they must not partially overlap (src == dst is
+ * allowed).  Runs H2D || kernel || D2H pipelined over the context's staging slots and
+ * returns when dst is complete. */
+int vf_invert_host(vf_ctx *ctx, const uint8_t *src, uint8_t *dst, size_t nbytes);
+
+/* Invert a batch of `n` frames of `frame_bytes` each, packed back to back in `src`;
+ * results packed the same way in `dst`.  Replaces the per-frame loop
+ * worker.py:35-57 -> inverter.py:41 for a batch.  Same rules as vf_invert_host. */
+int vf_invert_batch_host(vf_ctx *ctx, const uint8_t *src, uint8_t *dst,
+                         size_t frame_bytes, int n);
+
+/* Invert `n` separately allocated frames (srcs[i] -> dsts[i], nbytes[i] bytes each; sizes
+ * may differ, e.g. a mixed 480p/1080p/4K batch).  Frames are gathered into the staging
+ * slots, filtered with one kernel launch per slot and scattered back, so small frames are
+ * not paid for one launch each.  Replaces worker.py:50-57 + inverter.py:29-46 for a batch
+ * of raw frames. */
+int vf_invert_frames_host(vf_ctx *ctx, const uint8_t *const *srcs, uint8_t *const *dsts,
+                          const size_t *nbytes, int n);
+
+/* ---- device-resident filtering (asynchronous) -------------------------------------- */
+
+/* Enqueue the invert kernel on `stream` over device memory: ddst[i] = ~dsrc[i].
+ * Returns after the launch (does not synchronise).  Kernel-only path used by benchmarks
+ * and by callers that keep frames resident in HBM. */
+int vf_invert_device(vf_ctx *ctx, const void *dsrc, void *ddst, size_t nbytes, void *stream);
+
+/* Enqueue one launch over `n` device frames given by device-memory descriptor arrays
+ * (dsrcs/ddsts/nbytes are themselves arrays in DEVICE memory, n entries each).  For
+ * HBM-resident frame pools whose frames are not contiguous. */
+int vf_invert_device_frames(vf_ctx *ctx, const void *const *dsrcs, void *const *ddsts,
+                            const size_t *nbytes, int n, size_t total_bytes, void *stream);
+
+/* ---- memory helpers --------------------------------------------------------------- */
+
+int vf_alloc_device(vf_ctx *ctx, size_t nbytes, void **out);
+int vf_free_device(vf_ctx *ctx, void *p);
+/* page-locked host memory (DMA-able without staging) */
+int vf_alloc_host(vf_ctx *ctx, size_t nbytes, void **out);
+int vf_free_host(vf_ctx *ctx, void *p);
+/* page-lock an existing host range (e.g. a shared-memory frame ring) in place */
+int vf_host_register(vf_ctx *ctx, void *p, size_t nbytes);
+int vf_host_unregister(vf_ctx *ctx, void *p);
+/* asynchronous copies on `stream` (synchronous w.r.t. the host if the host side is pageable) */
+int vf_upload(vf_ctx *ctx, void *ddst, const void *hsrc, size_t nbytes, void *stream);
+int vf_download(vf_ctx *ctx, void *hdst, const void *dsrc, size_t nbytes, void *stream);
+int vf_memset_device(vf_ctx *ctx, void *d, int value, size_t nbytes, void *stream);
+/* wait for `stream` (NULL = every stream of the context and the device) */
+int vf_sync(vf_ctx *ctx, void *stream);
+
+/* ---- timing ----------------------------------------------------------------------- */
+
+/* Sum of kernel durations (ms, hipEvents) of the last host->host call on ctx. */
+int vf_elapsed_ms(const vf_ctx *ctx, float *out_ms);
+
+/* Benchmark loop over HBM-resident buffers: for step s in [0, steps) launch the invert
+ * kernel from srcs[s % nbuf] to dsts[s % nbuf] (`nbytes` each, host arrays of device
+ * pointers) on `stream`, with a hipEvent recorded before and after each launch; then
+ * synchronise and write each launch's duration (ms) to per_launch_ms[s] (may be NULL). */
+int vf_bench_device_ring(vf_ctx *ctx, void *const *srcs, void *const *dsts, int nbuf,
+                         size_t nbytes, int steps, void *stream, float *per_launch_ms);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* VFILTER_H */

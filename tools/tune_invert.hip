@@ -1,0 +1,147 @@
+// tune_invert.hip — kernel-variant sweep for the invert kernel on MI355X.
+//
+// Runs every (variant, grid cap) pair in interleaved rounds inside ONE process (guide §5.4
+// rule 24) over a ring of HBM buffers far larger than the 256 MiB Infinity Cache, so the
+// numbers are HBM rates, not cache rates.  Prints median / min / max algorithmic GB/s
+// (2 bytes moved per byte filtered) per pair, and checks every variant's output bytes.
+//
+//   tools/tune_invert [batch_bytes] [ring] [rounds] [launches]
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "vf_internal.h"
+
+#define CK(x)                                                                       \
+  do {                                                                              \
+    hipError_t e = (x);                                                             \
+    if (e != hipSuccess) {                                                          \
+      std::fprintf(stderr, "%s: %s (line %d)\n", #x, hipGetErrorString(e), __LINE__); \
+      std::exit(1);                                                                 \
+    }                                                                               \
+  } while (0)
+
+__global__ void fill_kernel(uint8_t *p, size_t n, uint32_t seed) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (; i < n; i += stride) {
+    uint32_t x = (uint32_t)i * 2654435761u ^ seed;
+    x ^= x >> 13;
+    x *= 0x5bd1e995u;
+    x ^= x >> 15;
+    p[i] = (uint8_t)x;
+  }
+}
+
+__global__ void check_kernel(const uint8_t *a, const uint8_t *b, size_t n, int *bad) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (; i < n; i += stride)
+    if ((uint8_t)~a[i] != b[i]) atomicAdd(bad, 1);
+}
+
+static const char *vname(int v) { return vf::variant_name(v); }
+
+int main(int argc, char **argv) {
+  size_t batch = argc > 1 ? std::strtoull(argv[1], nullptr, 0) : (size_t)32 * 1920 * 1080 * 3;
+  int ring = argc > 2 ? std::atoi(argv[2]) : 6;
+  int rounds = argc > 3 ? std::atoi(argv[3]) : 7;
+  int launches = argc > 4 ? std::atoi(argv[4]) : 24;
+  hipDeviceProp_t prop;
+  CK(hipGetDeviceProperties(&prop, 0));
+  const int cus = prop.multiProcessorCount;
+  std::printf("device %s, %d CUs, batch %zu B, ring %d (%.2f GB in+out)\n", prop.gcnArchName, cus,
+              batch, ring, 2.0 * batch * ring / 1e9);
+  std::vector<uint8_t *> src(ring), dst(ring);
+  for (int r = 0; r < ring; ++r) {
+    CK(hipMalloc(&src[r], batch));
+    CK(hipMalloc(&dst[r], batch));
+    hipLaunchKernelGGL(fill_kernel, dim3(4096), dim3(256), 0, 0, src[r], batch, 1234u + r);
+  }
+  int *bad;
+  CK(hipMalloc(&bad, sizeof(int)));
+  CK(hipDeviceSynchronize());
+
+  struct Cfg { int variant; int blocks; };
+  std::vector<Cfg> cfgs;
+  const int mults[] = {2, 4, 8, 16, 32, 1 << 20};  // blocks per CU cap; huge = one tile per block
+  const char *only = std::getenv("TUNE_VARIANTS");  // e.g. "0,1,2"
+  for (int v = 0; v < vf::kVariantCount; ++v) {
+    if (only && !std::strstr(only, std::to_string(v).c_str())) continue;
+    for (int m : mults) cfgs.push_back({v, (int)std::min<long>((long)cus * m, 1 << 30)});
+  }
+
+  // correctness of every variant (unaligned tail exercised with batch - 7 bytes)
+  for (const Cfg &c : cfgs) {
+    vf::LaunchCfg lc;
+    lc.variant = c.variant;
+    lc.max_blocks = c.blocks;
+    CK(hipMemset(dst[0], 0, batch));
+    CK(vf::launch_invert(src[0] + 3, dst[0] + 3, batch - 7, lc, 0));
+    CK(hipMemset(bad, 0, sizeof(int)));
+    hipLaunchKernelGGL(check_kernel, dim3(4096), dim3(256), 0, 0, src[0] + 3, dst[0] + 3,
+                       batch - 7, bad);
+    int h = 0;
+    CK(hipMemcpy(&h, bad, sizeof(int), hipMemcpyDeviceToHost));
+    if (h) {
+      std::printf("MISMATCH variant %s blocks %d: %d bad bytes\n", vname(c.variant), c.blocks, h);
+      return 2;
+    }
+  }
+  std::printf("all %zu variants bit-exact\n", cfgs.size());
+
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  std::vector<std::vector<double>> gbs(cfgs.size());
+  int slot = 0;
+  for (int rd = 0; rd < rounds; ++rd) {
+    for (size_t ci = 0; ci < cfgs.size(); ++ci) {
+      vf::LaunchCfg lc;
+      lc.variant = cfgs[ci].variant;
+      lc.max_blocks = cfgs[ci].blocks;
+      CK(vf::launch_invert(src[slot], dst[slot], batch, lc, 0));  // warm
+      slot = (slot + 1) % ring;
+      CK(hipEventRecord(e0, 0));
+      for (int l = 0; l < launches; ++l) {
+        CK(vf::launch_invert(src[slot], dst[slot], batch, lc, 0));
+        slot = (slot + 1) % ring;
+      }
+      CK(hipEventRecord(e1, 0));
+      CK(hipEventSynchronize(e1));
+      float ms = 0.f;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      gbs[ci].push_back(2.0 * batch * launches / (ms * 1e-3) / 1e9);
+    }
+  }
+  std::printf("%-8s %10s %10s %10s %10s %8s\n", "variant", "blocks", "median", "min", "max", "frac");
+  for (size_t ci = 0; ci < cfgs.size(); ++ci) {
+    auto v = gbs[ci];
+    std::sort(v.begin(), v.end());
+    std::printf("%-8s %10d %10.1f %10.1f %10.1f %8.3f\n", vname(cfgs[ci].variant), cfgs[ci].blocks,
+                v[v.size() / 2], v.front(), v.back(), v[v.size() / 2] / 8000.0);
+  }
+  // reference point: hipMemcpyDtoD of the same bytes (same traffic as the filter)
+  std::vector<double> cp;
+  for (int rd = 0; rd < rounds; ++rd) {
+    CK(hipEventRecord(e0, 0));
+    for (int l = 0; l < launches; ++l) {
+      CK(hipMemcpyAsync(dst[slot], src[slot], batch, hipMemcpyDeviceToDevice, 0));
+      slot = (slot + 1) % ring;
+    }
+    CK(hipEventRecord(e1, 0));
+    CK(hipEventSynchronize(e1));
+    float ms = 0.f;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    cp.push_back(2.0 * batch * launches / (ms * 1e-3) / 1e9);
+  }
+  std::sort(cp.begin(), cp.end());
+  std::printf("%-8s %10s %10.1f %10.1f %10.1f %8.3f\n", "hipMemcpyD2D", "-", cp[cp.size() / 2],
+              cp.front(), cp.back(), cp[cp.size() / 2] / 8000.0);
+  return 0;
+}
