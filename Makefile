@@ -20,11 +20,14 @@ $(LIB): $(CSRC)/vf_kernels.hip $(CSRC)/vf_api.hip $(CSRC)/vf_internal.h include/
 oracle:
 	$(MAKE) -C oracle
 
-tools: tools/tune_invert
+tools: tools/tune_invert tools/pcie_probe
+
+tools/pcie_probe: tools/pcie_probe.hip
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 $< -o $@
 
 tools/tune_invert: tools/tune_invert.hip $(CSRC)/vf_kernels.hip $(CSRC)/vf_internal.h
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -Iinclude -I$(CSRC) tools/tune_invert.hip $(CSRC)/vf_kernels.hip -o $@
 
 clean:
-	rm -f $(LIB) tools/tune_invert
+	rm -f $(LIB) tools/tune_invert tools/pcie_probe
 	$(MAKE) -C oracle clean

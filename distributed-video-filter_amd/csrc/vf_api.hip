@@ -356,8 +356,8 @@ VF_EXPORT int vf_create(int device, size_t max_frame_bytes, int max_batch, vf_ct
   ctx->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
   ctx->cfg.variant = (int)env_size("VF_VARIANT", (size_t)vf::kVariantU4NT);
   if (ctx->cfg.variant < 0 || ctx->cfg.variant >= vf::kVariantCount) ctx->cfg.variant = vf::kVariantU4NT;
-  ctx->cfg.max_blocks = (int)env_size("VF_MAX_BLOCKS", (size_t)ctx->num_cus * 16);
-  if (ctx->cfg.max_blocks < 1) ctx->cfg.max_blocks = ctx->num_cus * 16;
+  ctx->cfg.max_blocks = (int)env_size("VF_MAX_BLOCKS", (size_t)ctx->num_cus * 32);
+  if (ctx->cfg.max_blocks < 1) ctx->cfg.max_blocks = ctx->num_cus * 32;
   ctx->nslots = (int)std::min<size_t>(kMaxSlots, std::max<size_t>(2, env_size("VF_SLOTS", 4)));
   size_t want = max_frame_bytes ? max_frame_bytes * (size_t)max_batch : (size_t)8 << 20;
   size_t slot = env_size("VF_SLOT_BYTES", std::min(want, (size_t)8 << 20));
@@ -595,33 +595,47 @@ VF_EXPORT int vf_elapsed_ms(const vf_ctx *ctx, float *out_ms) {
 }
 
 VF_EXPORT int vf_bench_device_ring(vf_ctx *ctx, void *const *srcs, void *const *dsts, int nbuf,
-                                   size_t nbytes, int steps, void *stream, float *per_launch_ms) {
+                                   size_t nbytes, int steps, void *stream, float *per_launch_ms,
+                                   float *region_ms) {
   VF_CHECK_CTX(ctx);
   if (!srcs || !dsts || nbuf < 1 || steps < 0)
     return set_err(ctx, VF_E_INVALID, 0, "vf_bench_device_ring: bad arguments");
   VF_HIP(ctx, hipSetDevice(ctx->device));
   hipStream_t st = (hipStream_t)stream;
-  std::vector<hipEvent_t> ev(2 * (size_t)steps, nullptr);
+  const bool each = per_launch_ms != nullptr;
+  std::vector<hipEvent_t> ev((each ? 2 * (size_t)steps : 0) + 2, nullptr);
   int rc = VF_OK;
   for (auto &e : ev) {
     hipError_t h = hipEventCreate(&e);
     if (h != hipSuccess) { rc = fail_hip(ctx, h, "hipEventCreate", __LINE__); break; }
   }
+  hipEvent_t r0 = ev[ev.size() - 2], r1 = ev[ev.size() - 1];
+  if (rc == VF_OK) {
+    hipError_t h = hipEventRecord(r0, st);
+    if (h != hipSuccess) rc = fail_hip(ctx, h, "hipEventRecord", __LINE__);
+  }
   for (int s = 0; s < steps && rc == VF_OK; ++s) {
-    hipError_t h = hipEventRecord(ev[2 * s], st);
+    hipError_t h = each ? hipEventRecord(ev[2 * s], st) : hipSuccess;
     if (h == hipSuccess) h = vf::launch_invert(srcs[s % nbuf], dsts[s % nbuf], nbytes, ctx->cfg, st);
-    if (h == hipSuccess) h = hipEventRecord(ev[2 * s + 1], st);
+    if (h == hipSuccess && each) h = hipEventRecord(ev[2 * s + 1], st);
     if (h != hipSuccess) rc = fail_hip(ctx, h, "bench launch", __LINE__);
   }
   if (rc == VF_OK) {
-    hipError_t h = hipStreamSynchronize(st);
+    hipError_t h = hipEventRecord(r1, st);
+    if (h == hipSuccess) h = hipStreamSynchronize(st);
     if (h != hipSuccess) rc = fail_hip(ctx, h, "hipStreamSynchronize", __LINE__);
   }
-  for (int s = 0; s < steps && rc == VF_OK && per_launch_ms; ++s) {
+  for (int s = 0; s < steps && rc == VF_OK && each; ++s) {
     float ms = 0.f;
     hipError_t h = hipEventElapsedTime(&ms, ev[2 * s], ev[2 * s + 1]);
     if (h != hipSuccess) { rc = fail_hip(ctx, h, "hipEventElapsedTime", __LINE__); break; }
     per_launch_ms[s] = ms;
+  }
+  if (rc == VF_OK && region_ms) {
+    float ms = 0.f;
+    hipError_t h = hipEventElapsedTime(&ms, r0, r1);
+    if (h != hipSuccess) rc = fail_hip(ctx, h, "hipEventElapsedTime", __LINE__);
+    *region_ms = ms;
   }
   for (auto &e : ev)
     if (e) (void)hipEventDestroy(e);

@@ -12,7 +12,7 @@ constexpr int kBlock = 256;  // 4 waves of 64 lanes
 // Un = n independent 16-B loads in flight per lane; NT = nontemporal loads and stores
 // (`global_load/store_dwordx4 ... nt`), NTL / NTS = nontemporal on one side only.
 enum Variant : int {
-  kVariantU4NT = 0,  // default: measured 6.29 TB/s at 16 blocks/CU (profiles/r01_tune.txt)
+  kVariantU4NT = 0,  // default: 6.32 TB/s at 32 blocks/CU (profiles/r01_tune_sweep2.txt)
   kVariantU2NT = 1,
   kVariantU8NT = 2,
   kVariantU1NT = 3,
@@ -29,7 +29,7 @@ const char *variant_name(int v);
 
 struct LaunchCfg {
   int variant = kVariantU4NT;
-  int max_blocks = 4096;  // grid cap: 16 workgroups per CU on 256 CUs
+  int max_blocks = 8192;  // grid cap: 32 workgroups per CU on 256 CUs
 };
 
 hipError_t launch_invert(const void *dsrc, void *ddst, size_t nbytes, const LaunchCfg &cfg,

@@ -58,7 +58,8 @@ SIGNATURES = {
     "vf_memset_device": (ctypes.c_int, [_vp, _vp, ctypes.c_int, _sz, _vp]),
     "vf_sync": (ctypes.c_int, [_vp, _vp]),
     "vf_elapsed_ms": (ctypes.c_int, [_vp, _c_float_p]),
-    "vf_bench_device_ring": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_int, _sz, ctypes.c_int, _vp, _c_float_p]),
+    "vf_bench_device_ring": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_int, _sz, ctypes.c_int, _vp, _c_float_p,
+                                            _c_float_p]),
 }
 
 
@@ -234,14 +235,18 @@ class Context:
         return ms.value
 
     def bench_device_ring(self, srcs: Sequence[int], dsts: Sequence[int], nbytes: int, steps: int,
-                          stream: int = 0) -> np.ndarray:
+                          stream: int = 0, per_launch: bool = False):
+        """Launch ``steps`` kernels back to back over the ring; returns (region_ms,
+        per-launch ms array or None).  See vf_bench_device_ring."""
         nbuf = len(srcs)
         sa = (ctypes.c_void_p * nbuf)(*srcs)
         da = (ctypes.c_void_p * nbuf)(*dsts)
-        out = np.zeros(max(steps, 1), dtype=np.float32)
-        self._check(self._lib.vf_bench_device_ring(self._ctx, sa, da, nbuf, nbytes, steps, stream or None,
-                                                   out.ctypes.data_as(_c_float_p)))
-        return out[:steps]
+        out = np.zeros(max(steps, 1), dtype=np.float32) if per_launch else None
+        region = ctypes.c_float(0.0)
+        self._check(self._lib.vf_bench_device_ring(
+            self._ctx, sa, da, nbuf, nbytes, steps, stream or None,
+            out.ctypes.data_as(_c_float_p) if per_launch else None, ctypes.byref(region)))
+        return region.value, (out[:steps] if per_launch else None)
 
 
 _default_ctx: Optional[Context] = None

@@ -1,0 +1,362 @@
+"""Message transport between distributor and workers.
+
+The reference uses ZeroMQ over TCP: the distributor binds a ROUTER (dispatch,
+distributor.py:30-31) and a PULL (collect, :34-35); each worker connects a DEALER
+(worker.py:20-21) and a PUSH (:24-25).  Two interchangeable implementations of those four
+roles live here:
+
+  "zmq"  pyzmq, exactly the reference's sockets and multipart framing, so this build's
+         distributor and workers interoperate with the reference's (needs pyzmq; on this
+         image only /opt/conda/bin/python3.9 has it);
+  "tcp"  stdlib sockets with the same roles and semantics (multipart messages; ROUTER
+         prefixes the peer identity; DEALER/PUSH connect lazily and retry), for
+         interpreters without pyzmq — e.g. the GPU box's main python3.
+
+Large frames should not ride either of them between processes of one node: see
+``shm.FrameRing`` (frames in a page-locked shared-memory ring, only indices on the wire).
+
+Wire framing of "tcp": message = u32 nparts, then per part u64 length + bytes (little endian).
+"""
+from __future__ import annotations
+
+import itertools
+import queue
+import select
+import socket
+import struct
+import threading
+import time
+from typing import List, Optional, Sequence, Tuple
+
+_HDR = struct.Struct("<I")
+_LEN = struct.Struct("<Q")
+
+
+def zmq_available() -> bool:
+    try:
+        import zmq  # noqa: F401
+        return True
+    except Exception:
+        return False
+
+
+def resolve(kind: str) -> str:
+    if kind == "auto":
+        return "zmq" if zmq_available() else "tcp"
+    if kind not in ("zmq", "tcp"):
+        raise ValueError(f"unknown transport {kind!r} (zmq | tcp | auto)")
+    return kind
+
+
+# ---------------------------------------------------------------------------------------
+# stdlib TCP implementation
+# ---------------------------------------------------------------------------------------
+
+def _recv_exact(sock: socket.socket, n: int) -> bytearray:
+    buf = bytearray(n)
+    view = memoryview(buf)
+    got = 0
+    while got < n:
+        k = sock.recv_into(view[got:], n - got)
+        if k == 0:
+            raise ConnectionError("peer closed")
+        got += k
+    return buf
+
+
+def _recv_msg(sock: socket.socket) -> List[bytes]:
+    (nparts,) = _HDR.unpack(_recv_exact(sock, _HDR.size))
+    parts = []
+    for _ in range(nparts):
+        (n,) = _LEN.unpack(_recv_exact(sock, _LEN.size))
+        parts.append(bytes(_recv_exact(sock, n)) if n < (1 << 16) else _recv_exact(sock, n))
+    return parts
+
+
+def _send_msg(sock: socket.socket, parts: Sequence) -> None:
+    bufs = [_HDR.pack(len(parts))]
+    for p in parts:
+        mv = memoryview(p).cast("B") if not isinstance(p, (bytes, bytearray)) else p
+        bufs.append(_LEN.pack(len(mv)))
+        bufs.append(mv)
+    # gather-write; sendmsg may send partially, so finish with sendall on the remainder
+    total = sum(len(b) for b in bufs)
+    sent = sock.sendmsg(bufs)
+    if sent < total:
+        for b in bufs:
+            if sent >= len(b):
+                sent -= len(b)
+                continue
+            sock.sendall(memoryview(b)[sent:])
+            sent = 0
+
+
+def _bind_addr(host: str) -> str:
+    return "0.0.0.0" if host in ("*", "", None) else host
+
+
+class _Listener:
+    """Accepts peers; every message from any peer lands in one queue as (peer_id, parts)."""
+
+    def __init__(self, host: str, port: int):
+        self.sock = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+        self.sock.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+        self.sock.bind((_bind_addr(host), port))
+        self.sock.listen(64)
+        self.port = self.sock.getsockname()[1]
+        self.inbox: "queue.Queue[Tuple[bytes, List[bytes]]]" = queue.Queue()
+        self.peers = {}
+        self._ids = itertools.count(1)
+        self._lock = threading.Lock()
+        self._closed = False
+        threading.Thread(target=self._accept_loop, daemon=True).start()
+
+    def _accept_loop(self):
+        while not self._closed:
+            try:
+                conn, _ = self.sock.accept()
+            except OSError:
+                return
+            conn.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+            pid = b"\x00" + next(self._ids).to_bytes(4, "big")  # ZeroMQ-style 5-byte identity
+            with self._lock:
+                self.peers[pid] = (conn, threading.Lock())
+            threading.Thread(target=self._read_loop, args=(pid, conn), daemon=True).start()
+
+    def _read_loop(self, pid, conn):
+        try:
+            while not self._closed:
+                self.inbox.put((pid, _recv_msg(conn)))
+        except (ConnectionError, OSError):
+            pass
+        finally:
+            with self._lock:
+                self.peers.pop(pid, None)
+            try:
+                conn.close()
+            except OSError:
+                pass
+
+    def poll(self, timeout_ms: int) -> bool:
+        if not self.inbox.empty():
+            return True
+        deadline = time.monotonic() + timeout_ms / 1000.0
+        while time.monotonic() < deadline:
+            time.sleep(0.0002)
+            if not self.inbox.empty():
+                return True
+        return False
+
+    def recv(self, timeout_ms: Optional[int] = None):
+        try:
+            return self.inbox.get(timeout=None if timeout_ms is None else timeout_ms / 1000.0)
+        except queue.Empty:
+            return None
+
+    def send_to(self, pid: bytes, parts: Sequence) -> bool:
+        with self._lock:
+            ent = self.peers.get(pid)
+        if ent is None:
+            return False  # ROUTER drops messages to unknown peers
+        conn, lk = ent
+        with lk:
+            try:
+                _send_msg(conn, parts)
+                return True
+            except OSError:
+                return False
+
+    def close(self):
+        self._closed = True
+        try:
+            self.sock.close()
+        except OSError:
+            pass
+        with self._lock:
+            for conn, _ in self.peers.values():
+                try:
+                    conn.close()
+                except OSError:
+                    pass
+            self.peers.clear()
+
+
+class _Connection:
+    """Connecting side (DEALER / PUSH): connects lazily, retrying until the peer binds."""
+
+    def __init__(self, host: str, port: int, connect_timeout: float = 30.0):
+        self.addr = ("127.0.0.1" if host in ("localhost", "*") else host, port)
+        self.connect_timeout = connect_timeout
+        self.sock: Optional[socket.socket] = None
+        self._lock = threading.Lock()
+
+    def _ensure(self):
+        if self.sock is not None:
+            return
+        deadline = time.monotonic() + self.connect_timeout
+        while True:
+            try:
+                s = socket.create_connection(self.addr, timeout=2.0)
+                s.settimeout(None)
+                s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+                self.sock = s
+                return
+            except OSError:
+                if time.monotonic() > deadline:
+                    raise
+                time.sleep(0.05)
+
+    def send(self, parts: Sequence) -> None:
+        with self._lock:
+            self._ensure()
+            _send_msg(self.sock, parts)
+
+    def poll(self, timeout_ms: int) -> bool:
+        self._ensure()
+        r, _, _ = select.select([self.sock], [], [], timeout_ms / 1000.0)
+        return bool(r)
+
+    def recv(self) -> List[bytes]:
+        self._ensure()
+        return _recv_msg(self.sock)
+
+    def close(self):
+        if self.sock is not None:
+            try:
+                self.sock.close()
+            except OSError:
+                pass
+            self.sock = None
+
+
+# ---------------------------------------------------------------------------------------
+# role objects used by the distributor and the worker
+# ---------------------------------------------------------------------------------------
+
+class RouterEnd:
+    """Distributor dispatch socket (reference: ROUTER bind, distributor.py:30-31)."""
+
+    def __init__(self, kind: str, host: str, port: int, ctx=None):
+        self.kind = resolve(kind)
+        if self.kind == "zmq":
+            import zmq
+            self._zmq = zmq
+            self.sock = ctx.socket(zmq.ROUTER)
+            self.sock.bind(f"tcp://{host if host not in ('localhost',) else '127.0.0.1'}:{port}")
+            self.port = int(self.sock.getsockopt_string(zmq.LAST_ENDPOINT).rsplit(":", 1)[1])
+        else:
+            self.sock = _Listener(host, port)
+            self.port = self.sock.port
+
+    def poll(self, timeout_ms: int) -> bool:
+        return bool(self.sock.poll(timeout_ms))
+
+    def recv(self) -> Tuple[bytes, List[bytes]]:
+        if self.kind == "zmq":
+            parts = self.sock.recv_multipart(self._zmq.NOBLOCK)
+            return parts[0], parts[1:]
+        got = self.sock.recv(0)
+        if got is None:
+            raise BlockingIOError
+        return got
+
+    def send(self, peer: bytes, parts: Sequence) -> bool:
+        if self.kind == "zmq":
+            self.sock.send_multipart([peer] + list(parts), copy=False)
+            return True
+        return self.sock.send_to(peer, parts)
+
+    def close(self):
+        self.sock.close()
+
+
+class PullEnd:
+    """Distributor collect socket (reference: PULL bind, distributor.py:34-35)."""
+
+    def __init__(self, kind: str, host: str, port: int, ctx=None):
+        self.kind = resolve(kind)
+        if self.kind == "zmq":
+            import zmq
+            self._zmq = zmq
+            self.sock = ctx.socket(zmq.PULL)
+            self.sock.bind(f"tcp://{host if host not in ('localhost',) else '127.0.0.1'}:{port}")
+            self.port = int(self.sock.getsockopt_string(zmq.LAST_ENDPOINT).rsplit(":", 1)[1])
+        else:
+            self.sock = _Listener(host, port)
+            self.port = self.sock.port
+
+    def poll(self, timeout_ms: int) -> bool:
+        return bool(self.sock.poll(timeout_ms))
+
+    def recv(self) -> List[bytes]:
+        if self.kind == "zmq":
+            return self.sock.recv_multipart(self._zmq.NOBLOCK)
+        got = self.sock.recv(0)
+        if got is None:
+            raise BlockingIOError
+        return got[1]
+
+    def close(self):
+        self.sock.close()
+
+
+class DealerEnd:
+    """Worker request socket (reference: DEALER connect, worker.py:20-21)."""
+
+    def __init__(self, kind: str, host: str, port: int, ctx=None):
+        self.kind = resolve(kind)
+        if self.kind == "zmq":
+            import zmq
+            self._zmq = zmq
+            self.sock = ctx.socket(zmq.DEALER)
+            self.sock.connect(f"tcp://{host}:{port}")
+        else:
+            self.sock = _Connection(host, port)
+
+    def send(self, parts: Sequence) -> None:
+        if self.kind == "zmq":
+            self.sock.send_multipart(list(parts), self._zmq.NOBLOCK)
+        else:
+            self.sock.send(parts)
+
+    def poll(self, timeout_ms: int) -> bool:
+        return bool(self.sock.poll(timeout_ms))
+
+    def recv(self) -> List[bytes]:
+        if self.kind == "zmq":
+            return self.sock.recv_multipart(self._zmq.NOBLOCK)
+        return self.sock.recv()
+
+    def close(self):
+        self.sock.close(0) if self.kind == "zmq" else self.sock.close()
+
+
+class PushEnd:
+    """Worker result socket (reference: PUSH connect, worker.py:24-25)."""
+
+    def __init__(self, kind: str, host: str, port: int, ctx=None):
+        self.kind = resolve(kind)
+        if self.kind == "zmq":
+            import zmq
+            self._zmq = zmq
+            self.sock = ctx.socket(zmq.PUSH)
+            self.sock.connect(f"tcp://{host}:{port}")
+        else:
+            self.sock = _Connection(host, port)
+
+    def send(self, parts: Sequence) -> None:
+        if self.kind == "zmq":
+            self.sock.send_multipart(list(parts), self._zmq.NOBLOCK, copy=False)
+        else:
+            self.sock.send(parts)
+
+    def close(self):
+        self.sock.close(0) if self.kind == "zmq" else self.sock.close()
+
+
+def make_context(kind: str):
+    """A zmq.Context for the "zmq" transport, else None."""
+    if resolve(kind) == "zmq":
+        import zmq
+        return zmq.Context()
+    return None

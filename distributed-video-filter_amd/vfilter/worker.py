@@ -1,0 +1,200 @@
+"""Worker runtime: the per-process frame loop (reference: worker.py:5-80).
+
+Plugin API unchanged: subclass ``Worker`` and implement ``__call__(frame) -> bytes-like``
+(worker.py:78-80).  The loop pulls frames from a distributor, calls the plugin, and pushes
+results back.  Two protocols (``vfilter.wire``):
+
+  v0  the reference loop, message for message (worker.py:35-76): send "READY" (NOBLOCK),
+      poll 10 ms, receive [index, frame], call the plugin, send the 5-part result.  Use it
+      against the reference's own distributor.py.
+  v1  batched and pipelined: keep ``depth`` credit requests of ``batch`` frames in flight,
+      hand each received batch to ``process_batch`` (default: the plugin per frame; a GPU
+      plugin overrides it with one gathered device call), send one result message per
+      batch.  Frames may arrive in a shared-memory ring (``vfilter.shm``); the worker then
+      maps the ring, page-locks it once for the GPU and writes results in place.
+
+Per-frame exceptions are caught, counted and reported (the reference prints and drops the
+frame, worker.py:74-76; v1 additionally tells the distributor which index failed so an
+in-order consumer does not wait for it).  One worker process owns one GPU.
+"""
+from __future__ import annotations
+
+import os
+import time
+from typing import List, Optional, Sequence
+
+from . import transport as tp
+from . import wire
+from .shm import FrameRing
+
+
+class Worker:
+    def __init__(self, host: str = "localhost", distribute_port: int = 5555, collect_port: int = 5556, *,
+                 transport: str = "auto", protocol: str = "v1", batch: int = 1, depth: int = 2,
+                 verbose: bool = False):
+        self.host = host
+        self.distribute_port = distribute_port
+        self.collect_port = collect_port
+        self.running = False
+        self.shutdown_requested = False
+        self.process_id = os.getpid()                       # worker.py:14
+        if protocol not in ("v0", "v1"):
+            raise ValueError("protocol must be 'v0' (reference) or 'v1'")
+        self.protocol = protocol
+        self.batch = max(1, int(batch))
+        self.depth = max(1, int(depth))
+        self.verbose = verbose
+        self.transport = tp.resolve(transport)
+        self._zctx = tp.make_context(self.transport)
+        self.dealer_socket = tp.DealerEnd(self.transport, host, distribute_port, self._zctx)   # worker.py:20-21
+        self.collect_socket = tp.PushEnd(self.transport, host, collect_port, self._zctx)       # worker.py:24-25
+        self.frames_processed = 0
+        self.errors = 0
+        self._ring: Optional[FrameRing] = None
+        self._ring_name: Optional[str] = None
+        if verbose:
+            print(f"Worker started on ports {distribute_port} (request) and {collect_port} (send)")
+            print(f"Process ID: {self.process_id}")
+
+    # -- plugin API (worker.py:78-80) ----------------------------------------------------
+    def __call__(self, frame):
+        raise NotImplementedError("Subclasses must implement __call__ method")
+
+    def process_batch(self, frames: Sequence, metas: Sequence[wire.FrameMeta], outs: Sequence) -> List:
+        """Filter a batch.  ``outs[i]`` is a writable buffer for frame i's result when the
+        frame lives in the shared-memory ring, else None.  Returns, per frame, the result
+        (bytes-like; ignored where ``outs[i]`` was given and filled in place) or an
+        Exception instance for a frame that failed.  Default: the plugin, frame by frame."""
+        results = []
+        for f, o in zip(frames, outs):
+            try:
+                r = self(f)
+                if o is not None:
+                    o[:] = memoryview(r).cast("B")
+                results.append(r)
+            except Exception as e:  # worker.py:74-76
+                results.append(e)
+        return results
+
+    def on_ring_attached(self, ring: FrameRing) -> None:
+        """Hook: a GPU worker page-locks the ring here."""
+
+    # -- loop --------------------------------------------------------------------------
+    def start(self, max_frames: Optional[int] = None):
+        """Run until ``running`` is cleared (signal) or ``max_frames`` results were sent."""
+        self.running = True
+        if self.verbose:
+            print("Worker is running...")
+        try:
+            if self.protocol == "v0":
+                self._loop_v0(max_frames)
+            else:
+                self._loop_v1(max_frames)
+        finally:
+            self.running = False
+
+    def stop(self):
+        self.running = False
+
+    def close(self):
+        self.running = False
+        if self._ring is not None:
+            self._ring.close()
+            self._ring = None
+        self.dealer_socket.close()
+        self.collect_socket.close()
+        if self._zctx is not None:
+            self._zctx.term()
+
+    def _loop_v0(self, max_frames):
+        """worker.py:35-76, with the per-frame print gated by ``verbose``."""
+        while self.running and (max_frames is None or self.frames_processed < max_frames):
+            try:
+                try:
+                    self.dealer_socket.send(wire.encode_request(version=0))      # worker.py:39
+                except BlockingIOError:
+                    time.sleep(0.001)
+                    continue
+                except Exception as e:
+                    if type(e).__name__ == "Again":
+                        time.sleep(0.001)
+                        continue
+                    raise
+                if self.dealer_socket.poll(10):                               # worker.py:46
+                    start_time = time.time()                                  # worker.py:47
+                    d = wire.decode_dispatch(self.dealer_socket.recv())       # worker.py:50-51
+                    meta, frame = d.metas[0], d.payloads[0]
+                    if self.verbose:
+                        print(f"Processing frame {meta.index}")
+                    try:
+                        processed = self(frame)                               # worker.py:57
+                    except Exception as e:                                    # worker.py:74-76
+                        self.errors += 1
+                        print(f"Error in worker: {e}")
+                        continue
+                    end_time = time.time()                                    # worker.py:59
+                    self.collect_socket.send(wire.encode_result_v0(meta.index, self.process_id,
+                                                                   start_time, end_time, processed))
+                    self.frames_processed += 1
+            except Exception as e:
+                print(f"Error in worker: {e}")
+                continue
+
+    def _attach_ring(self, name: str, slot_bytes: int) -> FrameRing:
+        if self._ring is None or self._ring_name != name:
+            if self._ring is not None:
+                self._ring.close()
+            self._ring = FrameRing(name=name, slot_bytes=slot_bytes)
+            self._ring_name = name
+            self.on_ring_attached(self._ring)
+        return self._ring
+
+    def _loop_v1(self, max_frames):
+        outstanding = 0
+        while self.running and (max_frames is None or self.frames_processed < max_frames):
+            while outstanding < self.depth:
+                self.dealer_socket.send(wire.encode_request(self.batch, shm=True))
+                outstanding += 1
+            if not self.dealer_socket.poll(10):
+                continue
+            parts = self.dealer_socket.recv()
+            start_time = time.time()
+            try:
+                d = wire.decode_dispatch(parts)
+            except Exception as e:
+                print(f"Error in worker: bad dispatch message: {e}")
+                continue
+            if d.version == 1:
+                outstanding -= 1
+            ring = None
+            if d.ring is not None:
+                ring = self._attach_ring(d.ring["name"], int(d.ring["slot_bytes"]))
+            frames, outs = [], []
+            for m, p in zip(d.metas, d.payloads):
+                if m.slot is not None:
+                    frames.append(ring.in_view(m.slot, m.nbytes))
+                    outs.append(ring.out_view(m.slot, m.nbytes))
+                else:
+                    frames.append(p)
+                    outs.append(None)
+            if self.verbose:
+                print(f"Processing frames {[m.index for m in d.metas]}")
+            try:
+                results = self.process_batch(frames, d.metas, outs)
+            except Exception as e:
+                results = [e] * len(frames)
+            end_time = time.time()
+            metas, payloads = [], []
+            for m, r in zip(d.metas, results):
+                om = wire.FrameMeta(index=m.index, nbytes=m.nbytes, shape=m.shape, slot=m.slot,
+                                    start=start_time, end=end_time)
+                if isinstance(r, Exception):
+                    self.errors += 1
+                    om.error = f"{type(r).__name__}: {r}"
+                    print(f"Error in worker: frame {m.index}: {r}")
+                    payloads.append(None)
+                else:
+                    payloads.append(None if m.slot is not None else r)
+                metas.append(om)
+            self.collect_socket.send(wire.encode_result(self.process_id, metas, payloads))
+            self.frames_processed += len(metas)

@@ -138,10 +138,13 @@ int vf_elapsed_ms(const vf_ctx *ctx, float *out_ms);
 
 /* Benchmark loop over HBM-resident buffers: for step s in [0, steps) launch the invert
  * kernel from srcs[s % nbuf] to dsts[s % nbuf] (`nbytes` each, host arrays of device
- * pointers) on `stream`, with a hipEvent recorded before and after each launch; then
- * synchronise and write each launch's duration (ms) to per_launch_ms[s] (may be NULL). */
+ * pointers) back to back on `stream`, then synchronise.  A hipEvent pair brackets the whole
+ * sequence; its duration (ms) goes to *region_ms (may be NULL).  If per_launch_ms is not
+ * NULL, an extra event pair is recorded around every launch and each launch's duration goes
+ * to per_launch_ms[s] (the pairs add a few microseconds of gap per launch). */
 int vf_bench_device_ring(vf_ctx *ctx, void *const *srcs, void *const *dsts, int nbuf,
-                         size_t nbytes, int steps, void *stream, float *per_launch_ms);
+                         size_t nbytes, int steps, void *stream, float *per_launch_ms,
+                         float *region_ms);
 
 #ifdef __cplusplus
 }
