@@ -6,9 +6,12 @@
 //   * the one-frame-per-iteration worker loop   worker.py:35-57     -> vf_invert_batch_host,
 //                                                                      vf_invert_frames_host
 // Host->host calls run a slot pipeline: the byte stream (one range, a packed batch, or a
-// gather list of frames) is cut into slot-sized chunks; chunk i uses slot i % S, whose own
-// HIP stream carries H2D -> kernel -> D2H, so DMA in, the kernel and DMA out of different
-// chunks overlap across the slot streams (the copy engines run both directions at once).
+// gather list of frames) is cut into slot-sized chunks; chunk i uses slot i % S.  Two HIP
+// streams carry the work: the IN stream runs H2D(i) -> kernel(i), the OUT stream waits on
+// kernel(i)'s event and runs D2H(i).  Keeping the two directions on separate streams puts
+// them on separate SDMA engines, so DMA in, the kernel and DMA out of different chunks all
+// overlap (one stream per slot serialises both directions on one engine: measured 28 GB/s
+// each way vs 46 GB/s with split streams, profiles/r01_pcie_probe.txt).
 // Pageable caller memory is staged through pinned slot buffers by a small host copy pool;
 // caller memory that is already page-locked (vf_alloc_host / vf_host_register, e.g. a
 // shared-memory frame ring) is DMA'd directly with no host copy.
@@ -45,7 +48,8 @@ thread_local ErrState g_thread_err;
 // ---- host copy pool -------------------------------------------------------------------
 // memcpy of large staging chunks split over a few persistent threads: one core moves
 // ~10 GB/s, well under one PCIe Gen5 x16 direction, so a single-threaded stage would cap
-// the end-to-end rate.
+// the end-to-end rate (1080p x 32 pageable: 30.5 GB/s each way with 4 threads, 40.5 with 8;
+// pinned, i.e. no staging: 42.9).
 class CopyPool {
  public:
   explicit CopyPool(int nthreads) : n_(std::max(1, nthreads)) {
@@ -124,8 +128,8 @@ struct OutPiece {
 };
 
 struct Slot {
-  hipStream_t stream = nullptr;
-  hipEvent_t k0 = nullptr, k1 = nullptr;
+  hipEvent_t k0 = nullptr, k1 = nullptr;  // kernel start / end (on the IN stream)
+  hipEvent_t done = nullptr;              // D2H complete (on the OUT stream)
   uint8_t *pin_in = nullptr, *pin_out = nullptr;
   uint8_t *d_in = nullptr, *d_out = nullptr;
   bool busy = false;
@@ -155,6 +159,7 @@ struct vf_ctx {
   int num_cus = 256;
   int nslots = 4;
   size_t slot_bytes = 0;
+  hipStream_t s_in = nullptr, s_out = nullptr;
   Slot slots[kMaxSlots];
   vf::LaunchCfg cfg;
   CopyPool *pool = nullptr;
@@ -209,25 +214,29 @@ bool is_pinned(const void *p) {
 }
 
 int release_slots(vf_ctx *ctx) {
+  if (ctx->s_in) (void)hipStreamSynchronize(ctx->s_in);
+  if (ctx->s_out) (void)hipStreamSynchronize(ctx->s_out);
   for (int i = 0; i < kMaxSlots; ++i) {
     Slot &s = ctx->slots[i];
-    if (s.stream) (void)hipStreamSynchronize(s.stream);
     if (s.k0) (void)hipEventDestroy(s.k0);
     if (s.k1) (void)hipEventDestroy(s.k1);
+    if (s.done) (void)hipEventDestroy(s.done);
     if (s.pin_in) (void)hipHostFree(s.pin_in);
     if (s.pin_out) (void)hipHostFree(s.pin_out);
     if (s.d_in) (void)hipFree(s.d_in);
     if (s.d_out) (void)hipFree(s.d_out);
-    if (s.stream) (void)hipStreamDestroy(s.stream);
     s = Slot();
   }
+  if (ctx->s_in) (void)hipStreamDestroy(ctx->s_in);
+  if (ctx->s_out) (void)hipStreamDestroy(ctx->s_out);
+  ctx->s_in = ctx->s_out = nullptr;
   return VF_OK;
 }
 
 // Wait for slot `s`, scatter its staged output, add its kernel time.
 int complete_slot(vf_ctx *ctx, Slot &s) {
   if (!s.busy) return VF_OK;
-  VF_HIP(ctx, hipStreamSynchronize(s.stream));
+  VF_HIP(ctx, hipEventSynchronize(s.done));
   float ms = 0.f;
   if (hipEventElapsedTime(&ms, s.k0, s.k1) == hipSuccess) ctx->last_kernel_ms += ms;
   if (s.staged_out)
@@ -248,6 +257,11 @@ int run_pipeline(vf_ctx *ctx, const Seg *segs, size_t nseg) {
     if (segs[i].len && direct && !(is_pinned(segs[i].src) && is_pinned(segs[i].dst))) direct = false;
   }
   if (total == 0) return VF_OK;
+  // Chunk size: the slot size for big calls; for small calls at least 2 chunks per slot so
+  // the pipeline fills (480p x 32 = 29 MB in 16 MiB chunks was 2 chunks: no overlap).
+  const size_t kMinChunk = (size_t)1 << 20;
+  size_t chunk = (total / (2 * (size_t)ctx->nslots) + 65535) & ~(size_t)65535;
+  chunk = std::min(ctx->slot_bytes, std::max(kMinChunk, chunk));
   size_t seg = 0, seg_off = 0;
   int next = 0;
   int rc = VF_OK;
@@ -258,13 +272,13 @@ int run_pipeline(vf_ctx *ctx, const Seg *segs, size_t nseg) {
     s.out.clear();
     // Fill the slot from the segment cursor.
     size_t filled = 0;
-    while (seg < nseg && filled < ctx->slot_bytes) {
+    while (seg < nseg && filled < chunk) {
       const Seg &g = segs[seg];
-      size_t take = std::min(g.len - seg_off, ctx->slot_bytes - filled);
+      size_t take = std::min(g.len - seg_off, chunk - filled);
       if (take) {
         if (direct) {
           hipError_t e = hipMemcpyAsync(s.d_in + filled, g.src + seg_off, take,
-                                        hipMemcpyHostToDevice, s.stream);
+                                        hipMemcpyHostToDevice, ctx->s_in);
           if (e != hipSuccess) { rc = fail_hip(ctx, e, "hipMemcpyAsync(H2D)", __LINE__); break; }
         } else {
           ctx->pool->copy(s.pin_in + filled, g.src + seg_off, take);
@@ -278,20 +292,22 @@ int run_pipeline(vf_ctx *ctx, const Seg *segs, size_t nseg) {
     if (rc != VF_OK) break;
     if (filled == 0) break;
     hipError_t e = hipSuccess;
-    if (!direct) e = hipMemcpyAsync(s.d_in, s.pin_in, filled, hipMemcpyHostToDevice, s.stream);
-    if (e == hipSuccess) e = hipEventRecord(s.k0, s.stream);
-    if (e == hipSuccess) e = vf::launch_invert(s.d_in, s.d_out, filled, ctx->cfg, s.stream);
-    if (e == hipSuccess) e = hipEventRecord(s.k1, s.stream);
+    if (!direct) e = hipMemcpyAsync(s.d_in, s.pin_in, filled, hipMemcpyHostToDevice, ctx->s_in);
+    if (e == hipSuccess) e = hipEventRecord(s.k0, ctx->s_in);
+    if (e == hipSuccess) e = vf::launch_invert(s.d_in, s.d_out, filled, ctx->cfg, ctx->s_in);
+    if (e == hipSuccess) e = hipEventRecord(s.k1, ctx->s_in);
+    if (e == hipSuccess) e = hipStreamWaitEvent(ctx->s_out, s.k1, 0);
     if (e == hipSuccess) {
       if (direct) {
         for (const OutPiece &p : s.out) {
-          e = hipMemcpyAsync(p.dst, s.d_out + p.off, p.len, hipMemcpyDeviceToHost, s.stream);
+          e = hipMemcpyAsync(p.dst, s.d_out + p.off, p.len, hipMemcpyDeviceToHost, ctx->s_out);
           if (e != hipSuccess) break;
         }
       } else {
-        e = hipMemcpyAsync(s.pin_out, s.d_out, filled, hipMemcpyDeviceToHost, s.stream);
+        e = hipMemcpyAsync(s.pin_out, s.d_out, filled, hipMemcpyDeviceToHost, ctx->s_out);
       }
     }
+    if (e == hipSuccess) e = hipEventRecord(s.done, ctx->s_out);
     if (e != hipSuccess) { rc = fail_hip(ctx, e, "slot submit", __LINE__); break; }
     s.staged_out = !direct;
     s.busy = true;
@@ -360,7 +376,7 @@ VF_EXPORT int vf_create(int device, size_t max_frame_bytes, int max_batch, vf_ct
   if (ctx->cfg.max_blocks < 1) ctx->cfg.max_blocks = ctx->num_cus * 32;
   ctx->nslots = (int)std::min<size_t>(kMaxSlots, std::max<size_t>(2, env_size("VF_SLOTS", 4)));
   size_t want = max_frame_bytes ? max_frame_bytes * (size_t)max_batch : (size_t)8 << 20;
-  size_t slot = env_size("VF_SLOT_BYTES", std::min(want, (size_t)8 << 20));
+  size_t slot = env_size("VF_SLOT_BYTES", std::min(want, (size_t)16 << 20));
   slot = std::max<size_t>(slot, (size_t)1 << 20);
   slot = std::min<size_t>(slot, (size_t)64 << 20);
   slot = (slot + 4095) & ~(size_t)4095;
@@ -368,11 +384,15 @@ VF_EXPORT int vf_create(int device, size_t max_frame_bytes, int max_batch, vf_ct
   int rc = VF_OK;
   e = hipSetDevice(device);
   if (e != hipSuccess) rc = fail_hip(ctx, e, "hipSetDevice", __LINE__);
+  if (rc == VF_OK &&
+      ((e = hipStreamCreateWithFlags(&ctx->s_in, hipStreamNonBlocking)) != hipSuccess ||
+       (e = hipStreamCreateWithFlags(&ctx->s_out, hipStreamNonBlocking)) != hipSuccess))
+    rc = fail_hip(ctx, e, "hipStreamCreateWithFlags", __LINE__);
   for (int i = 0; i < ctx->nslots && rc == VF_OK; ++i) {
     Slot &s = ctx->slots[i];
-    if ((e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking)) != hipSuccess ||
-        (e = hipEventCreate(&s.k0)) != hipSuccess || (e = hipEventCreate(&s.k1)) != hipSuccess) {
-      rc = fail_hip(ctx, e, "stream/event create", __LINE__);
+    if ((e = hipEventCreate(&s.k0)) != hipSuccess || (e = hipEventCreate(&s.k1)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming)) != hipSuccess) {
+      rc = fail_hip(ctx, e, "event create", __LINE__);
       break;
     }
     if ((e = hipHostMalloc((void **)&s.pin_in, slot, hipHostMallocDefault)) != hipSuccess ||
@@ -391,7 +411,7 @@ VF_EXPORT int vf_create(int device, size_t max_frame_bytes, int max_batch, vf_ct
     delete ctx;
     return rc;
   }
-  ctx->pool = new CopyPool((int)env_size("VF_HOST_THREADS", 4));
+  ctx->pool = new CopyPool((int)env_size("VF_HOST_THREADS", 8));
   *out = ctx;
   return VF_OK;
 }

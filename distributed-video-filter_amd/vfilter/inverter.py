@@ -1,0 +1,142 @@
+"""InverterWorker: the reference's filter plugin on the MI355X (reference: inverter.py:9-64).
+
+``InverterWorker.__call__(frame_bytes) -> bytes`` keeps the reference's contract
+(inverter.py:29-46): decode (JPEG, or raw bytes), optional artificial ``delay``, invert,
+re-encode.  The invert is ``vfilter.bitwise_not`` — hand-written gfx950 kernels via
+libvfilter_hip.so — instead of ``cv2.bitwise_not`` (inverter.py:41).  ``process_batch``
+inverts a whole dispatched batch with ONE gathered device call (H2D || kernel || D2H), and
+when frames arrive in the shared-memory ring the ring is page-locked once so the GPU DMAs
+straight from/to it.
+
+Raw frames: the reference reshapes every raw frame to 480x480x3 (inverter.py:34) and drops
+any other size with a ValueError (worker.py:74-76).  The invert needs no shape, so any size
+is accepted here; the v1 wire format carries the shape when a producer provides it.
+
+JPEG (the reference default, ``use_jpeg=True``, inverter.py:10) needs PyTurboJPEG, which is
+not installed on this image; ``use_jpeg=True`` therefore raises at construction exactly as
+the reference does at import (``from turbojpeg import TurboJPEG``, inverter.py:7).  GPU JPEG
+is SURVEY §8f rank 4.
+"""
+from __future__ import annotations
+
+import argparse
+import signal
+import time
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from . import wire
+from ._lib import Context, default_device
+from .worker import Worker
+
+
+class InverterWorker(Worker):
+    def __init__(self, host: str = "localhost", distribute_port: int = 5555, collect_port: int = 5556,
+                 delay: float = 0.0, use_jpeg: bool = True, *, device: Optional[int] = None,
+                 max_frame_bytes: int = 3840 * 2160 * 3, install_signal_handlers: bool = True, **worker_kw):
+        self.jpeg = None
+        if use_jpeg:
+            from turbojpeg import TurboJPEG  # raises ImportError when absent, like inverter.py:7
+            self.jpeg = TurboJPEG()
+        super().__init__(host, distribute_port, collect_port, **worker_kw)
+        self.delay = delay
+        self.device = default_device() if device is None else device
+        self.ctx = Context(self.device, max_frame_bytes=max_frame_bytes, max_batch=max(1, self.batch))
+        self._registered: List[int] = []
+        if install_signal_handlers:                                  # inverter.py:16-18
+            signal.signal(signal.SIGINT, self._signal_handler)
+            signal.signal(signal.SIGTERM, self._signal_handler)
+        if self.verbose:
+            print("Inverter worker started")
+            print(f"Processing delay: {self.delay} seconds")
+
+    def _signal_handler(self, signum, frame):                        # inverter.py:22-27
+        if not self.shutdown_requested:
+            self.shutdown_requested = True
+            print(f"\nReceived signal {signum}, shutting down...")
+            self.running = False
+
+    # -- one frame (inverter.py:29-46) ------------------------------------------------------
+    def __call__(self, frame_bytes):
+        if self.jpeg:
+            frame = self.jpeg.decode(frame_bytes)                   # inverter.py:32
+        else:
+            frame = np.frombuffer(frame_bytes, dtype=np.uint8)      # inverter.py:34, any size
+        if self.delay > 0:                                          # inverter.py:37-38
+            time.sleep(self.delay)
+        out = np.empty_like(frame)
+        if frame.nbytes:
+            self.ctx.invert_host(frame, out, frame.nbytes)          # inverter.py:41
+        if self.jpeg:
+            return self.jpeg.encode(out)                            # inverter.py:44
+        return out                                                   # inverter.py:46 (buffer, no copy)
+
+    # -- a dispatched batch: one gathered device call ------------------------------------
+    def process_batch(self, frames: Sequence, metas: Sequence[wire.FrameMeta], outs: Sequence) -> List:
+        if self.jpeg:
+            return super().process_batch(frames, metas, outs)
+        if self.delay > 0:
+            time.sleep(self.delay * len(frames))
+        srcs, dsts, sizes, results = [], [], [], []
+        for f, o in zip(frames, outs):
+            src = f if isinstance(f, np.ndarray) else np.frombuffer(f, dtype=np.uint8)
+            dst = o if o is not None else np.empty(src.nbytes, np.uint8)
+            srcs.append(src)
+            dsts.append(dst)
+            sizes.append(src.nbytes)
+            results.append(dst)
+        try:
+            self.ctx.invert_frames_host(srcs, dsts, sizes)
+        except Exception as e:
+            return [e] * len(frames)
+        return results
+
+    def on_ring_attached(self, ring) -> None:
+        """Page-lock the whole shared-memory ring once: the slot pipeline then DMAs straight
+        from the input halves and into the output halves (no staging copy)."""
+        try:
+            self._registered.append(self.ctx.host_register(ring.buf, ring.nbytes))
+        except Exception as e:  # still correct through staging, just slower
+            print(f"Inverter worker: could not page-lock ring {ring.name}: {e}")
+
+    def close(self):
+        for a in self._registered:
+            try:
+                self.ctx.host_unregister(a)
+            except Exception:
+                pass
+        self._registered.clear()
+        super().close()
+        self.ctx.close()
+
+
+def main(argv=None):
+    """inverter.py:48-61 plus the GPU worker's knobs."""
+    ap = argparse.ArgumentParser(description="Inverter worker for video processing (MI355X backend)")
+    ap.add_argument("--distribute-port", type=int, default=5555,
+                    help="Port to request frames from webcam app (default: 5555)")
+    ap.add_argument("--collect-port", type=int, default=5556,
+                    help="Port to send inverted frames to webcam app (default: 5556)")
+    ap.add_argument("--delay", type=float, default=0.0,
+                    help="Artificial processing delay in seconds (default: 0.0)")
+    ap.add_argument("--host", default="localhost", help="distributor host (reference: hard-coded localhost)")
+    ap.add_argument("--jpeg", action="store_true", help="JPEG frames (needs PyTurboJPEG); default raw")
+    ap.add_argument("--device", type=int, default=None, help="GPU ordinal (default: VF_DEVICE / LOCAL_RANK / 0)")
+    ap.add_argument("--batch", type=int, default=8, help="frames per request (protocol v1)")
+    ap.add_argument("--protocol", choices=("v0", "v1"), default="v1",
+                    help="v0 = the reference wire protocol (use against the reference distributor.py)")
+    ap.add_argument("--transport", choices=("auto", "zmq", "tcp"), default="auto")
+    ap.add_argument("--verbose", action="store_true")
+    args = ap.parse_args(argv)
+    worker = InverterWorker(args.host, args.distribute_port, args.collect_port, args.delay,
+                            use_jpeg=args.jpeg, device=args.device, batch=args.batch,
+                            protocol=args.protocol, transport=args.transport, verbose=args.verbose)
+    try:
+        worker.start()
+    finally:
+        worker.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -33,7 +33,12 @@ class FrameRing:
                 raise ValueError("FrameRing: nslots and slot_bytes must be positive")
             self.slot_bytes = _round_up(slot_bytes)
             self.nslots = nslots
-            self.shm = shared_memory.SharedMemory(create=True, size=self.nslots * 2 * self.slot_bytes)
+            size = self.nslots * 2 * self.slot_bytes
+            free = shm_free_bytes()
+            if free is not None and size > free:
+                # a tmpfs segment larger than the free space maps fine and SIGBUSes on write
+                raise MemoryError(f"FrameRing of {size} B exceeds free /dev/shm ({free} B)")
+            self.shm = shared_memory.SharedMemory(create=True, size=size)
             self.owner = True
         else:
             self.shm = shared_memory.SharedMemory(name=name)
@@ -95,6 +100,15 @@ class FrameRing:
                 self.shm.unlink()
             except FileNotFoundError:
                 pass
+
+
+def shm_free_bytes() -> Optional[int]:
+    try:
+        import os
+        st = os.statvfs("/dev/shm")
+        return st.f_bavail * st.f_frsize
+    except (OSError, AttributeError):
+        return None
 
 
 def _untrack(shm: shared_memory.SharedMemory) -> None:

@@ -23,6 +23,8 @@ import os
 import time
 from typing import List, Optional, Sequence
 
+import numpy as np
+
 from . import transport as tp
 from . import wire
 from .shm import FrameRing
@@ -70,7 +72,7 @@ class Worker:
             try:
                 r = self(f)
                 if o is not None:
-                    o[:] = memoryview(r).cast("B")
+                    o[:] = np.frombuffer(r, dtype=np.uint8)
                 results.append(r)
             except Exception as e:  # worker.py:74-76
                 results.append(e)

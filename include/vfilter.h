@@ -61,8 +61,9 @@ const char *vf_status_string(int status);
 int vf_device_count(int *out_count);
 
 /* Create a context on `device`.  Allocates the pinned host staging ring and device slot
- * buffers used by the host->host entry points (each slot holds `max_frame_bytes` x
- * `max_batch` bytes, clamped to [1 MiB, 64 MiB]) and creates one HIP stream per slot.
+ * buffers used by the host->host entry points (VF_SLOTS slots, default 4, each of
+ * min(`max_frame_bytes` x `max_batch`, 16 MiB) bytes; VF_SLOT_BYTES overrides, clamped to
+ * [1 MiB, 64 MiB]) and two HIP streams (H2D + kernel, D2H: one SDMA engine per direction).
  * Replaces the per-process filter state of InverterWorker.__init__ (inverter.py:10-20). */
 int vf_create(int device, size_t max_frame_bytes, int max_batch, vf_ctx **out);
 

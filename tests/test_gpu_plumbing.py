@@ -1,0 +1,100 @@
+"""The product worker (InverterWorker on libvfilter_hip.so) behind the distributor, on the
+GPU: BASELINE configs[2] (4K, batch 16, frame-index sharded, in-order reassembly) and
+configs[3] (mixed 480p/1080p/4K) at small frame counts, bit-exact against the oracle.
+Worker processes share the box's one GPU (2 processes <= the 16-process limit)."""
+import os
+import threading
+import time
+
+import numpy as np
+import pytest
+
+from _plumbing import spawn_workers, stop_workers
+from oracle import oracle
+from vfilter.distributor import Distributor
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(d, frames, n_workers, batch, timeout=60):
+    stop, procs = spawn_workers(n_workers, d.distribute_port, d.collect_port, protocol="v1", batch=batch,
+                                kind="gpu")
+    try:
+        th = threading.Thread(target=lambda: [d.add_frame_for_distribution(f) for f in frames])
+        th.start()
+        infos = []
+        for i in range(len(frames)):
+            item = d.get_next_frame(timeout=timeout)
+            assert item is not None, f"frame {i} never came back: {d.ordering_stats()}"
+            idx, data, info = item
+            assert idx == i
+            assert np.array_equal(np.frombuffer(data, np.uint8), oracle.invert(frames[i]).reshape(-1)), i
+            infos.append(info)
+        th.join()
+        return infos
+    finally:
+        stop_workers(stop, procs)
+
+
+@pytest.mark.timeout(180)
+def test_config3_4k_batch16_sharded_in_order_ring():
+    d = Distributor(0, 0, policy="shard", reassembly="ordered", shard_workers=2, shard_chunk=16,
+                    queue_size=64, ring_slots=24, ring_slot_bytes=2160 * 3840 * 3, transport="tcp",
+                    host="127.0.0.1", verbose=False)
+    d.start()
+    try:
+        frames = [oracle.synthetic_frame(i % 4, 2160, 3840) for i in range(64)]
+        stop, procs = spawn_workers(2, d.distribute_port, d.collect_port, protocol="v1", batch=16, kind="gpu")
+        try:
+            time.sleep(3.0)  # both workers register (GPU context creation) before frames flow
+            th = threading.Thread(target=lambda: [d.add_frame_for_distribution(f) for f in frames])
+            th.start()
+            owners = []
+            for i in range(len(frames)):
+                item = d.get_next_frame(timeout=60)
+                assert item is not None, d.ordering_stats()
+                idx, data, info = item
+                assert idx == i
+                assert np.array_equal(np.frombuffer(data, np.uint8), oracle.invert(frames[i]).reshape(-1))
+                owners.append(info["process_id"])
+            th.join()
+        finally:
+            stop_workers(stop, procs)
+        chunks = [set(owners[c * 16:(c + 1) * 16]) for c in range(4)]
+        assert all(len(c) == 1 for c in chunks) and chunks[0] != chunks[1] and chunks[0] == chunks[2]
+        assert d.ring.free_slots() == 24
+    finally:
+        d.cleanup()
+
+
+@pytest.mark.timeout(180)
+def test_config4_mixed_resolution_pull_tcp_payloads():
+    shapes = [(480, 640), (1080, 1920), (2160, 3840)]
+    frames = [oracle.synthetic_frame(i, *shapes[i % 3]) for i in range(24)]
+    d = Distributor(0, 0, policy="pull", reassembly="ordered", queue_size=16, transport="tcp",
+                    host="127.0.0.1", verbose=False)
+    d.start()
+    try:
+        infos = _run(d, frames, 2, batch=4)
+        assert [i["shape"] for i in infos[:3]] == [list(s) + [3] for s in shapes]
+        s = d.ordering_stats()
+        assert s["released"] == 24 and s["lost"] == 0
+    finally:
+        d.cleanup()
+
+
+@pytest.mark.timeout(120)
+def test_inverter_worker_call_matches_reference_raw_path():
+    """InverterWorker.__call__ on a 480x480 raw frame == the reference's raw path output
+    (inverter.py:34 -> :41 -> :46), and any other size works too (the reference drops it)."""
+    from vfilter.inverter import InverterWorker
+    w = InverterWorker("127.0.0.1", 1, 1, 0.0, use_jpeg=False, install_signal_handlers=False, transport="tcp")
+    try:
+        x = oracle.synthetic_frame(9, 480, 480).tobytes()
+        assert bytes(w(x)) == oracle.reference_raw_call(x)
+        y = oracle.synthetic_frame(9, 1080, 1920).tobytes()
+        assert bytes(w(y)) == oracle.invert_bytes(y)
+        with pytest.raises(ImportError):
+            InverterWorker("127.0.0.1", 1, 1, 0.0, use_jpeg=True, install_signal_handlers=False, transport="tcp")
+    finally:
+        w.close()

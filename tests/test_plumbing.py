@@ -1,0 +1,281 @@
+"""Distributor / worker plumbing on the CPU (BASELINE configs[0] and the ordering logic of
+configs[2]/[3]), with the stdlib TCP transport and a test plugin whose arithmetic is the
+oracle.  The GPU versions of these flows are in test_gpu_plumbing.py."""
+import glob
+import json
+import os
+import random
+import threading
+import time
+
+import numpy as np
+import pytest
+
+from _plumbing import spawn_workers, stop_workers
+from oracle import oracle
+from vfilter import wire
+from vfilter import transport as tp
+from vfilter.distributor import Distributor
+from vfilter.reorder import DisplayBuffer, OrderedBuffer
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+# ---- reassembly policies ----------------------------------------------------------------
+
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "ref_display_*.json"))))
+def test_display_buffer_matches_reference_trace(path):
+    d = json.load(open(path))
+    b = DisplayBuffer(d["frame_delay"], d["frame_buffer_size"])
+    for i, (op, rec) in enumerate(zip(d["ops"], d["records"])):
+        got = {"op": op}
+        if op[0] == "recv":
+            b.receive(op[1], oracle.payload_for(op[1]), "4242", 1.0 + op[1], 1.5 + op[1])
+        elif op[0] == "update":
+            got["ret"] = b.update_display_frame()
+        else:
+            fd = b.get_frame_to_display()
+            got["ret"] = None if fd is None else oracle.payload_index(fd)
+        got.update({"keys": sorted(b.received_frames), "current_display_frame": b.current_display_frame,
+                    "latest_received_frame": b.latest_received_frame})
+        assert got == rec, f"{os.path.basename(path)} op #{i}"
+    e = d["stored_entry"]
+    ent = b.received_frames[e["index"]]
+    assert (ent["process_id"], ent["start_time"], ent["end_time"]) == (e["process_id"], e["start_time"], e["end_time"])
+
+
+def test_display_buffer_matches_oracle_on_random_streams():
+    rng = random.Random(3)
+    for trial in range(30):
+        fd, bs = rng.randint(0, 8), rng.randint(1, 60)
+        ref = oracle.RefReorderBuffer(fd, bs)
+        got = DisplayBuffer(fd, bs)
+        for _ in range(400):
+            r = rng.random()
+            if r < 0.6:
+                i = rng.randint(0, 300)
+                ref.receive(i, i)
+                got.receive(i, i, "p", 0.0, 0.0)
+            elif r < 0.8:
+                assert ref.update_display_frame() == got.update_display_frame()
+            else:
+                assert ref.get_frame_to_display() == got.get_frame_to_display()
+            assert sorted(ref.received_frames) == sorted(got.received_frames)
+            assert ref.current_display_frame == got.current_display_frame
+
+
+def test_ordered_buffer_releases_each_index_once_in_order():
+    rng = np.random.default_rng(0)
+    n = 500
+    order = np.argsort(np.arange(n) + rng.uniform(0, 25, n))
+    lost = set(rng.choice(n, 10, replace=False).tolist())
+    b = OrderedBuffer()
+    out = []
+    for k, i in enumerate(order):
+        i = int(i)
+        if i in lost:
+            b.mark_lost(i)
+        else:
+            b.push(i, i * 7, now=float(k))
+        out += [x[0] for x in b.pop_ready(now=float(k))]
+    assert out == [i for i in range(n) if i not in lost]
+    s = b.stats()
+    assert s["released"] == n - len(lost) and s["lost"] == len(lost) and s["buffered"] == 0
+    assert s["max_depth"] >= 1 and s["out_of_order"] > 0
+
+
+# ---- wire -----------------------------------------------------------------------------------
+
+def test_wire_v0_is_the_reference_layout():
+    assert wire.encode_request(version=0) == [b"READY"]
+    assert wire.encode_dispatch_v0(12, b"abc") == [b"12", b"abc"]
+    parts = wire.encode_result_v0(12, 4242, 1.25, 2.5, b"xyz")
+    assert parts[:4] == [b"12", b"4242", b"1.25", b"2.5"]
+    r = wire.decode_result(parts)
+    assert r.version == 0 and r.pid == "4242" and r.metas[0].index == 12 and r.payloads[0] == b"xyz"
+    d = wire.decode_dispatch([b"7", b"frame"])
+    assert d.version == 0 and d.metas[0].index == 7 and d.payloads == [b"frame"]
+
+
+def test_wire_v1_roundtrip_with_ring_and_errors():
+    metas = [wire.FrameMeta(0, 5, [1, 1, 5]), wire.FrameMeta(1, 9, None, slot=3), wire.FrameMeta(2, 2)]
+    parts = wire.encode_dispatch(metas, [b"aaaaa", None, b"bb"], ring={"name": "r", "slot_bytes": 4096})
+    d = wire.decode_dispatch(parts)
+    assert [m.index for m in d.metas] == [0, 1, 2] and d.payloads == [b"aaaaa", None, b"bb"]
+    assert d.ring == {"name": "r", "slot_bytes": 4096} and d.metas[0].shape == [1, 1, 5]
+    rm = [wire.FrameMeta(0, 5, start=1.0, end=2.0), wire.FrameMeta(1, 9, slot=3), wire.FrameMeta(2, 2, error="boom")]
+    r = wire.decode_result(wire.encode_result(99, rm, [b"zzzzz", None, None]))
+    assert r.pid == "99" and r.payloads == [b"zzzzz", None, None] and r.metas[2].error == "boom"
+    assert wire.decode_request(wire.encode_request(8, shm=True)) == wire.Request(1, 8, True)
+    assert wire.decode_request([b"HELLO"]) is None
+
+
+# ---- transport -------------------------------------------------------------------------------
+
+def test_tcp_transport_roles():
+    router = tp.RouterEnd("tcp", "127.0.0.1", 0)
+    pull = tp.PullEnd("tcp", "127.0.0.1", 0)
+    dealer = tp.DealerEnd("tcp", "127.0.0.1", router.port)
+    push = tp.PushEnd("tcp", "127.0.0.1", pull.port)
+    big = np.random.default_rng(1).integers(0, 256, 3 << 20, dtype=np.uint8)
+    try:
+        dealer.send([b"READY"])
+        assert router.poll(2000)
+        peer, parts = router.recv()
+        assert parts == [b"READY"] and len(peer) == 5
+        assert router.send(peer, [b"1", big])
+        assert dealer.poll(2000)
+        got = dealer.recv()
+        assert got[0] == b"1" and bytes(got[1]) == big.tobytes()
+        push.send([b"a", b"", memoryview(big)[:10]])
+        assert pull.poll(2000)
+        assert [bytes(x) for x in pull.recv()] == [b"a", b"", big[:10].tobytes()]
+        assert not router.send(b"\x00nope", [b"x"])  # unknown peer: dropped, like ROUTER
+    finally:
+        for s in (dealer, push, router, pull):
+            s.close()
+
+
+# ---- end-to-end plumbing with worker processes -------------------------------------------------
+
+def _dist(**kw):
+    kw.setdefault("transport", "tcp")
+    kw.setdefault("host", "127.0.0.1")
+    kw.setdefault("verbose", False)
+    d = Distributor(0, 0, **kw)
+    d.start()
+    return d
+
+
+def _frames(n, shapes):
+    return [oracle.synthetic_frame(i, *shapes[i % len(shapes)]) for i in range(n)]
+
+
+def _drain_ordered(d, frames, timeout=30.0):
+    got = []
+    for i in range(len(frames)):
+        item = d.get_next_frame(timeout=timeout)
+        assert item is not None, f"timed out waiting for frame {i}: {d.ordering_stats()}"
+        idx, data, info = item
+        assert idx == i
+        assert bytes(data) == oracle.invert_bytes(frames[i].tobytes()), f"frame {i} differs"
+        got.append(info)
+    return got
+
+
+@pytest.mark.timeout(120)
+def test_config1_latest_policy_two_v0_workers():
+    """configs[0]: 640x480 frames through the distributor + 2 CPU workers speaking the
+    reference protocol (v0); reference policy: latest-wins dispatch, lossy display."""
+    d = _dist(policy="latest", reassembly="display", frame_delay=2)
+    stop, procs = spawn_workers(2, d.distribute_port, d.collect_port, protocol="v0")
+    try:
+        frames = _frames(40, [(480, 640)])
+        sent = []
+        for f in frames:
+            sent.append(d.add_frame_for_distribution(f.tobytes()))
+            time.sleep(0.02)  # 50 fps offered
+        t0 = time.time()
+        while time.time() - t0 < 10 and d.results_received < 20:
+            time.sleep(0.05)
+        assert d.results_received >= 20
+        with d._lock:
+            snap = {i: e for i, e in d.received_frames.items()}
+        assert snap
+        for i, e in snap.items():
+            assert bytes(e["frame_data"]) == oracle.invert_bytes(frames[i].tobytes())
+            assert e["start_time"] <= e["end_time"]
+        assert d.update_display_frame() in (True, False)
+        shown = d.get_frame_to_display()
+        assert shown is not None and any(bytes(shown) == bytes(e["frame_data"]) for e in snap.values())
+        st = d.get_frame_stats()
+        assert st["total_frames_processed"] == 40 and st["frame_delay"] == 2
+        pids = {e["process_id"] for e in snap.values()}
+        assert len(pids) >= 1
+    finally:
+        stop_workers(stop, procs)
+        d.cleanup()
+
+
+@pytest.mark.timeout(120)
+def test_lossless_pull_ordered_two_workers():
+    d = _dist(policy="pull", reassembly="ordered", queue_size=32)
+    stop, procs = spawn_workers(2, d.distribute_port, d.collect_port, protocol="v1", batch=4)
+    try:
+        frames = _frames(80, [(120, 160), (97, 33), (480, 640)])
+        th = threading.Thread(target=lambda: [d.add_frame_for_distribution(f) for f in frames])
+        th.start()
+        infos = _drain_ordered(d, frames)
+        th.join()
+        assert len({i["process_id"] for i in infos}) == 2  # both workers took part
+        s = d.ordering_stats()
+        assert s["released"] == 80 and s["lost"] == 0 and s["frames_dropped"] == 0
+        assert infos[2]["shape"] == [480, 640, 3]
+    finally:
+        stop_workers(stop, procs)
+        d.cleanup()
+
+
+@pytest.mark.timeout(120)
+def test_shard_policy_assigns_index_chunks_round_robin():
+    d = _dist(policy="shard", reassembly="ordered", shard_workers=2, shard_chunk=4, queue_size=64)
+    stop, procs = spawn_workers(2, d.distribute_port, d.collect_port, protocol="v1", batch=4)
+    try:
+        time.sleep(1.0)  # let both workers register before frames arrive
+        frames = _frames(48, [(64, 64)])
+        for f in frames:
+            d.add_frame_for_distribution(f)
+        infos = _drain_ordered(d, frames)
+        owner = [infos[c * 4]["process_id"] for c in range(12)]
+        for c in range(12):  # a chunk stays on one worker; chunks alternate
+            assert {infos[c * 4 + k]["process_id"] for k in range(4)} == {owner[c]}
+        assert len(set(owner)) == 2 and all(owner[c] == owner[c % 2] for c in range(12))
+    finally:
+        stop_workers(stop, procs)
+        d.cleanup()
+
+
+@pytest.mark.timeout(120)
+def test_shared_memory_ring_mixed_resolutions():
+    """configs[3]-shaped stream (mixed sizes) through the shared-memory ring: only slot
+    numbers cross the sockets; results are read from the ring's output halves."""
+    shapes = [(480, 640), (720, 1280), (1080, 1920)]
+    d = _dist(policy="pull", reassembly="ordered", queue_size=16, ring_slots=12,
+              ring_slot_bytes=1080 * 1920 * 3)
+    stop, procs = spawn_workers(2, d.distribute_port, d.collect_port, protocol="v1", batch=3)
+    try:
+        frames = _frames(30, shapes)
+        th = threading.Thread(target=lambda: [d.add_frame_for_distribution(f) for f in frames])
+        th.start()
+        _drain_ordered(d, frames)
+        th.join()
+        assert d.ring.free_slots() == 12  # every slot returned
+        s = d.ordering_stats()
+        assert s["released"] == 30 and s["reorder_wait_max_ms"] >= 0.0
+    finally:
+        stop_workers(stop, procs)
+        d.cleanup()
+
+
+@pytest.mark.timeout(120)
+def test_failed_frames_are_reported_and_skipped():
+    """A worker that fails a frame reports it (v1 "error"); the in-order consumer skips it
+    instead of waiting forever (the reference just loses it, worker.py:74-76)."""
+    d = _dist(policy="pull", reassembly="ordered", queue_size=16)
+    stop, procs = spawn_workers(1, d.distribute_port, d.collect_port, protocol="v1", batch=2)
+    try:
+        frames = _frames(6, [(8, 8)])
+        for f in frames:
+            d.add_frame_for_distribution(f)
+        _drain_ordered(d, frames)
+        # a result message that reports an error for index 6 (what a failing plugin sends)
+        d._on_result(wire.Result("1", [wire.FrameMeta(6, 3, error="ValueError: bad")], [None]))
+        d.add_frame_for_distribution(b"abc")  # index 6 is already accounted for as lost
+        f7 = oracle.synthetic_frame(7, 8, 8)
+        d.add_frame_for_distribution(f7)
+        item = d.get_next_frame(timeout=20)
+        assert item is not None and item[0] == 7 and bytes(item[1]) == oracle.invert_bytes(f7.tobytes())
+        assert d.ordering_stats()["lost"] == 1 and d.result_errors == 1
+    finally:
+        stop_workers(stop, procs)
+        d.cleanup()

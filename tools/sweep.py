@@ -89,6 +89,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "sweep.jsonl"))
     ap.add_argument("--quick", action="store_true")
+    ap.add_argument("--e2e-only", action="store_true")
     args = ap.parse_args()
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
     ctx = Context(0, max_frame_bytes=2160 * 3840 * 3, max_batch=4)
@@ -99,10 +100,10 @@ def main():
             f.write(json.dumps(r) + "\n")
             f.flush()
             print(json.dumps(r), flush=True)
-        for tag, b in points:
+        for tag, b in ([] if args.e2e_only else points):
             h, w = SIZES[tag]
             emit(kernel_point(ctx, tag, h, w, b))
-        for b in sweep:  # configs[4]: one launch over the whole resident batch
+        for b in ([] if args.e2e_only else sweep):  # configs[4]: one launch over the resident batch
             emit(kernel_point(ctx, "1080p", 1080, 1920, b, ring_min_bytes=0, steps=6))
         for tag, b in (("480p", 32), ("1080p", 32), ("4k", 16)):
             h, w = SIZES[tag]
