@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <condition_variable>
 #include <cstdarg>
@@ -128,8 +129,10 @@ struct OutPiece {
 };
 
 struct Slot {
-  hipEvent_t k0 = nullptr, k1 = nullptr;  // kernel start / end (on the IN stream)
-  hipEvent_t done = nullptr;              // D2H complete (on the OUT stream)
+  hipEvent_t h0 = nullptr;                // H2D start (IN stream)
+  hipEvent_t k0 = nullptr, k1 = nullptr;  // kernel start / end (IN stream)
+  hipEvent_t done = nullptr;              // D2H complete (OUT stream)
+  size_t bytes = 0;
   uint8_t *pin_in = nullptr, *pin_out = nullptr;
   uint8_t *d_in = nullptr, *d_out = nullptr;
   bool busy = false;
@@ -166,6 +169,11 @@ struct vf_ctx {
   int hip = 0;
   char msg[512] = "no error";
   float last_kernel_ms = 0.f;
+  hipEvent_t t0 = nullptr;  // start of the last host->host call (IN stream)
+  // per chunk of the last host->host call: {H2D start, kernel start, kernel end, D2H end}
+  // in ms after t0, and the chunk's bytes (vf_last_timeline)
+  std::vector<std::array<float, 4>> timeline;
+  std::vector<size_t> timeline_bytes;
 };
 
 namespace {
@@ -218,6 +226,7 @@ int release_slots(vf_ctx *ctx) {
   if (ctx->s_out) (void)hipStreamSynchronize(ctx->s_out);
   for (int i = 0; i < kMaxSlots; ++i) {
     Slot &s = ctx->slots[i];
+    if (s.h0) (void)hipEventDestroy(s.h0);
     if (s.k0) (void)hipEventDestroy(s.k0);
     if (s.k1) (void)hipEventDestroy(s.k1);
     if (s.done) (void)hipEventDestroy(s.done);
@@ -227,6 +236,8 @@ int release_slots(vf_ctx *ctx) {
     if (s.d_out) (void)hipFree(s.d_out);
     s = Slot();
   }
+  if (ctx->t0) (void)hipEventDestroy(ctx->t0);
+  ctx->t0 = nullptr;
   if (ctx->s_in) (void)hipStreamDestroy(ctx->s_in);
   if (ctx->s_out) (void)hipStreamDestroy(ctx->s_out);
   ctx->s_in = ctx->s_out = nullptr;
@@ -239,6 +250,12 @@ int complete_slot(vf_ctx *ctx, Slot &s) {
   VF_HIP(ctx, hipEventSynchronize(s.done));
   float ms = 0.f;
   if (hipEventElapsedTime(&ms, s.k0, s.k1) == hipSuccess) ctx->last_kernel_ms += ms;
+  std::array<float, 4> tl{};
+  hipEvent_t evs[4] = {s.h0, s.k0, s.k1, s.done};
+  for (int i = 0; i < 4; ++i)
+    if (hipEventElapsedTime(&tl[i], ctx->t0, evs[i]) != hipSuccess) tl[i] = -1.f;
+  ctx->timeline.push_back(tl);
+  ctx->timeline_bytes.push_back(s.bytes);
   if (s.staged_out)
     for (const OutPiece &p : s.out) ctx->pool->copy(p.dst, s.pin_out + p.off, p.len);
   s.out.clear();
@@ -250,6 +267,8 @@ int complete_slot(vf_ctx *ctx, Slot &s) {
 int run_pipeline(vf_ctx *ctx, const Seg *segs, size_t nseg) {
   VF_HIP(ctx, hipSetDevice(ctx->device));
   ctx->last_kernel_ms = 0.f;
+  ctx->timeline.clear();
+  ctx->timeline_bytes.clear();
   bool direct = true;  // every source and destination page-locked?
   size_t total = 0;
   for (size_t i = 0; i < nseg; ++i) {
@@ -265,11 +284,16 @@ int run_pipeline(vf_ctx *ctx, const Seg *segs, size_t nseg) {
   size_t seg = 0, seg_off = 0;
   int next = 0;
   int rc = VF_OK;
+  VF_HIP(ctx, hipEventRecord(ctx->t0, ctx->s_in));
   while (seg < nseg && rc == VF_OK) {
     Slot &s = ctx->slots[next];
     next = (next + 1) % ctx->nslots;
     if ((rc = complete_slot(ctx, s)) != VF_OK) break;
     s.out.clear();
+    if (direct) {  // direct H2D copies are issued while filling
+      hipError_t e = hipEventRecord(s.h0, ctx->s_in);
+      if (e != hipSuccess) { rc = fail_hip(ctx, e, "hipEventRecord", __LINE__); break; }
+    }
     // Fill the slot from the segment cursor.
     size_t filled = 0;
     while (seg < nseg && filled < chunk) {
@@ -292,7 +316,9 @@ int run_pipeline(vf_ctx *ctx, const Seg *segs, size_t nseg) {
     if (rc != VF_OK) break;
     if (filled == 0) break;
     hipError_t e = hipSuccess;
-    if (!direct) e = hipMemcpyAsync(s.d_in, s.pin_in, filled, hipMemcpyHostToDevice, ctx->s_in);
+    if (!direct) e = hipEventRecord(s.h0, ctx->s_in);
+    if (!direct && e == hipSuccess)
+      e = hipMemcpyAsync(s.d_in, s.pin_in, filled, hipMemcpyHostToDevice, ctx->s_in);
     if (e == hipSuccess) e = hipEventRecord(s.k0, ctx->s_in);
     if (e == hipSuccess) e = vf::launch_invert(s.d_in, s.d_out, filled, ctx->cfg, ctx->s_in);
     if (e == hipSuccess) e = hipEventRecord(s.k1, ctx->s_in);
@@ -310,6 +336,7 @@ int run_pipeline(vf_ctx *ctx, const Seg *segs, size_t nseg) {
     if (e == hipSuccess) e = hipEventRecord(s.done, ctx->s_out);
     if (e != hipSuccess) { rc = fail_hip(ctx, e, "slot submit", __LINE__); break; }
     s.staged_out = !direct;
+    s.bytes = filled;
     s.busy = true;
   }
   // Drain in submission order (oldest first).
@@ -388,10 +415,12 @@ VF_EXPORT int vf_create(int device, size_t max_frame_bytes, int max_batch, vf_ct
       ((e = hipStreamCreateWithFlags(&ctx->s_in, hipStreamNonBlocking)) != hipSuccess ||
        (e = hipStreamCreateWithFlags(&ctx->s_out, hipStreamNonBlocking)) != hipSuccess))
     rc = fail_hip(ctx, e, "hipStreamCreateWithFlags", __LINE__);
+  if (rc == VF_OK && (e = hipEventCreate(&ctx->t0)) != hipSuccess)
+    rc = fail_hip(ctx, e, "hipEventCreate", __LINE__);
   for (int i = 0; i < ctx->nslots && rc == VF_OK; ++i) {
     Slot &s = ctx->slots[i];
-    if ((e = hipEventCreate(&s.k0)) != hipSuccess || (e = hipEventCreate(&s.k1)) != hipSuccess ||
-        (e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming)) != hipSuccess) {
+    if ((e = hipEventCreate(&s.h0)) != hipSuccess || (e = hipEventCreate(&s.k0)) != hipSuccess ||
+        (e = hipEventCreate(&s.k1)) != hipSuccess || (e = hipEventCreate(&s.done)) != hipSuccess) {
       rc = fail_hip(ctx, e, "event create", __LINE__);
       break;
     }
@@ -611,6 +640,19 @@ VF_EXPORT int vf_sync(vf_ctx *ctx, void *stream) {
 VF_EXPORT int vf_elapsed_ms(const vf_ctx *ctx, float *out_ms) {
   if (!ctx || !out_ms) return set_err(nullptr, VF_E_INVALID, 0, "vf_elapsed_ms: NULL argument");
   *out_ms = ctx->last_kernel_ms;
+  return VF_OK;
+}
+
+VF_EXPORT int vf_last_timeline(const vf_ctx *ctx, float *out4, size_t *chunk_bytes, int max_chunks,
+                               int *n_chunks) {
+  if (!ctx || !n_chunks) return set_err(nullptr, VF_E_INVALID, 0, "vf_last_timeline: NULL argument");
+  const int n = (int)ctx->timeline.size();
+  *n_chunks = n;
+  for (int i = 0; i < n && i < max_chunks; ++i) {
+    if (out4)
+      for (int j = 0; j < 4; ++j) out4[4 * i + j] = ctx->timeline[i][j];
+    if (chunk_bytes) chunk_bytes[i] = ctx->timeline_bytes[i];
+  }
   return VF_OK;
 }
 

@@ -58,6 +58,7 @@ SIGNATURES = {
     "vf_memset_device": (ctypes.c_int, [_vp, _vp, ctypes.c_int, _sz, _vp]),
     "vf_sync": (ctypes.c_int, [_vp, _vp]),
     "vf_elapsed_ms": (ctypes.c_int, [_vp, _c_float_p]),
+    "vf_last_timeline": (ctypes.c_int, [_vp, _c_float_p, ctypes.POINTER(_sz), ctypes.c_int, _c_int_p]),
     "vf_bench_device_ring": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_int, _sz, ctypes.c_int, _vp, _c_float_p,
                                             _c_float_p]),
 }
@@ -233,6 +234,18 @@ class Context:
         ms = ctypes.c_float(0.0)
         self._check(self._lib.vf_elapsed_ms(self._ctx, ctypes.byref(ms)))
         return ms.value
+
+    def last_timeline(self) -> list:
+        """[(bytes, h2d_start_ms, kernel_start_ms, kernel_end_ms, d2h_end_ms), ...] per chunk
+        of the last host->host call, ms after the call's start event."""
+        n = ctypes.c_int(0)
+        self._check(self._lib.vf_last_timeline(self._ctx, None, None, 0, ctypes.byref(n)))
+        if n.value == 0:
+            return []
+        out = (ctypes.c_float * (4 * n.value))()
+        nb = (ctypes.c_size_t * n.value)()
+        self._check(self._lib.vf_last_timeline(self._ctx, out, nb, n.value, ctypes.byref(n)))
+        return [(int(nb[i]),) + tuple(float(out[4 * i + j]) for j in range(4)) for i in range(n.value)]
 
     def bench_device_ring(self, srcs: Sequence[int], dsts: Sequence[int], nbytes: int, steps: int,
                           stream: int = 0, per_launch: bool = False):

@@ -40,6 +40,7 @@ import numpy as np
 from . import transport as tp
 from . import wire
 from .reorder import DisplayBuffer, OrderedBuffer
+from .sharding import chunk_owner
 from .shm import FrameRing
 
 
@@ -188,11 +189,37 @@ class Distributor:
                                    "end_relative_time": end_time - self.trace_start_time, "event_ph": "X",
                                    "pid": pid})
 
+    GPU_TIDS = {"H2D": 1, "kernel": 2, "D2H": 3}
+
+    def log_gpu_span(self, name: str, begin_time: float, end_time: float, pid, nbytes: int = 0):
+        """A GPU span of a worker batch (H2D / kernel / D2H), shown on its own track under
+        the worker's pid next to the reference's per-frame events."""
+        if not self.enable_trace_export:
+            return
+        self.frame_timings.append({"event_ph": "G", "name": name, "begin_time": begin_time, "end_time": end_time,
+                                   "begin_relative_time": begin_time - self.trace_start_time,
+                                   "end_relative_time": end_time - self.trace_start_time, "pid": pid,
+                                   "bytes": nbytes})
+
     def trace_events(self) -> List[dict]:
-        """Chrome-trace events in the reference's schema (distributor.py:107-138)."""
+        """Chrome-trace events in the reference's schema (distributor.py:107-138), plus GPU
+        spans ("ph": "X" on tids 1-3 of the worker's pid, named by "M" metadata events)."""
         tid = threading.get_ident()
         ev = []
+        named = set()
         for t in self.frame_timings:
+            if t["event_ph"] == "G":
+                gtid = self.GPU_TIDS.get(t["name"], 9)
+                if (t["pid"], gtid) not in named:
+                    named.add((t["pid"], gtid))
+                    ev.append({"name": "thread_name", "ph": "M", "pid": t["pid"], "tid": gtid,
+                               "args": {"name": f"GPU {t['name']}"}})
+                dur = t["end_relative_time"] - t["begin_relative_time"]
+                ev.append({"name": f"GPU {t['name']}", "cat": "gpu", "ph": "X",
+                           "ts": int(t["begin_relative_time"] * 1e6), "dur": max(0, int(dur * 1e6)),
+                           "pid": t["pid"], "tid": gtid,
+                           "args": {"bytes": t["bytes"], "GBps": (t["bytes"] / dur / 1e9) if dur > 0 else None}})
+                continue
             if t["event_ph"] == "i":
                 ev.append({"name": f"Frame {t['frame_index']} - {t['event_type']}", "cat": "video_frames",
                            "ph": "i", "ts": int(t["relative_time"] * 1e6), "pid": os.getpid(), "tid": tid,
@@ -261,7 +288,7 @@ class Distributor:
                 if self.policy == "pull":
                     self._pending.append(item)
                 else:
-                    self._shard_pending[(frame_index // self.shard_chunk) % self.shard_workers].append(item)
+                    self._shard_pending[chunk_owner(frame_index, self.shard_chunk, self.shard_workers)].append(item)
                 self._cv.notify_all()
             self.log_frame_timing(frame_index, timestamp, "frame_captured")
         return frame_index
@@ -421,6 +448,10 @@ class Distributor:
                 continue
 
     def _on_result(self, res: wire.Result):
+        pid_val = int(res.pid) if res.pid.isdigit() else res.pid
+        for sp in res.spans:
+            self.log_gpu_span(sp.get("name", "?"), float(sp["begin"]), float(sp["end"]), pid_val,
+                              int(sp.get("bytes", 0)))
         for m, payload in zip(res.metas, res.payloads):
             self.log_frame_complete_timing(m.index, m.start, m.end, "frame_inverted_received",
                                            int(res.pid) if res.pid.isdigit() else res.pid)

@@ -86,10 +86,12 @@ class InverterWorker(Worker):
             dsts.append(dst)
             sizes.append(src.nbytes)
             results.append(dst)
+        t_call = time.time()
         try:
             self.ctx.invert_frames_host(srcs, dsts, sizes)
         except Exception as e:
             return [e] * len(frames)
+        self.last_spans = gpu_spans(self.ctx.last_timeline(), t_call)
         return results
 
     def on_ring_attached(self, ring) -> None:
@@ -109,6 +111,19 @@ class InverterWorker(Worker):
         self._registered.clear()
         super().close()
         self.ctx.close()
+
+
+def gpu_spans(timeline, t_call: float) -> List[dict]:
+    """Per-chunk {H2D, kernel, D2H} spans in wall-clock seconds: the call's start event is
+    taken as ``t_call`` (the host time just before the call)."""
+    spans = []
+    for nbytes, h0, k0, k1, d1 in timeline:
+        if min(h0, k0, k1, d1) < 0:
+            continue
+        spans.append({"name": "H2D", "begin": t_call + h0 / 1e3, "end": t_call + k0 / 1e3, "bytes": nbytes})
+        spans.append({"name": "kernel", "begin": t_call + k0 / 1e3, "end": t_call + k1 / 1e3, "bytes": nbytes})
+        spans.append({"name": "D2H", "begin": t_call + k1 / 1e3, "end": t_call + d1 / 1e3, "bytes": nbytes})
+    return spans
 
 
 def main(argv=None):

@@ -17,9 +17,11 @@ tag part that can never be a decimal index string, so a v1 peer can always tell 
             frame_0, ..., frame_{k-1}]
            (frames whose "slot" is set travel in the shared-memory ring and have no part)
   result   ["RESULT1", json{"pid": p, "frames": [{"index", "shape", "nbytes", "slot",
-                                                 "start", "end", "error"}...]}, out_0, ...]
-A v1 worker talking to a v0 (reference) distributor sends "READY" and reads 2 parts; a v1
-distributor answers a bare "READY" with a v0 dispatch.  Either side of the reference can
+                                                 "start", "end", "error"}...],
+                            "spans": [{"name", "begin", "end", "bytes"}...] (GPU timeline)},
+            out_0, ...]
+A worker run with protocol v0 against the reference distributor sends "READY" and reads 2
+parts; this build's distributor answers a bare "READY" with a v0 dispatch.  Either side of the reference can
 therefore be swapped for this build's independently.
 """
 from __future__ import annotations
@@ -80,6 +82,9 @@ class Result:
     metas: List[FrameMeta]
     payloads: List[Optional[bytes]] = field(default_factory=list)
     version: int = 1
+    # GPU spans of the batch: [{"name": "H2D"|"kernel"|"D2H", "begin": t, "end": t, "bytes": n}]
+    # (wall-clock seconds, like start/end), for the distributor's Perfetto export
+    spans: List[dict] = field(default_factory=list)
 
 
 # ---- requests -------------------------------------------------------------------------
@@ -137,8 +142,11 @@ def encode_result_v0(index: int, pid, start: float, end: float, frame) -> List:
     return [str(index).encode(), str(pid).encode(), str(start).encode(), str(end).encode(), frame]
 
 
-def encode_result(pid, metas: Sequence[FrameMeta], payloads: Sequence) -> List:
-    head = json.dumps({"pid": str(pid), "frames": [m.to_json() for m in metas]}).encode()
+def encode_result(pid, metas: Sequence[FrameMeta], payloads: Sequence, spans: Optional[List[dict]] = None) -> List:
+    d = {"pid": str(pid), "frames": [m.to_json() for m in metas]}
+    if spans:
+        d["spans"] = spans
+    head = json.dumps(d).encode()
     return [RESULT_V1, head] + [p for m, p in zip(metas, payloads) if m.slot is None and m.error is None]
 
 
@@ -154,4 +162,4 @@ def decode_result(parts: Sequence) -> Result:
     metas = [FrameMeta.from_json(x) for x in d["frames"]]
     it = iter(parts[2:])
     payloads = [None if (m.slot is not None or m.error is not None) else next(it) for m in metas]
-    return Result(str(d["pid"]), metas, payloads, version=1)
+    return Result(str(d["pid"]), metas, payloads, version=1, spans=list(d.get("spans", [])))

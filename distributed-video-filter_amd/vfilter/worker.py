@@ -52,6 +52,7 @@ class Worker:
         self.collect_socket = tp.PushEnd(self.transport, host, collect_port, self._zctx)       # worker.py:24-25
         self.frames_processed = 0
         self.errors = 0
+        self.last_spans: List[dict] = []  # GPU spans of the last batch (set by process_batch)
         self._ring: Optional[FrameRing] = None
         self._ring_name: Optional[str] = None
         if verbose:
@@ -181,6 +182,7 @@ class Worker:
                     outs.append(None)
             if self.verbose:
                 print(f"Processing frames {[m.index for m in d.metas]}")
+            self.last_spans = []
             try:
                 results = self.process_batch(frames, d.metas, outs)
             except Exception as e:
@@ -198,5 +200,5 @@ class Worker:
                 else:
                     payloads.append(None if m.slot is not None else r)
                 metas.append(om)
-            self.collect_socket.send(wire.encode_result(self.process_id, metas, payloads))
+            self.collect_socket.send(wire.encode_result(self.process_id, metas, payloads, self.last_spans))
             self.frames_processed += len(metas)

@@ -137,6 +137,13 @@ int vf_sync(vf_ctx *ctx, void *stream);
 /* Sum of kernel durations (ms, hipEvents) of the last host->host call on ctx. */
 int vf_elapsed_ms(const vf_ctx *ctx, float *out_ms);
 
+/* Per-chunk GPU timeline of the last host->host call (for Perfetto spans, the GPU side of
+ * the reference's trace export, distributor.py:63-171).  For chunk i < min(n, max_chunks):
+ * out4[4i..4i+3] = {H2D start, kernel start, kernel end, D2H end} in ms after the call's
+ * start event, chunk_bytes[i] = its size (either array may be NULL).  *n_chunks = n. */
+int vf_last_timeline(const vf_ctx *ctx, float *out4, size_t *chunk_bytes, int max_chunks,
+                     int *n_chunks);
+
 /* Benchmark loop over HBM-resident buffers: for step s in [0, steps) launch the invert
  * kernel from srcs[s % nbuf] to dsts[s % nbuf] (`nbytes` each, host arrays of device
  * pointers) back to back on `stream`, then synchronise.  A hipEvent pair brackets the whole

@@ -214,3 +214,15 @@ def test_hbm_resident_sweep_point_batch256(vf_ctx):
     finally:
         for p in (ds, d1, d2):
             vf_ctx.free_device(p)
+
+
+def test_timeline_chunks_cover_the_call(vf_ctx):
+    """vf_last_timeline: one record per chunk, bytes sum to the call, H2D <= kernel <= D2H."""
+    x = np.random.default_rng(1).integers(0, 256, 3 * (16 << 20) + 123, dtype=np.uint8)
+    y = np.empty_like(x)
+    vf_ctx.invert_host(x, y, x.nbytes)
+    tl = vf_ctx.last_timeline()
+    assert len(tl) >= 3 and sum(t[0] for t in tl) == x.nbytes
+    for nb, h0, k0, k1, d1 in tl:
+        assert 0.0 <= h0 <= k0 <= k1 <= d1
+    assert np.array_equal(y, oracle.invert(x))

@@ -71,7 +71,7 @@ def test_config3_4k_batch16_sharded_in_order_ring():
 def test_config4_mixed_resolution_pull_tcp_payloads():
     shapes = [(480, 640), (1080, 1920), (2160, 3840)]
     frames = [oracle.synthetic_frame(i, *shapes[i % 3]) for i in range(24)]
-    d = Distributor(0, 0, policy="pull", reassembly="ordered", queue_size=16, transport="tcp",
+    d = Distributor(0, 0, 5, True, policy="pull", reassembly="ordered", queue_size=16, transport="tcp",
                     host="127.0.0.1", verbose=False)
     d.start()
     try:
@@ -79,6 +79,12 @@ def test_config4_mixed_resolution_pull_tcp_payloads():
         assert [i["shape"] for i in infos[:3]] == [list(s) + [3] for s in shapes]
         s = d.ordering_stats()
         assert s["released"] == 24 and s["lost"] == 0
+        # GPU spans from the workers' slot events reach the trace (H2D -> kernel -> D2H)
+        ev = [e for e in d.trace_events() if e.get("cat") == "gpu"]
+        kern = [e for e in ev if e["name"] == "GPU kernel"]
+        assert kern and all(e["tid"] == 2 and e["dur"] >= 0 for e in kern)
+        assert sum(e["args"]["bytes"] for e in kern) == sum(f.nbytes for f in frames)
+        assert {e["name"] for e in ev} == {"GPU H2D", "GPU kernel", "GPU D2H"}
     finally:
         d.cleanup()
 

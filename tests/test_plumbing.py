@@ -279,3 +279,35 @@ def test_failed_frames_are_reported_and_skipped():
     finally:
         stop_workers(stop, procs)
         d.cleanup()
+
+
+def test_perfetto_trace_reference_schema_plus_gpu_spans(tmp_path):
+    """export_perfetto_trace writes the reference's Chrome-trace schema
+    (distributor.py:100-146): 'i' capture instants, 'X' worker spans keyed by worker pid; plus
+    GPU spans on named tracks of the worker's pid."""
+    d = Distributor(0, 0, 5, True, transport="tcp", host="127.0.0.1", verbose=False,
+                    trace_file=str(tmp_path / "t.pftrace"))
+    try:
+        t0 = d.trace_start_time
+        d.add_frame_for_distribution(b"abc", t0 + 0.5)
+        res = wire.Result("4242", [wire.FrameMeta(0, 3, start=t0 + 1.0, end=t0 + 1.25)], [b"xyz"],
+                          spans=[{"name": "H2D", "begin": t0 + 1.0, "end": t0 + 1.1, "bytes": 3},
+                                 {"name": "kernel", "begin": t0 + 1.1, "end": t0 + 1.15, "bytes": 3},
+                                 {"name": "D2H", "begin": t0 + 1.15, "end": t0 + 1.2, "bytes": 3}])
+        d._on_result(res)
+        d.export_perfetto_trace()
+        ev = json.load(open(tmp_path / "t.pftrace"))["traceEvents"]
+        inst = [e for e in ev if e["ph"] == "i"]
+        assert inst[0]["name"] == "Frame 0 - frame_captured" and inst[0]["cat"] == "video_frames"
+        assert inst[0]["ts"] == 500000 and inst[0]["args"]["absolute_timestamp"] == t0 + 0.5
+        xs = [e for e in ev if e["ph"] == "X" and e.get("cat") != "gpu"]
+        assert xs[0]["name"] == "Frame 0 - frame_inverted_received" and xs[0]["pid"] == 4242
+        assert xs[0]["ts"] == 1000000 and xs[0]["dur"] == 250000
+        assert abs(xs[0]["args"]["duration_ms"] - 250.0) < 1e-6
+        gpu = [e for e in ev if e.get("cat") == "gpu"]
+        assert [g["name"] for g in gpu] == ["GPU H2D", "GPU kernel", "GPU D2H"]
+        assert [g["tid"] for g in gpu] == [1, 2, 3] and all(g["pid"] == 4242 for g in gpu)
+        meta = [e for e in ev if e["ph"] == "M"]
+        assert {m["args"]["name"] for m in meta} == {"GPU H2D", "GPU kernel", "GPU D2H"}
+    finally:
+        d.cleanup()

@@ -13,6 +13,7 @@ import argparse
 import ctypes
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -90,7 +91,13 @@ def main():
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "sweep.jsonl"))
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--e2e-only", action="store_true")
+    ap.add_argument("--c5-point", type=int, default=0, help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.c5_point:
+        c = Context(0)
+        print(json.dumps(kernel_point(c, "1080p", 1080, 1920, args.c5_point, ring_min_bytes=0, steps=6)))
+        c.close()
+        return
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
     ctx = Context(0, max_frame_bytes=2160 * 3840 * 3, max_batch=4)
     points = [("480p", 32), ("480p", 256), ("1080p", 32), ("4k", 16), ("4k", 64)]
@@ -103,8 +110,15 @@ def main():
         for tag, b in ([] if args.e2e_only else points):
             h, w = SIZES[tag]
             emit(kernel_point(ctx, tag, h, w, b))
-        for b in ([] if args.e2e_only else sweep):  # configs[4]: one launch over the resident batch
-            emit(kernel_point(ctx, "1080p", 1080, 1920, b, ring_min_bytes=0, steps=6))
+        # configs[4]: one launch over the whole resident batch.  Each point runs in a fresh
+        # process: after many alloc/free cycles a multi-GB hipMalloc measured up to 20 % slower
+        # (profiles/r01_large_buffers.txt), which a worker that allocates once never sees.
+        for b in ([] if args.e2e_only else sweep):
+            r = subprocess.run([sys.executable, os.path.abspath(__file__), "--c5-point", str(b)],
+                               capture_output=True, text=True, timeout=300)
+            if r.returncode != 0:
+                raise RuntimeError(f"configs[4] point {b} failed: {r.stderr[-500:]}")
+            emit(json.loads(r.stdout.strip().splitlines()[-1]))
         for tag, b in (("480p", 32), ("1080p", 32), ("4k", 16)):
             h, w = SIZES[tag]
             emit(e2e_point(ctx, tag, h, w, b))

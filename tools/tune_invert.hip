@@ -47,7 +47,49 @@ __global__ void check_kernel(const uint8_t *a, const uint8_t *b, size_t n, int *
 
 static const char *vname(int v) { return vf::variant_name(v); }
 
+// Large single-buffer experiment (configs[4]): one src of `bytes`, dst at several offsets
+// from a bigger allocation, and the same bytes as one launch vs sub-range launches.
+static int large_mode(size_t bytes, int reps) {
+  vf::LaunchCfg lc;
+  uint8_t *src, *dst;
+  const size_t pad = (size_t)64 << 20;
+  CK(hipMalloc(&src, bytes));
+  CK(hipMalloc(&dst, bytes + pad));
+  hipLaunchKernelGGL(fill_kernel, dim3(4096), dim3(256), 0, 0, src, bytes, 77u);
+  CK(hipDeviceSynchronize());
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  std::printf("large-buffer mode: %zu B, src %p dst %p (dst-src = %lld)\n", bytes, (void *)src,
+              (void *)dst, (long long)(dst - src));
+  const size_t offs[] = {0, 4096, 65536, (size_t)1 << 20, (size_t)2 << 20, (size_t)8 << 20,
+                         (size_t)32 << 20};
+  const size_t subs[] = {0, (size_t)199065600, (size_t)1 << 30};
+  for (size_t sub : subs) {
+    for (size_t off : offs) {
+      std::vector<double> v;
+      for (int r = 0; r < reps; ++r) {
+        CK(hipEventRecord(e0, 0));
+        const size_t step = sub ? sub : bytes;
+        for (size_t o = 0; o < bytes; o += step)
+          CK(vf::launch_invert(src + o, dst + off + o, std::min(step, bytes - o), lc, 0));
+        CK(hipEventRecord(e1, 0));
+        CK(hipEventSynchronize(e1));
+        float ms = 0.f;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        v.push_back(2.0 * bytes / (ms * 1e-3) / 1e9);
+      }
+      std::sort(v.begin(), v.end());
+      std::printf("sub-launch %12zu  dst offset %10zu : median %7.1f GB/s (min %7.1f max %7.1f)\n", sub,
+                  off, v[v.size() / 2], v.front(), v.back());
+    }
+  }
+  return 0;
+}
+
 int main(int argc, char **argv) {
+  if (argc > 2 && std::strcmp(argv[1], "large") == 0)
+    return large_mode(std::strtoull(argv[2], nullptr, 0), argc > 3 ? std::atoi(argv[3]) : 5);
   size_t batch = argc > 1 ? std::strtoull(argv[1], nullptr, 0) : (size_t)32 * 1920 * 1080 * 3;
   int ring = argc > 2 ? std::atoi(argv[2]) : 6;
   int rounds = argc > 3 ? std::atoi(argv[3]) : 7;
