@@ -206,10 +206,13 @@ def main():
     from vfilter import Context
 
     have_gpu = torch.cuda.is_available()
+    # one GPU per rank (LOCAL_RANK); VF_DEVICE + BENCH_DIST_BACKEND=gloo rehearse N ranks on
+    # one card (the timing barrier is the only cross-rank operation, so gloo is enough)
+    device = int(os.environ.get("VF_DEVICE", local_rank))
+    backend = os.environ.get("BENCH_DIST_BACKEND") or ("nccl" if have_gpu else "gloo")
+    if have_gpu:
+        torch.cuda.set_device(device)
     if world > 1:
-        backend = "nccl" if have_gpu else "gloo"
-        if have_gpu:
-            torch.cuda.set_device(local_rank)
         dist.init_process_group(backend, rank=rank, world_size=world)
 
     def barrier_sync():
@@ -220,9 +223,9 @@ def main():
         if have_gpu:
             torch.cuda.synchronize()
 
-    ctx = Context(local_rank, max_frame_bytes=FRAME_BYTES, max_batch=args.batch)
+    ctx = Context(device, max_frame_bytes=FRAME_BYTES, max_batch=args.batch)
     srcs, dsts, batch_bytes, host_batch = make_ring(ctx, args.batch, args.ring_gb, np, rank, world)
-    log(f"rank {rank}: ring {len(srcs)} x 2 x {batch_bytes / 1e6:.1f} MB on device {local_rank}")
+    log(f"rank {rank}: ring {len(srcs)} x 2 x {batch_bytes / 1e6:.1f} MB on device {device}")
 
     if args.warmup:
         ctx.bench_device_ring(srcs, dsts, batch_bytes, args.warmup)
@@ -237,7 +240,8 @@ def main():
     _, isolated = ctx.bench_device_ring(srcs, dsts, batch_bytes, min(args.steps, 60), per_launch=True)
 
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if have_gpu else "cpu")
+        t = torch.tensor([elapsed], dtype=torch.float64,
+                         device="cuda" if (have_gpu and backend == "nccl") else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 

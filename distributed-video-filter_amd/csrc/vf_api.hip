@@ -174,6 +174,16 @@ struct vf_ctx {
   // in ms after t0, and the chunk's bytes (vf_last_timeline)
   std::vector<std::array<float, 4>> timeline;
   std::vector<size_t> timeline_bytes;
+  // asynchronous submissions (page-locked memory only; vf_invert_frames_async)
+  static constexpr int kTickets = 32;
+  hipEvent_t tk_start[kTickets] = {};
+  hipEvent_t tk_end[kTickets] = {};
+  uint64_t tk_next = 1;       // id of the next submission
+  uint64_t tk_done_upto = 0;  // every submission with id <= this has completed
+  int async_slot = 0;         // next device slot for an asynchronous chunk
+  bool slot_used[kMaxSlots] = {};
+  // host ranges page-locked through this context (vf_alloc_host / vf_host_register)
+  std::vector<std::pair<uintptr_t, size_t>> pinned;
 };
 
 namespace {
@@ -210,6 +220,20 @@ int fail_hip(vf_ctx *ctx, hipError_t e, const char *what, int line) {
     if (!(ctx)) return set_err(nullptr, VF_E_INVALID, 0, "%s: ctx is NULL", __func__); \
   } while (0)
 
+bool is_pinned(const void *p);
+
+// [p, p+len) inside a range this context page-locked?  Avoids a runtime query per frame.
+bool in_pinned_cache(const vf_ctx *ctx, const void *p, size_t len) {
+  const uintptr_t a = (uintptr_t)p;
+  for (const auto &r : ctx->pinned)
+    if (a >= r.first && a + len <= r.first + r.second) return true;
+  return false;
+}
+
+bool is_pinned_range(const vf_ctx *ctx, const void *p, size_t len) {
+  return in_pinned_cache(ctx, p, len) || is_pinned(p);
+}
+
 bool is_pinned(const void *p) {
   hipPointerAttribute_t a;
   std::memset(&a, 0, sizeof a);
@@ -238,6 +262,11 @@ int release_slots(vf_ctx *ctx) {
   }
   if (ctx->t0) (void)hipEventDestroy(ctx->t0);
   ctx->t0 = nullptr;
+  for (int i = 0; i < vf_ctx::kTickets; ++i) {
+    if (ctx->tk_start[i]) (void)hipEventDestroy(ctx->tk_start[i]);
+    if (ctx->tk_end[i]) (void)hipEventDestroy(ctx->tk_end[i]);
+    ctx->tk_start[i] = ctx->tk_end[i] = nullptr;
+  }
   if (ctx->s_in) (void)hipStreamDestroy(ctx->s_in);
   if (ctx->s_out) (void)hipStreamDestroy(ctx->s_out);
   ctx->s_in = ctx->s_out = nullptr;
@@ -264,23 +293,46 @@ int complete_slot(vf_ctx *ctx, Slot &s) {
 }
 
 // The slot pipeline over a list of segments (see file header).
+// Chunk size: the slot size for big calls; for small calls at least 2 chunks per slot so
+// the pipeline fills (480p x 32 = 29 MB in 16 MiB chunks was 2 chunks: no overlap).
+size_t chunk_size(const vf_ctx *ctx, size_t total) {
+  const size_t kMinChunk = (size_t)1 << 20;
+  size_t chunk = (total / (2 * (size_t)ctx->nslots) + 65535) & ~(size_t)65535;
+  return std::min(ctx->slot_bytes, std::max(kMinChunk, chunk));
+}
+
+bool all_pinned(const vf_ctx *ctx, const Seg *segs, size_t nseg, size_t *total) {
+  bool direct = true;
+  *total = 0;
+  for (size_t i = 0; i < nseg; ++i) {
+    *total += segs[i].len;
+    if (segs[i].len && direct &&
+        !(is_pinned_range(ctx, segs[i].src, segs[i].len) && is_pinned_range(ctx, segs[i].dst, segs[i].len)))
+      direct = false;
+  }
+  return direct;
+}
+
+// Wait for every asynchronous submission (before the synchronous path reuses the slots).
+int drain_async(vf_ctx *ctx) {
+  if (ctx->tk_done_upto + 1 < ctx->tk_next) {
+    VF_HIP(ctx, hipStreamSynchronize(ctx->s_out));
+    ctx->tk_done_upto = ctx->tk_next - 1;
+  }
+  return VF_OK;
+}
+
 int run_pipeline(vf_ctx *ctx, const Seg *segs, size_t nseg) {
   VF_HIP(ctx, hipSetDevice(ctx->device));
+  int rc0 = drain_async(ctx);
+  if (rc0 != VF_OK) return rc0;
   ctx->last_kernel_ms = 0.f;
   ctx->timeline.clear();
   ctx->timeline_bytes.clear();
-  bool direct = true;  // every source and destination page-locked?
   size_t total = 0;
-  for (size_t i = 0; i < nseg; ++i) {
-    total += segs[i].len;
-    if (segs[i].len && direct && !(is_pinned(segs[i].src) && is_pinned(segs[i].dst))) direct = false;
-  }
+  const bool direct = all_pinned(ctx, segs, nseg, &total);  // every byte page-locked?
   if (total == 0) return VF_OK;
-  // Chunk size: the slot size for big calls; for small calls at least 2 chunks per slot so
-  // the pipeline fills (480p x 32 = 29 MB in 16 MiB chunks was 2 chunks: no overlap).
-  const size_t kMinChunk = (size_t)1 << 20;
-  size_t chunk = (total / (2 * (size_t)ctx->nslots) + 65535) & ~(size_t)65535;
-  chunk = std::min(ctx->slot_bytes, std::max(kMinChunk, chunk));
+  const size_t chunk = chunk_size(ctx, total);
   size_t seg = 0, seg_off = 0;
   int next = 0;
   int rc = VF_OK;
@@ -346,6 +398,62 @@ int run_pipeline(vf_ctx *ctx, const Seg *segs, size_t nseg) {
     if (rc == VF_OK) rc = r;
   }
   return rc;
+}
+
+// Asynchronous form for page-locked memory: the whole chain is enqueued and the call
+// returns.  Slot reuse is ordered on the device (the IN stream waits for the slot's last D2H
+// before overwriting its device output), so the host never blocks; a worker can receive
+// and enqueue batch i+1 while batch i is still moving.
+int submit_async(vf_ctx *ctx, const Seg *segs, size_t nseg, uint64_t *ticket) {
+  VF_HIP(ctx, hipSetDevice(ctx->device));
+  size_t total = 0;
+  if (!all_pinned(ctx, segs, nseg, &total))
+    return set_err(ctx, VF_E_INVALID, 0,
+                   "vf_invert_frames_async: every buffer must be page-locked "
+                   "(vf_alloc_host / vf_host_register); use vf_invert_frames_host otherwise");
+  const uint64_t t = ctx->tk_next;
+  const int k = (int)(t % vf_ctx::kTickets);
+  if (t > (uint64_t)vf_ctx::kTickets && ctx->tk_done_upto < t - vf_ctx::kTickets) {
+    VF_HIP(ctx, hipEventSynchronize(ctx->tk_end[k]));  // bound the submissions in flight
+    ctx->tk_done_upto = t - vf_ctx::kTickets;
+  }
+  VF_HIP(ctx, hipEventRecord(ctx->tk_start[k], ctx->s_in));
+  const size_t chunk = chunk_size(ctx, total);
+  size_t seg = 0, seg_off = 0;
+  hipError_t e = hipSuccess;
+  while (seg < nseg && e == hipSuccess) {
+    const int si = ctx->async_slot;
+    ctx->async_slot = (si + 1) % ctx->nslots;
+    Slot &s = ctx->slots[si];
+    if (ctx->slot_used[si]) e = hipStreamWaitEvent(ctx->s_in, s.done, 0);
+    s.out.clear();
+    size_t filled = 0;
+    while (e == hipSuccess && seg < nseg && filled < chunk) {
+      const Seg &g = segs[seg];
+      size_t take = std::min(g.len - seg_off, chunk - filled);
+      if (take) {
+        e = hipMemcpyAsync(s.d_in + filled, g.src + seg_off, take, hipMemcpyHostToDevice, ctx->s_in);
+        s.out.push_back(OutPiece{g.dst + seg_off, filled, take});
+        filled += take;
+        seg_off += take;
+      }
+      if (seg_off == g.len) { ++seg; seg_off = 0; }
+    }
+    if (filled == 0) break;
+    if (e == hipSuccess) e = vf::launch_invert(s.d_in, s.d_out, filled, ctx->cfg, ctx->s_in);
+    if (e == hipSuccess) e = hipEventRecord(s.k1, ctx->s_in);
+    if (e == hipSuccess) e = hipStreamWaitEvent(ctx->s_out, s.k1, 0);
+    for (size_t i = 0; i < s.out.size() && e == hipSuccess; ++i)
+      e = hipMemcpyAsync(s.out[i].dst, s.d_out + s.out[i].off, s.out[i].len, hipMemcpyDeviceToHost,
+                         ctx->s_out);
+    if (e == hipSuccess) e = hipEventRecord(s.done, ctx->s_out);
+    ctx->slot_used[si] = true;
+  }
+  if (e == hipSuccess) e = hipEventRecord(ctx->tk_end[k], ctx->s_out);
+  if (e != hipSuccess) return fail_hip(ctx, e, "vf_invert_frames_async", __LINE__);
+  ctx->tk_next = t + 1;
+  *ticket = t;
+  return VF_OK;
 }
 
 }  // namespace
@@ -417,6 +525,10 @@ VF_EXPORT int vf_create(int device, size_t max_frame_bytes, int max_batch, vf_ct
     rc = fail_hip(ctx, e, "hipStreamCreateWithFlags", __LINE__);
   if (rc == VF_OK && (e = hipEventCreate(&ctx->t0)) != hipSuccess)
     rc = fail_hip(ctx, e, "hipEventCreate", __LINE__);
+  for (int i = 0; i < vf_ctx::kTickets && rc == VF_OK; ++i)
+    if ((e = hipEventCreate(&ctx->tk_start[i])) != hipSuccess ||
+        (e = hipEventCreate(&ctx->tk_end[i])) != hipSuccess)
+      rc = fail_hip(ctx, e, "hipEventCreate", __LINE__);
   for (int i = 0; i < ctx->nslots && rc == VF_OK; ++i) {
     Slot &s = ctx->slots[i];
     if ((e = hipEventCreate(&s.h0)) != hipSuccess || (e = hipEventCreate(&s.k0)) != hipSuccess ||
@@ -514,6 +626,72 @@ VF_EXPORT int vf_invert_frames_host(vf_ctx *ctx, const uint8_t *const *srcs, uin
   return run_pipeline(ctx, segs.data(), segs.size());
 }
 
+// ---- asynchronous host -> host (page-locked memory) ----------------------------------------
+
+VF_EXPORT int vf_invert_frames_async(vf_ctx *ctx, const uint8_t *const *srcs, uint8_t *const *dsts,
+                                     const size_t *nbytes, int n, uint64_t *ticket) {
+  VF_CHECK_CTX(ctx);
+  if (!ticket) return set_err(ctx, VF_E_INVALID, 0, "vf_invert_frames_async: ticket is NULL");
+  *ticket = 0;
+  if (n < 0) return set_err(ctx, VF_E_INVALID, 0, "vf_invert_frames_async: n < 0");
+  if (n > 0 && (!srcs || !dsts || !nbytes))
+    return set_err(ctx, VF_E_INVALID, 0, "vf_invert_frames_async: NULL array");
+  std::vector<Seg> segs;
+  segs.reserve((size_t)n);
+  for (int i = 0; i < n; ++i) {
+    if (nbytes[i] == 0) continue;
+    if (!srcs[i] || !dsts[i])
+      return set_err(ctx, VF_E_INVALID, 0, "vf_invert_frames_async: frame %d has a NULL buffer", i);
+    if (overlaps_partially(srcs[i], dsts[i], nbytes[i]))
+      return set_err(ctx, VF_E_INVALID, 0, "vf_invert_frames_async: frame %d src/dst partially overlap", i);
+    segs.push_back(Seg{srcs[i], dsts[i], nbytes[i]});
+  }
+  return submit_async(ctx, segs.data(), segs.size(), ticket);
+}
+
+VF_EXPORT int vf_wait(vf_ctx *ctx, uint64_t ticket, float *gpu_ms) {
+  VF_CHECK_CTX(ctx);
+  if (gpu_ms) *gpu_ms = -1.f;
+  if (ticket == 0 || ticket >= ctx->tk_next)
+    return set_err(ctx, VF_E_INVALID, 0, "vf_wait: unknown ticket %llu", (unsigned long long)ticket);
+  const int k = (int)(ticket % vf_ctx::kTickets);
+  const bool recycled = ticket + vf_ctx::kTickets < ctx->tk_next;  // events reused since
+  if (ticket > ctx->tk_done_upto) {
+    // If the event was re-recorded for a later submission, waiting for it still covers this
+    // one: the OUT stream completes submissions in order.
+    VF_HIP(ctx, hipSetDevice(ctx->device));
+    VF_HIP(ctx, hipEventSynchronize(ctx->tk_end[k]));
+    ctx->tk_done_upto = ticket;
+  }
+  if (gpu_ms && !recycled) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, ctx->tk_start[k], ctx->tk_end[k]) == hipSuccess) *gpu_ms = ms;
+  }
+  return VF_OK;
+}
+
+VF_EXPORT int vf_query(vf_ctx *ctx, uint64_t ticket, int *done) {
+  VF_CHECK_CTX(ctx);
+  if (!done) return set_err(ctx, VF_E_INVALID, 0, "vf_query: done is NULL");
+  if (ticket == 0 || ticket >= ctx->tk_next)
+    return set_err(ctx, VF_E_INVALID, 0, "vf_query: unknown ticket %llu", (unsigned long long)ticket);
+  if (ticket <= ctx->tk_done_upto || ticket + vf_ctx::kTickets < ctx->tk_next) {
+    *done = 1;
+    return VF_OK;
+  }
+  hipError_t e = hipEventQuery(ctx->tk_end[ticket % vf_ctx::kTickets]);
+  if (e == hipSuccess) {
+    *done = 1;
+    ctx->tk_done_upto = std::max(ctx->tk_done_upto, ticket);
+  } else if (e == hipErrorNotReady) {
+    (void)hipGetLastError();
+    *done = 0;
+  } else {
+    return fail_hip(ctx, e, "hipEventQuery", __LINE__);
+  }
+  return VF_OK;
+}
+
 // ---- device-resident ---------------------------------------------------------------------
 
 VF_EXPORT int vf_invert_device(vf_ctx *ctx, const void *dsrc, void *ddst, size_t nbytes,
@@ -572,12 +750,23 @@ VF_EXPORT int vf_alloc_host(vf_ctx *ctx, size_t nbytes, void **out) {
   hipError_t e = hipHostMalloc(out, nbytes ? nbytes : 1, hipHostMallocDefault);
   if (e != hipSuccess)
     return set_err(ctx, VF_E_NOMEM, (int)e, "hipHostMalloc(%zu) failed: %s", nbytes, hipGetErrorString(e));
+  ctx->pinned.emplace_back((uintptr_t)*out, nbytes ? nbytes : 1);
   return VF_OK;
+}
+
+static void forget_pinned(vf_ctx *ctx, void *p) {
+  auto &v = ctx->pinned;
+  v.erase(std::remove_if(v.begin(), v.end(), [p](const std::pair<uintptr_t, size_t> &r) {
+            return r.first == (uintptr_t)p;
+          }), v.end());
 }
 
 VF_EXPORT int vf_free_host(vf_ctx *ctx, void *p) {
   VF_CHECK_CTX(ctx);
   if (!p) return VF_OK;
+  int rc = drain_async(ctx);
+  if (rc != VF_OK) return rc;
+  forget_pinned(ctx, p);
   VF_HIP(ctx, hipHostFree(p));
   return VF_OK;
 }
@@ -587,12 +776,16 @@ VF_EXPORT int vf_host_register(vf_ctx *ctx, void *p, size_t nbytes) {
   if (!p || !nbytes) return set_err(ctx, VF_E_INVALID, 0, "vf_host_register: empty range");
   VF_HIP(ctx, hipSetDevice(ctx->device));
   VF_HIP(ctx, hipHostRegister(p, nbytes, hipHostRegisterDefault));
+  ctx->pinned.emplace_back((uintptr_t)p, nbytes);
   return VF_OK;
 }
 
 VF_EXPORT int vf_host_unregister(vf_ctx *ctx, void *p) {
   VF_CHECK_CTX(ctx);
   if (!p) return VF_OK;
+  int rc = drain_async(ctx);
+  if (rc != VF_OK) return rc;
+  forget_pinned(ctx, p);
   VF_HIP(ctx, hipHostUnregister(p));
   return VF_OK;
 }

@@ -45,6 +45,9 @@ SIGNATURES = {
     "vf_invert_host": (ctypes.c_int, [_vp, _u8p, _u8p, _sz]),
     "vf_invert_batch_host": (ctypes.c_int, [_vp, _u8p, _u8p, _sz, ctypes.c_int]),
     "vf_invert_frames_host": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_int]),
+    "vf_invert_frames_async": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64)]),
+    "vf_wait": (ctypes.c_int, [_vp, ctypes.c_uint64, _c_float_p]),
+    "vf_query": (ctypes.c_int, [_vp, ctypes.c_uint64, _c_int_p]),
     "vf_invert_device": (ctypes.c_int, [_vp, _vp, _vp, _sz, _vp]),
     "vf_invert_device_frames": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_int, _sz, _vp]),
     "vf_alloc_device": (ctypes.c_int, [_vp, _sz, ctypes.POINTER(_vp)]),
@@ -182,6 +185,31 @@ class Context:
         da = (ctypes.c_void_p * n)(*[_addr(d) for d in dsts])
         na = (ctypes.c_size_t * n)(*[int(b) for b in nbytes])
         self._check(self._lib.vf_invert_frames_host(self._ctx, sa, da, na, n))
+
+    # -- host -> host, asynchronous (page-locked buffers) -----------------------------------
+    def invert_frames_async(self, srcs: Sequence, dsts: Sequence, nbytes: Sequence[int]) -> int:
+        """Enqueue a batch whose buffers are all page-locked; returns a ticket for ``wait``.
+        The caller keeps the buffers alive until the ticket completes."""
+        n = len(srcs)
+        if not (len(dsts) == n == len(nbytes)):
+            raise ValueError("srcs, dsts and nbytes must have the same length")
+        sa = (ctypes.c_void_p * n)(*[_addr(s) for s in srcs])
+        da = (ctypes.c_void_p * n)(*[_addr(d) for d in dsts])
+        na = (ctypes.c_size_t * n)(*[int(b) for b in nbytes])
+        t = ctypes.c_uint64(0)
+        self._check(self._lib.vf_invert_frames_async(self._ctx, sa, da, na, n, ctypes.byref(t)))
+        return t.value
+
+    def wait(self, ticket: int) -> float:
+        """Block until ``ticket`` completes; returns its device time in ms (-1 if unknown)."""
+        ms = ctypes.c_float(-1.0)
+        self._check(self._lib.vf_wait(self._ctx, ticket, ctypes.byref(ms)))
+        return ms.value
+
+    def query(self, ticket: int) -> bool:
+        done = ctypes.c_int(0)
+        self._check(self._lib.vf_query(self._ctx, ticket, ctypes.byref(done)))
+        return bool(done.value)
 
     # -- device-resident ------------------------------------------------------------------
     def invert_device(self, dsrc: int, ddst: int, nbytes: int, stream: int = 0) -> None:

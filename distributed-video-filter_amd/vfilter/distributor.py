@@ -62,7 +62,10 @@ class Distributor:
                  enable_trace_export: bool = False, *, policy: str = "latest", reassembly: str = "display",
                  transport: str = "auto", host: str = "*", queue_size: int = 10, frame_buffer_size: int = 50,
                  ring_slots: int = 0, ring_slot_bytes: int = 0, shard_workers: int = 0, shard_chunk: int = 1,
-                 trace_file: str = "webcam_frame_timing.pftrace", verbose: bool = True):
+                 trace_file: str = "webcam_frame_timing.pftrace", verbose: bool = True, zero_copy: bool = False):
+        if zero_copy and (ring_slots < 1 or reassembly != "ordered"):
+            raise ValueError("zero_copy needs ring_slots > 0 and reassembly='ordered'")
+        self.zero_copy = zero_copy
         if policy not in ("latest", "pull", "shard"):
             raise ValueError("policy must be latest | pull | shard")
         if reassembly not in ("display", "ordered"):
@@ -189,7 +192,7 @@ class Distributor:
                                    "end_relative_time": end_time - self.trace_start_time, "event_ph": "X",
                                    "pid": pid})
 
-    GPU_TIDS = {"H2D": 1, "kernel": 2, "D2H": 3}
+    GPU_TIDS = {"H2D": 1, "kernel": 2, "D2H": 3, "batch": 4}  # "batch" = H2D..D2H of an async batch
 
     def log_gpu_span(self, name: str, begin_time: float, end_time: float, pid, nbytes: int = 0):
         """A GPU span of a worker batch (H2D / kernel / D2H), shown on its own track under
@@ -260,15 +263,35 @@ class Distributor:
         nbytes = frame.nbytes if isinstance(frame, np.ndarray) else len(frame)
         slot = None
         if self.ring is not None:
-            if nbytes > self.ring.slot_bytes:
-                raise ValueError(f"frame of {nbytes} B exceeds ring slot of {self.ring.slot_bytes} B")
-            slot = self.ring.acquire(timeout=None if (block and self.policy != "latest") else 0)
-            if slot is None and self.policy == "latest":
-                slot = self._evict_oldest_queued_slot()
+            slot = self.reserve_frame(nbytes, block)
             if slot is None:
                 return -1
             self.ring.in_view(slot, nbytes)[:] = np.frombuffer(frame, dtype=np.uint8) \
                 if not isinstance(frame, np.ndarray) else frame.reshape(-1).view(np.uint8)
+        return self._enqueue(None if slot is not None else frame, nbytes, shape, slot, timestamp, block)
+
+    # ---- zero-copy ingest (ring mode) ------------------------------------------------------
+    def reserve_frame(self, nbytes: int, block: bool = True) -> Optional[int]:
+        """Reserve a ring slot for a frame of ``nbytes``; fill ``frame_view(slot, nbytes)`` in
+        place (e.g. decode or capture straight into it), then ``commit_frame``.  Returns None
+        when no slot is free and ``block`` is False."""
+        if self.ring is None:
+            raise RuntimeError("reserve_frame needs ring_slots > 0")
+        if nbytes > self.ring.slot_bytes:
+            raise ValueError(f"frame of {nbytes} B exceeds ring slot of {self.ring.slot_bytes} B")
+        slot = self.ring.acquire(timeout=None if (block and self.policy != "latest") else 0)
+        if slot is None and self.policy == "latest":
+            slot = self._evict_oldest_queued_slot()
+        return slot
+
+    def frame_view(self, slot: int, nbytes: int) -> np.ndarray:
+        return self.ring.in_view(slot, nbytes)
+
+    def commit_frame(self, slot: int, nbytes: int, shape=None, timestamp=None, block: bool = True) -> int:
+        """Queue the frame written into ``slot``; returns its index (as add_frame_for_distribution)."""
+        return self._enqueue(None, nbytes, shape, slot, time.time() if timestamp is None else timestamp, block)
+
+    def _enqueue(self, frame, nbytes: int, shape, slot: Optional[int], timestamp: float, block: bool) -> int:
         with self._cv:
             frame_index = self.frame_index_counter          # distributor.py:179-180
             self.frame_index_counter += 1
@@ -465,17 +488,20 @@ class Distributor:
                         self._cv.notify_all()
                 continue
             if m.slot is not None:
-                data = bytes(self.ring.out_view(m.slot, m.nbytes))
+                # zero-copy: hand out the slot's output half; the consumer releases it
+                data = self.ring.out_view(m.slot, m.nbytes) if self.zero_copy else \
+                    bytes(self.ring.out_view(m.slot, m.nbytes))
             else:
                 data = payload
             with self._cv:
-                self._free_slot(m.index)
+                if not (self.zero_copy and m.slot is not None):
+                    self._free_slot(m.index)
                 self.results_received += 1
                 if self.reassembly == "display":
                     self._display.receive(m.index, data, res.pid, m.start, m.end)
                 else:
                     self._ordered.push(m.index, data, {"process_id": res.pid, "start_time": m.start,
-                                                       "end_time": m.end, "shape": m.shape})
+                                                       "end_time": m.end, "shape": m.shape, "slot": m.slot})
                     self._released.extend(self._ordered.pop_ready())
                 self._cv.notify_all()
 
@@ -513,6 +539,15 @@ class Distributor:
                     return None
                 self._cv.wait(rem if rem is not None else 0.1)
             return self._released.popleft()
+
+    def release_frame(self, index: int) -> None:
+        """zero_copy: return frame ``index``'s ring slot once its result view is consumed."""
+        with self._cv:
+            self._free_slot(index)
+
+    def num_workers(self) -> int:
+        with self._lock:
+            return len(self._peers)
 
     def ordering_stats(self) -> dict:
         with self._lock:

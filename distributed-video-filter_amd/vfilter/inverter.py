@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import argparse
 import signal
+import threading
 import time
 from typing import List, Optional, Sequence
 
@@ -39,6 +40,7 @@ class InverterWorker(Worker):
         if use_jpeg:
             from turbojpeg import TurboJPEG  # raises ImportError when absent, like inverter.py:7
             self.jpeg = TurboJPEG()
+        worker_kw.setdefault("inflight", 2)  # batch i on the GPU while batch i+1 is received
         super().__init__(host, distribute_port, collect_port, **worker_kw)
         self.delay = delay
         self.device = default_device() if device is None else device
@@ -94,6 +96,32 @@ class InverterWorker(Worker):
         self.last_spans = gpu_spans(self.ctx.last_timeline(), t_call)
         return results
 
+    # -- ring batches: asynchronous submission -------------------------------------------
+    def submit_batch(self, frames: Sequence, metas: Sequence[wire.FrameMeta], outs: Sequence):
+        """Frames in the page-locked ring go through vf_invert_frames_async: the whole batch
+        is queued on the device and the worker loop goes back to receiving at once."""
+        if self.jpeg or self.delay > 0 or not self._registered or any(o is None for o in outs):
+            return super().submit_batch(frames, metas, outs)
+        try:
+            ticket = self.ctx.invert_frames_async(frames, outs, [f.nbytes for f in frames])
+        except Exception:
+            return super().submit_batch(frames, metas, outs)  # e.g. ring not page-locked
+        return ("gpu", ticket, list(outs), sum(f.nbytes for f in frames))
+
+    def poll_batch(self, handle, block: bool):
+        if handle[0] != "gpu":
+            return super().poll_batch(handle, block)
+        _, ticket, outs, nbytes = handle
+        if not block and not self.ctx.query(ticket):
+            return None
+        try:
+            ms = self.ctx.wait(ticket)
+        except Exception as e:
+            return [e] * len(outs), []
+        t_end = time.time()
+        spans = [{"name": "batch", "begin": t_end - ms / 1e3, "end": t_end, "bytes": nbytes}] if ms >= 0 else []
+        return outs, spans
+
     def on_ring_attached(self, ring) -> None:
         """Page-lock the whole shared-memory ring once: the slot pipeline then DMAs straight
         from the input halves and into the output halves (no staging copy)."""
@@ -139,13 +167,14 @@ def main(argv=None):
     ap.add_argument("--jpeg", action="store_true", help="JPEG frames (needs PyTurboJPEG); default raw")
     ap.add_argument("--device", type=int, default=None, help="GPU ordinal (default: VF_DEVICE / LOCAL_RANK / 0)")
     ap.add_argument("--batch", type=int, default=8, help="frames per request (protocol v1)")
+    ap.add_argument("--inflight", type=int, default=2, help="batches in progress at once (protocol v1)")
     ap.add_argument("--protocol", choices=("v0", "v1"), default="v1",
                     help="v0 = the reference wire protocol (use against the reference distributor.py)")
     ap.add_argument("--transport", choices=("auto", "zmq", "tcp"), default="auto")
     ap.add_argument("--verbose", action="store_true")
     args = ap.parse_args(argv)
     worker = InverterWorker(args.host, args.distribute_port, args.collect_port, args.delay,
-                            use_jpeg=args.jpeg, device=args.device, batch=args.batch,
+                            use_jpeg=args.jpeg, device=args.device, batch=args.batch, inflight=args.inflight,
                             protocol=args.protocol, transport=args.transport, verbose=args.verbose)
     try:
         worker.start()

@@ -19,7 +19,9 @@ in-order consumer does not wait for it).  One worker process owns one GPU.
 """
 from __future__ import annotations
 
+import collections
 import os
+import threading
 import time
 from typing import List, Optional, Sequence
 
@@ -32,8 +34,8 @@ from .shm import FrameRing
 
 class Worker:
     def __init__(self, host: str = "localhost", distribute_port: int = 5555, collect_port: int = 5556, *,
-                 transport: str = "auto", protocol: str = "v1", batch: int = 1, depth: int = 2,
-                 verbose: bool = False):
+                 transport: str = "auto", protocol: str = "v1", batch: int = 1, depth: int = 0,
+                 inflight: int = 1, verbose: bool = False):
         self.host = host
         self.distribute_port = distribute_port
         self.collect_port = collect_port
@@ -44,7 +46,8 @@ class Worker:
             raise ValueError("protocol must be 'v0' (reference) or 'v1'")
         self.protocol = protocol
         self.batch = max(1, int(batch))
-        self.depth = max(1, int(depth))
+        # requests kept outstanding: one more than the batches that can be in processing
+        self.depth = int(depth) if depth else max(1, int(inflight)) + 1
         self.verbose = verbose
         self.transport = tp.resolve(transport)
         self._zctx = tp.make_context(self.transport)
@@ -52,7 +55,9 @@ class Worker:
         self.collect_socket = tp.PushEnd(self.transport, host, collect_port, self._zctx)       # worker.py:24-25
         self.frames_processed = 0
         self.errors = 0
-        self.last_spans: List[dict] = []  # GPU spans of the last batch (set by process_batch)
+        self.inflight = max(1, int(inflight))  # batches in progress at once (protocol v1)
+        self._tls = threading.local()
+        self._ring_lock = threading.Lock()
         self._ring: Optional[FrameRing] = None
         self._ring_name: Optional[str] = None
         if verbose:
@@ -143,22 +148,96 @@ class Worker:
                 print(f"Error in worker: {e}")
                 continue
 
+    @property
+    def last_spans(self) -> List[dict]:
+        """GPU spans of the batch the calling thread processed last (set by process_batch)."""
+        return getattr(self._tls, "spans", [])
+
+    @last_spans.setter
+    def last_spans(self, spans: List[dict]) -> None:
+        self._tls.spans = spans
+
     def _attach_ring(self, name: str, slot_bytes: int) -> FrameRing:
-        if self._ring is None or self._ring_name != name:
-            if self._ring is not None:
-                self._ring.close()
-            self._ring = FrameRing(name=name, slot_bytes=slot_bytes)
-            self._ring_name = name
-            self.on_ring_attached(self._ring)
-        return self._ring
+        with self._ring_lock:
+            if self._ring is None or self._ring_name != name:
+                if self._ring is not None:
+                    self._ring.close()
+                self._ring = FrameRing(name=name, slot_bytes=slot_bytes)
+                self._ring_name = name
+                self.on_ring_attached(self._ring)
+            return self._ring
+
+    # -- asynchronous batch hooks (a GPU plugin overrides these) ----------------------------
+    def submit_batch(self, frames: Sequence, metas: Sequence[wire.FrameMeta], outs: Sequence):
+        """Start a batch and return a handle for ``poll_batch``.  Default: run
+        ``process_batch`` now (synchronously)."""
+        self.last_spans = []
+        try:
+            results = self.process_batch(frames, metas, outs)
+        except Exception as e:
+            results = [e] * len(frames)
+        return ("done", results, self.last_spans)
+
+    def poll_batch(self, handle, block: bool):
+        """(results, spans) once the batch behind ``handle`` is complete, else None (only
+        when ``block`` is False)."""
+        return handle[1], handle[2]
+
+    def _start_job(self, d: wire.Dispatch, start_time: float):
+        ring = None
+        if d.ring is not None:
+            ring = self._attach_ring(d.ring["name"], int(d.ring["slot_bytes"]))
+        frames, outs = [], []
+        for m, p in zip(d.metas, d.payloads):
+            if m.slot is not None:
+                frames.append(ring.in_view(m.slot, m.nbytes))
+                outs.append(ring.out_view(m.slot, m.nbytes))
+            else:
+                frames.append(p)
+                outs.append(None)
+        if self.verbose:
+            print(f"Processing frames {[m.index for m in d.metas]}")
+        return d, start_time, self.submit_batch(frames, d.metas, outs)
+
+    def _finish_job(self, job, block: bool) -> bool:
+        d, start_time, handle = job
+        got = self.poll_batch(handle, block)
+        if got is None:
+            return False
+        results, spans = got
+        end_time = time.time()
+        metas, payloads = [], []
+        for m, r in zip(d.metas, results):
+            om = wire.FrameMeta(index=m.index, nbytes=m.nbytes, shape=m.shape, slot=m.slot,
+                                start=start_time, end=end_time)
+            if isinstance(r, Exception):
+                om.error = f"{type(r).__name__}: {r}"
+                self.errors += 1
+                print(f"Error in worker: frame {m.index}: {r}")
+                payloads.append(None)
+            else:
+                payloads.append(None if m.slot is not None else r)
+            metas.append(om)
+        self.collect_socket.send(wire.encode_result(self.process_id, metas, payloads, spans))
+        self.frames_processed += len(metas)
+        return True
 
     def _loop_v1(self, max_frames):
+        """Credit loop: ``depth`` requests outstanding; up to ``inflight`` received batches
+        in progress at once (a GPU plugin submits them asynchronously, so the device works
+        on batch i while this loop receives and submits batch i+1); results go out in
+        arrival order."""
         outstanding = 0
+        jobs: "collections.deque" = collections.deque()
         while self.running and (max_frames is None or self.frames_processed < max_frames):
             while outstanding < self.depth:
                 self.dealer_socket.send(wire.encode_request(self.batch, shm=True))
                 outstanding += 1
-            if not self.dealer_socket.poll(10):
+            while jobs and self._finish_job(jobs[0], block=len(jobs) >= self.inflight):
+                jobs.popleft()
+            if len(jobs) >= self.inflight:
+                continue
+            if not self.dealer_socket.poll(1 if jobs else 10):
                 continue
             parts = self.dealer_socket.recv()
             start_time = time.time()
@@ -169,36 +248,6 @@ class Worker:
                 continue
             if d.version == 1:
                 outstanding -= 1
-            ring = None
-            if d.ring is not None:
-                ring = self._attach_ring(d.ring["name"], int(d.ring["slot_bytes"]))
-            frames, outs = [], []
-            for m, p in zip(d.metas, d.payloads):
-                if m.slot is not None:
-                    frames.append(ring.in_view(m.slot, m.nbytes))
-                    outs.append(ring.out_view(m.slot, m.nbytes))
-                else:
-                    frames.append(p)
-                    outs.append(None)
-            if self.verbose:
-                print(f"Processing frames {[m.index for m in d.metas]}")
-            self.last_spans = []
-            try:
-                results = self.process_batch(frames, d.metas, outs)
-            except Exception as e:
-                results = [e] * len(frames)
-            end_time = time.time()
-            metas, payloads = [], []
-            for m, r in zip(d.metas, results):
-                om = wire.FrameMeta(index=m.index, nbytes=m.nbytes, shape=m.shape, slot=m.slot,
-                                    start=start_time, end=end_time)
-                if isinstance(r, Exception):
-                    self.errors += 1
-                    om.error = f"{type(r).__name__}: {r}"
-                    print(f"Error in worker: frame {m.index}: {r}")
-                    payloads.append(None)
-                else:
-                    payloads.append(None if m.slot is not None else r)
-                metas.append(om)
-            self.collect_socket.send(wire.encode_result(self.process_id, metas, payloads, self.last_spans))
-            self.frames_processed += len(metas)
+            jobs.append(self._start_job(d, start_time))
+        while jobs:  # finish what was accepted before stopping
+            self._finish_job(jobs.popleft(), block=True)

@@ -226,3 +226,40 @@ def test_timeline_chunks_cover_the_call(vf_ctx):
     for nb, h0, k0, k1, d1 in tl:
         assert 0.0 <= h0 <= k0 <= k1 <= d1
     assert np.array_equal(y, oracle.invert(x))
+
+
+def test_async_frames_on_pinned_memory(vf_ctx):
+    """vf_invert_frames_async: several batches queued back to back on page-locked memory,
+    completed out of host order (wait on the last first), every byte exact; pageable
+    buffers are refused, and a synchronous call after async ones sees consistent slots."""
+    sizes = [1080 * 1920 * 3, 480 * 640 * 3, 17 * 13 * 3, 2160 * 3840 * 3]
+    total = sum(sizes)
+    nb = 6
+    ps = [vf_ctx.alloc_host(total) for _ in range(nb)]
+    pd = [vf_ctx.alloc_host(total) for _ in range(nb)]
+    try:
+        hs = [np.ctypeslib.as_array((ctypes.c_uint8 * total).from_address(p)) for p in ps]
+        hd = [np.ctypeslib.as_array((ctypes.c_uint8 * total).from_address(p)) for p in pd]
+        for b in range(nb):
+            hs[b][:] = np.random.default_rng(b).integers(0, 256, total, dtype=np.uint8)
+        tickets = []
+        for b in range(nb):
+            offs = np.cumsum([0] + sizes[:-1])
+            srcs = [ps[b] + int(o) for o in offs]
+            dsts = [pd[b] + int(o) for o in offs]
+            tickets.append(vf_ctx.invert_frames_async(srcs, dsts, sizes))
+        assert tickets == sorted(tickets) and len(set(tickets)) == nb
+        assert vf_ctx.wait(tickets[-1]) >= 0.0
+        for t in tickets:
+            assert vf_ctx.query(t)
+            vf_ctx.wait(t)
+        for b in range(nb):
+            assert np.array_equal(hd[b], oracle.invert(hs[b])), b
+        x = np.zeros(1000, np.uint8)
+        with pytest.raises(vfilter.VFilterError, match="page-locked"):
+            vf_ctx.invert_frames_async([x], [np.empty_like(x)], [1000])
+        y = oracle.synthetic_frame(77, 480, 640)  # sync path after async work
+        assert np.array_equal(vfilter.bitwise_not(y, ctx=vf_ctx), oracle.invert(y))
+    finally:
+        for p in ps + pd:
+            vf_ctx.free_host(p)

@@ -311,3 +311,33 @@ def test_perfetto_trace_reference_schema_plus_gpu_spans(tmp_path):
         assert {m["args"]["name"] for m in meta} == {"GPU H2D", "GPU kernel", "GPU D2H"}
     finally:
         d.cleanup()
+
+
+@pytest.mark.timeout(120)
+def test_zero_copy_reserve_commit_and_release():
+    """Ring mode without host copies in the distributor: the producer fills a reserved slot
+    in place; the ordered consumer reads the result view and releases the slot."""
+    d = _dist(policy="pull", reassembly="ordered", queue_size=8, ring_slots=6, ring_slot_bytes=64 * 64 * 3,
+              zero_copy=True)
+    stop, procs = spawn_workers(1, d.distribute_port, d.collect_port, protocol="v1", batch=2)
+    try:
+        frames = _frames(20, [(64, 64), (32, 16)])
+
+        def produce():
+            for f in frames:
+                slot = d.reserve_frame(f.nbytes)
+                d.frame_view(slot, f.nbytes)[:] = f.reshape(-1)
+                d.commit_frame(slot, f.nbytes, shape=list(f.shape))
+
+        th = threading.Thread(target=produce)
+        th.start()
+        for i, f in enumerate(frames):
+            idx, view, info = d.get_next_frame(timeout=20)
+            assert idx == i and isinstance(view, np.ndarray)
+            assert view.tobytes() == oracle.invert_bytes(f.tobytes())
+            d.release_frame(idx)
+        th.join()
+        assert d.ring.free_slots() == 6
+    finally:
+        stop_workers(stop, procs)
+        d.cleanup()

@@ -1,0 +1,172 @@
+#!/usr/bin/env python3
+"""Distributor-level throughput: BASELINE.json configs[2] (4K, batch 16, frame-index sharded
+over N workers, in-order reassembly) and configs[3] (mixed 480p/1080p/4K stream, ordering
+overhead), host->host through the whole fan-out.
+
+One Distributor (lossless ``shard`` or ``pull`` policy, ``ordered`` reassembly, shared-memory
+ring, zero-copy in and out) feeds N ``python -m vfilter.inverter`` worker processes, worker i
+on GPU i % G.  Each worker page-locks the ring, so frames go ring -> GPU -> ring by DMA.
+Reported: delivered frames/s in index order, GB/s each way, per-frame latency (commit ->
+in-order release), reorder wait and buffer depth.
+
+  python tools/pipeline_bench.py --workers 2 --size 4k --batch 16 --frames 512
+  python tools/pipeline_bench.py --workers 2 --size mixed --policy pull
+
+Producer modes: ``resident`` (default) — ring slots are filled once with random bytes and
+frames are committed without a host copy, isolating distribution + PCIe + kernel +
+reassembly; ``copy`` — each frame is copied into its slot from a pre-generated frame (what a
+producer that cannot decode straight into the ring pays).
+"""
+import argparse
+import json
+import os
+import signal
+import subprocess
+import sys
+import threading
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "distributed-video-filter_amd")
+sys.path.insert(0, PKG)
+
+import numpy as np  # noqa: E402
+
+from vfilter.distributor import Distributor  # noqa: E402
+from vfilter.shm import shm_free_bytes  # noqa: E402
+from vfilter.synthetic import SIZES  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workers", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=0, help="devices to spread workers over (0 = all visible)")
+    ap.add_argument("--size", default="1080p", choices=list(SIZES) + ["mixed"])
+    ap.add_argument("--frames", type=int, default=512)
+    ap.add_argument("--batch", type=int, default=16)
+    ap.add_argument("--policy", default="shard", choices=("shard", "pull"))
+    ap.add_argument("--producer", default="resident", choices=("resident", "copy"))
+    ap.add_argument("--ring-slots", type=int, default=0, help="0 = 4 batches per worker, capped by /dev/shm")
+    ap.add_argument("--verify-every", type=int, default=64)
+    ap.add_argument("--inflight", type=int, default=2, help="batches in progress per worker")
+    ap.add_argument("--out", default="")
+    args = ap.parse_args()
+
+    shapes = [SIZES["480p"], SIZES["1080p"], SIZES["4k"]] if args.size == "mixed" else [SIZES[args.size]]
+    fbytes = [h * w * 3 for h, w in shapes]
+    slot_bytes = max(fbytes)
+    slots = args.ring_slots or 4 * args.batch * args.workers
+    free = shm_free_bytes()
+    if free is not None:
+        slots = max(2 * args.batch, min(slots, int(free * 0.6) // (2 * slot_bytes)))
+    ngpu = args.gpus
+    if ngpu <= 0:
+        from vfilter import device_count
+        ngpu = max(1, device_count())
+
+    d = Distributor(0, 0, policy=args.policy, reassembly="ordered", transport="tcp", host="127.0.0.1",
+                    queue_size=4 * args.batch * args.workers, ring_slots=slots, ring_slot_bytes=slot_bytes,
+                    shard_workers=args.workers, shard_chunk=args.batch, zero_copy=True, verbose=False)
+    d.start()
+    env = dict(os.environ, PYTHONPATH=PKG + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    procs = []
+    for i in range(args.workers):
+        e = dict(env, VF_DEVICE=str(i % ngpu))
+        procs.append(subprocess.Popen([sys.executable, "-m", "vfilter.inverter", "--host", "127.0.0.1",
+                                       "--distribute-port", str(d.distribute_port), "--collect-port",
+                                       str(d.collect_port), "--batch", str(args.batch), "--transport", "tcp",
+                                       "--inflight", str(args.inflight)],
+                                      env=e, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE))
+    result = {}
+    try:
+        t0 = time.time()
+        while d.num_workers() < args.workers:
+            if time.time() - t0 > 120 or any(p.poll() is not None for p in procs):
+                raise RuntimeError("workers did not come up: " +
+                                   " | ".join((p.stderr.read() or b"").decode()[-300:] for p in procs if p.poll() is not None))
+            time.sleep(0.05)
+
+        rng = np.random.default_rng(0)
+        # resident content: each slot's input half holds random bytes once
+        for s in range(slots):
+            d.ring.in_view(s, slot_bytes)[:] = rng.integers(0, 256, slot_bytes, dtype=np.uint8)
+        pregen = [rng.integers(0, 256, fb, dtype=np.uint8) for fb in fbytes]
+        # warmup: every worker maps and page-locks the ring on its first batch (hipHostRegister
+        # of the whole ring, ~0.15 s per GB) -- a one-off start-up cost kept out of the timing
+        warm = 2 * args.batch * args.workers * len(shapes)
+        n = args.frames
+        commit_t = np.zeros(warm + n)
+        release_t = np.zeros(warm + n)
+        errors = []
+        started = threading.Event()
+
+        def produce():
+            for i in range(warm + n):
+                if i == warm:
+                    started.wait()
+                k = i % len(shapes)
+                nb = fbytes[k]
+                slot = d.reserve_frame(nb)
+                if args.producer == "copy":
+                    d.frame_view(slot, nb)[:] = pregen[k]
+                commit_t[i] = time.perf_counter()
+                d.commit_frame(slot, nb, shape=[shapes[k][0], shapes[k][1], 3])
+
+        th = threading.Thread(target=produce, daemon=True)
+        th.start()
+        total_bytes = 0
+        for i in range(warm + n):
+            if i == warm:
+                d_stats0 = d.ordering_stats()
+                t_start = time.perf_counter()
+                started.set()
+            item = d.get_next_frame(timeout=120)
+            if item is None:
+                raise RuntimeError(f"frame {i} never arrived: {d.ordering_stats()}")
+            idx, view, info = item
+            if idx != i:
+                errors.append(f"order: got {idx} expected {i}")
+            src = d.ring.in_view(info["slot"], view.nbytes)
+            if i % args.verify_every == 0:
+                ok = np.array_equal(view, np.bitwise_not(src))  # sanity check of the sample
+            else:
+                ok = np.array_equal(view[:4096], np.bitwise_not(src[:4096]))
+            if not ok:
+                errors.append(f"frame {i} differs")
+            if i >= warm:
+                total_bytes += view.nbytes
+            release_t[i] = time.perf_counter()
+            d.release_frame(idx)
+        t_end = time.perf_counter()
+        th.join()
+        el = t_end - t_start
+        lat = (release_t[warm:] - commit_t[warm:]) * 1e3
+        st = d.ordering_stats()
+        st["max_depth"] = max(st["max_depth"], d_stats0["max_depth"])
+        result = {"kind": "pipeline", "size": args.size, "workers": args.workers, "gpus": min(ngpu, args.workers),
+                  "inflight_per_worker": args.inflight,
+                  "policy": args.policy, "producer": args.producer, "batch": args.batch, "frames": n,
+                  "ring_slots": slots, "fps": round(n / el, 1), "GBps_each_way": round(total_bytes / el / 1e9, 2),
+                  "latency_ms_mean": round(float(lat.mean()), 3), "latency_ms_p99": round(float(np.percentile(lat, 99)), 3),
+                  "reorder_wait_mean_ms": round(st["reorder_wait_mean_ms"], 3),
+                  "reorder_wait_max_ms": round(st["reorder_wait_max_ms"], 3), "max_buffer_depth": st["max_depth"],
+                  "out_of_order_arrivals": st["out_of_order"], "errors": errors[:5], "n_errors": len(errors)}
+        print(json.dumps(result), flush=True)
+        if args.out:
+            with open(args.out, "a") as f:
+                f.write(json.dumps(result) + "\n")
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.send_signal(signal.SIGTERM)
+        for p in procs:
+            try:
+                p.wait(15)
+            except subprocess.TimeoutExpired:
+                p.kill()
+        d.cleanup()
+    return 0 if result and not result["n_errors"] else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())
