@@ -14,8 +14,8 @@ all: lib oracle
 
 lib: $(LIB)
 
-$(LIB): $(CSRC)/vf_kernels.hip $(CSRC)/vf_api.hip $(CSRC)/vf_internal.h include/vfilter.h
-	$(HIPCC) $(HIPFLAGS) $(LDFLAGS) $(CSRC)/vf_kernels.hip $(CSRC)/vf_api.hip -o $@
+$(LIB): $(CSRC)/vf_kernels.hip $(CSRC)/vf_engine.hip $(CSRC)/vf_api.hip $(CSRC)/vf_internal.h include/vfilter.h
+	$(HIPCC) $(HIPFLAGS) $(LDFLAGS) -pthread $(CSRC)/vf_kernels.hip $(CSRC)/vf_engine.hip $(CSRC)/vf_api.hip -o $@
 
 oracle:
 	$(MAKE) -C oracle

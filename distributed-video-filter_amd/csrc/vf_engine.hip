@@ -1,0 +1,452 @@
+// vf_engine.hip — the host->host pipeline engine of a vf_ctx.
+//
+// What it replaces: the reference filters one frame per loop iteration, synchronously, in
+// the worker process (worker.py:35-57 -> inverter.py:41).  Here every host->host request
+// (one frame, a packed batch, a gather list of frames; synchronous or asynchronous) becomes
+// a JOB queued to one engine thread per context, which streams the jobs' bytes through a
+// ring of device slots without draining between jobs:
+//
+//   fill    slot i: (pageable: copy the chunk into the slot's pinned staging buffer)
+//           H2D -> invert kernel on the IN stream, event k1
+//   d2h     once k1 has fired: D2H on the OUT stream, event done
+//   retire  once done has fired: (pageable: scatter the staged result) -> slot free
+//
+// The engine reacts to event completion on the host instead of chaining the two streams
+// with hipStreamWaitEvent.  Measured on MI355X (tools/pcie_probe.hip): device-side
+// cross-stream waits enqueued while earlier batches are still executing drop the pipeline
+// from 45 to 26 GB/s per direction; the host-driven form holds 45-46 GB/s with work queued
+// concurrently (profiles/r01_pcie_probe_pipelines.txt).  IN and OUT are separate streams, so
+// the two directions run on separate SDMA engines at once.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+
+#include "vf_internal.h"
+
+namespace vf {
+
+namespace {
+constexpr int kStatusHip = -2;  // VF_E_HIP
+
+size_t env_or(const char *name, size_t dflt) {
+  const char *v = std::getenv(name);
+  if (!v || !*v) return dflt;
+  char *end = nullptr;
+  unsigned long long x = std::strtoull(v, &end, 0);
+  return (end && *end == 0) ? (size_t)x : dflt;
+}
+
+bool fired(hipEvent_t e, hipError_t *err) {
+  hipError_t q = hipEventQuery(e);
+  if (q == hipSuccess) return true;
+  (void)hipGetLastError();  // clear hipErrorNotReady so it cannot leak into a later check
+  if (q != hipErrorNotReady) *err = q;
+  return false;
+}
+}  // namespace
+
+// ---- host copy pool -----------------------------------------------------------------------
+CopyPool::CopyPool(int nthreads) : n_(std::max(1, nthreads)) {
+  for (int i = 1; i < n_; ++i) threads_.emplace_back([this, i] { run(i); });
+}
+
+CopyPool::~CopyPool() {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    stop_ = true;
+    ++gen_;
+  }
+  cv_.notify_all();
+  for (auto &t : threads_) t.join();
+}
+
+void CopyPool::copy(uint8_t *dst, const uint8_t *src, size_t len) {
+  if (len < kSplitMin || n_ == 1) {
+    std::memcpy(dst, src, len);
+    return;
+  }
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    dst_ = dst;
+    src_ = src;
+    len_ = len;
+    pending_ = n_ - 1;
+    ++gen_;
+  }
+  cv_.notify_all();
+  part(0);
+  std::unique_lock<std::mutex> lk(mu_);
+  done_cv_.wait(lk, [this] { return pending_ == 0; });
+}
+
+void CopyPool::part(int i) {
+  size_t per = (len_ / n_ + 63) & ~size_t(63);
+  size_t b = std::min(len_, per * (size_t)i);
+  size_t e = (i == n_ - 1) ? len_ : std::min(len_, b + per);
+  if (e > b) std::memcpy(dst_ + b, src_ + b, e - b);
+}
+
+void CopyPool::run(int i) {
+  uint64_t seen = 0;
+  for (;;) {
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      cv_.wait(lk, [&] { return gen_ != seen; });
+      seen = gen_;
+      if (stop_) return;
+    }
+    part(i);
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      if (--pending_ == 0) done_cv_.notify_one();
+    }
+  }
+}
+
+// ---- engine: construction --------------------------------------------------------------------
+
+Engine::~Engine() {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    stop_ = true;
+  }
+  cv_.notify_all();
+  if (thread_.joinable()) thread_.join();
+  (void)hipSetDevice(device_);
+  if (s_in_) (void)hipStreamSynchronize(s_in_);
+  if (s_out_) (void)hipStreamSynchronize(s_out_);
+  for (auto &s : slots_) {
+    for (hipEvent_t e : {s.h0, s.k0, s.k1, s.done})
+      if (e) (void)hipEventDestroy(e);
+    if (s.pin_in) (void)hipHostFree(s.pin_in);
+    if (s.pin_out) (void)hipHostFree(s.pin_out);
+    if (s.d_in) (void)hipFree(s.d_in);
+    if (s.d_out) (void)hipFree(s.d_out);
+  }
+  for (hipEvent_t e : free_events_) (void)hipEventDestroy(e);
+  if (s_in_) (void)hipStreamDestroy(s_in_);
+  if (s_out_) (void)hipStreamDestroy(s_out_);
+}
+
+hipError_t Engine::init(int device, int nslots, size_t slot_bytes, const LaunchCfg &cfg,
+                        std::string *err) {
+  device_ = device;
+  cfg_ = cfg;
+  slot_bytes_ = slot_bytes;
+  pool_.reset(new CopyPool((int)env_or("VF_HOST_THREADS", 8)));
+  hipError_t e = hipSetDevice(device);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&s_in_, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&s_out_, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    *err = std::string("stream creation failed: ") + hipGetErrorString(e);
+    return e;
+  }
+  slots_.resize((size_t)nslots);
+  for (auto &s : slots_) {
+    if ((e = hipEventCreate(&s.h0)) != hipSuccess || (e = hipEventCreate(&s.k0)) != hipSuccess ||
+        (e = hipEventCreate(&s.k1)) != hipSuccess || (e = hipEventCreate(&s.done)) != hipSuccess) {
+      *err = std::string("event creation failed: ") + hipGetErrorString(e);
+      return e;
+    }
+    if ((e = hipHostMalloc((void **)&s.pin_in, slot_bytes, hipHostMallocDefault)) != hipSuccess ||
+        (e = hipHostMalloc((void **)&s.pin_out, slot_bytes, hipHostMallocDefault)) != hipSuccess ||
+        (e = hipMalloc((void **)&s.d_in, slot_bytes)) != hipSuccess ||
+        (e = hipMalloc((void **)&s.d_out, slot_bytes)) != hipSuccess) {
+      char buf[160];
+      std::snprintf(buf, sizeof buf, "slot allocation of %zu bytes failed: %s", slot_bytes,
+                    hipGetErrorString(e));
+      *err = buf;
+      return e;
+    }
+  }
+  thread_ = std::thread([this] { run(); });
+  return hipSuccess;
+}
+
+// ---- page-locked range registry (so `direct` needs no runtime query per frame) ----------------
+
+void Engine::note_pinned(const void *p, size_t n) {
+  std::lock_guard<std::mutex> lk(pin_mu_);
+  pinned_.emplace_back((uintptr_t)p, n);
+}
+
+void Engine::forget_pinned(const void *p) {
+  std::lock_guard<std::mutex> lk(pin_mu_);
+  pinned_.erase(std::remove_if(pinned_.begin(), pinned_.end(),
+                               [p](const std::pair<uintptr_t, size_t> &r) { return r.first == (uintptr_t)p; }),
+                pinned_.end());
+}
+
+bool Engine::is_pinned(const void *p, size_t len) {
+  {
+    std::lock_guard<std::mutex> lk(pin_mu_);
+    const uintptr_t a = (uintptr_t)p;
+    for (const auto &r : pinned_)
+      if (a >= r.first && a + len <= r.first + r.second) return true;
+  }
+  hipPointerAttribute_t attr;
+  std::memset(&attr, 0, sizeof attr);
+  if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+    (void)hipGetLastError();  // pageable pointers report an error on some runtimes
+    return false;
+  }
+  return attr.type == hipMemoryTypeHost;
+}
+
+// ---- engine: caller side ---------------------------------------------------------------------
+
+uint64_t Engine::submit(std::vector<Seg> &&segs) {
+  auto job = std::make_unique<Job>();
+  for (const Seg &s : segs) {
+    job->total += s.len;
+    if (job->direct && s.len && !(is_pinned(s.src, s.len) && is_pinned(s.dst, s.len))) job->direct = false;
+  }
+  // Chunk size: the slot size for big jobs; small jobs still get >= 2 chunks per slot so the
+  // ring fills (480p x 32 = 29 MB in 16 MiB chunks is only 2 chunks).
+  const size_t kMinChunk = (size_t)1 << 20;
+  size_t chunk = (job->total / (2 * slots_.size()) + 65535) & ~(size_t)65535;
+  job->chunk = std::min(slot_bytes_, std::max(kMinChunk, chunk));
+  job->segs = std::move(segs);
+  std::lock_guard<std::mutex> lk(mu_);
+  const uint64_t id = next_id_++;
+  job->id = id;
+  if (broken_ || job->total == 0) {
+    JobResult r;
+    if (broken_) {
+      r.status = kStatusHip;
+      r.msg = "the context's pipeline failed earlier; destroy and recreate the context";
+    }
+    results_[id] = std::move(r);
+    done_cv_.notify_all();
+    return id;
+  }
+  unfinished_.insert(id);
+  pending_.push_back(std::move(job));
+  cv_.notify_all();
+  return id;
+}
+
+bool Engine::wait(uint64_t id, JobResult *out) {
+  std::unique_lock<std::mutex> lk(mu_);
+  if (id == 0 || id >= next_id_) return false;
+  done_cv_.wait(lk, [&] { return unfinished_.count(id) == 0; });
+  auto it = results_.find(id);
+  if (it != results_.end()) {
+    if (out) *out = std::move(it->second);
+    results_.erase(it);
+  } else if (out) {
+    *out = JobResult();  // collected before, or trimmed after kMaxResults newer jobs
+  }
+  return true;
+}
+
+bool Engine::query(uint64_t id, bool *done) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (id == 0 || id >= next_id_) return false;
+  *done = unfinished_.count(id) == 0;
+  return true;
+}
+
+void Engine::drain() {
+  std::unique_lock<std::mutex> lk(mu_);
+  done_cv_.wait(lk, [&] { return unfinished_.empty(); });
+}
+
+// ---- engine thread -----------------------------------------------------------------------
+
+void Engine::fail_all(hipError_t e, const char *what) {
+  char buf[256];
+  std::snprintf(buf, sizeof buf, "%s failed: %s (%s)", what, hipGetErrorString(e), hipGetErrorName(e));
+  std::lock_guard<std::mutex> lk(mu_);
+  broken_ = true;
+  for (uint64_t id : unfinished_) {
+    JobResult r;
+    r.status = kStatusHip;
+    r.hip = e;
+    r.msg = buf;
+    results_[id] = std::move(r);
+  }
+  unfinished_.clear();
+  for (auto &s : slots_) {
+    s.state = Slot::kFree;
+    s.job = nullptr;
+  }
+  pending_.clear();
+  live_.clear();
+  done_cv_.notify_all();
+}
+
+bool Engine::step_fill() {
+  Slot &s = slots_[fill_];
+  if (s.state != Slot::kFree) return false;
+  Job *job = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (pending_.empty()) return false;
+    job = pending_.front().get();
+  }
+  hipError_t e = hipSuccess;
+  if (!job->started) {
+    job->start = take_event();
+    if (!job->start) {
+      fail_all(hipErrorOutOfMemory, "hipEventCreate");
+      return true;
+    }
+    e = hipEventRecord(job->start, s_in_);
+    job->started = true;
+  }
+  s.pieces.clear();
+  size_t filled = 0;
+  while (job->seg < job->segs.size() && filled < job->chunk) {
+    const Seg &g = job->segs[job->seg];
+    const size_t take = std::min(g.len - job->seg_off, job->chunk - filled);
+    if (take) {
+      if (!job->direct) pool_->copy(s.pin_in + filled, g.src + job->seg_off, take);
+      s.pieces.push_back(Piece{g.src + job->seg_off, g.dst + job->seg_off, filled, take});
+      filled += take;
+      job->seg_off += take;
+    }
+    if (job->seg_off == g.len) {
+      ++job->seg;
+      job->seg_off = 0;
+    }
+  }
+  if (e == hipSuccess) e = hipEventRecord(s.h0, s_in_);
+  if (job->direct) {
+    for (size_t i = 0; i < s.pieces.size() && e == hipSuccess; ++i)
+      e = hipMemcpyAsync(s.d_in + s.pieces[i].off, s.pieces[i].src, s.pieces[i].len,
+                         hipMemcpyHostToDevice, s_in_);
+  } else if (e == hipSuccess) {
+    e = hipMemcpyAsync(s.d_in, s.pin_in, filled, hipMemcpyHostToDevice, s_in_);
+  }
+  if (e == hipSuccess) e = hipEventRecord(s.k0, s_in_);
+  if (e == hipSuccess) e = launch_invert(s.d_in, s.d_out, filled, cfg_, s_in_);
+  if (e == hipSuccess) e = hipEventRecord(s.k1, s_in_);
+  if (e != hipSuccess) {
+    fail_all(e, "chunk submit");
+    return true;
+  }
+  s.job = job;
+  s.bytes = filled;
+  s.state = Slot::kIn;
+  ++job->chunks_submitted;
+  fill_ = (fill_ + 1) % slots_.size();
+  if (job->seg >= job->segs.size()) {  // every byte of the job is in a slot
+    std::lock_guard<std::mutex> lk(mu_);
+    job->all_submitted = true;
+    live_.push_back(std::move(pending_.front()));
+    pending_.pop_front();
+  }
+  return true;
+}
+
+bool Engine::step_d2h() {
+  Slot &s = slots_[d2h_];
+  if (s.state != Slot::kIn) return false;
+  hipError_t err = hipSuccess;
+  if (!fired(s.k1, &err)) {
+    if (err != hipSuccess) fail_all(err, "hipEventQuery");
+    return err != hipSuccess;
+  }
+  hipError_t e = hipSuccess;
+  if (s.job->direct) {
+    for (size_t i = 0; i < s.pieces.size() && e == hipSuccess; ++i)
+      e = hipMemcpyAsync(s.pieces[i].dst, s.d_out + s.pieces[i].off, s.pieces[i].len,
+                         hipMemcpyDeviceToHost, s_out_);
+  } else {
+    e = hipMemcpyAsync(s.pin_out, s.d_out, s.bytes, hipMemcpyDeviceToHost, s_out_);
+  }
+  if (e == hipSuccess) e = hipEventRecord(s.done, s_out_);
+  if (e != hipSuccess) {
+    fail_all(e, "D2H submit");
+    return true;
+  }
+  s.state = Slot::kOut;
+  d2h_ = (d2h_ + 1) % slots_.size();
+  return true;
+}
+
+bool Engine::step_retire() {
+  Slot &s = slots_[retire_];
+  if (s.state != Slot::kOut) return false;
+  hipError_t err = hipSuccess;
+  if (!fired(s.done, &err)) {
+    if (err != hipSuccess) fail_all(err, "hipEventQuery");
+    return err != hipSuccess;
+  }
+  Job *job = s.job;
+  if (!job->direct)
+    for (const Piece &p : s.pieces) pool_->copy(p.dst, s.pin_out + p.off, p.len);
+  float ms = 0.f;
+  if (hipEventElapsedTime(&ms, s.k0, s.k1) == hipSuccess) job->kernel_ms += ms;
+  ChunkTime ct{s.bytes, -1.f, -1.f, -1.f, -1.f};
+  hipEvent_t evs[4] = {s.h0, s.k0, s.k1, s.done};
+  float *at[4] = {&ct.h2d_start, &ct.kernel_start, &ct.kernel_end, &ct.d2h_end};
+  for (int i = 0; i < 4; ++i)
+    if (hipEventElapsedTime(at[i], job->start, evs[i]) != hipSuccess) *at[i] = -1.f;
+  job->timeline.push_back(ct);
+  ++job->chunks_done;
+  s.state = Slot::kFree;
+  s.job = nullptr;
+  retire_ = (retire_ + 1) % slots_.size();
+  if (job->all_submitted && job->chunks_done == job->chunks_submitted) {
+    JobResult r;
+    r.kernel_ms = job->kernel_ms;
+    r.gpu_ms = job->timeline.back().d2h_end;
+    r.timeline = std::move(job->timeline);
+    give_event(job->start);
+    std::lock_guard<std::mutex> lk(mu_);
+    results_[job->id] = std::move(r);
+    while (results_.size() > kMaxResults) results_.erase(results_.begin());
+    unfinished_.erase(job->id);
+    for (auto it = live_.begin(); it != live_.end(); ++it)
+      if (it->get() == job) {
+        live_.erase(it);
+        break;
+      }
+    done_cv_.notify_all();
+  }
+  return true;
+}
+
+hipEvent_t Engine::take_event() {
+  if (!free_events_.empty()) {
+    hipEvent_t e = free_events_.back();
+    free_events_.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  return hipEventCreate(&e) == hipSuccess ? e : nullptr;
+}
+
+void Engine::give_event(hipEvent_t e) {
+  if (e) free_events_.push_back(e);
+}
+
+int Engine::busy_slots() const {
+  int n = 0;
+  for (const auto &s : slots_) n += s.state != Slot::kFree;
+  return n;
+}
+
+void Engine::run() {
+  (void)hipSetDevice(device_);
+  for (;;) {
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      cv_.wait(lk, [&] { return stop_ || !pending_.empty() || busy_slots() > 0; });
+      if (stop_ && pending_.empty() && busy_slots() == 0) return;
+    }
+    bool progress = false;
+    // retire first (frees a slot), then start the D2H of finished kernels, then refill
+    while (step_retire()) progress = true;
+    while (step_d2h()) progress = true;
+    while (step_fill()) progress = true;
+    if (!progress) std::this_thread::yield();
+  }
+}
+
+}  // namespace vf

@@ -1,7 +1,19 @@
-// vf_internal.h — shared between the kernel TU and the C-ABI TU (not installed).
+// vf_internal.h — shared between the kernel, engine and C-ABI translation units (not installed).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stddef.h>
+#include <stdint.h>
+
+#include <condition_variable>
+#include <deque>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <set>
+#include <string>
+#include <thread>
+#include <utility>
+#include <vector>
 
 namespace vf {
 
@@ -38,5 +50,132 @@ hipError_t launch_invert(const void *dsrc, void *ddst, size_t nbytes, const Laun
 hipError_t launch_invert_frames(const void *const *dsrcs, void *const *ddsts,
                                 const size_t *nbytes, int n, size_t total_bytes,
                                 const LaunchCfg &cfg, hipStream_t stream);
+
+// ---- host -> host pipeline (vf_engine.hip) --------------------------------------------------
+
+// memcpy of large staging chunks split over a few persistent threads: one core moves
+// ~10 GB/s, well under one PCIe Gen5 x16 direction (1080p x 32 pageable: 30.5 GB/s each way
+// with 4 threads, 40.5 with 8; pinned, i.e. no staging: 42.9).
+class CopyPool {
+ public:
+  explicit CopyPool(int nthreads);
+  ~CopyPool();
+  void copy(uint8_t *dst, const uint8_t *src, size_t len);
+
+ private:
+  static constexpr size_t kSplitMin = 1 << 20;
+  void part(int i);
+  void run(int i);
+  int n_;
+  std::vector<std::thread> threads_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_cv_;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+  int pending_ = 0;
+  uint8_t *dst_ = nullptr;
+  const uint8_t *src_ = nullptr;
+  size_t len_ = 0;
+};
+
+// A contiguous run of a job's byte stream: src[0..len) -> dst[0..len).
+struct Seg {
+  const uint8_t *src;
+  uint8_t *dst;
+  size_t len;
+};
+
+// One chunk's GPU timeline, ms after its job's start event.
+struct ChunkTime {
+  size_t bytes;
+  float h2d_start, kernel_start, kernel_end, d2h_end;
+};
+
+struct JobResult {
+  int status = 0;  // VF_OK or a VF_E_* code
+  hipError_t hip = hipSuccess;
+  std::string msg;
+  float kernel_ms = 0.f;  // sum of the job's kernel durations
+  float gpu_ms = -1.f;    // job start -> last D2H done
+  std::vector<ChunkTime> timeline;
+};
+
+class Engine {
+ public:
+  Engine() = default;
+  ~Engine();  // finishes queued jobs, joins the thread, frees the slots
+  hipError_t init(int device, int nslots, size_t slot_bytes, const LaunchCfg &cfg, std::string *err);
+
+  uint64_t submit(std::vector<Seg> &&segs);  // returns the job id (> 0); never blocks on the GPU
+  bool wait(uint64_t id, JobResult *out);    // false: unknown id
+  bool query(uint64_t id, bool *done);       // false: unknown id
+  void drain();                              // wait for every submitted job
+
+  void note_pinned(const void *p, size_t n);
+  void forget_pinned(const void *p);
+  bool is_pinned(const void *p, size_t len);
+
+ private:
+  struct Piece {
+    const uint8_t *src;
+    uint8_t *dst;
+    size_t off;  // offset in the slot
+    size_t len;
+  };
+  struct Job {
+    uint64_t id = 0;
+    std::vector<Seg> segs;
+    bool direct = true;  // every byte page-locked: DMA straight from/to the caller
+    size_t total = 0, chunk = 0;
+    size_t seg = 0, seg_off = 0;  // fill cursor
+    int chunks_submitted = 0, chunks_done = 0;
+    bool started = false, all_submitted = false;
+    hipEvent_t start = nullptr;
+    float kernel_ms = 0.f;
+    std::vector<ChunkTime> timeline;
+  };
+  struct Slot {
+    enum State { kFree, kIn, kOut } state = kFree;
+    hipEvent_t h0 = nullptr, k0 = nullptr, k1 = nullptr, done = nullptr;
+    uint8_t *pin_in = nullptr, *pin_out = nullptr;
+    uint8_t *d_in = nullptr, *d_out = nullptr;
+    Job *job = nullptr;
+    size_t bytes = 0;
+    std::vector<Piece> pieces;
+  };
+  static constexpr size_t kMaxResults = 1024;
+
+  void run();
+  bool step_fill();
+  bool step_d2h();
+  bool step_retire();
+  void fail_all(hipError_t e, const char *what);
+  int busy_slots() const;
+  hipEvent_t take_event();
+  void give_event(hipEvent_t e);
+
+  int device_ = 0;
+  LaunchCfg cfg_;
+  size_t slot_bytes_ = 0;
+  hipStream_t s_in_ = nullptr, s_out_ = nullptr;
+  std::vector<Slot> slots_;
+  size_t fill_ = 0, d2h_ = 0, retire_ = 0;
+  std::unique_ptr<CopyPool> pool_;
+  std::vector<hipEvent_t> free_events_;
+
+  std::mutex mu_;  // guards everything below
+  std::condition_variable cv_, done_cv_;
+  bool stop_ = false;
+  bool broken_ = false;
+  uint64_t next_id_ = 1;
+  std::deque<std::unique_ptr<Job>> pending_;  // jobs with bytes not yet in a slot
+  std::vector<std::unique_ptr<Job>> live_;    // fully queued, not yet retired
+  std::set<uint64_t> unfinished_;
+  std::map<uint64_t, JobResult> results_;     // finished, not yet collected by wait()
+
+  std::mutex pin_mu_;
+  std::vector<std::pair<uintptr_t, size_t>> pinned_;
+  std::thread thread_;
+};
 
 }  // namespace vf

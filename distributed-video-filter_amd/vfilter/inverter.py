@@ -96,31 +96,37 @@ class InverterWorker(Worker):
         self.last_spans = gpu_spans(self.ctx.last_timeline(), t_call)
         return results
 
-    # -- ring batches: asynchronous submission -------------------------------------------
+    # -- asynchronous submission ---------------------------------------------------------
     def submit_batch(self, frames: Sequence, metas: Sequence[wire.FrameMeta], outs: Sequence):
-        """Frames in the page-locked ring go through vf_invert_frames_async: the whole batch
-        is queued on the device and the worker loop goes back to receiving at once."""
-        if self.jpeg or self.delay > 0 or not self._registered or any(o is None for o in outs):
+        """Queue the batch with vf_invert_frames_async and return to receiving at once: the
+        context's engine thread streams consecutive batches through the GPU back to back.
+        Ring frames (page-locked) are DMA'd in place; socket payloads are staged."""
+        if self.jpeg or self.delay > 0:
             return super().submit_batch(frames, metas, outs)
+        srcs, dsts = [], []
+        for f, o in zip(frames, outs):
+            src = f if isinstance(f, np.ndarray) else np.frombuffer(f, dtype=np.uint8)
+            srcs.append(src)
+            dsts.append(o if o is not None else np.empty(src.nbytes, np.uint8))
         try:
-            ticket = self.ctx.invert_frames_async(frames, outs, [f.nbytes for f in frames])
-        except Exception:
-            return super().submit_batch(frames, metas, outs)  # e.g. ring not page-locked
-        return ("gpu", ticket, list(outs), sum(f.nbytes for f in frames))
+            ticket = self.ctx.invert_frames_async(srcs, dsts, [s.nbytes for s in srcs])
+        except Exception as e:
+            return ("done", [e] * len(frames), [])
+        return ("gpu", ticket, srcs, dsts)  # srcs kept alive until the ticket completes
 
     def poll_batch(self, handle, block: bool):
         if handle[0] != "gpu":
             return super().poll_batch(handle, block)
-        _, ticket, outs, nbytes = handle
+        _, ticket, _srcs, dsts = handle
         if not block and not self.ctx.query(ticket):
             return None
         try:
             ms = self.ctx.wait(ticket)
         except Exception as e:
-            return [e] * len(outs), []
+            return [e] * len(dsts), []
         t_end = time.time()
-        spans = [{"name": "batch", "begin": t_end - ms / 1e3, "end": t_end, "bytes": nbytes}] if ms >= 0 else []
-        return outs, spans
+        spans = gpu_spans(self.ctx.last_timeline(), t_end - ms / 1e3) if ms >= 0 else []
+        return dsts, spans
 
     def on_ring_attached(self, ring) -> None:
         """Page-lock the whole shared-memory ring once: the slot pipeline then DMAs straight

@@ -102,19 +102,21 @@ int vf_invert_batch_host(vf_ctx *ctx, const uint8_t *src, uint8_t *dst,
 int vf_invert_frames_host(vf_ctx *ctx, const uint8_t *const *srcs, uint8_t *const *dsts,
                           const size_t *nbytes, int n);
 
-/* ---- host -> host, asynchronous (page-locked memory only) ---------------------------- */
+/* ---- host -> host, asynchronous ------------------------------------------------------ */
 
-/* Enqueue the filter for `n` frames (srcs[i] -> dsts[i], nbytes[i] each) whose buffers are
- * all page-locked (vf_alloc_host, or vf_host_register such as a worker's shared-memory frame
- * ring) and return at once with a ticket (> 0).  H2D, kernel and D2H of the whole batch are
- * queued on the device; slot reuse is ordered on the device, so the host never blocks and a
- * worker can receive and enqueue its next batch meanwhile (the asynchronous form of
- * vf_invert_frames_host / worker.py:57).  Pageable buffers: VF_E_INVALID. */
+/* Queue the filter for `n` frames (srcs[i] -> dsts[i], nbytes[i] each) and return at once
+ * with a ticket (> 0); the asynchronous form of vf_invert_frames_host (worker.py:57).  The
+ * context's engine thread streams queued batches through its slot ring back to back, so a
+ * worker can receive its next batch while this one moves.  The caller keeps every buffer
+ * alive and untouched until vf_wait(ticket) returns.  Page-locked buffers (vf_alloc_host,
+ * vf_host_register, e.g. a shared-memory frame ring) are DMA'd directly; pageable ones are
+ * staged by the engine. */
 int vf_invert_frames_async(vf_ctx *ctx, const uint8_t *const *srcs, uint8_t *const *dsts,
                            const size_t *nbytes, int n, uint64_t *ticket);
 
-/* Block until submission `ticket` has completed (its D2H landed).  *gpu_ms (may be NULL)
- * gets its device time from first H2D to last D2H, or -1 if no longer available. */
+/* Block until submission `ticket` has completed (its last D2H landed) and return its status.
+ * *gpu_ms (may be NULL) gets its device time from first H2D to last D2H (-1 if unknown).
+ * Also sets what vf_elapsed_ms / vf_last_timeline report. */
 int vf_wait(vf_ctx *ctx, uint64_t ticket, float *gpu_ms);
 
 /* *done = 1 if submission `ticket` has completed, else 0 (never blocks). */

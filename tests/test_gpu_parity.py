@@ -255,9 +255,18 @@ def test_async_frames_on_pinned_memory(vf_ctx):
             vf_ctx.wait(t)
         for b in range(nb):
             assert np.array_equal(hd[b], oracle.invert(hs[b])), b
-        x = np.zeros(1000, np.uint8)
-        with pytest.raises(vfilter.VFilterError, match="page-locked"):
-            vf_ctx.invert_frames_async([x], [np.empty_like(x)], [1000])
+        # pageable buffers go through the engine's staging copies, queued behind pinned jobs
+        xs = [oracle.synthetic_frame(60 + i, 480, 640) for i in range(3)]
+        ys = [np.empty_like(x) for x in xs]
+        t_pin = vf_ctx.invert_frames_async([ps[0]], [pd[0]], [sizes[0]])
+        t_pg = vf_ctx.invert_frames_async(xs, ys, [x.nbytes for x in xs])
+        vf_ctx.wait(t_pg)
+        assert vf_ctx.query(t_pin)  # jobs complete in submission order
+        vf_ctx.wait(t_pin)
+        for x, y_ in zip(xs, ys):
+            assert np.array_equal(y_, oracle.invert(x))
+        with pytest.raises(vfilter.VFilterError, match="unknown ticket"):
+            vf_ctx.wait(10 ** 9)
         y = oracle.synthetic_frame(77, 480, 640)  # sync path after async work
         assert np.array_equal(vfilter.bitwise_not(y, ctx=vf_ctx), oracle.invert(y))
     finally:

@@ -1,7 +1,6 @@
-mkdir -p gpurun_out; : > gpurun_out/async2.txt
-P="timeout -k 10 120 python -u tools/async_probe.py --batches 48"
-$P --ring 1 >> gpurun_out/async2.txt 2>&1 || exit 1
-VF_SLOTS=8 $P --ring 8 >> gpurun_out/async2.txt 2>&1 || exit 1
-VF_SLOT_BYTES=67108864 $P --ring 8 >> gpurun_out/async2.txt 2>&1 || exit 1
-VF_SLOTS=8 VF_SLOT_BYTES=33554432 $P --ring 8 >> gpurun_out/async2.txt 2>&1 || exit 1
-cat gpurun_out/async2.txt
+mkdir -p gpurun_out; : > gpurun_out/async4.txt
+timeout -k 10 150 ./tools/pcie_probe 1073741824 16777216 > gpurun_out/pcie4.txt 2>&1 || exit 1
+tail -6 gpurun_out/pcie4.txt
+timeout -k 10 120 python -u tools/async_probe.py >> gpurun_out/async4.txt 2>&1 || exit 1
+VF_WAIT_POLL=1 timeout -k 10 120 python -u tools/async_probe.py >> gpurun_out/async4.txt 2>&1 || exit 1
+cat gpurun_out/async4.txt
