@@ -1,4 +1,4 @@
-# distributor-level pipeline runs (configs[2]/[3]) on the 1-GPU box
+# distributor-level pipeline runs (configs[2]/[3]) on the 1-GPU box, + host->host sweep
 set -o pipefail
 mkdir -p gpurun_out
 rm -f gpurun_out/pipeline.jsonl gpurun_out/pipeline.log
@@ -12,3 +12,4 @@ run --workers 2 --size mixed --frames 1536 --batch 16 --policy pull
 run --workers 1 --size 480p --frames 4096 --batch 32
 run --workers 1 --size 1080p --frames 2048 --batch 16 --producer copy
 cat gpurun_out/pipeline.jsonl
+timeout -k 10 200 python -u tools/sweep.py --e2e-only --out gpurun_out/e2e_engine.jsonl > gpurun_out/e2e_engine.log 2>&1 && cat gpurun_out/e2e_engine.jsonl
