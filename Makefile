@@ -14,8 +14,11 @@ all: lib oracle
 
 lib: $(LIB)
 
-$(LIB): $(CSRC)/vf_kernels.hip $(CSRC)/vf_engine.hip $(CSRC)/vf_api.hip $(CSRC)/vf_internal.h include/vfilter.h
-	$(HIPCC) $(HIPFLAGS) $(LDFLAGS) -pthread $(CSRC)/vf_kernels.hip $(CSRC)/vf_engine.hip $(CSRC)/vf_api.hip -o $@
+SRCS := $(CSRC)/vf_kernels.hip $(CSRC)/vf_engine.hip $(CSRC)/vf_api.hip $(CSRC)/vf_jpeg_kernels.hip $(CSRC)/vf_jpeg_host.hip
+HDRS := $(CSRC)/vf_internal.h $(CSRC)/vf_jpeg.h $(CSRC)/vf_jpeg_codec.h include/vfilter.h
+
+$(LIB): $(SRCS) $(HDRS)
+	$(HIPCC) $(HIPFLAGS) $(LDFLAGS) -pthread $(SRCS) -o $@
 
 oracle:
 	$(MAKE) -C oracle

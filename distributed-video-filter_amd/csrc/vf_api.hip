@@ -25,6 +25,7 @@
 
 #include "../../include/vfilter.h"
 #include "vf_internal.h"
+#include "vf_jpeg_codec.h"
 
 #define VF_EXPORT extern "C" __attribute__((visibility("default")))
 
@@ -58,6 +59,7 @@ struct vf_ctx {
   // results of the last host->host job waited on (vf_elapsed_ms / vf_last_timeline)
   float last_kernel_ms = 0.f;
   std::vector<vf::ChunkTime> timeline;
+  vf::jpeg::Codec *jpeg = nullptr;  // created on first JPEG call
 };
 
 namespace {
@@ -149,6 +151,7 @@ VF_EXPORT const char *vf_status_string(int status) {
     case VF_E_HIP: return "VF_E_HIP: HIP runtime error";
     case VF_E_NOMEM: return "VF_E_NOMEM: out of memory";
     case VF_E_NODEVICE: return "VF_E_NODEVICE: no usable gfx950 device";
+    case VF_E_JPEG: return "VF_E_JPEG: malformed or unsupported JPEG";
     default: return "unknown vfilter status";
   }
 }
@@ -211,6 +214,7 @@ VF_EXPORT int vf_create(int device, size_t max_frame_bytes, int max_batch, vf_ct
 
 VF_EXPORT int vf_destroy(vf_ctx *ctx) {
   if (!ctx) return VF_OK;
+  delete ctx->jpeg;
   delete ctx->engine;  // finishes queued jobs first
   delete ctx;
   return VF_OK;
@@ -483,4 +487,93 @@ VF_EXPORT int vf_bench_device_ring(vf_ctx *ctx, void *const *srcs, void *const *
   for (auto &e : ev)
     if (e) (void)hipEventDestroy(e);
   return rc;
+}
+
+// ---- JPEG (inverter.py:32 / :41 / :44 in the default use_jpeg=True mode) --------------------
+
+namespace {
+
+int jpeg_codec(vf_ctx *ctx, vf::jpeg::Codec **out) {
+  if (!ctx->jpeg) {
+    ctx->jpeg = new (std::nothrow) vf::jpeg::Codec(ctx->device);
+    if (!ctx->jpeg) return set_err(ctx, VF_E_NOMEM, 0, "JPEG codec: out of host memory");
+  }
+  *out = ctx->jpeg;
+  return VF_OK;
+}
+
+int jpeg_status(vf_ctx *ctx, int rc, const std::string &msg) {
+  if (rc == VF_OK) return VF_OK;
+  return set_err(ctx, rc, 0, "%s", msg.c_str());
+}
+
+}  // namespace
+
+VF_EXPORT int vf_jpeg_header(const uint8_t *jpeg, size_t size, int *width, int *height, int *subsamp,
+                             int *colorspace) {
+  if (!width || !height || !subsamp || !colorspace)
+    return set_err(nullptr, VF_E_INVALID, 0, "vf_jpeg_header: NULL output pointer");
+  std::string err;
+  const int rc = vf::jpeg::header_info(jpeg, size, width, height, subsamp, colorspace, &err);
+  return rc == VF_OK ? VF_OK : set_err(nullptr, rc, 0, "vf_jpeg_header: %s", err.c_str());
+}
+
+VF_EXPORT size_t vf_jpeg_buffer_size(int width, int height, int subsamp) {
+  return vf::jpeg::buffer_size(width, height, subsamp);
+}
+
+VF_EXPORT int vf_jpeg_encode(vf_ctx *ctx, const uint8_t *const *imgs, const int *widths, const int *heights, int n,
+                             int pixel_format, int quality, int subsamp, int flags, uint8_t *const *outs,
+                             const size_t *caps, size_t *sizes) {
+  VF_CHECK_CTX(ctx);
+  if (n < 0 || (n > 0 && (!imgs || !widths || !heights || !outs || !caps || !sizes)))
+    return set_err(ctx, VF_E_INVALID, 0, "vf_jpeg_encode: bad arguments");
+  if (n > 65535) return set_err(ctx, VF_E_INVALID, 0, "vf_jpeg_encode: at most 65535 frames per call");
+  vf::jpeg::Codec *c = nullptr;
+  int rc = jpeg_codec(ctx, &c);
+  if (rc) return rc;
+  std::string err;
+  rc = c->encode(imgs, widths, heights, n, pixel_format, quality, subsamp, flags, outs, caps, sizes, &err);
+  return jpeg_status(ctx, rc, "vf_jpeg_encode: " + err);
+}
+
+VF_EXPORT int vf_jpeg_decode(vf_ctx *ctx, const uint8_t *const *jpegs, const size_t *jpeg_sizes, int n,
+                             int pixel_format, int flags, uint8_t *const *outs, const size_t *caps) {
+  VF_CHECK_CTX(ctx);
+  if (n < 0 || (n > 0 && (!jpegs || !jpeg_sizes || !outs || !caps)))
+    return set_err(ctx, VF_E_INVALID, 0, "vf_jpeg_decode: bad arguments");
+  if (n > 65535) return set_err(ctx, VF_E_INVALID, 0, "vf_jpeg_decode: at most 65535 frames per call");
+  vf::jpeg::Codec *c = nullptr;
+  int rc = jpeg_codec(ctx, &c);
+  if (rc) return rc;
+  std::string err;
+  rc = c->decode(jpegs, jpeg_sizes, n, pixel_format, flags, outs, caps, &err);
+  return jpeg_status(ctx, rc, "vf_jpeg_decode: " + err);
+}
+
+VF_EXPORT int vf_jpeg_invert(vf_ctx *ctx, const uint8_t *const *jpegs, const size_t *jpeg_sizes, int n, int quality,
+                             int subsamp, int flags, uint8_t *const *outs, const size_t *caps, size_t *sizes) {
+  VF_CHECK_CTX(ctx);
+  if (n < 0 || (n > 0 && (!jpegs || !jpeg_sizes || !outs || !caps || !sizes)))
+    return set_err(ctx, VF_E_INVALID, 0, "vf_jpeg_invert: bad arguments");
+  if (n > 65535) return set_err(ctx, VF_E_INVALID, 0, "vf_jpeg_invert: at most 65535 frames per call");
+  vf::jpeg::Codec *c = nullptr;
+  int rc = jpeg_codec(ctx, &c);
+  if (rc) return rc;
+  std::string err;
+  rc = c->invert(jpegs, jpeg_sizes, n, quality, subsamp, flags, outs, caps, sizes, &err);
+  return jpeg_status(ctx, rc, "vf_jpeg_invert: " + err);
+}
+
+VF_EXPORT int vf_jpeg_bench_invert(vf_ctx *ctx, const uint8_t *const *jpegs, const size_t *jpeg_sizes, int n,
+                                   int quality, int subsamp, int flags, int iters, float *ms, float *stage_ms) {
+  VF_CHECK_CTX(ctx);
+  if (n <= 0 || n > 65535 || !jpegs || !jpeg_sizes || !ms || iters <= 0)
+    return set_err(ctx, VF_E_INVALID, 0, "vf_jpeg_bench_invert: bad arguments");
+  vf::jpeg::Codec *c = nullptr;
+  int rc = jpeg_codec(ctx, &c);
+  if (rc) return rc;
+  std::string err;
+  rc = c->bench_invert(jpegs, jpeg_sizes, n, quality, subsamp, flags, iters, ms, stage_ms, &err);
+  return jpeg_status(ctx, rc, "vf_jpeg_bench_invert: " + err);
 }

@@ -1,0 +1,124 @@
+// vf_jpeg.h — shared between the JPEG kernels (vf_jpeg_kernels.hip) and their host side
+// (vf_jpeg_host.hip).  Not installed.
+//
+// The reference's default mode (use_jpeg=True) decodes, inverts and re-encodes every frame
+// with PyTurboJPEG (inverter.py:32 -> :41 -> :44).  These structures describe one batch of
+// frames laid out in HBM for the gfx950 baseline-JPEG codec; see DESIGN.md "JPEG".
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace vf {
+namespace jpeg {
+
+constexpr int kMaxBpm = 10;     // blocks per MCU (T.81 B.2.3)
+constexpr int kSubBits = 1024;  // bits per Huffman-decoding subsequence
+constexpr int kTile = 4096;     // bytes per (un)stuffing tile
+constexpr int kMaxPasses = 64;  // sync-pass flags kept on the device
+constexpr int kLook = 9;        // Huffman lookahead bits
+
+// MCU geometry of one frame (libjpeg jdinput.c / jcmaster.c per-scan setup, restated)
+struct Geom {
+  int32_t w, h, ncomp, bpm;
+  int32_t maxh, maxv, mcux, mcuy, nmcu, nblocks;
+  int32_t hs[3], vs[3];  // sampling factors
+  int32_t mh[3], mv[3];  // blocks of the component per MCU (1x1 in a single-component scan)
+  int32_t wb[3], hb[3];  // width/height_in_blocks (real blocks)
+  int32_t pw[3], ph[3];  // component plane in samples (whole MCUs)
+  int32_t cfirst[3];     // first block-in-MCU of the component
+  int8_t bcomp[kMaxBpm], bxo[kMaxBpm], byo[kMaxBpm];  // block-in-MCU -> component, x/y (blocks)
+  int8_t pad_[2];
+};
+
+bool make_geom(int w, int h, int ncomp, const int *hs, const int *vs, Geom *g);
+
+// Encoder tables: jcdctmgr.c reciprocal divisors, jchuff.c derived code tables
+struct EncTables {
+  uint16_t recip[2][64];  // natural order; [0] luma, [1] chroma
+  uint16_t corr[2][64];
+  int16_t shift[2][64];
+  uint32_t dc[2][16];   // (code << 8) | size by magnitude category
+  uint32_t ac[2][256];  // (code << 8) | size by run/size symbol
+};
+
+// Huffman decoding table: jdhuff.c derived table plus a kLook-bit lookahead
+struct HuffDec {
+  uint16_t fast[1 << kLook];  // (length << 8) | symbol for codes of <= kLook bits, else 0
+  int32_t maxcode[18];
+  int32_t valoff[18];
+  uint8_t vals[256];
+};
+
+struct DecFrame {
+  Geom g;
+  uint16_t q[3][64];       // dequantisation per component, natural order
+  HuffDec dc[3], ac[3];    // per component (kept adjacent: loaded into LDS as one block)
+  uint64_t in_off;         // raw entropy-coded bytes in the batch input buffer (16-aligned)
+  uint32_t in_len;
+  uint32_t ntiles;         // kTile tiles over the raw bytes
+  uint32_t tile0;          // first tile slot
+  uint32_t sub0;           // first subsequence slot
+  uint32_t nsub_max;       // subsequence slots (ceil(in_len * 8 / kSubBits))
+  uint32_t flags;          // bit 0: fancy upsampling allowed
+  uint64_t us_off;         // unstuffed stream in the unstuffed buffer (16-aligned)
+  uint64_t blk0;           // first block in the batch coefficient buffer
+  uint64_t dcbase[3];      // per-component DC sequences in the DC buffer
+  uint64_t plane_off[3];   // component planes in the plane buffer
+  uint64_t out_off;        // interleaved pixels in the pixel buffer
+};
+
+struct EncFrame {
+  Geom g;
+  uint64_t img_off;     // interleaved input pixels in the pixel buffer
+  uint64_t blk0;        // first block in the batch coefficient buffer
+  uint64_t bits_off;    // packed bitstream (bytes, 16-aligned) in the bit buffer
+  uint64_t out_off;     // finished JPEG in the output buffer
+  uint32_t hdr_off, hdr_len;  // header bytes in the header buffer
+  uint32_t tile0, ntiles_max;  // stuffing tiles
+};
+
+// Segmented scans over per-frame arrays (Huffman bit offsets, block counts, DC prediction,
+// tile counts): segment s covers elements [base, base + len) and owns tile-sum slots
+// [tile0, tile0 + ceil(len / kScanTile)).
+constexpr int kScanPerThread = 8;
+constexpr int kScanTile = 256 * kScanPerThread;
+struct ScanSeg {
+  uint64_t base;
+  uint32_t len;
+  uint32_t tile0;
+};
+
+// ---- launchers (vf_jpeg_kernels.hip) ----------------------------------------------------
+hipError_t scan_u32(const ScanSeg *segs, int nseg, uint32_t max_tiles, const uint32_t *in, uint32_t *out,
+                    uint32_t *tsum, uint32_t *totals, bool inclusive, hipStream_t s);
+hipError_t scan_i32(const ScanSeg *segs, int nseg, uint32_t max_tiles, const int32_t *in, int32_t *out,
+                    int32_t *tsum, int32_t *totals, bool inclusive, hipStream_t s);
+
+hipError_t dec_unstuff_count(const DecFrame *fr, int n, uint32_t max_tiles, const uint8_t *in,
+                             uint32_t *tile_cnt, hipStream_t s);
+hipError_t dec_unstuff_write(const DecFrame *fr, int n, uint32_t max_tiles, const uint8_t *in,
+                             const uint32_t *tile_off, const uint32_t *us_len, uint8_t *us, hipStream_t s);
+hipError_t dec_sync(const DecFrame *fr, int n, uint32_t max_sub, const uint8_t *us, const uint32_t *us_len,
+                    const uint64_t *exit_in, uint64_t *exit_out, const uint32_t *cnt_in, uint32_t *cnt_out,
+                    uint64_t *used, uint32_t *changed, int pass, hipStream_t s);
+hipError_t dec_write(const DecFrame *fr, int n, uint32_t max_sub, const uint8_t *us, const uint32_t *us_len,
+                     const uint64_t *exits, const uint32_t *bstart, int16_t *coef, int32_t *dcseq,
+                     hipStream_t s);
+hipError_t dec_idct(const DecFrame *fr, int n, uint32_t max_blocks, const int16_t *coef, const int32_t *dcseq,
+                    uint8_t *planes, hipStream_t s);
+hipError_t dec_color(const DecFrame *fr, int n, int max_w, int max_h, const uint8_t *planes, uint8_t *pix,
+                     int bgr, int invert, hipStream_t s);
+
+hipError_t enc_fdct(const EncFrame *fr, int n, uint32_t max_blocks, const EncTables *tab, const uint8_t *pix,
+                    int16_t *coef, int bgr, int fastdct, hipStream_t s);
+hipError_t enc_huff(const EncFrame *fr, int n, uint32_t max_blocks, const EncTables *tab, const int16_t *coef,
+                    uint32_t *bits, const uint32_t *bitoff, uint8_t *stream, bool emit, hipStream_t s);
+hipError_t enc_ff_count(const EncFrame *fr, int n, uint32_t max_tiles, const uint32_t *total_bits,
+                        const uint8_t *stream, uint32_t *tile_cnt, hipStream_t s);
+hipError_t enc_ff_write(const EncFrame *fr, int n, uint32_t max_tiles, const uint32_t *total_bits,
+                        const uint8_t *stream, const uint32_t *tile_off, const uint32_t *nff,
+                        const uint8_t *hdr, uint8_t *out, uint64_t *out_size, hipStream_t s);
+
+}  // namespace jpeg
+}  // namespace vf

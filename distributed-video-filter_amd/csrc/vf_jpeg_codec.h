@@ -1,0 +1,106 @@
+// vf_jpeg_codec.h — the per-context JPEG codec object behind the vf_jpeg_* entry points.
+// Not installed.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <vector>
+
+#include "vf_jpeg.h"
+
+namespace vf {
+namespace jpeg {
+
+// status codes (match VF_* in include/vfilter.h)
+constexpr int kOk = 0;
+constexpr int kInvalid = -1;
+constexpr int kHip = -2;
+constexpr int kNoMem = -3;
+constexpr int kJpeg = -5;
+
+// TurboJPEG flag bits honoured (turbojpeg.h)
+constexpr int kFlagFastUpsample = 256;
+constexpr int kFlagFastDct = 2048;
+
+// grow-only device / pinned buffers
+struct DevBuf {
+  void *p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t n);
+  template <typename T>
+  T *as() const {
+    return static_cast<T *>(p);
+  }
+  ~DevBuf();
+};
+
+struct HostBuf {
+  void *p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t n);
+  template <typename T>
+  T *as() const {
+    return static_cast<T *>(p);
+  }
+  ~HostBuf();
+};
+
+int header_info(const uint8_t *jpeg, size_t size, int *w, int *h, int *subsamp, int *colorspace, std::string *err);
+size_t buffer_size(int w, int h, int subsamp);
+
+class Codec {
+ public:
+  explicit Codec(int device);
+  ~Codec();
+  Codec(const Codec &) = delete;
+  Codec &operator=(const Codec &) = delete;
+
+  // host -> host; every call returns after its outputs are in the caller's buffers
+  int encode(const uint8_t *const *imgs, const int *ws, const int *hs, int n, int pixel_format, int quality,
+             int subsamp, int flags, uint8_t *const *outs, const size_t *caps, size_t *sizes, std::string *err);
+  int decode(const uint8_t *const *jpegs, const size_t *sizes, int n, int pixel_format, int flags,
+             uint8_t *const *outs, const size_t *caps, std::string *err);
+  int invert(const uint8_t *const *jpegs, const size_t *sizes, int n, int quality, int subsamp, int flags,
+             uint8_t *const *outs, const size_t *caps, size_t *out_sizes, std::string *err);
+  // the device part of invert() `iters` times on resident inputs; mean wall ms per iteration,
+  // stage_ms[0..6] = unstuff, sync, write, dc+idct, colour, fdct+huffman, stuffing; [7] = passes
+  int bench_invert(const uint8_t *const *jpegs, const size_t *sizes, int n, int quality, int subsamp, int flags,
+                   int iters, float *ms, float *stage_ms, std::string *err);
+
+ private:
+  int init(std::string *err);
+  int prepare_decode(const uint8_t *const *jpegs, const size_t *sizes, int n, int flags, std::string *err);
+  int run_decode(int bgr, bool invert, std::string *err);
+  int check_decode(std::string *err);
+  int prepare_encode(const int *ws, const int *hs, const uint64_t *img_offs, int n, int quality, int subsamp,
+                     bool fastdct, std::string *err);
+  int run_encode(int bgr, bool fastdct, std::string *err);
+  int fetch_jpegs(uint8_t *const *outs, const size_t *caps, size_t *sizes, std::string *err);
+
+  int device_;
+  hipStream_t s_ = nullptr;
+  hipEvent_t ev_[10] = {};
+
+  // decode layout
+  std::vector<DecFrame> dfr_;
+  int dn_ = 0, ndcseg_ = 0;
+  uint32_t dmax_tiles_ = 0, dmax_sub_ = 0, dmax_blocks_ = 0, dc_max_tiles_ = 0;
+  int dmax_w_ = 0, dmax_h_ = 0;
+  uint64_t dblocks_ = 0, dpix_bytes_ = 0;
+  int sync_passes_ = 0;
+  DevBuf d_in_, d_dfr_, d_segs_, d_tile_, d_tsum_, d_totals_, d_us_, d_exit_[2], d_cnt_[2], d_used_, d_bstart_,
+      d_changed_, d_coef_, d_dcseq_, d_planes_, d_pix_;
+
+  // encode layout
+  std::vector<EncFrame> efr_;
+  int en_ = 0;
+  uint32_t emax_blocks_ = 0, emax_tiles_ = 0;
+  uint64_t eblocks_ = 0, ebits_bytes_ = 0;
+  DevBuf d_efr_, d_etab_, d_hdr_, d_esegs_, d_etsum_, d_etotals_, d_ecoef_, d_bits_, d_bitoff_, d_stream_, d_ffcnt_,
+      d_out_, d_outsize_;
+
+  HostBuf h_stage_, h_out_;
+};
+
+}  // namespace jpeg
+}  // namespace vf

@@ -1,0 +1,945 @@
+// vf_jpeg_host.hip — host side of the gfx950 baseline-JPEG path: marker parsing, tables,
+// batch layout in HBM and the launch sequence of vf_jpeg_kernels.hip.
+//
+// What it replaces (reference default mode, use_jpeg=True):
+//   frame = self.jpeg.decode(frame_bytes)     inverter.py:32   -> Codec::decode
+//   inverted = cv2.bitwise_not(frame)         inverter.py:41   -> fused into the decode's colour stage
+//   return self.jpeg.encode(inverted)         inverter.py:44   -> Codec::encode
+// PyTurboJPEG defaults: quality 85, TJSAMP_422, TJPF_BGR, flags 0.  Marker syntax and table
+// construction follow libjpeg-turbo (jdmarker.c, jdhuff.c, jcparam.c, jcmarker.c, jchuff.c,
+// jcdctmgr.c), restated here for the product; oracle/vf_jpeg_oracle.c is the checker.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "vf_jpeg.h"
+#include "vf_jpeg_codec.h"
+
+namespace vf {
+namespace jpeg {
+
+namespace {
+
+const uint8_t kNatH[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
+                           12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
+                           35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
+                           58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+
+// ITU T.81 Annex K (jcparam.c std tables)
+const unsigned kLumaQ[64] = {16, 11, 10, 16, 24,  40,  51,  61,  12, 12, 14, 19, 26,  58,  60,  55,
+                             14, 13, 16, 24, 40,  57,  69,  56,  14, 17, 22, 29, 51,  87,  80,  62,
+                             18, 22, 37, 56, 68,  109, 103, 77,  24, 35, 55, 64, 81,  104, 113, 92,
+                             49, 64, 78, 87, 103, 121, 120, 101, 72, 92, 95, 98, 112, 100, 103, 99};
+const unsigned kChromaQ[64] = {17, 18, 24, 47, 99, 99, 99, 99, 18, 21, 26, 66, 99, 99, 99, 99,
+                               24, 26, 56, 99, 99, 99, 99, 99, 47, 66, 99, 99, 99, 99, 99, 99,
+                               99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99,
+                               99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99};
+const uint8_t kDcLBits[17] = {0, 0, 1, 5, 1, 1, 1, 1, 1, 1, 0, 0, 0, 0, 0, 0, 0};
+const uint8_t kDcCBits[17] = {0, 0, 3, 1, 1, 1, 1, 1, 1, 1, 1, 1, 0, 0, 0, 0, 0};
+const uint8_t kDcVals[12] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11};
+const uint8_t kAcLBits[17] = {0, 0, 2, 1, 3, 3, 2, 4, 3, 5, 5, 4, 4, 0, 0, 1, 0x7d};
+const uint8_t kAcLVals[162] = {
+    0x01, 0x02, 0x03, 0x00, 0x04, 0x11, 0x05, 0x12, 0x21, 0x31, 0x41, 0x06, 0x13, 0x51, 0x61, 0x07, 0x22,
+    0x71, 0x14, 0x32, 0x81, 0x91, 0xa1, 0x08, 0x23, 0x42, 0xb1, 0xc1, 0x15, 0x52, 0xd1, 0xf0, 0x24, 0x33,
+    0x62, 0x72, 0x82, 0x09, 0x0a, 0x16, 0x17, 0x18, 0x19, 0x1a, 0x25, 0x26, 0x27, 0x28, 0x29, 0x2a, 0x34,
+    0x35, 0x36, 0x37, 0x38, 0x39, 0x3a, 0x43, 0x44, 0x45, 0x46, 0x47, 0x48, 0x49, 0x4a, 0x53, 0x54, 0x55,
+    0x56, 0x57, 0x58, 0x59, 0x5a, 0x63, 0x64, 0x65, 0x66, 0x67, 0x68, 0x69, 0x6a, 0x73, 0x74, 0x75, 0x76,
+    0x77, 0x78, 0x79, 0x7a, 0x83, 0x84, 0x85, 0x86, 0x87, 0x88, 0x89, 0x8a, 0x92, 0x93, 0x94, 0x95, 0x96,
+    0x97, 0x98, 0x99, 0x9a, 0xa2, 0xa3, 0xa4, 0xa5, 0xa6, 0xa7, 0xa8, 0xa9, 0xaa, 0xb2, 0xb3, 0xb4, 0xb5,
+    0xb6, 0xb7, 0xb8, 0xb9, 0xba, 0xc2, 0xc3, 0xc4, 0xc5, 0xc6, 0xc7, 0xc8, 0xc9, 0xca, 0xd2, 0xd3, 0xd4,
+    0xd5, 0xd6, 0xd7, 0xd8, 0xd9, 0xda, 0xe1, 0xe2, 0xe3, 0xe4, 0xe5, 0xe6, 0xe7, 0xe8, 0xe9, 0xea, 0xf1,
+    0xf2, 0xf3, 0xf4, 0xf5, 0xf6, 0xf7, 0xf8, 0xf9, 0xfa};
+const uint8_t kAcCBits[17] = {0, 0, 2, 1, 2, 4, 4, 3, 4, 7, 5, 4, 4, 0, 1, 2, 0x77};
+const uint8_t kAcCVals[162] = {
+    0x00, 0x01, 0x02, 0x03, 0x11, 0x04, 0x05, 0x21, 0x31, 0x06, 0x12, 0x41, 0x51, 0x07, 0x61, 0x71, 0x13,
+    0x22, 0x32, 0x81, 0x08, 0x14, 0x42, 0x91, 0xa1, 0xb1, 0xc1, 0x09, 0x23, 0x33, 0x52, 0xf0, 0x15, 0x62,
+    0x72, 0xd1, 0x0a, 0x16, 0x24, 0x34, 0xe1, 0x25, 0xf1, 0x17, 0x18, 0x19, 0x1a, 0x26, 0x27, 0x28, 0x29,
+    0x2a, 0x35, 0x36, 0x37, 0x38, 0x39, 0x3a, 0x43, 0x44, 0x45, 0x46, 0x47, 0x48, 0x49, 0x4a, 0x53, 0x54,
+    0x55, 0x56, 0x57, 0x58, 0x59, 0x5a, 0x63, 0x64, 0x65, 0x66, 0x67, 0x68, 0x69, 0x6a, 0x73, 0x74, 0x75,
+    0x76, 0x77, 0x78, 0x79, 0x7a, 0x82, 0x83, 0x84, 0x85, 0x86, 0x87, 0x88, 0x89, 0x8a, 0x92, 0x93, 0x94,
+    0x95, 0x96, 0x97, 0x98, 0x99, 0x9a, 0xa2, 0xa3, 0xa4, 0xa5, 0xa6, 0xa7, 0xa8, 0xa9, 0xaa, 0xb2, 0xb3,
+    0xb4, 0xb5, 0xb6, 0xb7, 0xb8, 0xb9, 0xba, 0xc2, 0xc3, 0xc4, 0xc5, 0xc6, 0xc7, 0xc8, 0xc9, 0xca, 0xd2,
+    0xd3, 0xd4, 0xd5, 0xd6, 0xd7, 0xd8, 0xd9, 0xda, 0xe2, 0xe3, 0xe4, 0xe5, 0xe6, 0xe7, 0xe8, 0xe9, 0xea,
+    0xf2, 0xf3, 0xf4, 0xf5, 0xf6, 0xf7, 0xf8, 0xf9, 0xfa};
+const int16_t kAanScales[64] = {
+    16384, 22725, 21407, 19266, 16384, 12873, 8867,  4520,  22725, 31521, 29692, 26722, 22725,
+    17855, 12299, 6270,  21407, 29692, 27969, 25172, 21407, 16819, 11585, 5906,  19266, 26722,
+    25172, 22654, 19266, 15137, 10426, 5315,  16384, 22725, 21407, 19266, 16384, 12873, 8867,
+    4520,  12873, 17855, 16819, 15137, 12873, 10114, 6967,  3552,  8867,  12299, 11585, 10426,
+    8867,  6967,  4799,  2446,  4520,  6270,  5906,  5315,  4520,  3552,  2446,  1247};
+const int kSampH[5] = {1, 2, 2, 1, 1};  // TJSAMP_444, 422, 420, GRAY, 440 (turbojpeg.h tjMCUWidth/8)
+const int kSampV[5] = {1, 1, 2, 1, 2};
+
+int ceil_div(int a, int b) { return (a + b - 1) / b; }
+size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// jcparam.c jpeg_quality_scaling + jpeg_add_quant_table(force_baseline = TRUE)
+void quality_table(int quality, bool chroma, uint16_t out[64]) {
+  quality = std::min(100, std::max(1, quality));
+  const int scale = quality < 50 ? 5000 / quality : 200 - quality * 2;
+  for (int i = 0; i < 64; ++i) {
+    long t = ((long)(chroma ? kChromaQ : kLumaQ)[i] * scale + 50L) / 100L;
+    out[i] = (uint16_t)std::min(255L, std::max(1L, t));
+  }
+}
+
+// jchuff.c jpeg_make_c_derived_tbl -> (code << 8) | size by symbol
+void code_table(const uint8_t bits[17], const uint8_t *vals, uint32_t *out, int nslots) {
+  std::memset(out, 0, sizeof(uint32_t) * (size_t)nslots);
+  uint32_t code = 0;
+  int p = 0;
+  for (int l = 1; l <= 16; ++l) {
+    for (int i = 0; i < bits[l]; ++i, ++p, ++code)
+      if (vals[p] < nslots) out[vals[p]] = (code << 8) | (uint32_t)l;
+    code <<= 1;
+  }
+}
+
+// jdhuff.c jpeg_make_d_derived_tbl + a kLook-bit lookahead
+bool decode_table(const uint8_t bits[17], const uint8_t *vals, HuffDec *t) {
+  std::memset(t, 0, sizeof *t);
+  int p = 0;
+  uint32_t code = 0;
+  for (int l = 1; l <= 16; ++l) {
+    if (bits[l]) {
+      t->valoff[l] = p - (int32_t)code;
+      for (int i = 0; i < bits[l]; ++i, ++p, ++code) {
+        if (p >= 256) return false;
+        t->vals[p] = vals[p];
+        if (l <= kLook) {
+          const uint32_t base = code << (kLook - l);
+          for (uint32_t s = 0; s < (1u << (kLook - l)); ++s) t->fast[base + s] = (uint16_t)((l << 8) | vals[p]);
+        }
+      }
+      t->maxcode[l] = (int32_t)code - 1;
+      if (code > (1u << l)) return false;  // over-subscribed table
+    } else {
+      t->maxcode[l] = -1;
+    }
+    code <<= 1;
+  }
+  t->maxcode[17] = 0xFFFFF;
+  return true;
+}
+
+struct Parsed {
+  int w = 0, h = 0, ncomp = 0, restart = 0;
+  int id[3] = {}, hs[3] = {}, vs[3] = {}, tq[3] = {}, td[3] = {}, ta[3] = {};
+  uint16_t qt[4][64] = {};
+  uint8_t dcbits[4][17] = {}, acbits[4][17] = {};
+  uint8_t dcvals[4][256] = {}, acvals[4][256] = {};
+  int qdef = 0, dcdef = 0, acdef = 0;
+  size_t scan_off = 0, scan_end = 0;
+};
+
+// jdmarker.c restated for baseline / extended sequential Huffman, one interleaved scan
+int parse(const uint8_t *b, size_t n, Parsed *P, std::string *err) {
+  auto fail = [&](const char *m) {
+    *err = m;
+    return -1;
+  };
+  if (n < 4 || b[0] != 0xFF || b[1] != 0xD8) return fail("not a JPEG (no SOI)");
+  size_t p = 2;
+  bool sof = false;
+  for (;;) {
+    while (p < n && b[p] != 0xFF) p++;
+    while (p < n && b[p] == 0xFF) p++;
+    if (p >= n) return fail("truncated JPEG (no SOS)");
+    const int m = b[p++];
+    if (m == 0xD9) return fail("EOI before SOS");
+    if (m == 0x01 || (m >= 0xD0 && m <= 0xD7)) continue;
+    if (p + 2 > n) return fail("truncated marker");
+    const size_t len = ((size_t)b[p] << 8) | b[p + 1];
+    if (len < 2 || p + len > n) return fail("truncated marker segment");
+    const uint8_t *s = b + p + 2, *e = b + p + len;
+    if (m == 0xDB) {
+      while (s < e) {
+        const int pq = s[0] >> 4, tq = s[0] & 15;
+        ++s;
+        if (tq > 3 || s + (pq ? 128 : 64) > e) return fail("bad DQT");
+        for (int i = 0; i < 64; ++i) P->qt[tq][kNatH[i]] = pq ? (uint16_t)((s[2 * i] << 8) | s[2 * i + 1]) : s[i];
+        P->qdef |= 1 << tq;
+        s += pq ? 128 : 64;
+      }
+    } else if (m == 0xC4) {
+      while (s < e) {
+        if (s + 17 > e) return fail("bad DHT");
+        const int tc = s[0] >> 4, th = s[0] & 15;
+        if (tc > 1 || th > 3) return fail("bad DHT class/id");
+        int cnt = 0;
+        for (int l = 1; l <= 16; ++l) cnt += s[l];
+        if (cnt > 256 || s + 17 + cnt > e) return fail("bad DHT counts");
+        uint8_t *bits = tc ? P->acbits[th] : P->dcbits[th];
+        uint8_t *vals = tc ? P->acvals[th] : P->dcvals[th];
+        bits[0] = 0;
+        std::memcpy(bits + 1, s + 1, 16);
+        std::memcpy(vals, s + 17, (size_t)cnt);
+        (tc ? P->acdef : P->dcdef) |= 1 << th;
+        s += 17 + cnt;
+      }
+    } else if (m == 0xC0 || m == 0xC1) {
+      if (len < 8 || s[0] != 8) return fail("only 8-bit sequential JPEG is supported");
+      P->h = (s[1] << 8) | s[2];
+      P->w = (s[3] << 8) | s[4];
+      P->ncomp = s[5];
+      if (P->ncomp != 1 && P->ncomp != 3) return fail("only 1- or 3-component JPEG is supported");
+      if ((int)len != 8 + 3 * P->ncomp || !P->w || !P->h) return fail("bad SOF");
+      for (int c = 0; c < P->ncomp; ++c) {
+        P->id[c] = s[6 + 3 * c];
+        P->hs[c] = s[7 + 3 * c] >> 4;
+        P->vs[c] = s[7 + 3 * c] & 15;
+        P->tq[c] = s[8 + 3 * c];
+        if (P->hs[c] < 1 || P->hs[c] > 4 || P->vs[c] < 1 || P->vs[c] > 4 || P->tq[c] > 3) return fail("bad SOF");
+      }
+      sof = true;
+    } else if (m >= 0xC2 && m <= 0xCF && m != 0xC4 && m != 0xC8 && m != 0xCC) {
+      return fail("progressive / lossless / arithmetic JPEG is not supported");
+    } else if (m == 0xDD) {
+      if (len != 4) return fail("bad DRI");
+      P->restart = (s[0] << 8) | s[1];
+    } else if (m == 0xDA) {
+      if (!sof) return fail("SOS before SOF");
+      const int ns = s[0];
+      if (ns != P->ncomp || (int)len != 6 + 2 * ns) return fail("only single-scan interleaved JPEG is supported");
+      for (int i = 0; i < ns; ++i) {
+        if (s[1 + 2 * i] != P->id[i]) return fail("scan component order differs from the frame");
+        P->td[i] = s[2 + 2 * i] >> 4;
+        P->ta[i] = s[2 + 2 * i] & 15;
+        if (P->td[i] > 3 || P->ta[i] > 3) return fail("bad SOS table id");
+      }
+      if (s[1 + 2 * ns] != 0 || s[2 + 2 * ns] != 63 || s[3 + 2 * ns] != 0) return fail("not a baseline scan");
+      P->scan_off = p + len;
+      size_t q = P->scan_off;
+      while (q + 1 < n) {
+        if (b[q] == 0xFF && b[q + 1] != 0x00 && !(b[q + 1] >= 0xD0 && b[q + 1] <= 0xD7) && b[q + 1] != 0xFF) break;
+        ++q;
+      }
+      P->scan_end = q + 1 < n ? q : n;
+      for (int c = 0; c < P->ncomp; ++c)
+        if (!(P->qdef >> P->tq[c] & 1) || !(P->dcdef >> P->td[c] & 1) || !(P->acdef >> P->ta[c] & 1))
+          return fail("scan refers to an undefined table");
+      return 0;
+    }
+    p += len;
+  }
+}
+
+int subsamp_of(const Parsed &P) {
+  if (P.ncomp == 1) return 3;  // TJSAMP_GRAY
+  if (P.hs[1] != 1 || P.vs[1] != 1 || P.hs[2] != 1 || P.vs[2] != 1) return -1;
+  for (int s = 0; s < 5; ++s)
+    if (s != 3 && P.hs[0] == kSampH[s] && P.vs[0] == kSampV[s]) return s;
+  if (P.hs[0] == 4 && P.vs[0] == 1) return 5;  // TJSAMP_411
+  return -1;
+}
+
+// jcmarker.c: SOI, JFIF APP0, DQT(s), SOF0, DHT(s), SOS for the TurboJPEG defaults
+size_t write_header(int w, int h, int quality, int subsamp, uint8_t *o) {
+  size_t n = 0;
+  auto b = [&](int v) { o[n++] = (uint8_t)v; };
+  auto u16 = [&](int v) {
+    b(v >> 8);
+    b(v & 0xFF);
+  };
+  const int nc = subsamp == 3 ? 1 : 3;
+  uint16_t q[2][64];
+  quality_table(quality, false, q[0]);
+  quality_table(quality, true, q[1]);
+  b(0xFF);
+  b(0xD8);
+  const uint8_t app0[18] = {0xFF, 0xE0, 0, 16, 'J', 'F', 'I', 'F', 0, 1, 1, 0, 0, 1, 0, 1, 0, 0};
+  for (uint8_t v : app0) b(v);
+  for (int t = 0; t < (nc == 3 ? 2 : 1); ++t) {
+    b(0xFF);
+    b(0xDB);
+    u16(67);
+    b(t);
+    for (int i = 0; i < 64; ++i) b(q[t][kNatH[i]]);
+  }
+  b(0xFF);
+  b(0xC0);
+  u16(8 + 3 * nc);
+  b(8);
+  u16(h);
+  u16(w);
+  b(nc);
+  for (int c = 0; c < nc; ++c) {
+    b(c + 1);
+    b(c == 0 ? (kSampH[subsamp] << 4) | kSampV[subsamp] : 0x11);
+    b(c == 0 ? 0 : 1);
+  }
+  auto dht = [&](int idx, const uint8_t *bits, const uint8_t *vals) {
+    int cnt = 0;
+    for (int l = 1; l <= 16; ++l) cnt += bits[l];
+    b(0xFF);
+    b(0xC4);
+    u16(19 + cnt);
+    b(idx);
+    for (int l = 1; l <= 16; ++l) b(bits[l]);
+    for (int i = 0; i < cnt; ++i) b(vals[i]);
+  };
+  dht(0x00, kDcLBits, kDcVals);
+  dht(0x10, kAcLBits, kAcLVals);
+  if (nc == 3) {
+    dht(0x01, kDcCBits, kDcVals);
+    dht(0x11, kAcCBits, kAcCVals);
+  }
+  b(0xFF);
+  b(0xDA);
+  u16(6 + 2 * nc);
+  b(nc);
+  for (int c = 0; c < nc; ++c) {
+    b(c + 1);
+    b(c == 0 ? 0x00 : 0x11);
+  }
+  b(0);
+  b(63);
+  b(0);
+  return n;
+}
+
+// jcdctmgr.c start_pass_fdctmgr + compute_reciprocal (16-bit DCTELEM, the SIMD build)
+void build_enc_tables(int quality, bool fastdct, EncTables *t) {
+  std::memset(t, 0, sizeof *t);
+  for (int tb = 0; tb < 2; ++tb) {
+    uint16_t q[64];
+    quality_table(quality, tb == 1, q);
+    for (int i = 0; i < 64; ++i) {
+      const uint32_t divisor = fastdct ? (uint32_t)(((int32_t)q[i] * kAanScales[i] + (1 << 10)) >> 11)
+                                       : (uint32_t)q[i] << 3;
+      if (divisor == 1) {
+        t->recip[tb][i] = 1;
+        t->corr[tb][i] = 0;
+        t->shift[tb][i] = -16;
+        continue;
+      }
+      const int b = 31 - __builtin_clz(divisor);
+      int r = 16 + b;
+      uint32_t fq = (1u << r) / divisor, fr = (1u << r) % divisor, c = divisor / 2;
+      if (fr == 0) {
+        fq >>= 1;
+        --r;
+      } else if (fr <= divisor / 2u) {
+        ++c;
+      } else {
+        ++fq;
+      }
+      t->recip[tb][i] = (uint16_t)fq;
+      t->corr[tb][i] = (uint16_t)c;
+      t->shift[tb][i] = (int16_t)(r - 16);
+    }
+  }
+  code_table(kDcLBits, kDcVals, t->dc[0], 16);
+  code_table(kDcCBits, kDcVals, t->dc[1], 16);
+  code_table(kAcLBits, kAcLVals, t->ac[0], 256);
+  code_table(kAcCBits, kAcCVals, t->ac[1], 256);
+}
+
+// worst case per block: DC 16 + 11 bits, 63 AC codes of 16 + 10 bits
+constexpr size_t kMaxBlockBytes = (27 + 63 * 26 + 7) / 8 + 1;
+
+}  // namespace
+
+bool make_geom(int w, int h, int ncomp, const int *hs, const int *vs, Geom *g) {
+  std::memset(g, 0, sizeof *g);
+  if (w <= 0 || h <= 0 || w > 65535 || h > 65535 || (ncomp != 1 && ncomp != 3)) return false;
+  int maxh = 1, maxv = 1;
+  for (int k = 0; k < ncomp; ++k) {
+    if (hs[k] < 1 || hs[k] > 4 || vs[k] < 1 || vs[k] > 4) return false;
+    maxh = std::max(maxh, hs[k]);
+    maxv = std::max(maxv, vs[k]);
+  }
+  for (int k = 0; k < ncomp; ++k)
+    if (maxh % hs[k] || maxv % vs[k]) return false;
+  g->w = w;
+  g->h = h;
+  g->ncomp = ncomp;
+  g->maxh = maxh;
+  g->maxv = maxv;
+  if (ncomp == 1) {  // non-interleaved scan: one block per MCU
+    g->hs[0] = hs[0];
+    g->vs[0] = vs[0];
+    g->mh[0] = g->mv[0] = 1;
+    g->wb[0] = ceil_div(w * hs[0], 8 * maxh);
+    g->hb[0] = ceil_div(h * vs[0], 8 * maxv);
+    g->mcux = g->wb[0];
+    g->mcuy = g->hb[0];
+    g->pw[0] = g->wb[0] * 8;
+    g->ph[0] = g->hb[0] * 8;
+    g->bpm = 1;
+  } else {
+    g->mcux = ceil_div(w, 8 * maxh);
+    g->mcuy = ceil_div(h, 8 * maxv);
+    int b = 0;
+    for (int k = 0; k < 3; ++k) {
+      g->hs[k] = hs[k];
+      g->vs[k] = vs[k];
+      g->mh[k] = hs[k];
+      g->mv[k] = vs[k];
+      g->wb[k] = ceil_div(w * hs[k], 8 * maxh);
+      g->hb[k] = ceil_div(h * vs[k], 8 * maxv);
+      g->pw[k] = g->mcux * hs[k] * 8;
+      g->ph[k] = g->mcuy * vs[k] * 8;
+      g->cfirst[k] = b;
+      for (int yi = 0; yi < vs[k]; ++yi)
+        for (int xi = 0; xi < hs[k]; ++xi) {
+          if (b >= kMaxBpm) return false;
+          g->bcomp[b] = (int8_t)k;
+          g->bxo[b] = (int8_t)xi;
+          g->byo[b] = (int8_t)yi;
+          ++b;
+        }
+    }
+    g->bpm = b;
+  }
+  const long long nm = (long long)g->mcux * g->mcuy;
+  if (nm * g->bpm > (1ll << 30)) return false;
+  g->nmcu = (int32_t)nm;
+  g->nblocks = (int32_t)(nm * g->bpm);
+  return true;
+}
+
+// ---- device / pinned buffers ---------------------------------------------------------------
+
+hipError_t DevBuf::ensure(size_t n) {
+  if (n <= cap) return hipSuccess;
+  if (p) (void)hipFree(p);
+  p = nullptr;
+  cap = 0;
+  n = align_up(std::max<size_t>(n, 256), 1 << 20);
+  hipError_t e = hipMalloc(&p, n);
+  if (e == hipSuccess) cap = n;
+  return e;
+}
+
+DevBuf::~DevBuf() {
+  if (p) (void)hipFree(p);
+}
+
+hipError_t HostBuf::ensure(size_t n) {
+  if (n <= cap) return hipSuccess;
+  if (p) (void)hipHostFree(p);
+  p = nullptr;
+  cap = 0;
+  n = align_up(std::max<size_t>(n, 256), 1 << 20);
+  hipError_t e = hipHostMalloc(&p, n, hipHostMallocDefault);
+  if (e == hipSuccess) cap = n;
+  return e;
+}
+
+HostBuf::~HostBuf() {
+  if (p) (void)hipHostFree(p);
+}
+
+// ---- codec -------------------------------------------------------------------------------------
+
+Codec::Codec(int device) : device_(device) {}
+
+Codec::~Codec() {
+  (void)hipSetDevice(device_);
+  if (s_) {
+    (void)hipStreamSynchronize(s_);
+    (void)hipStreamDestroy(s_);
+  }
+  for (hipEvent_t e : ev_)
+    if (e) (void)hipEventDestroy(e);
+}
+
+#define CK(call)                                                                          \
+  do {                                                                                    \
+    hipError_t e_ = (call);                                                               \
+    if (e_ != hipSuccess) {                                                               \
+      *err = std::string(#call) + ": " + hipGetErrorString(e_);                           \
+      return e_ == hipErrorOutOfMemory || e_ == hipErrorMemoryAllocation ? kNoMem : kHip; \
+    }                                                                                     \
+  } while (0)
+
+int Codec::init(std::string *err) {
+  if (s_) return kOk;
+  CK(hipSetDevice(device_));
+  CK(hipStreamCreateWithFlags(&s_, hipStreamNonBlocking));
+  for (hipEvent_t &e : ev_) CK(hipEventCreate(&e));
+  return kOk;
+}
+
+// Host parse of every frame + batch layout + upload of inputs and descriptors.
+int Codec::prepare_decode(const uint8_t *const *jpegs, const size_t *sizes, int n, int flags, std::string *err) {
+  if (n <= 0) {
+    *err = "empty batch";
+    return kInvalid;
+  }
+  dfr_.assign((size_t)n, DecFrame());
+  std::vector<Parsed> parsed((size_t)n);
+  uint64_t in_off = 0, us_off = 0, blk = 0, dcoff = 0, plane = 0, pix = 0;
+  uint32_t tiles = 0, subs = 0;
+  dmax_tiles_ = dmax_sub_ = dmax_blocks_ = 0;
+  dmax_w_ = dmax_h_ = 0;
+  for (int f = 0; f < n; ++f) {
+    Parsed &P = parsed[(size_t)f];
+    if (!jpegs[f] || parse(jpegs[f], sizes[f], &P, err) != 0) {
+      if (!jpegs[f]) *err = "NULL JPEG buffer";
+      *err = "frame " + std::to_string(f) + ": " + *err;
+      return kJpeg;
+    }
+    if (P.restart) {
+      *err = "frame " + std::to_string(f) + ": restart intervals (DRI) are not supported by the GPU decoder yet";
+      return kJpeg;
+    }
+    DecFrame &F = dfr_[(size_t)f];
+    if (!make_geom(P.w, P.h, P.ncomp, P.hs, P.vs, &F.g)) {
+      *err = "frame " + std::to_string(f) + ": unsupported sampling geometry";
+      return kJpeg;
+    }
+    for (int c = 0; c < P.ncomp; ++c) {
+      std::memcpy(F.q[c], P.qt[P.tq[c]], sizeof F.q[c]);
+      if (!decode_table(P.dcbits[P.td[c]], P.dcvals[P.td[c]], &F.dc[c]) ||
+          !decode_table(P.acbits[P.ta[c]], P.acvals[P.ta[c]], &F.ac[c])) {
+        *err = "frame " + std::to_string(f) + ": bad Huffman table";
+        return kJpeg;
+      }
+    }
+    const size_t len = P.scan_end - P.scan_off;
+    if (len == 0 || len > (1u << 28)) {
+      *err = "frame " + std::to_string(f) + ": empty or oversized entropy-coded segment";
+      return kJpeg;
+    }
+    F.in_off = in_off;
+    F.in_len = (uint32_t)len;
+    F.ntiles = (uint32_t)((len + kTile - 1) / kTile);
+    F.tile0 = tiles;
+    F.sub0 = subs;
+    F.nsub_max = (uint32_t)((len * 8 + kSubBits - 1) / kSubBits);
+    F.flags = (flags & kFlagFastUpsample) ? 0u : 1u;
+    F.us_off = us_off;
+    F.blk0 = blk;
+    for (int c = 0; c < P.ncomp; ++c) {
+      F.dcbase[c] = dcoff;
+      dcoff += (uint64_t)F.g.nmcu * F.g.mh[c] * F.g.mv[c];
+      F.plane_off[c] = plane;
+      plane += align_up((size_t)F.g.pw[c] * F.g.ph[c], 256);
+    }
+    F.out_off = pix;
+    pix += align_up((size_t)P.w * P.h * 3, 256);
+    in_off += align_up(len, 16);
+    us_off += align_up(len + 64, 16);
+    blk += (uint64_t)F.g.nblocks;
+    tiles += F.ntiles;
+    subs += F.nsub_max;
+    dmax_tiles_ = std::max(dmax_tiles_, F.ntiles);
+    dmax_sub_ = std::max(dmax_sub_, F.nsub_max);
+    dmax_blocks_ = std::max(dmax_blocks_, (uint32_t)F.g.nblocks);
+    dmax_w_ = std::max(dmax_w_, P.w);
+    dmax_h_ = std::max(dmax_h_, P.h);
+  }
+  dn_ = n;
+  dblocks_ = blk;
+  dpix_bytes_ = pix;
+  // scan segments: [0, n) unstuff tiles, [n, 2n) subsequence counts, then DC sequences
+  std::vector<ScanSeg> segs;
+  uint32_t t0 = 0;
+  auto add = [&](uint64_t base, uint32_t len) {
+    segs.push_back(ScanSeg{base, len, t0});
+    t0 += (len + kScanTile - 1) / kScanTile;
+  };
+  for (auto &F : dfr_) add(F.tile0, F.ntiles);
+  for (auto &F : dfr_) add(F.sub0, F.nsub_max);
+  ndcseg_ = 0;
+  dc_max_tiles_ = 0;
+  for (auto &F : dfr_)
+    for (int c = 0; c < F.g.ncomp; ++c) {
+      const uint32_t len = (uint32_t)((uint64_t)F.g.nmcu * F.g.mh[c] * F.g.mv[c]);
+      add(F.dcbase[c], len);
+      dc_max_tiles_ = std::max(dc_max_tiles_, (len + kScanTile - 1) / kScanTile);
+      ++ndcseg_;
+    }
+  // staging: inputs packed, then uploaded in one copy
+  CK(h_stage_.ensure(in_off));
+  for (int f = 0; f < n; ++f) {
+    const Parsed &P = parsed[(size_t)f];
+    std::memcpy(h_stage_.as<uint8_t>() + dfr_[(size_t)f].in_off, jpegs[f] + P.scan_off, P.scan_end - P.scan_off);
+  }
+  CK(hipSetDevice(device_));
+  CK(d_in_.ensure(in_off));
+  CK(d_dfr_.ensure(sizeof(DecFrame) * (size_t)n));
+  CK(d_segs_.ensure(sizeof(ScanSeg) * segs.size()));
+  CK(d_tile_.ensure(sizeof(uint32_t) * tiles));
+  CK(d_tsum_.ensure(sizeof(int32_t) * (t0 + 1)));
+  CK(d_totals_.ensure(sizeof(int32_t) * segs.size()));
+  CK(d_us_.ensure(us_off));
+  CK(d_exit_[0].ensure(sizeof(uint64_t) * subs));
+  CK(d_exit_[1].ensure(sizeof(uint64_t) * subs));
+  CK(d_cnt_[0].ensure(sizeof(uint32_t) * subs));
+  CK(d_cnt_[1].ensure(sizeof(uint32_t) * subs));
+  CK(d_used_.ensure(sizeof(uint64_t) * subs));
+  CK(d_bstart_.ensure(sizeof(uint32_t) * subs));
+  CK(d_changed_.ensure(sizeof(uint32_t) * kMaxPasses));
+  CK(d_coef_.ensure(blk * 128));
+  CK(d_dcseq_.ensure(sizeof(int32_t) * (dcoff + 1)));
+  CK(d_planes_.ensure(plane));
+  CK(d_pix_.ensure(pix));
+  CK(hipMemcpyAsync(d_in_.p, h_stage_.p, in_off, hipMemcpyHostToDevice, s_));
+  CK(hipMemcpyAsync(d_dfr_.p, dfr_.data(), sizeof(DecFrame) * (size_t)n, hipMemcpyHostToDevice, s_));
+  CK(hipMemcpyAsync(d_segs_.p, segs.data(), sizeof(ScanSeg) * segs.size(), hipMemcpyHostToDevice, s_));
+  // the pinned staging buffer is reused below: make sure the upload has consumed it
+  CK(hipStreamSynchronize(s_));
+  return kOk;
+}
+
+// Device part of the decode: unstuff -> sync passes -> write -> DC -> IDCT -> colour.
+int Codec::run_decode(int bgr, bool invert, std::string *err) {
+  const DecFrame *fr = d_dfr_.as<DecFrame>();
+  const ScanSeg *segs = d_segs_.as<ScanSeg>();
+  const int n = dn_;
+  CK(hipEventRecord(ev_[0], s_));
+  // 1. unstuff
+  CK(dec_unstuff_count(fr, n, dmax_tiles_, d_in_.as<uint8_t>(), d_tile_.as<uint32_t>(), s_));
+  uint32_t *us_len = d_totals_.as<uint32_t>();  // totals of segments [0, n)
+  CK(scan_u32(segs, n, (dmax_tiles_ + kScanTile - 1) / kScanTile, d_tile_.as<uint32_t>(), d_tile_.as<uint32_t>(),
+              d_tsum_.as<uint32_t>(), us_len, false, s_));
+  CK(dec_unstuff_write(fr, n, dmax_tiles_, d_in_.as<uint8_t>(), d_tile_.as<uint32_t>(), us_len,
+                       d_us_.as<uint8_t>(), s_));
+  CK(hipEventRecord(ev_[1], s_));
+  // 2. synchronise the subsequence entry states
+  CK(hipMemsetAsync(d_changed_.p, 0, sizeof(uint32_t) * kMaxPasses, s_));
+  int pass = 0, last = 0;
+  uint32_t flag = 1;
+  for (;;) {
+    const int a = pass & 1;
+    CK(dec_sync(fr, n, dmax_sub_, d_us_.as<uint8_t>(), us_len, d_exit_[a ^ 1].as<uint64_t>(),
+                d_exit_[a].as<uint64_t>(), d_cnt_[a ^ 1].as<uint32_t>(), d_cnt_[a].as<uint32_t>(),
+                d_used_.as<uint64_t>(), d_changed_.as<uint32_t>() + (pass % kMaxPasses), pass > 0 ? 1 : 0, s_));
+    last = a;
+    ++pass;
+    if (pass < 3) continue;  // passes 0..2 are queued without a host round trip
+    CK(hipMemcpyAsync(&flag, d_changed_.as<uint32_t>() + ((pass - 1) % kMaxPasses), sizeof flag,
+                      hipMemcpyDeviceToHost, s_));
+    CK(hipStreamSynchronize(s_));
+    if (!flag) break;
+    CK(hipMemsetAsync(d_changed_.as<uint32_t>() + (pass % kMaxPasses), 0, sizeof(uint32_t), s_));
+    if (pass > (int)dmax_sub_ + 2) {
+      *err = "Huffman synchronisation did not converge (corrupt stream?)";
+      return kJpeg;
+    }
+  }
+  sync_passes_ = pass;
+  CK(hipEventRecord(ev_[2], s_));
+  // 3. block offsets of the subsequences, then the write pass
+  uint32_t *blocks_total = d_totals_.as<uint32_t>() + n;
+  CK(scan_u32(segs + n, n, (dmax_sub_ + kScanTile - 1) / kScanTile, d_cnt_[last].as<uint32_t>(),
+              d_bstart_.as<uint32_t>(), d_tsum_.as<uint32_t>(), blocks_total, false, s_));
+  CK(hipMemsetAsync(d_coef_.p, 0, dblocks_ * 128, s_));
+  CK(dec_write(fr, n, dmax_sub_, d_us_.as<uint8_t>(), us_len, d_exit_[last].as<uint64_t>(),
+               d_bstart_.as<uint32_t>(), d_coef_.as<int16_t>(), d_dcseq_.as<int32_t>(), s_));
+  CK(hipEventRecord(ev_[3], s_));
+  // 4. DC prediction (inclusive scan per component sequence)
+  CK(scan_i32(segs + 2 * n, ndcseg_, dc_max_tiles_, d_dcseq_.as<int32_t>(), d_dcseq_.as<int32_t>(),
+              d_tsum_.as<int32_t>(), nullptr, true, s_));
+  // 5. IDCT, 6. upsample + colour (+ invert)
+  CK(dec_idct(fr, n, dmax_blocks_, d_coef_.as<int16_t>(), d_dcseq_.as<int32_t>(), d_planes_.as<uint8_t>(), s_));
+  CK(hipEventRecord(ev_[4], s_));
+  CK(dec_color(fr, n, dmax_w_, dmax_h_, d_planes_.as<uint8_t>(), d_pix_.as<uint8_t>(), bgr, invert ? 1 : 0, s_));
+  CK(hipEventRecord(ev_[5], s_));
+  return kOk;
+}
+
+// Check that every frame decoded all its blocks (reads the totals written by run_decode).
+int Codec::check_decode(std::string *err) {
+  std::vector<uint32_t> tot((size_t)dn_);
+  CK(hipMemcpyAsync(tot.data(), d_totals_.as<uint32_t>() + dn_, sizeof(uint32_t) * (size_t)dn_,
+                    hipMemcpyDeviceToHost, s_));
+  CK(hipStreamSynchronize(s_));
+  for (int f = 0; f < dn_; ++f)
+    if (tot[(size_t)f] < (uint32_t)dfr_[(size_t)f].g.nblocks) {
+      *err = "frame " + std::to_string(f) + ": entropy-coded data ends after " + std::to_string(tot[(size_t)f]) +
+             " of " + std::to_string(dfr_[(size_t)f].g.nblocks) + " blocks (truncated or corrupt JPEG)";
+      return kJpeg;
+    }
+  return kOk;
+}
+
+// Layout + tables + headers for encoding n frames whose pixels sit in d_pix_ at img_offs.
+int Codec::prepare_encode(const int *ws, const int *hs, const uint64_t *img_offs, int n, int quality, int subsamp,
+                          bool fastdct, std::string *err) {
+  if (subsamp < 0 || subsamp > 4) {
+    *err = "unsupported subsampling (TJSAMP_444, 422, 420, GRAY, 440)";
+    return kInvalid;
+  }
+  efr_.assign((size_t)n, EncFrame());
+  std::vector<uint8_t> hdr;
+  uint64_t blk = 0, bits = 0, out = 0;
+  uint32_t tiles = 0;
+  emax_blocks_ = emax_tiles_ = 0;
+  const int nc = subsamp == 3 ? 1 : 3;
+  const int hsamp[3] = {kSampH[subsamp], 1, 1}, vsamp[3] = {kSampV[subsamp], 1, 1};
+  for (int f = 0; f < n; ++f) {
+    EncFrame &F = efr_[(size_t)f];
+    if (!make_geom(ws[f], hs[f], nc, hsamp, vsamp, &F.g)) {
+      *err = "frame " + std::to_string(f) + ": bad image size";
+      return kInvalid;
+    }
+    F.img_off = img_offs[f];
+    F.blk0 = blk;
+    F.bits_off = bits;
+    const uint64_t bits_cap = align_up((size_t)F.g.nblocks * kMaxBlockBytes + 16, 256);
+    F.out_off = out;
+    F.hdr_off = (uint32_t)hdr.size();
+    uint8_t h[1024];
+    F.hdr_len = (uint32_t)write_header(ws[f], hs[f], quality, subsamp, h);
+    hdr.insert(hdr.end(), h, h + F.hdr_len);
+    F.tile0 = tiles;
+    F.ntiles_max = (uint32_t)((bits_cap + kTile - 1) / kTile);
+    blk += (uint64_t)F.g.nblocks;
+    bits += bits_cap;
+    out += align_up(F.hdr_len + 2 * bits_cap + 2, 256);
+    tiles += F.ntiles_max;
+    emax_blocks_ = std::max(emax_blocks_, (uint32_t)F.g.nblocks);
+    emax_tiles_ = std::max(emax_tiles_, F.ntiles_max);
+  }
+  en_ = n;
+  eblocks_ = blk;
+  ebits_bytes_ = bits;
+  std::vector<ScanSeg> segs;
+  uint32_t t0 = 0;
+  auto add = [&](uint64_t base, uint32_t len) {
+    segs.push_back(ScanSeg{base, len, t0});
+    t0 += (len + kScanTile - 1) / kScanTile;
+  };
+  for (auto &F : efr_) add(F.blk0, (uint32_t)F.g.nblocks);
+  for (auto &F : efr_) add(F.tile0, F.ntiles_max);
+  EncTables tab;
+  build_enc_tables(quality, fastdct, &tab);
+  CK(hipSetDevice(device_));
+  CK(d_efr_.ensure(sizeof(EncFrame) * (size_t)n));
+  CK(d_etab_.ensure(sizeof(EncTables)));
+  CK(d_hdr_.ensure(hdr.size()));
+  CK(d_esegs_.ensure(sizeof(ScanSeg) * segs.size()));
+  CK(d_etsum_.ensure(sizeof(uint32_t) * (t0 + 1)));
+  CK(d_etotals_.ensure(sizeof(uint32_t) * segs.size()));
+  CK(d_ecoef_.ensure(blk * 128));
+  CK(d_bits_.ensure(sizeof(uint32_t) * blk));
+  CK(d_bitoff_.ensure(sizeof(uint32_t) * blk));
+  CK(d_stream_.ensure(bits));
+  CK(d_ffcnt_.ensure(sizeof(uint32_t) * tiles));
+  CK(d_out_.ensure(out));
+  CK(d_outsize_.ensure(sizeof(uint64_t) * (size_t)n));
+  // small tables go through pageable memcpy (synchronous w.r.t. the host buffers)
+  CK(hipMemcpyAsync(d_efr_.p, efr_.data(), sizeof(EncFrame) * (size_t)n, hipMemcpyHostToDevice, s_));
+  CK(hipMemcpyAsync(d_etab_.p, &tab, sizeof tab, hipMemcpyHostToDevice, s_));
+  CK(hipMemcpyAsync(d_hdr_.p, hdr.data(), hdr.size(), hipMemcpyHostToDevice, s_));
+  CK(hipMemcpyAsync(d_esegs_.p, segs.data(), sizeof(ScanSeg) * segs.size(), hipMemcpyHostToDevice, s_));
+  CK(hipStreamSynchronize(s_));
+  return kOk;
+}
+
+int Codec::run_encode(int bgr, bool fastdct, std::string *err) {
+  const EncFrame *fr = d_efr_.as<EncFrame>();
+  const EncTables *tab = d_etab_.as<EncTables>();
+  const ScanSeg *segs = d_esegs_.as<ScanSeg>();
+  const int n = en_;
+  CK(hipEventRecord(ev_[6], s_));
+  CK(enc_fdct(fr, n, emax_blocks_, tab, d_pix_.as<uint8_t>(), d_ecoef_.as<int16_t>(), bgr, fastdct ? 1 : 0, s_));
+  CK(enc_huff(fr, n, emax_blocks_, tab, d_ecoef_.as<int16_t>(), d_bits_.as<uint32_t>(), nullptr, nullptr, false, s_));
+  uint32_t *total_bits = d_etotals_.as<uint32_t>();
+  CK(scan_u32(segs, n, (emax_blocks_ + kScanTile - 1) / kScanTile, d_bits_.as<uint32_t>(), d_bitoff_.as<uint32_t>(),
+              d_etsum_.as<uint32_t>(), total_bits, false, s_));
+  CK(hipMemsetAsync(d_stream_.p, 0, ebits_bytes_, s_));
+  CK(enc_huff(fr, n, emax_blocks_, tab, d_ecoef_.as<int16_t>(), nullptr, d_bitoff_.as<uint32_t>(),
+              d_stream_.as<uint8_t>(), true, s_));
+  CK(hipEventRecord(ev_[7], s_));
+  CK(enc_ff_count(fr, n, emax_tiles_, total_bits, d_stream_.as<uint8_t>(), d_ffcnt_.as<uint32_t>(), s_));
+  uint32_t *nff = d_etotals_.as<uint32_t>() + n;
+  CK(scan_u32(segs + n, n, (emax_tiles_ + kScanTile - 1) / kScanTile, d_ffcnt_.as<uint32_t>(),
+              d_ffcnt_.as<uint32_t>(), d_etsum_.as<uint32_t>(), nff, false, s_));
+  CK(enc_ff_write(fr, n, emax_tiles_, total_bits, d_stream_.as<uint8_t>(), d_ffcnt_.as<uint32_t>(), nff,
+                  d_hdr_.as<uint8_t>(), d_out_.as<uint8_t>(), d_outsize_.as<uint64_t>(), s_));
+  CK(hipEventRecord(ev_[8], s_));
+  return kOk;
+}
+
+// Sizes -> caps check -> D2H of every JPEG into the caller's buffers.
+int Codec::fetch_jpegs(uint8_t *const *outs, const size_t *caps, size_t *sizes, std::string *err) {
+  const int n = en_;
+  std::vector<uint64_t> sz((size_t)n);
+  CK(hipMemcpyAsync(sz.data(), d_outsize_.p, sizeof(uint64_t) * (size_t)n, hipMemcpyDeviceToHost, s_));
+  CK(hipStreamSynchronize(s_));
+  uint64_t total = 0;
+  for (int f = 0; f < n; ++f) {
+    sizes[f] = (size_t)sz[(size_t)f];
+    total += align_up(sz[(size_t)f], 64);
+  }
+  for (int f = 0; f < n; ++f)
+    if (sz[(size_t)f] > caps[f] || !outs[f]) {
+      *err = "frame " + std::to_string(f) + ": output buffer of " + std::to_string(caps[f]) +
+             " bytes is too small for the " + std::to_string(sz[(size_t)f]) + "-byte JPEG";
+      return kInvalid;
+    }
+  CK(h_out_.ensure(total));
+  uint64_t off = 0;
+  std::vector<uint64_t> offs((size_t)n);
+  for (int f = 0; f < n; ++f) {
+    offs[(size_t)f] = off;
+    CK(hipMemcpyAsync(h_out_.as<uint8_t>() + off, d_out_.as<uint8_t>() + efr_[(size_t)f].out_off, sz[(size_t)f],
+                      hipMemcpyDeviceToHost, s_));
+    off += align_up(sz[(size_t)f], 64);
+  }
+  CK(hipStreamSynchronize(s_));
+  for (int f = 0; f < n; ++f) std::memcpy(outs[f], h_out_.as<uint8_t>() + offs[(size_t)f], sz[(size_t)f]);
+  return kOk;
+}
+
+// ---- public operations ---------------------------------------------------------------------------
+
+int Codec::encode(const uint8_t *const *imgs, const int *ws, const int *hs, int n, int pixel_format, int quality,
+                  int subsamp, int flags, uint8_t *const *outs, const size_t *caps, size_t *sizes, std::string *err) {
+  int rc = init(err);
+  if (rc) return rc;
+  if (n <= 0) return kOk;
+  if (pixel_format != 0 && pixel_format != 1) {
+    *err = "pixel_format must be TJPF_RGB (0) or TJPF_BGR (1)";
+    return kInvalid;
+  }
+  std::vector<uint64_t> offs((size_t)n);
+  uint64_t pix = 0;
+  for (int f = 0; f < n; ++f) {
+    if (!imgs[f] || ws[f] <= 0 || hs[f] <= 0 || ws[f] > 65535 || hs[f] > 65535) {
+      *err = "frame " + std::to_string(f) + ": bad image";
+      return kInvalid;
+    }
+    offs[(size_t)f] = pix;
+    pix += align_up((size_t)ws[f] * hs[f] * 3, 256);
+  }
+  const bool fast = (flags & kFlagFastDct) != 0;
+  if ((rc = prepare_encode(ws, hs, offs.data(), n, quality, subsamp, fast, err))) return rc;
+  CK(h_stage_.ensure(pix));
+  CK(d_pix_.ensure(pix));
+  for (int f = 0; f < n; ++f)
+    std::memcpy(h_stage_.as<uint8_t>() + offs[(size_t)f], imgs[f], (size_t)ws[f] * hs[f] * 3);
+  CK(hipMemcpyAsync(d_pix_.p, h_stage_.p, pix, hipMemcpyHostToDevice, s_));
+  if ((rc = run_encode(pixel_format, fast, err))) return rc;
+  return fetch_jpegs(outs, caps, sizes, err);
+}
+
+int Codec::decode(const uint8_t *const *jpegs, const size_t *jsizes, int n, int pixel_format, int flags,
+                  uint8_t *const *outs, const size_t *caps, std::string *err) {
+  int rc = init(err);
+  if (rc) return rc;
+  if (n <= 0) return kOk;
+  if (pixel_format != 0 && pixel_format != 1) {
+    *err = "pixel_format must be TJPF_RGB (0) or TJPF_BGR (1)";
+    return kInvalid;
+  }
+  if ((rc = prepare_decode(jpegs, jsizes, n, flags, err))) return rc;
+  for (int f = 0; f < n; ++f) {
+    const size_t need = (size_t)dfr_[(size_t)f].g.w * dfr_[(size_t)f].g.h * 3;
+    if (!outs[f] || caps[f] < need) {
+      *err = "frame " + std::to_string(f) + ": output buffer smaller than " + std::to_string(need) + " bytes";
+      return kInvalid;
+    }
+  }
+  if ((rc = run_decode(pixel_format, false, err))) return rc;
+  if ((rc = check_decode(err))) return rc;
+  CK(h_out_.ensure(dpix_bytes_));
+  CK(hipMemcpyAsync(h_out_.p, d_pix_.p, dpix_bytes_, hipMemcpyDeviceToHost, s_));
+  CK(hipStreamSynchronize(s_));
+  for (int f = 0; f < n; ++f)
+    std::memcpy(outs[f], h_out_.as<uint8_t>() + dfr_[(size_t)f].out_off,
+                (size_t)dfr_[(size_t)f].g.w * dfr_[(size_t)f].g.h * 3);
+  return kOk;
+}
+
+int Codec::invert(const uint8_t *const *jpegs, const size_t *jsizes, int n, int quality, int subsamp, int flags,
+                  uint8_t *const *outs, const size_t *caps, size_t *sizes, std::string *err) {
+  int rc = init(err);
+  if (rc) return rc;
+  if (n <= 0) return kOk;
+  if ((rc = prepare_decode(jpegs, jsizes, n, flags, err))) return rc;
+  std::vector<int> ws((size_t)n), hs((size_t)n);
+  std::vector<uint64_t> offs((size_t)n);
+  for (int f = 0; f < n; ++f) {
+    ws[(size_t)f] = dfr_[(size_t)f].g.w;
+    hs[(size_t)f] = dfr_[(size_t)f].g.h;
+    offs[(size_t)f] = dfr_[(size_t)f].out_off;
+  }
+  const bool fast = (flags & kFlagFastDct) != 0;
+  if ((rc = prepare_encode(ws.data(), hs.data(), offs.data(), n, quality, subsamp, fast, err))) return rc;
+  // decode (BGR, inverted: cv2.bitwise_not, inverter.py:41) straight into the encoder's input
+  if ((rc = run_decode(1, true, err))) return rc;
+  if ((rc = run_encode(1, fast, err))) return rc;
+  if ((rc = check_decode(err))) return rc;
+  return fetch_jpegs(outs, caps, sizes, err);
+}
+
+int Codec::bench_invert(const uint8_t *const *jpegs, const size_t *jsizes, int n, int quality, int subsamp,
+                        int flags, int iters, float *ms, float *stage_ms, std::string *err) {
+  int rc = init(err);
+  if (rc) return rc;
+  if (n <= 0 || iters <= 0) {
+    *err = "bench_invert: empty batch or iters <= 0";
+    return kInvalid;
+  }
+  if ((rc = prepare_decode(jpegs, jsizes, n, flags, err))) return rc;
+  std::vector<int> ws((size_t)n), hs((size_t)n);
+  std::vector<uint64_t> offs((size_t)n);
+  for (int f = 0; f < n; ++f) {
+    ws[(size_t)f] = dfr_[(size_t)f].g.w;
+    hs[(size_t)f] = dfr_[(size_t)f].g.h;
+    offs[(size_t)f] = dfr_[(size_t)f].out_off;
+  }
+  const bool fast = (flags & kFlagFastDct) != 0;
+  if ((rc = prepare_encode(ws.data(), hs.data(), offs.data(), n, quality, subsamp, fast, err))) return rc;
+  float acc[8] = {0};
+  double total_ms = 0;
+  int passes = 0;
+  for (int it = 0; it < iters; ++it) {
+    CK(hipStreamSynchronize(s_));
+    const auto t0 = std::chrono::steady_clock::now();
+    if ((rc = run_decode(1, true, err))) return rc;
+    if ((rc = run_encode(1, fast, err))) return rc;
+    CK(hipStreamSynchronize(s_));
+    total_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    passes += sync_passes_;
+    // stage times: unstuff, sync, write, dc+idct, colour, fdct+huff, stuff
+    const int pairs[7][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 4}, {4, 5}, {6, 7}, {7, 8}};
+    for (int i = 0; i < 7; ++i) {
+      float t = 0.f;
+      if (hipEventElapsedTime(&t, ev_[pairs[i][0]], ev_[pairs[i][1]]) == hipSuccess) acc[i] += t;
+    }
+  }
+  if ((rc = check_decode(err))) return rc;
+  *ms = (float)(total_ms / iters);
+  if (stage_ms) {
+    for (int i = 0; i < 7; ++i) stage_ms[i] = acc[i] / iters;
+    stage_ms[7] = (float)passes / iters;  // mean sync passes
+  }
+  return kOk;
+}
+
+int header_info(const uint8_t *jpeg, size_t size, int *w, int *h, int *subsamp, int *colorspace, std::string *err) {
+  Parsed P;
+  if (!jpeg || parse(jpeg, size, &P, err) != 0) {
+    if (!jpeg) *err = "NULL JPEG buffer";
+    return kJpeg;
+  }
+  *w = P.w;
+  *h = P.h;
+  *subsamp = subsamp_of(P);
+  *colorspace = P.ncomp == 1 ? 2 : 1;  // TJCS_GRAY = 2, TJCS_YCbCr = 1
+  return kOk;
+}
+
+size_t buffer_size(int w, int h, int subsamp) {
+  if (w <= 0 || h <= 0 || subsamp < 0 || subsamp > 4) return 0;
+  const int nc = subsamp == 3 ? 1 : 3;
+  const int hsamp[3] = {kSampH[subsamp], 1, 1}, vsamp[3] = {kSampV[subsamp], 1, 1};
+  Geom g;
+  if (!make_geom(w, h, nc, hsamp, vsamp, &g)) return 0;
+  return 1024 + 2 * (size_t)g.nblocks * kMaxBlockBytes + 2;
+}
+
+}  // namespace jpeg
+}  // namespace vf

@@ -1,0 +1,1029 @@
+// vf_jpeg_kernels.hip — gfx950 kernels of the baseline-JPEG path.
+//
+// The reference's default mode (use_jpeg=True) runs, per frame, PyTurboJPEG decode ->
+// cv2.bitwise_not -> PyTurboJPEG encode (inverter.py:32 -> :41 -> :44; the app encodes at
+// webcam_app.py:110 and decodes at :140).  The integer arithmetic here is libjpeg-turbo's
+// (the codec under PyTurboJPEG), so outputs are bit-exact with it; oracle/vf_jpeg_oracle.c
+// restates the same algorithm on the CPU and is pinned against the image's libjpeg-turbo.
+//
+// Decoder (one batch of frames, grid.y = frame):
+//   unstuff      FF00 -> FF over 4 KiB tiles (count, segmented scan, compact)
+//   sync         parallel Huffman decoding over fixed 1024-bit subsequences.  A thread
+//                decodes its subsequence from a guessed entry state (bit position,
+//                coefficient index z, block-in-MCU c); JPEG's prefix codes re-synchronise
+//                within a few symbols, so after a pass every thread's exit state is right
+//                once its entry state is.  Passes feed each thread its predecessor's exit
+//                state until no exit state changes (Weissenberger & Schmidt, "Massively
+//                parallel Huffman decoding on GPUs", ICPP 2018 — self-synchronisation).
+//   write        the converged entry states + a scan of per-subsequence block counts give
+//                every subsequence its first block; coefficients land in zigzag order,
+//                DC differences in per-component sequences
+//   dc           segmented inclusive scan of the DC differences (jdhuff.c last_dc_val)
+//   idct         dequantise + islow IDCT (jidctint.c) into component planes
+//   color        fancy upsampling (jdsample.c) + YCbCr -> BGR (jdcolor.c), optionally ~x
+// Encoder:
+//   fdct         colour conversion (jccolor.c) + edge replication + downsampling
+//                (jcsample.c) + islow / ifast forward DCT + reciprocal quantisation
+//                (jcdctmgr.c), 8 lanes per block
+//   huff         per-block Huffman bit length (jchuff.c encode_one_block, dummy edge blocks
+//                of jccoefct.c), segmented exclusive scan, then each block emits its bits
+//                at its offset (atomicOr on the two boundary words)
+//   stuff        0xFF -> FF 00 with a tile scan; header, EOI
+// No MFMA / LDS tiling: the work is integer butterflies and bit manipulation; the entropy
+// stages are latency-bound per thread and are parallelised across blocks / subsequences.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "vf_jpeg.h"
+
+namespace vf {
+namespace jpeg {
+
+namespace {
+
+// zigzag position -> natural (row-major) index (jutils.c jpeg_natural_order)
+__constant__ uint8_t kNat[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
+                                 12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
+                                 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
+                                 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+
+__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+
+// ---- workgroup scans (256 threads = 4 waves of 64) -----------------------------------------
+template <typename T>
+__device__ __forceinline__ T wave_incl_scan(T x) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const T y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  return x;
+}
+
+// exclusive scan of v over the workgroup; *total = the sum.  sh: 4 T of LDS.
+template <typename T>
+__device__ __forceinline__ T wg_excl_scan(T v, T *sh, T *total) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const T x = wave_incl_scan(v);
+  if (lane == 63) sh[wid] = x;
+  __syncthreads();
+  T base = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const T s = sh[i];
+    if (i < wid) base += s;
+    tot += s;
+  }
+  __syncthreads();
+  *total = tot;
+  return base + x - v;
+}
+
+// ---- segmented scan ----------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void seg_tile_sum(const ScanSeg *segs, const T *in, T *tsum) {
+  const ScanSeg sg = segs[blockIdx.y];
+  const uint64_t t0 = (uint64_t)blockIdx.x * kScanTile;
+  if (t0 >= sg.len) return;
+  __shared__ T sh[4];
+  const uint64_t b0 = t0 + (uint64_t)threadIdx.x * kScanPerThread;
+  T acc = 0;
+#pragma unroll
+  for (int j = 0; j < kScanPerThread; ++j)
+    if (b0 + j < sg.len) acc += in[sg.base + b0 + j];
+  T tot;
+  (void)wg_excl_scan(acc, sh, &tot);
+  if (threadIdx.x == 0) tsum[sg.tile0 + blockIdx.x] = tot;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void seg_tsum_scan(const ScanSeg *segs, T *tsum, T *totals) {
+  const ScanSeg sg = segs[blockIdx.x];
+  const uint32_t nt = (uint32_t)((sg.len + kScanTile - 1) / kScanTile);
+  __shared__ T sh[4];
+  T carry = 0;
+  for (uint32_t c = 0; c < nt; c += 256) {
+    const uint32_t i = c + threadIdx.x;
+    const T v = i < nt ? tsum[sg.tile0 + i] : T(0);
+    T tot;
+    const T ex = wg_excl_scan(v, sh, &tot);
+    if (i < nt) tsum[sg.tile0 + i] = carry + ex;
+    carry += tot;
+  }
+  if (threadIdx.x == 0 && totals) totals[blockIdx.x] = carry;
+}
+
+template <typename T, bool INCL>
+__global__ __launch_bounds__(256) void seg_apply(const ScanSeg *segs, const T *in, const T *tsum, T *out) {
+  const ScanSeg sg = segs[blockIdx.y];
+  const uint64_t t0 = (uint64_t)blockIdx.x * kScanTile;
+  if (t0 >= sg.len) return;
+  __shared__ T sh[4];
+  const uint64_t b0 = t0 + (uint64_t)threadIdx.x * kScanPerThread;
+  T v[kScanPerThread];
+  T acc = 0;
+#pragma unroll
+  for (int j = 0; j < kScanPerThread; ++j) {
+    v[j] = b0 + j < sg.len ? in[sg.base + b0 + j] : T(0);
+    acc += v[j];
+  }
+  T tot;
+  T run = tsum[sg.tile0 + blockIdx.x] + wg_excl_scan(acc, sh, &tot);
+#pragma unroll
+  for (int j = 0; j < kScanPerThread; ++j) {
+    if (INCL) run += v[j];
+    if (b0 + j < sg.len) out[sg.base + b0 + j] = run;
+    if (!INCL) run += v[j];
+  }
+}
+
+template <typename T>
+hipError_t seg_scan(const ScanSeg *segs, int nseg, uint32_t max_tiles, const T *in, T *out, T *tsum,
+                    T *totals, bool inclusive, hipStream_t s) {
+  if (nseg <= 0 || max_tiles == 0) return hipSuccess;
+  const dim3 g(max_tiles, (unsigned)nseg);
+  hipLaunchKernelGGL(seg_tile_sum<T>, g, dim3(256), 0, s, segs, in, tsum);
+  hipLaunchKernelGGL(seg_tsum_scan<T>, dim3((unsigned)nseg), dim3(256), 0, s, segs, tsum, totals);
+  if (inclusive) hipLaunchKernelGGL((seg_apply<T, true>), g, dim3(256), 0, s, segs, in, tsum, out);
+  else hipLaunchKernelGGL((seg_apply<T, false>), g, dim3(256), 0, s, segs, in, tsum, out);
+  return hipGetLastError();
+}
+
+// ---- decoder: unstuffing --------------------------------------------------------------------
+
+// keep-mask of the 16 raw bytes [i0, i0 + 16): a 0x00 right after 0xFF is stuffing
+__device__ __forceinline__ uint32_t keep_mask(const uint8_t *s, uint32_t len, uint32_t i0, uint8_t *bytes) {
+  uint32_t m = 0;
+  uint8_t prev = i0 ? s[i0 - 1] : 0;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const uint32_t i = i0 + j;
+    const uint8_t b = i < len ? s[i] : 0;
+    bytes[j] = b;
+    if (i < len && !(b == 0 && prev == 0xFF)) m |= 1u << j;
+    prev = b;
+  }
+  return m;
+}
+
+__global__ __launch_bounds__(256) void k_unstuff_count(const DecFrame *fr, const uint8_t *in, uint32_t *cnt) {
+  const DecFrame &F = fr[blockIdx.y];
+  if (blockIdx.x >= F.ntiles) return;
+  __shared__ uint32_t sh[4];
+  uint8_t bytes[16];
+  const uint32_t i0 = blockIdx.x * kTile + threadIdx.x * 16;
+  const uint32_t m = keep_mask(in + F.in_off, F.in_len, i0, bytes);
+  uint32_t tot;
+  (void)wg_excl_scan((uint32_t)__popc(m), sh, &tot);
+  if (threadIdx.x == 0) cnt[F.tile0 + blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(256) void k_unstuff_write(const DecFrame *fr, const uint8_t *in, const uint32_t *off,
+                                                       const uint32_t *us_len, uint8_t *us) {
+  const DecFrame &F = fr[blockIdx.y];
+  if (blockIdx.x >= F.ntiles) return;
+  __shared__ uint32_t sh[4];
+  uint8_t bytes[16];
+  const uint32_t i0 = blockIdx.x * kTile + threadIdx.x * 16;
+  const uint32_t m = keep_mask(in + F.in_off, F.in_len, i0, bytes);
+  uint32_t tot;
+  uint32_t pos = off[F.tile0 + blockIdx.x] + wg_excl_scan((uint32_t)__popc(m), sh, &tot);
+  uint8_t *d = us + F.us_off;
+#pragma unroll
+  for (int j = 0; j < 16; ++j)
+    if (m >> j & 1) d[pos++] = bytes[j];
+  // zero tail for the bit reader (libjpeg feeds zeros past the data, jdhuff.c)
+  if (blockIdx.x == F.ntiles - 1 && threadIdx.x < 32) d[us_len[blockIdx.y] + threadIdx.x] = 0;
+}
+
+// ---- decoder: Huffman ------------------------------------------------------------------------
+
+struct BitReader {
+  const uint32_t *w;
+  uint64_t buf;  // next bits, left-aligned
+  uint32_t nb;   // valid bits in buf
+  uint32_t wi;   // next word to load
+  uint32_t pos;  // bit position of the next unread bit
+  __device__ __forceinline__ void init(const uint8_t *base, uint32_t p) {
+    w = reinterpret_cast<const uint32_t *>(base);
+    wi = p >> 5;
+    buf = ((uint64_t)bswap32(w[wi]) << 32) | bswap32(w[wi + 1]);
+    wi += 2;
+    const uint32_t sk = p & 31;
+    buf <<= sk;
+    nb = 64 - sk;
+    pos = p;
+  }
+  __device__ __forceinline__ void refill() {  // afterwards nb >= 33
+    if (nb <= 32) {
+      buf |= (uint64_t)bswap32(w[wi++]) << (32 - nb);
+      nb += 32;
+    }
+  }
+  __device__ __forceinline__ uint32_t peek(uint32_t n) const { return (uint32_t)(buf >> (64 - n)); }
+  __device__ __forceinline__ void skip(uint32_t n) {
+    buf <<= n;
+    nb -= n;
+    pos += n;
+  }
+};
+
+// jdhuff.c jpeg_huff_decode with a kLook-bit first level
+__device__ __forceinline__ uint32_t huff_sym(BitReader &br, const HuffDec &t) {
+  const uint32_t e = t.fast[br.peek(kLook)];
+  uint32_t len = e >> 8, sym = e & 0xFF;
+  if (len == 0) {
+    const uint32_t c16 = br.peek(16);
+    len = 16;
+    sym = 0;  // corrupt code: jdhuff.c returns 0
+    for (uint32_t l = kLook + 1; l <= 16; ++l) {
+      const int32_t c = (int32_t)(c16 >> (16 - l));
+      if (c <= t.maxcode[l]) {
+        sym = t.vals[(uint32_t)(c + t.valoff[l]) & 255];
+        len = l;
+        break;
+      }
+    }
+  }
+  br.skip(len);
+  return sym;
+}
+
+__device__ __forceinline__ int extend(uint32_t v, uint32_t s) {  // jdhuff.h HUFF_EXTEND
+  return v < (1u << (s - 1)) ? (int)v - (int)((1u << s) - 1) : (int)v;
+}
+
+__device__ __forceinline__ uint64_t pack_state(uint32_t pos, uint32_t z, uint32_t c) {
+  return ((uint64_t)pos << 16) | (z << 8) | c;
+}
+
+// Decode symbols from the reader's position until it reaches `end` (checked at symbol
+// boundaries).  State: z = next zigzag index of the current block (0 = DC next), c = its
+// block-in-MCU, blk = its block index (WRITE only), blocks = blocks completed.
+template <bool WRITE>
+__device__ __forceinline__ void decode_span(BitReader &br, uint32_t end, uint32_t &z, uint32_t &c,
+                                            uint32_t &blocks, const Geom &g, const HuffDec *dcT,
+                                            const HuffDec *acT, uint32_t blk, int16_t *coef, int32_t *dcseq,
+                                            const uint64_t *dcbase) {
+  while (br.pos < end) {
+    if (WRITE && blk >= (uint32_t)g.nblocks) break;
+    br.refill();
+    const int k = g.bcomp[c];
+    if (z == 0) {
+      uint32_t s = huff_sym(br, dcT[k]);
+      int v = 0;
+      if (s) {
+        if (s > 16) s = 16;  // corrupt table
+        v = extend(br.peek(s), s);
+        br.skip(s);
+      }
+      if (WRITE) {
+        const uint32_t mcu = blk / (uint32_t)g.bpm;
+        dcseq[dcbase[k] + (uint64_t)mcu * (g.mh[k] * g.mv[k]) + (c - g.cfirst[k])] = v;
+      }
+      z = 1;
+    } else {
+      const uint32_t rs = huff_sym(br, acT[k]);
+      const uint32_t r = rs >> 4, s = rs & 15;
+      if (s) {
+        z += r;
+        const int v = extend(br.peek(s), s);
+        br.skip(s);
+        if (WRITE) coef[(uint64_t)blk * 64 + (z < 63 ? z : 63)] = (int16_t)v;
+        z++;
+      } else if (r == 15) {
+        z += 16;
+      } else {
+        z = 64;
+      }
+    }
+    if (z >= 64) {
+      z = 0;
+      c = (c + 1 == (uint32_t)g.bpm) ? 0 : c + 1;
+      ++blocks;
+      ++blk;
+    }
+  }
+}
+
+__device__ __forceinline__ void load_tables(const DecFrame &F, HuffDec *tabs) {
+  const uint32_t *src = reinterpret_cast<const uint32_t *>(&F.dc[0]);
+  uint32_t *dst = reinterpret_cast<uint32_t *>(tabs);
+  constexpr uint32_t nw = 6 * sizeof(HuffDec) / 4;
+  for (uint32_t j = threadIdx.x; j < nw; j += 256) dst[j] = src[j];
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(256) void k_sync(const DecFrame *fr, const uint8_t *us, const uint32_t *us_len,
+                                              const uint64_t *exit_in, uint64_t *exit_out, const uint32_t *cnt_in,
+                                              uint32_t *cnt_out, uint64_t *used, uint32_t *changed, int pass) {
+  __shared__ HuffDec tabs[6];
+  const DecFrame &F = fr[blockIdx.y];
+  if (blockIdx.x * 256 >= F.nsub_max) return;
+  load_tables(F, tabs);
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= F.nsub_max) return;
+  const uint32_t gi = F.sub0 + i;
+  const uint32_t nbits = us_len[blockIdx.y] * 8u;
+  const uint32_t nsub = (nbits + kSubBits - 1) / kSubBits;
+  if (i >= nsub) {
+    cnt_out[gi] = 0;
+    exit_out[gi] = pack_state(nbits, 0, 0);
+    return;
+  }
+  uint64_t st;
+  if (i == 0) st = 0;
+  else if (pass == 0) st = pack_state(i * kSubBits, 0, 0);
+  else st = exit_in[gi - 1];
+  if (pass > 0 && st == used[gi]) {  // same entry state as last pass: same result
+    exit_out[gi] = exit_in[gi];
+    cnt_out[gi] = cnt_in[gi];
+    return;
+  }
+  used[gi] = st;
+  const uint32_t end = (i + 1 == nsub) ? nbits : (i + 1) * kSubBits;
+  BitReader br;
+  br.init(us + F.us_off, (uint32_t)(st >> 16));
+  uint32_t z = (st >> 8) & 0xFF, c = st & 0xFF, blocks = 0;
+  decode_span<false>(br, end, z, c, blocks, F.g, tabs, tabs + 3, 0, nullptr, nullptr, nullptr);
+  const uint64_t ex = pack_state(br.pos, z, c);
+  exit_out[gi] = ex;
+  cnt_out[gi] = blocks;
+  if (pass == 0 || ex != exit_in[gi] || blocks != cnt_in[gi]) atomicOr(changed, 1u);
+}
+
+__global__ __launch_bounds__(256) void k_write(const DecFrame *fr, const uint8_t *us, const uint32_t *us_len,
+                                               const uint64_t *exits, const uint32_t *bstart, int16_t *coef,
+                                               int32_t *dcseq) {
+  __shared__ HuffDec tabs[6];
+  const DecFrame &F = fr[blockIdx.y];
+  if (blockIdx.x * 256 >= F.nsub_max) return;
+  load_tables(F, tabs);
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  const uint32_t nbits = us_len[blockIdx.y] * 8u;
+  const uint32_t nsub = (nbits + kSubBits - 1) / kSubBits;
+  if (i >= nsub) return;
+  const uint32_t gi = F.sub0 + i;
+  const uint64_t st = i == 0 ? 0 : exits[gi - 1];
+  const uint32_t end = (i + 1 == nsub) ? nbits : (i + 1) * kSubBits;
+  BitReader br;
+  br.init(us + F.us_off, (uint32_t)(st >> 16));
+  uint32_t z = (st >> 8) & 0xFF, c = st & 0xFF, blocks = 0;
+  decode_span<true>(br, end, z, c, blocks, F.g, tabs, tabs + 3, bstart[gi], coef + F.blk0 * 64, dcseq,
+                    F.dcbase);
+}
+
+// ---- decoder: IDCT -------------------------------------------------------------------------
+
+#define FIX_0_298631336 2446
+#define FIX_0_390180644 3196
+#define FIX_0_541196100 4433
+#define FIX_0_765366865 6270
+#define FIX_0_899976223 7373
+#define FIX_1_175875602 9633
+#define FIX_1_501321110 12299
+#define FIX_1_847759065 15137
+#define FIX_1_961570560 16069
+#define FIX_2_053119869 16819
+#define FIX_2_562915447 20995
+#define FIX_3_072711026 25172
+#define DESCALE(x, n) (((x) + ((int32_t)1 << ((n)-1))) >> (n))
+
+// jidctint.c jpeg_idct_islow, one 8-point line; `shift` 11 (pass 1) or 18 (pass 2)
+__device__ __forceinline__ void idct_line(const int32_t in[8], int32_t out[8], int shift) {
+  int32_t tmp0, tmp1, tmp2, tmp3, tmp10, tmp11, tmp12, tmp13, z1, z2, z3, z4, z5;
+  z2 = in[2];
+  z3 = in[6];
+  z1 = (z2 + z3) * FIX_0_541196100;
+  tmp2 = z1 + z3 * -FIX_1_847759065;
+  tmp3 = z1 + z2 * FIX_0_765366865;
+  tmp0 = (in[0] + in[4]) * (1 << 13);
+  tmp1 = (in[0] - in[4]) * (1 << 13);
+  tmp10 = tmp0 + tmp3;
+  tmp13 = tmp0 - tmp3;
+  tmp11 = tmp1 + tmp2;
+  tmp12 = tmp1 - tmp2;
+  tmp0 = in[7];
+  tmp1 = in[5];
+  tmp2 = in[3];
+  tmp3 = in[1];
+  z1 = tmp0 + tmp3;
+  z2 = tmp1 + tmp2;
+  z3 = tmp0 + tmp2;
+  z4 = tmp1 + tmp3;
+  z5 = (z3 + z4) * FIX_1_175875602;
+  tmp0 *= FIX_0_298631336;
+  tmp1 *= FIX_2_053119869;
+  tmp2 *= FIX_3_072711026;
+  tmp3 *= FIX_1_501321110;
+  z1 *= -FIX_0_899976223;
+  z2 *= -FIX_2_562915447;
+  z3 *= -FIX_1_961570560;
+  z4 *= -FIX_0_390180644;
+  z3 += z5;
+  z4 += z5;
+  tmp0 += z1 + z3;
+  tmp1 += z2 + z4;
+  tmp2 += z2 + z3;
+  tmp3 += z1 + z4;
+  const int32_t r = (int32_t)1 << (shift - 1);
+  out[0] = (tmp10 + tmp3 + r) >> shift;
+  out[7] = (tmp10 - tmp3 + r) >> shift;
+  out[1] = (tmp11 + tmp2 + r) >> shift;
+  out[6] = (tmp11 - tmp2 + r) >> shift;
+  out[2] = (tmp12 + tmp1 + r) >> shift;
+  out[5] = (tmp12 - tmp1 + r) >> shift;
+  out[3] = (tmp13 + tmp0 + r) >> shift;
+  out[4] = (tmp13 - tmp0 + r) >> shift;
+}
+
+// jdmaster.c prepare_range_limit_table, post-IDCT part (RANGE_MASK 1023)
+__device__ __forceinline__ uint32_t idct_limit(int32_t x) {
+  const int32_t m = x & 1023;
+  return m < 128 ? (uint32_t)(m + 128) : m < 512 ? 255u : m < 896 ? 0u : (uint32_t)(m - 896);
+}
+
+__device__ __forceinline__ void block_pos(const Geom &g, uint32_t b, uint32_t *k, uint32_t *bx, uint32_t *by) {
+  const uint32_t mcu = b / (uint32_t)g.bpm, c = b % (uint32_t)g.bpm;
+  *k = (uint32_t)g.bcomp[c];
+  *bx = (mcu % (uint32_t)g.mcux) * (uint32_t)g.mh[*k] + (uint32_t)g.bxo[c];
+  *by = (mcu / (uint32_t)g.mcux) * (uint32_t)g.mv[*k] + (uint32_t)g.byo[c];
+}
+
+// 8 lanes per block, 32 blocks per workgroup
+__global__ __launch_bounds__(256) void k_idct(const DecFrame *fr, const int16_t *coef, const int32_t *dcseq,
+                                              uint8_t *planes) {
+  const DecFrame &F = fr[blockIdx.y];
+  const Geom &g = F.g;
+  if (blockIdx.x * 32 >= (uint32_t)g.nblocks) return;
+  __shared__ int32_t blkv[32][64];
+  __shared__ int32_t ws[32][8][9];
+  const uint32_t slot = threadIdx.x >> 3, r = threadIdx.x & 7;
+  const uint32_t b = blockIdx.x * 32 + slot;
+  const bool valid = b < (uint32_t)g.nblocks;
+  uint32_t k = 0, bx = 0, by = 0;
+  if (valid) {
+    block_pos(g, b, &k, &bx, &by);
+    const uint4 raw = *reinterpret_cast<const uint4 *>(coef + (F.blk0 + b) * 64 + r * 8);
+    const int16_t *v = reinterpret_cast<const int16_t *>(&raw);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t zz = r * 8 + j, n = kNat[zz];
+      int32_t x = v[j];
+      if (zz == 0) {
+        const uint32_t mcu = b / (uint32_t)g.bpm, c = b % (uint32_t)g.bpm;
+        x = (int16_t)dcseq[F.dcbase[k] + (uint64_t)mcu * (g.mh[k] * g.mv[k]) + (c - g.cfirst[k])];
+      }
+      blkv[slot][n] = x * (int32_t)F.q[k][n];
+    }
+  }
+  __syncthreads();
+  if (valid) {  // pass 1: column r
+    int32_t in[8], out[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) in[i] = blkv[slot][i * 8 + r];
+    idct_line(in, out, 11);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) ws[slot][i][r] = out[i];
+  }
+  __syncthreads();
+  if (valid) {  // pass 2: row r
+    int32_t in[8], out[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) in[i] = ws[slot][r][i];
+    idct_line(in, out, 18);
+    uint32_t lo = 0, hi = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      lo |= idct_limit(out[i]) << (8 * i);
+      hi |= idct_limit(out[i + 4]) << (8 * i);
+    }
+    uint8_t *p = planes + F.plane_off[k] + (uint64_t)(by * 8 + r) * (uint32_t)g.pw[k] + bx * 8;
+    *reinterpret_cast<uint2 *>(p) = make_uint2(lo, hi);
+  }
+}
+
+// ---- decoder: upsampling + colour ------------------------------------------------------------
+
+__device__ __forceinline__ int up_sample(const uint8_t *p, int pw, int dw, int dh, int he, int ve, bool fancy,
+                                         int x, int y) {
+  if (he == 1 && ve == 1) return p[(size_t)y * pw + x];
+  const int iy = y / ve < dh ? y / ve : dh - 1;
+  if (!fancy) return p[(size_t)iy * pw + x / he];
+  const uint8_t *r0 = p + (size_t)iy * pw;
+  if (he == 2 && ve == 1) {  // h2v1_fancy_upsample
+    const int i = x >> 1;
+    if (!(x & 1)) return i == 0 ? r0[0] : (3 * r0[i] + r0[i - 1] + 1) >> 2;
+    return i == dw - 1 ? r0[i] : (3 * r0[i] + r0[i + 1] + 2) >> 2;
+  }
+  int ny = (y & 1) ? iy + 1 : iy - 1;  // jdmainct.c context rows: edges replicate
+  ny = ny < 0 ? 0 : ny > dh - 1 ? dh - 1 : ny;
+  const uint8_t *r1 = p + (size_t)ny * pw;
+  if (he == 1) return (3 * r0[x] + r1[x] + ((y & 1) ? 2 : 1)) >> 2;  // h1v2_fancy_upsample
+  const int i = x >> 1;  // h2v2_fancy_upsample
+  const int t = 3 * r0[i] + r1[i];
+  if (!(x & 1)) return i == 0 ? (4 * t + 8) >> 4 : (3 * t + 3 * r0[i - 1] + r1[i - 1] + 8) >> 4;
+  return i == dw - 1 ? (4 * t + 7) >> 4 : (3 * t + 3 * r0[i + 1] + r1[i + 1] + 7) >> 4;
+}
+
+__device__ __forceinline__ uint32_t clamp255(int v) { return (uint32_t)(v < 0 ? 0 : v > 255 ? 255 : v); }
+
+__global__ __launch_bounds__(256) void k_color(const DecFrame *fr, const uint8_t *planes, uint8_t *pix, int bgr,
+                                               int invert) {
+  const DecFrame &F = fr[blockIdx.z];
+  const Geom &g = F.g;
+  const int y = blockIdx.y, x = blockIdx.x * 256 + threadIdx.x;
+  if (y >= g.h || x >= g.w) return;
+  int v[3];
+  for (int k = 0; k < g.ncomp; ++k) {
+    const int he = g.maxh / g.hs[k], ve = g.maxv / g.vs[k];
+    const int dw = (g.w * g.hs[k] + g.maxh - 1) / g.maxh, dh = (g.h * g.vs[k] + g.maxv - 1) / g.maxv;
+    const bool fancy = (F.flags & 1) && ((he == 2 && dw > 2) || (he == 1 && ve == 2));
+    v[k] = up_sample(planes + F.plane_off[k], g.pw[k], dw, dh, he, ve, fancy && (ve <= 2) && (he <= 2), x, y);
+  }
+  uint32_t r, gg, b;
+  if (g.ncomp == 1) {
+    r = gg = b = (uint32_t)v[0];
+  } else {  // jdcolor.c ycc_rgb_convert
+    const int xcr = v[2] - 128, xcb = v[1] - 128;
+    r = clamp255(v[0] + ((91881 * xcr + 32768) >> 16));
+    gg = clamp255(v[0] + ((-22554 * xcb + 32768 - 46802 * xcr) >> 16));
+    b = clamp255(v[0] + ((116130 * xcb + 32768) >> 16));
+  }
+  if (invert) {
+    r ^= 0xFF;
+    gg ^= 0xFF;
+    b ^= 0xFF;
+  }
+  uint8_t *o = pix + F.out_off + ((size_t)y * g.w + x) * 3;
+  o[0] = (uint8_t)(bgr ? b : r);
+  o[1] = (uint8_t)gg;
+  o[2] = (uint8_t)(bgr ? r : b);
+}
+
+// ---- encoder: colour + downsampling + FDCT + quantisation -----------------------------------
+
+// component k (0 = Y, 1 = Cb, 2 = Cr) of the pixel at (px, py), edges replicated (jccolor.c)
+__device__ __forceinline__ int comp_at(const uint8_t *img, int w, int h, int px, int py, int k, int ro, int bo) {
+  px = px < w ? px : w - 1;
+  py = py < h ? py : h - 1;
+  const uint8_t *p = img + ((size_t)py * w + px) * 3;
+  const int r = p[ro], g = p[1], b = p[bo];
+  if (k == 0) return (19595 * r + 38470 * g + 7471 * b + 32768) >> 16;
+  if (k == 1) return (-11059 * r - 21709 * g + 32768 * b + (128 << 16) + 32767) >> 16;
+  return (32768 * r - 27439 * g - 5329 * b + (128 << 16) + 32767) >> 16;
+}
+
+// sample (sx, sy) of component k's downsampled plane (jcsample.c + jcprepct.c edges)
+__device__ __forceinline__ int enc_sample(const Geom &g, const uint8_t *img, int k, int sx, int sy, int ro,
+                                          int bo) {
+  const int he = g.maxh / g.hs[k], ve = g.maxv / g.vs[k];
+  const int real_rows = ((g.h + g.maxv - 1) / g.maxv) * g.vs[k];
+  if (sy > real_rows - 1) sy = real_rows - 1;
+  if (he == 1 && ve == 1) return comp_at(img, g.w, g.h, sx, sy, k, ro, bo);
+  if (he == 2 && ve == 1)
+    return (comp_at(img, g.w, g.h, 2 * sx, sy, k, ro, bo) + comp_at(img, g.w, g.h, 2 * sx + 1, sy, k, ro, bo) +
+            (sx & 1)) >> 1;
+  if (he == 2 && ve == 2)
+    return (comp_at(img, g.w, g.h, 2 * sx, 2 * sy, k, ro, bo) + comp_at(img, g.w, g.h, 2 * sx + 1, 2 * sy, k, ro, bo) +
+            comp_at(img, g.w, g.h, 2 * sx, 2 * sy + 1, k, ro, bo) +
+            comp_at(img, g.w, g.h, 2 * sx + 1, 2 * sy + 1, k, ro, bo) + 1 + (sx & 1)) >> 2;
+  int sum = 0;  // int_downsample
+  for (int a = 0; a < ve; ++a)
+    for (int c = 0; c < he; ++c) sum += comp_at(img, g.w, g.h, sx * he + c, sy * ve + a, k, ro, bo);
+  return (sum + he * ve / 2) / (he * ve);
+}
+
+// jfdctint.c jpeg_fdct_islow, one line; pass 0 = rows, 1 = columns
+__device__ __forceinline__ void fdct_islow_line(int32_t p[8], int pass) {
+  int32_t tmp0 = p[0] + p[7], tmp7 = p[0] - p[7];
+  int32_t tmp1 = p[1] + p[6], tmp6 = p[1] - p[6];
+  int32_t tmp2 = p[2] + p[5], tmp5 = p[2] - p[5];
+  int32_t tmp3 = p[3] + p[4], tmp4 = p[3] - p[4];
+  const int32_t tmp10 = tmp0 + tmp3, tmp13 = tmp0 - tmp3;
+  const int32_t tmp11 = tmp1 + tmp2, tmp12 = tmp1 - tmp2;
+  const int sh = pass ? 15 : 11;
+  if (!pass) {
+    p[0] = (tmp10 + tmp11) * 4;
+    p[4] = (tmp10 - tmp11) * 4;
+  } else {
+    p[0] = DESCALE(tmp10 + tmp11, 2);
+    p[4] = DESCALE(tmp10 - tmp11, 2);
+  }
+  int32_t z1 = (tmp12 + tmp13) * FIX_0_541196100;
+  p[2] = DESCALE(z1 + tmp13 * FIX_0_765366865, sh);
+  p[6] = DESCALE(z1 + tmp12 * -FIX_1_847759065, sh);
+  z1 = tmp4 + tmp7;
+  int32_t z2 = tmp5 + tmp6, z3 = tmp4 + tmp6, z4 = tmp5 + tmp7;
+  const int32_t z5 = (z3 + z4) * FIX_1_175875602;
+  tmp4 *= FIX_0_298631336;
+  tmp5 *= FIX_2_053119869;
+  tmp6 *= FIX_3_072711026;
+  tmp7 *= FIX_1_501321110;
+  z1 *= -FIX_0_899976223;
+  z2 *= -FIX_2_562915447;
+  z3 *= -FIX_1_961570560;
+  z4 *= -FIX_0_390180644;
+  z3 += z5;
+  z4 += z5;
+  p[7] = DESCALE(tmp4 + z1 + z3, sh);
+  p[5] = DESCALE(tmp5 + z2 + z4, sh);
+  p[3] = DESCALE(tmp6 + z2 + z3, sh);
+  p[1] = DESCALE(tmp7 + z1 + z4, sh);
+}
+
+// jfdctfst.c jpeg_fdct_ifast, one line (both passes identical)
+__device__ __forceinline__ void fdct_ifast_line(int32_t p[8]) {
+  int32_t tmp0 = p[0] + p[7], tmp7 = p[0] - p[7];
+  int32_t tmp1 = p[1] + p[6], tmp6 = p[1] - p[6];
+  int32_t tmp2 = p[2] + p[5], tmp5 = p[2] - p[5];
+  int32_t tmp3 = p[3] + p[4], tmp4 = p[3] - p[4];
+  int32_t tmp10 = tmp0 + tmp3, tmp13 = tmp0 - tmp3;
+  int32_t tmp11 = tmp1 + tmp2, tmp12 = tmp1 - tmp2;
+  p[0] = tmp10 + tmp11;
+  p[4] = tmp10 - tmp11;
+  const int32_t z1 = ((tmp12 + tmp13) * 181) >> 8;
+  p[2] = tmp13 + z1;
+  p[6] = tmp13 - z1;
+  tmp10 = tmp4 + tmp5;
+  tmp11 = tmp5 + tmp6;
+  tmp12 = tmp6 + tmp7;
+  const int32_t z5 = ((tmp10 - tmp12) * 98) >> 8;
+  const int32_t z2 = ((tmp10 * 139) >> 8) + z5;
+  const int32_t z4 = ((tmp12 * 334) >> 8) + z5;
+  const int32_t z3 = (tmp11 * 181) >> 8;
+  const int32_t z11 = tmp7 + z3, z13 = tmp7 - z3;
+  p[5] = z13 + z2;
+  p[3] = z13 - z2;
+  p[1] = z11 + z4;
+  p[7] = z11 - z4;
+}
+
+// jcdctmgr.c quantize (16-bit DCTELEM reciprocal form)
+__device__ __forceinline__ int16_t quantize(int32_t x, uint32_t recip, uint32_t corr, int32_t shift) {
+  const int32_t t = (int16_t)x;
+  if (t < 0) {
+    const uint32_t p = ((uint32_t)(-t + (int32_t)corr) * recip) >> (shift + 16);
+    return (int16_t)(-(int16_t)p);
+  }
+  const uint32_t p = ((uint32_t)(t + (int32_t)corr) * recip) >> (shift + 16);
+  return (int16_t)p;
+}
+
+__global__ __launch_bounds__(256) void k_fdct(const EncFrame *fr, const EncTables *tab, const uint8_t *pix,
+                                              int16_t *coef, int bgr, int fastdct) {
+  const EncFrame &F = fr[blockIdx.y];
+  const Geom &g = F.g;
+  if (blockIdx.x * 32 >= (uint32_t)g.nblocks) return;
+  __shared__ int32_t ws[32][8][9];
+  __shared__ int16_t qo[32][64];
+  __shared__ uint16_t s_recip[2][64], s_corr[2][64];
+  __shared__ int16_t s_shift[2][64];
+  if (threadIdx.x < 128) {
+    const int t = threadIdx.x >> 6, i = threadIdx.x & 63;
+    s_recip[t][i] = tab->recip[t][i];
+    s_corr[t][i] = tab->corr[t][i];
+    s_shift[t][i] = tab->shift[t][i];
+  }
+  const uint32_t slot = threadIdx.x >> 3, r = threadIdx.x & 7;
+  const uint32_t b = blockIdx.x * 32 + slot;
+  uint32_t k = 0, bx = 0, by = 0;
+  bool real = false;
+  if (b < (uint32_t)g.nblocks) {
+    block_pos(g, b, &k, &bx, &by);
+    real = bx < (uint32_t)g.wb[k] && by < (uint32_t)g.hb[k];  // dummy blocks are made by enc_huff
+  }
+  const int ro = bgr ? 2 : 0, bo = 2 - ro;
+  const uint8_t *img = pix + F.img_off;
+  if (real) {  // pass 1: row r
+    int32_t v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = enc_sample(g, img, (int)k, (int)(bx * 8 + j), (int)(by * 8 + r), ro, bo) - 128;
+    if (fastdct) fdct_ifast_line(v);
+    else fdct_islow_line(v, 0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ws[slot][r][j] = v[j];
+  }
+  __syncthreads();
+  if (real) {  // pass 2: column r, quantised
+    int32_t v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = ws[slot][i][r];
+    if (fastdct) fdct_ifast_line(v);
+    else fdct_islow_line(v, 1);
+    const int t = k > 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int n = i * 8 + r;
+      qo[slot][n] = quantize(v[i], s_recip[t][n], s_corr[t][n], s_shift[t][n]);
+    }
+  }
+  __syncthreads();
+  if (real) {  // zigzag positions 8r .. 8r+7, one 16-byte store
+    int16_t o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = qo[slot][kNat[r * 8 + j]];
+    *reinterpret_cast<uint4 *>(coef + (F.blk0 + b) * 64 + r * 8) = *reinterpret_cast<const uint4 *>(o);
+  }
+}
+
+// ---- encoder: Huffman ------------------------------------------------------------------------
+
+// DC of block-in-MCU c of MCU `mcu`, following jccoefct.c for dummy blocks: a dummy block at
+// the right edge takes its left neighbour's DC, a dummy row at the bottom the DC of the
+// component's last block in the row above (within the MCU).
+__device__ __forceinline__ int enc_dc_of(const Geom &g, const int16_t *coef, uint32_t mcu, uint32_t c) {
+  const int k = g.bcomp[c];
+  int xi = g.bxo[c], yi = g.byo[c];
+  const int mx = (int)(mcu % (uint32_t)g.mcux), my = (int)(mcu / (uint32_t)g.mcux);
+  for (;;) {
+    const int bx = mx * g.mh[k] + xi, by = my * g.mv[k] + yi;
+    if (by >= g.hb[k]) {
+      yi -= 1;
+      xi = g.mh[k] - 1;
+      continue;
+    }
+    if (bx >= g.wb[k]) {
+      xi -= 1;
+      continue;
+    }
+    const uint32_t cc = (uint32_t)(g.cfirst[k] + yi * g.mh[k] + xi);
+    return coef[((uint64_t)mcu * g.bpm + cc) * 64];
+  }
+}
+
+template <bool EMIT>
+struct BitSink;
+
+template <>
+struct BitSink<false> {
+  uint32_t total = 0;
+  __device__ __forceinline__ void put(uint32_t, uint32_t size) { total += size; }
+  __device__ __forceinline__ void finish() {}
+};
+
+template <>
+struct BitSink<true> {
+  uint32_t *w;
+  uint32_t wi;
+  uint64_t acc;
+  uint32_t n;
+  bool first;
+  uint32_t total;
+  __device__ __forceinline__ BitSink(uint32_t *words, uint32_t off)
+      : w(words), wi(off >> 5), acc(0), n(off & 31), first(true), total(0) {}
+  __device__ __forceinline__ void put(uint32_t code, uint32_t size) {
+    acc = (acc << size) | code;
+    n += size;
+    if (n >= 32) {
+      n -= 32;
+      const uint32_t v = (uint32_t)(acc >> n);
+      if (first) atomicOr(w + wi, bswap32(v));  // shares its leading bits with the previous block
+      else w[wi] = bswap32(v);
+      first = false;
+      ++wi;
+      acc &= n ? ((1ull << n) - 1) : 0ull;
+    }
+  }
+  __device__ __forceinline__ void finish() {
+    if (n) atomicOr(w + wi, bswap32((uint32_t)(acc << (32 - n))));
+  }
+};
+
+template <bool EMIT>
+__device__ __forceinline__ uint32_t encode_block(const Geom &g, const int16_t *cb, uint32_t b,
+                                                 const uint32_t (*dcT)[16], const uint32_t (*acT)[256],
+                                                 BitSink<EMIT> &out) {
+  const uint32_t mcu = b / (uint32_t)g.bpm, c = b % (uint32_t)g.bpm;
+  const int k = g.bcomp[c];
+  const int t = k > 0;
+  const int dc = enc_dc_of(g, cb, mcu, c);
+  int pred = 0;
+  if ((int)c > g.cfirst[k]) pred = enc_dc_of(g, cb, mcu, c - 1);
+  else if (mcu > 0) pred = enc_dc_of(g, cb, mcu - 1, (uint32_t)(g.cfirst[k] + g.mh[k] * g.mv[k] - 1));
+  const int mx = (int)(mcu % (uint32_t)g.mcux), my = (int)(mcu / (uint32_t)g.mcux);
+  const bool dummy = mx * g.mh[k] + g.bxo[c] >= g.wb[k] || my * g.mv[k] + g.byo[c] >= g.hb[k];
+  // DC difference (jchuff.c encode_one_block)
+  const int diff = dc - pred;
+  const uint32_t a = (uint32_t)(diff < 0 ? -diff : diff);
+  const uint32_t nbits = a ? 32 - __clz(a) : 0;
+  uint32_t e = dcT[t][nbits];
+  out.put(e >> 8, e & 0xFF);
+  if (nbits) out.put((uint32_t)(diff < 0 ? diff - 1 : diff) & ((1u << nbits) - 1), nbits);
+  int run = 0;
+  if (!dummy) {
+    const uint4 *src = reinterpret_cast<const uint4 *>(cb + (uint64_t)b * 64);
+    for (int q = 0; q < 8; ++q) {
+      const uint4 raw = src[q];
+      const int16_t *vv = reinterpret_cast<const int16_t *>(&raw);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (q == 0 && j == 0) continue;
+        const int v = vv[j];
+        if (v == 0) {
+          ++run;
+          continue;
+        }
+        while (run > 15) {
+          e = acT[t][0xF0];
+          out.put(e >> 8, e & 0xFF);
+          run -= 16;
+        }
+        const uint32_t av = (uint32_t)(v < 0 ? -v : v);
+        const uint32_t nb = 32 - __clz(av);
+        e = acT[t][(run << 4) + nb];
+        out.put(e >> 8, e & 0xFF);
+        out.put((uint32_t)(v < 0 ? v - 1 : v) & ((1u << nb) - 1), nb);
+        run = 0;
+      }
+    }
+  } else {
+    run = 63;
+  }
+  if (run > 0) {
+    e = acT[t][0];
+    out.put(e >> 8, e & 0xFF);
+  }
+  return 0;
+}
+
+template <bool EMIT>
+__global__ __launch_bounds__(256) void k_huff(const EncFrame *fr, const EncTables *tab, const int16_t *coef,
+                                              uint32_t *bits, const uint32_t *bitoff, uint8_t *stream) {
+  const EncFrame &F = fr[blockIdx.y];
+  const Geom &g = F.g;
+  if (blockIdx.x * 256 >= (uint32_t)g.nblocks) return;
+  __shared__ uint32_t sdc[2][16], sac[2][256];
+  for (int i = threadIdx.x; i < 512; i += 256) sac[i >> 8][i & 255] = tab->ac[i >> 8][i & 255];
+  if (threadIdx.x < 32) sdc[threadIdx.x >> 4][threadIdx.x & 15] = tab->dc[threadIdx.x >> 4][threadIdx.x & 15];
+  __syncthreads();
+  const uint32_t b = blockIdx.x * 256 + threadIdx.x;
+  if (b >= (uint32_t)g.nblocks) return;
+  const int16_t *cb = coef + F.blk0 * 64;
+  if (EMIT) {
+    BitSink<true> out(reinterpret_cast<uint32_t *>(stream + F.bits_off), bitoff[F.blk0 + b]);
+    encode_block<true>(g, cb, b, sdc, sac, out);
+    out.finish();
+  } else {
+    BitSink<false> out;
+    encode_block<false>(g, cb, b, sdc, sac, out);
+    bits[F.blk0 + b] = out.total;
+  }
+}
+
+// ---- encoder: byte stuffing, header, EOI ------------------------------------------------------
+
+// the 16 bytes of the packed stream at i0, the final partial byte padded with ones
+__device__ __forceinline__ uint32_t ff_bytes(const uint8_t *s, uint32_t nbytes, uint32_t tb, uint32_t i0,
+                                             uint8_t *bytes) {
+  uint32_t n = 0;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const uint32_t i = i0 + j;
+    uint8_t v = i < nbytes ? s[i] : 0;
+    if (i == nbytes - 1 && (tb & 7)) v |= (uint8_t)(0xFF >> (tb & 7));
+    bytes[j] = v;
+    n += (i < nbytes && v == 0xFF);
+  }
+  return n;
+}
+
+__global__ __launch_bounds__(256) void k_ff_count(const EncFrame *fr, const uint32_t *total_bits,
+                                                  const uint8_t *stream, uint32_t *cnt) {
+  const EncFrame &F = fr[blockIdx.y];
+  if (blockIdx.x >= F.ntiles_max) return;
+  __shared__ uint32_t sh[4];
+  const uint32_t tb = total_bits[blockIdx.y], nbytes = (tb + 7) >> 3;
+  uint8_t bytes[16];
+  const uint32_t i0 = blockIdx.x * kTile + threadIdx.x * 16;
+  const uint32_t n = i0 < nbytes ? ff_bytes(stream + F.bits_off, nbytes, tb, i0, bytes) : 0;
+  uint32_t tot;
+  (void)wg_excl_scan(n, sh, &tot);
+  if (threadIdx.x == 0) cnt[F.tile0 + blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(256) void k_ff_write(const EncFrame *fr, const uint32_t *total_bits,
+                                                  const uint8_t *stream, const uint32_t *off, const uint32_t *nff,
+                                                  const uint8_t *hdr, uint8_t *out, uint64_t *out_size) {
+  const EncFrame &F = fr[blockIdx.y];
+  const uint32_t tb = total_bits[blockIdx.y], nbytes = (tb + 7) >> 3;
+  const uint32_t ntiles = (nbytes + kTile - 1) / kTile;
+  if (blockIdx.x >= ntiles) return;
+  __shared__ uint32_t sh[4];
+  uint8_t *o = out + F.out_off;
+  if (blockIdx.x == 0)
+    for (uint32_t j = threadIdx.x; j < F.hdr_len; j += 256) o[j] = hdr[F.hdr_off + j];
+  uint8_t bytes[16];
+  const uint32_t i0 = blockIdx.x * kTile + threadIdx.x * 16;
+  const uint32_t n = i0 < nbytes ? ff_bytes(stream + F.bits_off, nbytes, tb, i0, bytes) : 0;
+  uint32_t tot;
+  uint64_t pos = (uint64_t)F.hdr_len + i0 + off[F.tile0 + blockIdx.x] + wg_excl_scan(n, sh, &tot);
+  for (int j = 0; j < 16; ++j) {
+    if (i0 + j >= nbytes) break;
+    o[pos++] = bytes[j];
+    if (bytes[j] == 0xFF) o[pos++] = 0;
+  }
+  if (blockIdx.x == ntiles - 1 && threadIdx.x == 0) {
+    const uint64_t size = (uint64_t)F.hdr_len + nbytes + nff[blockIdx.y] + 2;
+    o[size - 2] = 0xFF;
+    o[size - 1] = 0xD9;
+    out_size[blockIdx.y] = size;
+  }
+}
+
+}  // namespace
+
+// ---- launchers -------------------------------------------------------------------------------
+
+hipError_t scan_u32(const ScanSeg *segs, int nseg, uint32_t max_tiles, const uint32_t *in, uint32_t *out,
+                    uint32_t *tsum, uint32_t *totals, bool inclusive, hipStream_t s) {
+  return seg_scan<uint32_t>(segs, nseg, max_tiles, in, out, tsum, totals, inclusive, s);
+}
+
+hipError_t scan_i32(const ScanSeg *segs, int nseg, uint32_t max_tiles, const int32_t *in, int32_t *out,
+                    int32_t *tsum, int32_t *totals, bool inclusive, hipStream_t s) {
+  return seg_scan<int32_t>(segs, nseg, max_tiles, in, out, tsum, totals, inclusive, s);
+}
+
+hipError_t dec_unstuff_count(const DecFrame *fr, int n, uint32_t max_tiles, const uint8_t *in, uint32_t *tile_cnt,
+                             hipStream_t s) {
+  if (n <= 0 || !max_tiles) return hipSuccess;
+  hipLaunchKernelGGL(k_unstuff_count, dim3(max_tiles, (unsigned)n), dim3(256), 0, s, fr, in, tile_cnt);
+  return hipGetLastError();
+}
+
+hipError_t dec_unstuff_write(const DecFrame *fr, int n, uint32_t max_tiles, const uint8_t *in,
+                             const uint32_t *tile_off, const uint32_t *us_len, uint8_t *us, hipStream_t s) {
+  if (n <= 0 || !max_tiles) return hipSuccess;
+  hipLaunchKernelGGL(k_unstuff_write, dim3(max_tiles, (unsigned)n), dim3(256), 0, s, fr, in, tile_off, us_len, us);
+  return hipGetLastError();
+}
+
+hipError_t dec_sync(const DecFrame *fr, int n, uint32_t max_sub, const uint8_t *us, const uint32_t *us_len,
+                    const uint64_t *exit_in, uint64_t *exit_out, const uint32_t *cnt_in, uint32_t *cnt_out,
+                    uint64_t *used, uint32_t *changed, int pass, hipStream_t s) {
+  if (n <= 0 || !max_sub) return hipSuccess;
+  hipLaunchKernelGGL(k_sync, dim3((max_sub + 255) / 256, (unsigned)n), dim3(256), 0, s, fr, us, us_len, exit_in,
+                     exit_out, cnt_in, cnt_out, used, changed, pass);
+  return hipGetLastError();
+}
+
+hipError_t dec_write(const DecFrame *fr, int n, uint32_t max_sub, const uint8_t *us, const uint32_t *us_len,
+                     const uint64_t *exits, const uint32_t *bstart, int16_t *coef, int32_t *dcseq, hipStream_t s) {
+  if (n <= 0 || !max_sub) return hipSuccess;
+  hipLaunchKernelGGL(k_write, dim3((max_sub + 255) / 256, (unsigned)n), dim3(256), 0, s, fr, us, us_len, exits,
+                     bstart, coef, dcseq);
+  return hipGetLastError();
+}
+
+hipError_t dec_idct(const DecFrame *fr, int n, uint32_t max_blocks, const int16_t *coef, const int32_t *dcseq,
+                    uint8_t *planes, hipStream_t s) {
+  if (n <= 0 || !max_blocks) return hipSuccess;
+  hipLaunchKernelGGL(k_idct, dim3((max_blocks + 31) / 32, (unsigned)n), dim3(256), 0, s, fr, coef, dcseq, planes);
+  return hipGetLastError();
+}
+
+hipError_t dec_color(const DecFrame *fr, int n, int max_w, int max_h, const uint8_t *planes, uint8_t *pix, int bgr,
+                     int invert, hipStream_t s) {
+  if (n <= 0 || max_w <= 0 || max_h <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_color, dim3((unsigned)((max_w + 255) / 256), (unsigned)max_h, (unsigned)n), dim3(256), 0, s,
+                     fr, planes, pix, bgr, invert);
+  return hipGetLastError();
+}
+
+hipError_t enc_fdct(const EncFrame *fr, int n, uint32_t max_blocks, const EncTables *tab, const uint8_t *pix,
+                    int16_t *coef, int bgr, int fastdct, hipStream_t s) {
+  if (n <= 0 || !max_blocks) return hipSuccess;
+  hipLaunchKernelGGL(k_fdct, dim3((max_blocks + 31) / 32, (unsigned)n), dim3(256), 0, s, fr, tab, pix, coef, bgr,
+                     fastdct);
+  return hipGetLastError();
+}
+
+hipError_t enc_huff(const EncFrame *fr, int n, uint32_t max_blocks, const EncTables *tab, const int16_t *coef,
+                    uint32_t *bits, const uint32_t *bitoff, uint8_t *stream, bool emit, hipStream_t s) {
+  if (n <= 0 || !max_blocks) return hipSuccess;
+  const dim3 g((max_blocks + 255) / 256, (unsigned)n);
+  if (emit) hipLaunchKernelGGL(k_huff<true>, g, dim3(256), 0, s, fr, tab, coef, bits, bitoff, stream);
+  else hipLaunchKernelGGL(k_huff<false>, g, dim3(256), 0, s, fr, tab, coef, bits, bitoff, stream);
+  return hipGetLastError();
+}
+
+hipError_t enc_ff_count(const EncFrame *fr, int n, uint32_t max_tiles, const uint32_t *total_bits,
+                        const uint8_t *stream, uint32_t *tile_cnt, hipStream_t s) {
+  if (n <= 0 || !max_tiles) return hipSuccess;
+  hipLaunchKernelGGL(k_ff_count, dim3(max_tiles, (unsigned)n), dim3(256), 0, s, fr, total_bits, stream, tile_cnt);
+  return hipGetLastError();
+}
+
+hipError_t enc_ff_write(const EncFrame *fr, int n, uint32_t max_tiles, const uint32_t *total_bits,
+                        const uint8_t *stream, const uint32_t *tile_off, const uint32_t *nff, const uint8_t *hdr,
+                        uint8_t *out, uint64_t *out_size, hipStream_t s) {
+  if (n <= 0 || !max_tiles) return hipSuccess;
+  hipLaunchKernelGGL(k_ff_write, dim3(max_tiles, (unsigned)n), dim3(256), 0, s, fr, total_bits, stream, tile_off,
+                     nff, hdr, out, out_size);
+  return hipGetLastError();
+}
+
+}  // namespace jpeg
+}  // namespace vf

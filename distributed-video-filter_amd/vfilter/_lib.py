@@ -18,13 +18,14 @@ from typing import Optional, Sequence
 import numpy as np
 
 LIB_NAME = "libvfilter_hip.so"
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 VF_OK = 0
 VF_E_INVALID = -1
 VF_E_HIP = -2
 VF_E_NOMEM = -3
 VF_E_NODEVICE = -4
+VF_E_JPEG = -5
 
 _c_int_p = ctypes.POINTER(ctypes.c_int)
 _c_float_p = ctypes.POINTER(ctypes.c_float)
@@ -64,6 +65,15 @@ SIGNATURES = {
     "vf_last_timeline": (ctypes.c_int, [_vp, _c_float_p, ctypes.POINTER(_sz), ctypes.c_int, _c_int_p]),
     "vf_bench_device_ring": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_int, _sz, ctypes.c_int, _vp, _c_float_p,
                                             _c_float_p]),
+    "vf_jpeg_header": (ctypes.c_int, [_vp, _sz, _c_int_p, _c_int_p, _c_int_p, _c_int_p]),
+    "vf_jpeg_buffer_size": (_sz, [ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+    "vf_jpeg_encode": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                      ctypes.c_int, _vp, _vp, _vp]),
+    "vf_jpeg_decode": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp, _vp]),
+    "vf_jpeg_invert": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp,
+                                      _vp, _vp]),
+    "vf_jpeg_bench_invert": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                            ctypes.c_int, _c_float_p, _c_float_p]),
 }
 
 
@@ -288,6 +298,98 @@ class Context:
             self._ctx, sa, da, nbuf, nbytes, steps, stream or None,
             out.ctypes.data_as(_c_float_p) if per_launch else None, ctypes.byref(region)))
         return region.value, (out[:steps] if per_launch else None)
+
+
+    # -- JPEG (default use_jpeg=True mode: inverter.py:32 -> :41 -> :44) -----------------------
+    @staticmethod
+    def _ptrs(bufs):
+        arrs = [b if isinstance(b, np.ndarray) else np.frombuffer(b, dtype=np.uint8) for b in bufs]
+        return arrs, (ctypes.c_void_p * len(arrs))(*[a.ctypes.data for a in arrs])
+
+    def jpeg_encode(self, imgs: Sequence[np.ndarray], pixel_format: int, quality: int, subsamp: int,
+                    flags: int = 0) -> list:
+        """Encode H x W x 3 uint8 images in one batched GPU pass; returns a list of bytes."""
+        n = len(imgs)
+        if n == 0:
+            return []
+        imgs = [np.ascontiguousarray(a, dtype=np.uint8) for a in imgs]
+        for a in imgs:
+            if a.ndim != 3 or a.shape[2] != 3:
+                raise ValueError("jpeg_encode: images must be H x W x 3 uint8")
+        _, ia = self._ptrs(imgs)
+        ws = (ctypes.c_int * n)(*[a.shape[1] for a in imgs])
+        hs = (ctypes.c_int * n)(*[a.shape[0] for a in imgs])
+        caps = [int(self._lib.vf_jpeg_buffer_size(a.shape[1], a.shape[0], subsamp)) for a in imgs]
+        if not all(caps):
+            raise ValueError("jpeg_encode: unsupported size or subsampling")
+        outs = [np.empty(c, np.uint8) for c in caps]
+        _, oa = self._ptrs(outs)
+        ca = (ctypes.c_size_t * n)(*caps)
+        sz = (ctypes.c_size_t * n)()
+        self._check(self._lib.vf_jpeg_encode(self._ctx, ia, ws, hs, n, pixel_format, quality, subsamp, flags,
+                                             oa, ca, sz))
+        return [outs[i][:sz[i]].tobytes() for i in range(n)]
+
+    def jpeg_decode(self, jpegs: Sequence, pixel_format: int, flags: int = 0) -> list:
+        """Decode JPEGs in one batched GPU pass; returns H x W x 3 uint8 arrays."""
+        n = len(jpegs)
+        if n == 0:
+            return []
+        srcs, ja = self._ptrs(jpegs)
+        outs = []
+        for s in srcs:
+            w, h, _, _ = jpeg_header(s)
+            outs.append(np.empty((h, w, 3), np.uint8))
+        _, oa = self._ptrs(outs)
+        js = (ctypes.c_size_t * n)(*[s.nbytes for s in srcs])
+        ca = (ctypes.c_size_t * n)(*[o.nbytes for o in outs])
+        self._check(self._lib.vf_jpeg_decode(self._ctx, ja, js, n, pixel_format, flags, oa, ca))
+        return outs
+
+    def jpeg_invert(self, jpegs: Sequence, quality: int, subsamp: int, flags: int = 0) -> list:
+        """decode -> bitwise_not -> encode for every JPEG, fused on the GPU; returns bytes."""
+        n = len(jpegs)
+        if n == 0:
+            return []
+        srcs, ja = self._ptrs(jpegs)
+        caps = []
+        for s in srcs:
+            w, h, _, _ = jpeg_header(s)
+            caps.append(int(self._lib.vf_jpeg_buffer_size(w, h, subsamp)))
+        if not all(caps):
+            raise ValueError("jpeg_invert: unsupported size or subsampling")
+        outs = [np.empty(c, np.uint8) for c in caps]
+        _, oa = self._ptrs(outs)
+        js = (ctypes.c_size_t * n)(*[s.nbytes for s in srcs])
+        ca = (ctypes.c_size_t * n)(*caps)
+        sz = (ctypes.c_size_t * n)()
+        self._check(self._lib.vf_jpeg_invert(self._ctx, ja, js, n, quality, subsamp, flags, oa, ca, sz))
+        return [outs[i][:sz[i]].tobytes() for i in range(n)]
+
+    def jpeg_bench_invert(self, jpegs: Sequence, quality: int, subsamp: int, flags: int = 0, iters: int = 10):
+        """(mean ms per batch, {stage: ms}) for the GPU part of jpeg_invert on resident inputs."""
+        n = len(jpegs)
+        srcs, ja = self._ptrs(jpegs)
+        js = (ctypes.c_size_t * n)(*[s.nbytes for s in srcs])
+        ms = ctypes.c_float(0)
+        st = (ctypes.c_float * 8)()
+        self._check(self._lib.vf_jpeg_bench_invert(self._ctx, ja, js, n, quality, subsamp, flags, iters,
+                                                   ctypes.byref(ms), st))
+        names = ("unstuff", "huffman_sync", "huffman_write", "dc_idct", "color_invert", "fdct_huffman",
+                 "stuffing", "sync_passes")
+        return ms.value, dict(zip(names, [float(x) for x in st]))
+
+
+def jpeg_header(jpeg) -> tuple:
+    """(width, height, TJSAMP_*, TJCS_*) of a JPEG; host-only (vf_jpeg_header)."""
+    lib = load_library()
+    a = jpeg if isinstance(jpeg, np.ndarray) else np.frombuffer(jpeg, dtype=np.uint8)
+    w, h, ss, cs = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    st = lib.vf_jpeg_header(a.ctypes.data, a.nbytes, ctypes.byref(w), ctypes.byref(h), ctypes.byref(ss),
+                            ctypes.byref(cs))
+    if st != VF_OK:
+        raise VFilterError(lib.vf_last_error(None).decode(), st)
+    return w.value, h.value, ss.value, cs.value
 
 
 _default_ctx: Optional[Context] = None

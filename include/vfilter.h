@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define VF_ABI_VERSION 1
+#define VF_ABI_VERSION 2
 
 /* status codes */
 #define VF_OK           0
@@ -46,6 +46,7 @@ extern "C" {
 #define VF_E_HIP       -2  /* a HIP runtime call failed; see vf_last_error / vf_last_hip_error */
 #define VF_E_NOMEM     -3  /* host or device allocation failed */
 #define VF_E_NODEVICE  -4  /* no usable gfx950 device / bad device ordinal */
+#define VF_E_JPEG      -5  /* malformed, truncated or unsupported JPEG stream */
 
 typedef struct vf_ctx vf_ctx;
 
@@ -173,6 +174,66 @@ int vf_last_timeline(const vf_ctx *ctx, float *out4, size_t *chunk_bytes, int ma
 int vf_bench_device_ring(vf_ctx *ctx, void *const *srcs, void *const *dsts, int nbuf,
                          size_t nbytes, int steps, void *stream, float *per_launch_ms,
                          float *region_ms);
+
+
+/* ---- JPEG: the reference's default mode (use_jpeg=True) ------------------------------
+ *
+ * With use_jpeg=True (the default, inverter.py:10) every frame travels as a JPEG made by
+ * PyTurboJPEG (webcam_app.py:110), and the worker runs
+ *     frame = self.jpeg.decode(frame_bytes)     # inverter.py:32
+ *     inverted = cv2.bitwise_not(frame)         # inverter.py:41
+ *     return self.jpeg.encode(inverted)         # inverter.py:44
+ * with PyTurboJPEG's defaults (quality 85, TJSAMP_422, TJPF_BGR, flags 0).  These entry
+ * points replace those TurboJPEG calls (tjDecompressHeader3 / tjDecompress2 / tjCompress2)
+ * with a gfx950 baseline-JPEG codec whose integer arithmetic is libjpeg-turbo's: outputs are
+ * bit-exact with libjpeg-turbo.  Constants below are TurboJPEG's (turbojpeg.h).
+ * Supported: 8-bit baseline / extended-sequential Huffman JPEG, 1 or 3 components, one
+ * interleaved scan, no restart markers (decode); TJSAMP_444/422/420/GRAY/440 (encode).
+ * Anything else returns VF_E_JPEG with a message. */
+#define VF_TJPF_RGB 0
+#define VF_TJPF_BGR 1
+#define VF_TJSAMP_444 0
+#define VF_TJSAMP_422 1
+#define VF_TJSAMP_420 2
+#define VF_TJSAMP_GRAY 3
+#define VF_TJSAMP_440 4
+#define VF_TJFLAG_FASTUPSAMPLE 256   /* replicate chroma instead of fancy upsampling */
+#define VF_TJFLAG_FASTDCT 2048       /* "ifast" forward DCT (else the accurate "islow") */
+#define VF_TJFLAG_ACCURATEDCT 4096   /* accepted; islow is the default */
+
+/* Header of one JPEG, no GPU work (replaces TurboJPEG.decode_header).  *subsamp = TJSAMP_*
+ * (-1 if none matches), *colorspace = TJCS_YCbCr (1) or TJCS_GRAY (2). */
+int vf_jpeg_header(const uint8_t *jpeg, size_t size, int *width, int *height, int *subsamp,
+                   int *colorspace);
+
+/* Worst-case size of a vf_jpeg_encode output (tjBufSize); 0 for bad arguments. */
+size_t vf_jpeg_buffer_size(int width, int height, int subsamp);
+
+/* Encode n images (inverter.py:44, webcam_app.py:110): imgs[i] is an interleaved 8-bit
+ * heights[i] x widths[i] x 3 image in pixel_format; outs[i] receives the JPEG (caps[i]
+ * bytes available), sizes[i] its length.  One batched pass on the GPU. */
+int vf_jpeg_encode(vf_ctx *ctx, const uint8_t *const *imgs, const int *widths, const int *heights,
+                   int n, int pixel_format, int quality, int subsamp, int flags,
+                   uint8_t *const *outs, const size_t *caps, size_t *sizes);
+
+/* Decode n JPEGs (inverter.py:32, webcam_app.py:140) into interleaved 8-bit pixels
+ * (outs[i] holds width x height x 3 bytes, caps[i] available). */
+int vf_jpeg_decode(vf_ctx *ctx, const uint8_t *const *jpegs, const size_t *jpeg_sizes, int n,
+                   int pixel_format, int flags, uint8_t *const *outs, const size_t *caps);
+
+/* The whole default-mode filter for n frames on the GPU: decode -> bitwise_not -> encode
+ * (inverter.py:32 -> :41 -> :44) with no host round trip of the pixels.  outs[i] receives
+ * the inverted JPEG (caps[i] bytes available), sizes[i] its length. */
+int vf_jpeg_invert(vf_ctx *ctx, const uint8_t *const *jpegs, const size_t *jpeg_sizes, int n,
+                   int quality, int subsamp, int flags, uint8_t *const *outs, const size_t *caps,
+                   size_t *sizes);
+
+/* Benchmark: the GPU part of vf_jpeg_invert (inputs already in HBM) run `iters` times; *ms =
+ * mean wall ms per iteration; stage_ms (may be NULL, 8 floats) = mean ms of unstuff, Huffman
+ * sync, Huffman write, DC+IDCT, colour+invert, FDCT+Huffman encode, byte stuffing, and the
+ * mean number of sync passes. */
+int vf_jpeg_bench_invert(vf_ctx *ctx, const uint8_t *const *jpegs, const size_t *jpeg_sizes, int n,
+                         int quality, int subsamp, int flags, int iters, float *ms, float *stage_ms);
 
 #ifdef __cplusplus
 }

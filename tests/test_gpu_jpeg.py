@@ -1,0 +1,121 @@
+"""Parity of the gfx950 JPEG path (the reference's default use_jpeg=True mode,
+inverter.py:32 -> :41 -> :44) against the CPU oracle and the golden vectors.
+
+The codec is integer arithmetic, so the bar is bit-exact: encoded bytes equal to the
+oracle's (which is pinned to libjpeg-turbo, tests/test_jpeg_oracle.py), decoded pixels equal,
+and the fused decode -> bitwise_not -> encode equal to the oracle's InverterWorker path.
+Edge cases: sizes that are not whole MCUs (1x1, 7x5, 17x13, ...), every TurboJPEG
+subsampling, quality 1..100, both forward DCTs, fancy and replicating upsampling, uniform
+noise (the largest coefficients), mixed-size batches, truncated / corrupt / unsupported
+streams (must raise, never return garbage).
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import jpeg as J
+from vfilter import VFilterError
+from vfilter.jpeg import TJFLAG_FASTDCT, TJFLAG_FASTUPSAMPLE, TurboJPEG
+
+pytestmark = pytest.mark.gpu
+
+SIZES = [(1, 1), (7, 5), (8, 8), (16, 16), (17, 13), (33, 9), (64, 48), (130, 66)]
+
+
+@pytest.fixture(scope="module")
+def tj(vf_ctx):
+    return TurboJPEG(ctx=vf_ctx)
+
+
+def _img(kind, seed, h, w):
+    if kind == "noise":
+        return np.random.default_rng(seed).integers(0, 256, (h, w, 3), dtype=np.uint8)
+    return J.synthetic_scene(seed, h, w)
+
+
+@pytest.mark.parametrize("subsamp", [0, 1, 2, 3, 4])
+def test_encode_matches_oracle_small(tj, subsamp):
+    for i, (h, w) in enumerate(SIZES):
+        for kind in ("scene", "noise"):
+            img = _img(kind, i, h, w)
+            for q, flags in ((85, 0), (50, TJFLAG_FASTDCT), (1, 0), (100, 0), (95, TJFLAG_FASTDCT)):
+                got = tj.encode(img, q, J.TJPF_BGR, subsamp, flags)
+                want = J.encode(img, q, J.TJPF_BGR, subsamp, flags)
+                assert got == want, (h, w, kind, subsamp, q, flags)
+
+
+def test_encode_batch_mixed_sizes(tj):
+    imgs = [_img("scene", s, h, w) for s, (h, w) in enumerate([(480, 640), (17, 13), (1080, 1920), (64, 48)])]
+    got = tj.encode_batch(imgs)
+    for img, g in zip(imgs, got):
+        assert g == J.encode(img)
+
+
+@pytest.mark.parametrize("subsamp", [0, 1, 2, 3, 4])
+def test_decode_matches_oracle_small(tj, subsamp):
+    for i, (h, w) in enumerate(SIZES):
+        for kind in ("scene", "noise"):
+            jpg = J.encode(_img(kind, 100 + i, h, w), 75, J.TJPF_BGR, subsamp)
+            for flags in (0, TJFLAG_FASTUPSAMPLE):
+                for pf in (J.TJPF_BGR, J.TJPF_RGB):
+                    got = tj.decode(jpg, pf, flags=flags)
+                    want = J.decode(jpg, pf, flags)
+                    assert got.shape == want.shape
+                    assert np.array_equal(got, want), (h, w, kind, subsamp, flags, pf)
+
+
+def test_decode_batch_1080p_and_480p(tj):
+    jpgs = [J.encode(_img("scene", s, h, w), 85, J.TJPF_BGR, ss)
+            for s, (h, w, ss) in enumerate([(1080, 1920, 1), (480, 640, 2), (1080, 1920, 0), (480, 640, 3)])]
+    for got, j in zip(tj.decode_batch(jpgs), jpgs):
+        assert np.array_equal(got, J.decode(j))
+
+
+def test_invert_is_decode_not_encode(tj):
+    """InverterWorker.__call__ with use_jpeg=True (inverter.py:31-44), fused on the GPU."""
+    jpgs = [J.encode(_img("scene", s, 480, 640)) for s in range(4)]
+    jpgs.append(J.encode(_img("noise", 9, 240, 320)))
+    got = tj.invert_batch(jpgs)
+    for g, j in zip(got, jpgs):
+        assert g == J.invert_jpeg(j)
+    assert tj.invert(jpgs[0]) == got[0]
+
+
+def test_invert_1080p_batch(tj):
+    jpgs = [J.encode(_img("scene", s, 1080, 1920)) for s in range(3)]
+    for g, j in zip(tj.invert_batch(jpgs), jpgs):
+        assert g == J.invert_jpeg(j)
+
+
+def test_golden_vectors(tj, golden_dir):
+    """Fixtures made by the image's libjpeg-turbo (tests/golden/make_jpeg_golden.py)."""
+    d = os.path.join(golden_dir, "jpeg")
+    with open(os.path.join(d, "manifest.json")) as f:
+        cases = json.load(f)["cases"]
+    for c in cases:
+        jpg = open(os.path.join(d, c["file"]), "rb").read()
+        px = tj.decode(jpg)
+        assert hashlib.sha256(px.tobytes()).hexdigest() == c["decoded_sha256"], c["file"]
+        assert hashlib.sha256(tj.invert(jpg)).hexdigest() == c["inverted_sha256"], c["file"]
+        if "reencoded_sha256" in c:
+            assert hashlib.sha256(tj.encode(px)).hexdigest() == c["reencoded_sha256"], c["file"]
+
+
+def test_bad_streams_raise(tj):
+    good = J.encode(_img("scene", 1, 64, 64))
+    with pytest.raises(VFilterError):
+        tj.decode(b"\xff\xd8\xff\xd9")
+    with pytest.raises(VFilterError):
+        tj.decode(b"not a jpeg at all")
+    with pytest.raises(VFilterError):
+        tj.decode(good[: len(good) // 2])  # truncated entropy data
+    prog = bytearray(good)
+    i = prog.find(b"\xff\xc0")
+    prog[i + 1] = 0xC2  # progressive SOF
+    with pytest.raises(VFilterError):
+        tj.decode(bytes(prog))
+    # the context stays usable after errors
+    assert np.array_equal(tj.decode(good), J.decode(good))
