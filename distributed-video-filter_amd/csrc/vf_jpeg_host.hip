@@ -615,7 +615,7 @@ int Codec::run_decode(int bgr, bool invert, std::string *err) {
                 d_used_.as<uint64_t>(), d_changed_.as<uint32_t>() + (pass % kMaxPasses), pass > 0 ? 1 : 0, s_));
     last = a;
     ++pass;
-    if (pass < 3) continue;  // passes 0..2 are queued without a host round trip
+    if (pass < 2) continue;  // passes 0 and 1 are queued without a host round trip
     CK(hipMemcpyAsync(&flag, d_changed_.as<uint32_t>() + ((pass - 1) % kMaxPasses), sizeof flag,
                       hipMemcpyDeviceToHost, s_));
     CK(hipStreamSynchronize(s_));

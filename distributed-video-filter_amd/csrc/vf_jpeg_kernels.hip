@@ -315,42 +315,70 @@ __device__ __forceinline__ void load_tables(const DecFrame &F, HuffDec *tabs) {
   __syncthreads();
 }
 
+// One sync pass.  Every thread decodes its subsequence from its entry state; then, inside
+// the workgroup, a thread whose entry differs from its predecessor's current exit takes that
+// exit and decodes again, until the workgroup is consistent (usually one extra round, as
+// the codes self-synchronise).  Across workgroups the entry of a workgroup's first thread is
+// the previous pass's exit of its predecessor; a pass that changes no exit state means the
+// whole chain is consistent, and its counts were made from the final entry states.
 __global__ __launch_bounds__(256) void k_sync(const DecFrame *fr, const uint8_t *us, const uint32_t *us_len,
                                               const uint64_t *exit_in, uint64_t *exit_out, const uint32_t *cnt_in,
                                               uint32_t *cnt_out, uint64_t *used, uint32_t *changed, int pass) {
   __shared__ HuffDec tabs[6];
+  __shared__ uint64_t s_exit[256];
   const DecFrame &F = fr[blockIdx.y];
   if (blockIdx.x * 256 >= F.nsub_max) return;
   load_tables(F, tabs);
-  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= F.nsub_max) return;
+  const uint32_t t = threadIdx.x;
+  const uint32_t i = blockIdx.x * 256 + t;
   const uint32_t gi = F.sub0 + i;
   const uint32_t nbits = us_len[blockIdx.y] * 8u;
   const uint32_t nsub = (nbits + kSubBits - 1) / kSubBits;
-  if (i >= nsub) {
-    cnt_out[gi] = 0;
-    exit_out[gi] = pack_state(nbits, 0, 0);
-    return;
+  const bool live = i < nsub;
+  const uint32_t end = (i + 1 >= nsub) ? nbits : (i + 1) * kSubBits;
+  uint64_t entry = 0, ex = pack_state(nbits, 0, 0);
+  uint32_t cnt = 0;
+  bool need = false;
+  if (live) {
+    if (i == 0) entry = 0;
+    else if (pass == 0) entry = pack_state(i * kSubBits, 0, 0);
+    else entry = exit_in[gi - 1];
+    if (pass > 0 && entry == used[gi]) {  // same entry as last pass: same result
+      ex = exit_in[gi];
+      cnt = cnt_in[gi];
+    } else {
+      need = true;
+    }
   }
-  uint64_t st;
-  if (i == 0) st = 0;
-  else if (pass == 0) st = pack_state(i * kSubBits, 0, 0);
-  else st = exit_in[gi - 1];
-  if (pass > 0 && st == used[gi]) {  // same entry state as last pass: same result
-    exit_out[gi] = exit_in[gi];
-    cnt_out[gi] = cnt_in[gi];
-    return;
+  for (;;) {
+    if (need) {
+      BitReader br;
+      br.init(us + F.us_off, (uint32_t)(entry >> 16));
+      uint32_t z = (entry >> 8) & 0xFF, c = entry & 0xFF;
+      cnt = 0;
+      decode_span<false>(br, end, z, c, cnt, F.g, tabs, tabs + 3, 0, nullptr, nullptr, nullptr);
+      ex = pack_state(br.pos, z, c);
+    }
+    s_exit[t] = ex;
+    __syncthreads();
+    need = false;
+    if (live && t > 0) {
+      const uint64_t e = s_exit[t - 1];
+      if (e != entry) {
+        entry = e;
+        need = true;
+      }
+    }
+    if (!__syncthreads_or(need)) break;  // also orders the s_exit reads before the next writes
   }
-  used[gi] = st;
-  const uint32_t end = (i + 1 == nsub) ? nbits : (i + 1) * kSubBits;
-  BitReader br;
-  br.init(us + F.us_off, (uint32_t)(st >> 16));
-  uint32_t z = (st >> 8) & 0xFF, c = st & 0xFF, blocks = 0;
-  decode_span<false>(br, end, z, c, blocks, F.g, tabs, tabs + 3, 0, nullptr, nullptr, nullptr);
-  const uint64_t ex = pack_state(br.pos, z, c);
-  exit_out[gi] = ex;
-  cnt_out[gi] = blocks;
-  if (pass == 0 || ex != exit_in[gi] || blocks != cnt_in[gi]) atomicOr(changed, 1u);
+  if (i < F.nsub_max) {
+    exit_out[gi] = ex;
+    cnt_out[gi] = cnt;
+    if (live) {
+      used[gi] = entry;
+      if (pass == 0 || ex != exit_in[gi]) atomicOr(changed, 1u);
+    }
+  }
 }
 
 __global__ __launch_bounds__(256) void k_write(const DecFrame *fr, const uint8_t *us, const uint32_t *us_len,
@@ -529,37 +557,104 @@ __device__ __forceinline__ int up_sample(const uint8_t *p, int pw, int dw, int d
 
 __device__ __forceinline__ uint32_t clamp255(int v) { return (uint32_t)(v < 0 ? 0 : v > 255 ? 255 : v); }
 
+// 8 horizontally adjacent output pixels per thread: one 8-byte load per full-size plane,
+// the chroma samples they need (+1 neighbour each side) for 2x horizontal subsampling, and
+// three 8-byte stores of interleaved output when the row is 8-byte aligned.
 __global__ __launch_bounds__(256) void k_color(const DecFrame *fr, const uint8_t *planes, uint8_t *pix, int bgr,
                                                int invert) {
   const DecFrame &F = fr[blockIdx.z];
   const Geom &g = F.g;
-  const int y = blockIdx.y, x = blockIdx.x * 256 + threadIdx.x;
-  if (y >= g.h || x >= g.w) return;
-  int v[3];
+  const int y = blockIdx.y, x0 = (blockIdx.x * 256 + threadIdx.x) * 8;
+  if (y >= g.h || x0 >= g.w) return;
+  int v[3][8];
   for (int k = 0; k < g.ncomp; ++k) {
+    const uint8_t *p = planes + F.plane_off[k];
+    const int pw = g.pw[k];
     const int he = g.maxh / g.hs[k], ve = g.maxv / g.vs[k];
     const int dw = (g.w * g.hs[k] + g.maxh - 1) / g.maxh, dh = (g.h * g.vs[k] + g.maxv - 1) / g.maxv;
     const bool fancy = (F.flags & 1) && ((he == 2 && dw > 2) || (he == 1 && ve == 2));
-    v[k] = up_sample(planes + F.plane_off[k], g.pw[k], dw, dh, he, ve, fancy && (ve <= 2) && (he <= 2), x, y);
+    if (he == 1 && ve == 1) {
+      const uint2 q = *reinterpret_cast<const uint2 *>(p + (size_t)y * pw + x0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[k][j] = (int)(((j < 4 ? q.x : q.y) >> (8 * (j & 3))) & 0xFF);
+    } else if (he == 2 && ve <= 2) {
+      const int iy = min(y / ve, dh - 1);
+      const uint8_t *r0 = p + (size_t)iy * pw;
+      const int i0 = x0 >> 1;
+      int cs[6];  // column values of chroma samples i0-1 .. i0+4 (edges clamped)
+      if (ve == 2 && fancy) {
+        int ny = (y & 1) ? iy + 1 : iy - 1;
+        ny = ny < 0 ? 0 : ny > dh - 1 ? dh - 1 : ny;
+        const uint8_t *r1 = p + (size_t)ny * pw;
+#pragma unroll
+        for (int m = 0; m < 6; ++m) {
+          const int ix = min(max(i0 - 1 + m, 0), dw - 1);
+          cs[m] = 3 * r0[ix] + r1[ix];
+        }
+      } else {
+#pragma unroll
+        for (int m = 0; m < 6; ++m) cs[m] = r0[min(max(i0 - 1 + m, 0), dw - 1)];
+      }
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int i = i0 + jj, c = cs[jj + 1];
+        int a, b;
+        if (!fancy) {
+          a = b = c;
+        } else if (ve == 1) {  // h2v1_fancy_upsample
+          a = i == 0 ? c : (3 * c + cs[jj] + 1) >> 2;
+          b = i == dw - 1 ? c : (3 * c + cs[jj + 2] + 2) >> 2;
+        } else {  // h2v2_fancy_upsample
+          a = i == 0 ? (4 * c + 8) >> 4 : (3 * c + cs[jj] + 8) >> 4;
+          b = i == dw - 1 ? (4 * c + 7) >> 4 : (3 * c + cs[jj + 2] + 7) >> 4;
+        }
+        v[k][2 * jj] = a;
+        v[k][2 * jj + 1] = b;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        v[k][j] = up_sample(p, pw, dw, dh, he, ve, fancy && he <= 2 && ve <= 2, min(x0 + j, g.w - 1), y);
+    }
   }
-  uint32_t r, gg, b;
-  if (g.ncomp == 1) {
-    r = gg = b = (uint32_t)v[0];
-  } else {  // jdcolor.c ycc_rgb_convert
-    const int xcr = v[2] - 128, xcb = v[1] - 128;
-    r = clamp255(v[0] + ((91881 * xcr + 32768) >> 16));
-    gg = clamp255(v[0] + ((-22554 * xcb + 32768 - 46802 * xcr) >> 16));
-    b = clamp255(v[0] + ((116130 * xcb + 32768) >> 16));
+  uint8_t o[24];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    uint32_t r, gg, b;
+    if (g.ncomp == 1) {
+      r = gg = b = (uint32_t)v[0][j];
+    } else {  // jdcolor.c ycc_rgb_convert
+      const int xcr = v[2][j] - 128, xcb = v[1][j] - 128;
+      r = clamp255(v[0][j] + ((91881 * xcr + 32768) >> 16));
+      gg = clamp255(v[0][j] + ((-22554 * xcb + 32768 - 46802 * xcr) >> 16));
+      b = clamp255(v[0][j] + ((116130 * xcb + 32768) >> 16));
+    }
+    if (invert) {
+      r ^= 0xFF;
+      gg ^= 0xFF;
+      b ^= 0xFF;
+    }
+    o[3 * j] = (uint8_t)(bgr ? b : r);
+    o[3 * j + 1] = (uint8_t)gg;
+    o[3 * j + 2] = (uint8_t)(bgr ? r : b);
   }
-  if (invert) {
-    r ^= 0xFF;
-    gg ^= 0xFF;
-    b ^= 0xFF;
+  uint8_t *dst = pix + F.out_off + ((size_t)y * g.w + x0) * 3;
+  if (x0 + 8 <= g.w && ((uintptr_t)dst & 7) == 0) {
+    uint2 *d2 = reinterpret_cast<uint2 *>(dst);
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      uint32_t lo = 0, hi = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        lo |= (uint32_t)o[8 * q + j] << (8 * j);
+        hi |= (uint32_t)o[8 * q + 4 + j] << (8 * j);
+      }
+      d2[q] = make_uint2(lo, hi);
+    }
+  } else {
+    const int n = min(8, g.w - x0) * 3;
+    for (int j = 0; j < n; ++j) dst[j] = o[j];
   }
-  uint8_t *o = pix + F.out_off + ((size_t)y * g.w + x) * 3;
-  o[0] = (uint8_t)(bgr ? b : r);
-  o[1] = (uint8_t)gg;
-  o[2] = (uint8_t)(bgr ? r : b);
 }
 
 // ---- encoder: colour + downsampling + FDCT + quantisation -----------------------------------
@@ -671,11 +766,59 @@ __device__ __forceinline__ int16_t quantize(int32_t x, uint32_t recip, uint32_t 
   return (int16_t)p;
 }
 
+// N adjacent pixels of row py from px (edges replicated: jccolor.c on expand_right_edge /
+// expand_bottom_edge input), split into r/g/b; 8-byte vector loads when the span is inside
+// the image and aligned.
+template <int N>
+__device__ __forceinline__ void load_rgb(const uint8_t *img, int w, int h, int px, int py, bool bgr, int *r, int *g,
+                                         int *b) {
+  py = py < h ? py : h - 1;
+  const uint8_t *src = img + ((size_t)py * w + px) * 3;
+  if (px + N <= w && ((uintptr_t)src & 7) == 0) {
+    uint32_t wd[N * 3 / 4];
+#pragma unroll
+    for (int q = 0; q < N * 3 / 8; ++q) {
+      const uint2 v = reinterpret_cast<const uint2 *>(src)[q];
+      wd[2 * q] = v.x;
+      wd[2 * q + 1] = v.y;
+    }
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      const int c0 = (int)((wd[(3 * j) / 4] >> (8 * ((3 * j) % 4))) & 0xFF);
+      const int c1 = (int)((wd[(3 * j + 1) / 4] >> (8 * ((3 * j + 1) % 4))) & 0xFF);
+      const int c2 = (int)((wd[(3 * j + 2) / 4] >> (8 * ((3 * j + 2) % 4))) & 0xFF);
+      r[j] = bgr ? c2 : c0;
+      g[j] = c1;
+      b[j] = bgr ? c0 : c2;
+    }
+  } else {
+    const uint8_t *row = img + (size_t)py * w * 3;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      const int x = px + j < w ? px + j : w - 1;
+      const uint8_t *q = row + (size_t)x * 3;
+      r[j] = bgr ? q[2] : q[0];
+      g[j] = q[1];
+      b[j] = bgr ? q[0] : q[2];
+    }
+  }
+}
+
+__device__ __forceinline__ int ycc_comp(int k, int r, int g, int b) {  // jccolor.c rgb_ycc_convert
+  if (k == 0) return (19595 * r + 38470 * g + 7471 * b + 32768) >> 16;
+  if (k == 1) return (-11059 * r - 21709 * g + 32768 * b + (128 << 16) + 32767) >> 16;
+  return (32768 * r - 27439 * g - 5329 * b + (128 << 16) + 32767) >> 16;
+}
+
+// 8 lanes per block.  A workgroup takes M = 32 / bpm whole MCUs and orders its 32 block
+// slots block-in-MCU-major (slot s -> block-in-MCU s / M of MCU s % M), so a wave's 8 blocks
+// are mostly one component and the luma / chroma sampling paths do not diverge in a wave.
 __global__ __launch_bounds__(256) void k_fdct(const EncFrame *fr, const EncTables *tab, const uint8_t *pix,
                                               int16_t *coef, int bgr, int fastdct) {
   const EncFrame &F = fr[blockIdx.y];
   const Geom &g = F.g;
-  if (blockIdx.x * 32 >= (uint32_t)g.nblocks) return;
+  const uint32_t M = 32 / (uint32_t)g.bpm;
+  if (blockIdx.x * M >= (uint32_t)g.nmcu) return;
   __shared__ int32_t ws[32][8][9];
   __shared__ int16_t qo[32][64];
   __shared__ uint16_t s_recip[2][64], s_corr[2][64];
@@ -687,19 +830,49 @@ __global__ __launch_bounds__(256) void k_fdct(const EncFrame *fr, const EncTable
     s_shift[t][i] = tab->shift[t][i];
   }
   const uint32_t slot = threadIdx.x >> 3, r = threadIdx.x & 7;
-  const uint32_t b = blockIdx.x * 32 + slot;
+  const uint32_t c = slot / M, mcu = blockIdx.x * M + slot % M;
+  const uint32_t b = mcu * (uint32_t)g.bpm + c;
   uint32_t k = 0, bx = 0, by = 0;
   bool real = false;
-  if (b < (uint32_t)g.nblocks) {
+  if (c < (uint32_t)g.bpm && mcu < (uint32_t)g.nmcu) {
     block_pos(g, b, &k, &bx, &by);
     real = bx < (uint32_t)g.wb[k] && by < (uint32_t)g.hb[k];  // dummy blocks are made by enc_huff
   }
-  const int ro = bgr ? 2 : 0, bo = 2 - ro;
   const uint8_t *img = pix + F.img_off;
-  if (real) {  // pass 1: row r
+  if (real) {  // pass 1: row r of the block's samples
+    const int he = g.maxh / g.hs[k], ve = g.maxv / g.vs[k];
+    const int real_rows = ((g.h + g.maxv - 1) / g.maxv) * g.vs[k];
+    const int sy = min((int)(by * 8 + r), real_rows - 1);
     int32_t v[8];
+    if (he == 1 && ve == 1) {
+      int R[8], G[8], B[8];
+      load_rgb<8>(img, g.w, g.h, (int)bx * 8, sy, bgr, R, G, B);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = enc_sample(g, img, (int)k, (int)(bx * 8 + j), (int)(by * 8 + r), ro, bo) - 128;
+      for (int j = 0; j < 8; ++j) v[j] = ycc_comp((int)k, R[j], G[j], B[j]);
+    } else if (he == 2 && ve == 1) {  // h2v1_downsample
+      int R[16], G[16], B[16];
+      load_rgb<16>(img, g.w, g.h, (int)bx * 16, sy, bgr, R, G, B);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        v[j] = (ycc_comp((int)k, R[2 * j], G[2 * j], B[2 * j]) +
+                ycc_comp((int)k, R[2 * j + 1], G[2 * j + 1], B[2 * j + 1]) + (j & 1)) >> 1;
+    } else if (he == 2 && ve == 2) {  // h2v2_downsample
+      int R[16], G[16], B[16], R2[16], G2[16], B2[16];
+      load_rgb<16>(img, g.w, g.h, (int)bx * 16, 2 * sy, bgr, R, G, B);
+      load_rgb<16>(img, g.w, g.h, (int)bx * 16, 2 * sy + 1, bgr, R2, G2, B2);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        v[j] = (ycc_comp((int)k, R[2 * j], G[2 * j], B[2 * j]) +
+                ycc_comp((int)k, R[2 * j + 1], G[2 * j + 1], B[2 * j + 1]) +
+                ycc_comp((int)k, R2[2 * j], G2[2 * j], B2[2 * j]) +
+                ycc_comp((int)k, R2[2 * j + 1], G2[2 * j + 1], B2[2 * j + 1]) + 1 + (j & 1)) >> 2;
+    } else {
+      const int ro = bgr ? 2 : 0, bo = 2 - ro;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = enc_sample(g, img, (int)k, (int)(bx * 8 + j), sy, ro, bo);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] -= 128;
     if (fastdct) fdct_ifast_line(v);
     else fdct_islow_line(v, 0);
 #pragma unroll
@@ -987,7 +1160,7 @@ hipError_t dec_idct(const DecFrame *fr, int n, uint32_t max_blocks, const int16_
 hipError_t dec_color(const DecFrame *fr, int n, int max_w, int max_h, const uint8_t *planes, uint8_t *pix, int bgr,
                      int invert, hipStream_t s) {
   if (n <= 0 || max_w <= 0 || max_h <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_color, dim3((unsigned)((max_w + 255) / 256), (unsigned)max_h, (unsigned)n), dim3(256), 0, s,
+  hipLaunchKernelGGL(k_color, dim3((unsigned)((max_w + 2047) / 2048), (unsigned)max_h, (unsigned)n), dim3(256), 0, s,
                      fr, planes, pix, bgr, invert);
   return hipGetLastError();
 }
@@ -995,7 +1168,8 @@ hipError_t dec_color(const DecFrame *fr, int n, int max_w, int max_h, const uint
 hipError_t enc_fdct(const EncFrame *fr, int n, uint32_t max_blocks, const EncTables *tab, const uint8_t *pix,
                     int16_t *coef, int bgr, int fastdct, hipStream_t s) {
   if (n <= 0 || !max_blocks) return hipSuccess;
-  hipLaunchKernelGGL(k_fdct, dim3((max_blocks + 31) / 32, (unsigned)n), dim3(256), 0, s, fr, tab, pix, coef, bgr,
+  // a workgroup takes bpm * (32 / bpm) >= 27 blocks (bpm <= 10)
+  hipLaunchKernelGGL(k_fdct, dim3((max_blocks + 26) / 27, (unsigned)n), dim3(256), 0, s, fr, tab, pix, coef, bgr,
                      fastdct);
   return hipGetLastError();
 }

@@ -29,22 +29,22 @@ import numpy as np
 
 from . import wire
 from ._lib import Context, default_device
+from .jpeg import TurboJPEG
 from .worker import Worker
 
 
 class InverterWorker(Worker):
     def __init__(self, host: str = "localhost", distribute_port: int = 5555, collect_port: int = 5556,
                  delay: float = 0.0, use_jpeg: bool = True, *, device: Optional[int] = None,
-                 max_frame_bytes: int = 3840 * 2160 * 3, install_signal_handlers: bool = True, **worker_kw):
-        self.jpeg = None
-        if use_jpeg:
-            from turbojpeg import TurboJPEG  # raises ImportError when absent, like inverter.py:7
-            self.jpeg = TurboJPEG()
+                 max_frame_bytes: int = 3840 * 2160 * 3, install_signal_handlers: bool = True,
+                 tj_version: int = 3, **worker_kw):
         worker_kw.setdefault("inflight", 2)  # batch i on the GPU while batch i+1 is received
         super().__init__(host, distribute_port, collect_port, **worker_kw)
         self.delay = delay
         self.device = default_device() if device is None else device
         self.ctx = Context(self.device, max_frame_bytes=max_frame_bytes, max_batch=max(1, self.batch))
+        # inverter.py:13 — TurboJPEG() with PyTurboJPEG's defaults, on this worker's GPU
+        self.jpeg = TurboJPEG(ctx=self.ctx, tj_version=tj_version) if use_jpeg else None
         self._registered: List[int] = []
         if install_signal_handlers:                                  # inverter.py:16-18
             signal.signal(signal.SIGINT, self._signal_handler)
@@ -61,6 +61,8 @@ class InverterWorker(Worker):
 
     # -- one frame (inverter.py:29-46) ------------------------------------------------------
     def __call__(self, frame_bytes):
+        if self.jpeg and self.delay <= 0:
+            return self.jpeg.invert(frame_bytes)                    # inverter.py:32 -> :41 -> :44, fused
         if self.jpeg:
             frame = self.jpeg.decode(frame_bytes)                   # inverter.py:32
         else:
@@ -76,6 +78,11 @@ class InverterWorker(Worker):
 
     # -- a dispatched batch: one gathered device call ------------------------------------
     def process_batch(self, frames: Sequence, metas: Sequence[wire.FrameMeta], outs: Sequence) -> List:
+        if self.jpeg and self.delay <= 0 and all(o is None for o in outs):
+            try:  # the whole batch in one fused GPU pass
+                return self.jpeg.invert_batch(list(frames))
+            except Exception:  # retry frame by frame so a bad frame fails alone (worker.py:74-76)
+                return super().process_batch(frames, metas, outs)
         if self.jpeg:
             return super().process_batch(frames, metas, outs)
         if self.delay > 0:

@@ -29,10 +29,10 @@ def _watch(stop_event, worker):
 
 
 def run_worker(dport, cport, stop_event, protocol="v1", batch=4, transport="tcp", kind="oracle",
-               delay=0.0, device=0):
+               delay=0.0, device=0, use_jpeg=False):
     if kind == "gpu":
         from vfilter.inverter import InverterWorker
-        w = InverterWorker("127.0.0.1", dport, cport, delay, use_jpeg=False, device=device,
+        w = InverterWorker("127.0.0.1", dport, cport, delay, use_jpeg=use_jpeg, device=device,
                            install_signal_handlers=False, batch=batch, protocol=protocol,
                            transport=transport)
     else:

@@ -100,7 +100,55 @@ def test_inverter_worker_call_matches_reference_raw_path():
         assert bytes(w(x)) == oracle.reference_raw_call(x)
         y = oracle.synthetic_frame(9, 1080, 1920).tobytes()
         assert bytes(w(y)) == oracle.invert_bytes(y)
-        with pytest.raises(ImportError):
-            InverterWorker("127.0.0.1", 1, 1, 0.0, use_jpeg=True, install_signal_handlers=False, transport="tcp")
     finally:
         w.close()
+
+
+@pytest.mark.timeout(120)
+def test_inverter_worker_jpeg_mode_matches_reference_path():
+    """use_jpeg=True (the reference default): __call__ = decode -> bitwise_not -> encode
+    (inverter.py:32 -> :41 -> :44), bit-exact with the oracle's restatement of PyTurboJPEG /
+    libjpeg-turbo; with --delay the unfused path gives the same bytes."""
+    from oracle import jpeg as J
+    from vfilter.inverter import InverterWorker
+    jpg = J.encode(J.synthetic_scene(4, 480, 640))
+    small = J.encode(J.synthetic_scene(5, 64, 48))
+    w = InverterWorker("127.0.0.1", 1, 1, 0.0, use_jpeg=True, install_signal_handlers=False, transport="tcp")
+    wd = InverterWorker("127.0.0.1", 1, 1, 0.001, use_jpeg=True, install_signal_handlers=False, transport="tcp")
+    try:
+        want = J.invert_jpeg(jpg)
+        assert bytes(w(jpg)) == want
+        assert bytes(wd(jpg)) == want
+        res = w.process_batch([jpg, small], [None, None], [None, None])
+        assert res[0] == want and res[1] == J.invert_jpeg(small)
+        bad = w.process_batch([jpg, b"\xff\xd8garbage"], [None, None], [None, None])
+        assert bad[0] == want and isinstance(bad[1], Exception)  # a bad frame fails alone
+    finally:
+        w.close()
+        wd.close()
+
+
+@pytest.mark.timeout(180)
+def test_jpeg_mode_through_distributor_in_order():
+    """The reference's default deployment: JPEG frames (webcam_app.py:110) through the
+    distributor to 2 GPU workers in JPEG mode and back in index order, bit-exact."""
+    from oracle import jpeg as J
+    jpgs = [J.encode(J.synthetic_scene(i, 480 if i % 2 else 1080, 640 if i % 2 else 1920)) for i in range(24)]
+    d = Distributor(0, 0, 5, True, policy="pull", reassembly="ordered", queue_size=16, transport="tcp",
+                    host="127.0.0.1", verbose=False)
+    d.start()
+    stop, procs = spawn_workers(2, d.distribute_port, d.collect_port, protocol="v1", batch=4, kind="gpu",
+                                use_jpeg=True)
+    try:
+        th = threading.Thread(target=lambda: [d.add_frame_for_distribution(j) for j in jpgs])
+        th.start()
+        for i in range(len(jpgs)):
+            item = d.get_next_frame(timeout=60)
+            assert item is not None, d.ordering_stats()
+            idx, data, _ = item
+            assert idx == i
+            assert bytes(data) == J.invert_jpeg(jpgs[i]), i
+        th.join()
+    finally:
+        stop_workers(stop, procs)
+        d.cleanup()
