@@ -17,6 +17,8 @@ Prints ONE JSON line on rank 0 (contract in the task statement), including
                 a new array each call, like cv2.bitwise_not), 1 host core, ~10 s sample
   end_to_end    host->host rate through vf_invert_batch_host (pageable and pinned): PCIe-bound,
                 reported beside value, never as value.
+  jpeg_mode     the reference's default use_jpeg=True path (decode -> invert -> encode) on 1080p
+                JPEGs: GPU-resident and host->host frames/s, with libjpeg-turbo on 1 core beside it.
 """
 from __future__ import annotations
 
@@ -55,6 +57,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="cpu_baseline sample length (0 = skip)")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC traffic passes")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host->host end-to-end leg")
+    ap.add_argument("--no-jpeg", action="store_true", help="skip the JPEG-mode leg (use_jpeg=True path)")
     ap.add_argument("--probe", action="store_true", help=argparse.SUPPRESS)  # child under rocprofv3
     return ap.parse_args()
 
@@ -197,6 +200,51 @@ def end_to_end(ctx, host_batch, batch, np, reps=8):
     return res
 
 
+def jpeg_mode(ctx, batch, iters=20):
+    """The reference's default mode (use_jpeg=True): decode -> bitwise_not -> encode per frame
+    (inverter.py:32 -> :41 -> :44) on 1080p JPEGs made with the PyTurboJPEG defaults (q85,
+    4:2:2) from camera-like synthetic scenes.  GPU-resident = the fused GPU pass with the
+    compressed batch already in HBM; host_to_host = Python bytes in, bytes out."""
+    from vfilter.jpeg import TurboJPEG
+    from vfilter.synthetic import synthetic_scene
+    tj = TurboJPEG(ctx=ctx)
+    scenes = [synthetic_scene(s, H, W) for s in range(8)]
+    enc = tj.encode_batch(scenes)  # the app's encode (webcam_app.py:110), on the GPU
+    jpgs = [enc[i % len(enc)] for i in range(batch)]
+    ctx.jpeg_bench_invert(jpgs, 85, 1, 0, iters=2)
+    ms, stages = ctx.jpeg_bench_invert(jpgs, 85, 1, 0, iters=iters)
+    tj.invert_batch(jpgs)
+    reps = 5
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        tj.invert_batch(jpgs)
+    h2h = (time.perf_counter() - t0) / reps
+    return {"workload": f"1080p JPEG (q85 4:2:2) decode -> bitwise_not -> encode, batch {batch}",
+            "gpu_resident_fps": round(batch / (ms / 1e3), 1), "gpu_resident_ms_per_batch": round(ms, 3),
+            "stages_ms": {k: round(v, 4) for k, v in stages.items()},
+            "host_to_host_fps": round(batch / h2h, 1),
+            "jpeg_bytes_mean": round(sum(len(j) for j in jpgs) / batch)}, jpgs
+
+
+def cpu_baseline_jpeg(jpgs, seconds):
+    """libjpeg-turbo 2.1.2 (the codec under PyTurboJPEG: the image's libjpeg.so.8, driven as
+    TurboJPEG drives it by oracle/jpeg_xcheck.c) decode + np.bitwise_not + encode per frame,
+    1 host core — the reference's default per-frame work (inverter.py:32-44)."""
+    import numpy as np
+    from oracle import jpeg as J
+    ok, why = J.libjpeg_available()
+    if not ok:
+        return {"value": None, "why": why}
+    n = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        J.libjpeg_encode(np.bitwise_not(J.libjpeg_decode(jpgs[n % len(jpgs)])), 85, J.TJPF_BGR, 1, False)
+        n += 1
+    dt = time.perf_counter() - t0
+    return {"value": round(n / dt, 2), "unit": "frames/s", "cores": 1, "kind": "reference",
+            "sample": f"{n} x 1080p JPEG frames ({dt:.1f} s) through libjpeg-turbo 2.1.2, 1 thread"}
+
+
 def main():
     args = parse()
     if args.probe:
@@ -267,9 +315,17 @@ def main():
     if rank == 0 and not args.no_e2e:
         e2e = end_to_end(ctx, host_batch, args.batch, np)
         log(f"end-to-end: {e2e}")
+    jpeg = None
+    jpgs = None
+    if rank == 0 and not args.no_jpeg:
+        jpeg, jpgs = jpeg_mode(ctx, args.batch)
+        log(f"jpeg mode: {jpeg}")
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         cpu = cpu_baseline(host_batch, args.batch, args.cpu_seconds, np)
         log(f"cpu baseline: {cpu}")
+        if jpeg is not None:
+            jpeg["cpu_reference"] = cpu_baseline_jpeg(jpgs, min(5.0, args.cpu_seconds))
+            log(f"jpeg cpu reference: {jpeg['cpu_reference']}")
 
     for s, d in zip(srcs, dsts):
         ctx.free_device(s)
@@ -308,6 +364,7 @@ def main():
                          "traffic_detail": traffic_detail},
             "cpu_baseline": cpu,
             "end_to_end": e2e,
+            "jpeg_mode": jpeg,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -1,6 +1,9 @@
 """Synthetic frames for benchmarks and demos: uniform uint8 from a seeded
 ``np.random.default_rng`` — the invert is data-independent, and uniform bytes exercise every
-lane and byte position.  Frame sizes used by BASELINE.json's configs are named here."""
+lane and byte position.  Frame sizes used by BASELINE.json's configs are named here.
+
+``synthetic_scene`` makes camera-like frames for the JPEG mode (the reference's default,
+inverter.py:32-44): JPEG of uniform noise is the codec's worst case, not a video frame."""
 from __future__ import annotations
 
 import numpy as np
@@ -22,3 +25,21 @@ def synthetic_batch(n: int, h: int, w: int, seed0: int = 0) -> np.ndarray:
     for i in range(n):
         out[i] = synthetic_frame(seed0 + i, h, w)
     return out
+
+
+def synthetic_scene(seed: int, h: int, w: int) -> np.ndarray:
+    """Smooth gradients, a few flat shapes with hard edges, texture and mild noise."""
+    rng = np.random.default_rng(seed)
+    y = np.linspace(0.0, 1.0, h, dtype=np.float64)[:, None]
+    x = np.linspace(0.0, 1.0, w, dtype=np.float64)[None, :]
+    img = np.empty((h, w, 3), np.float64)
+    for c in range(3):
+        a, b, p = rng.uniform(-80, 80), rng.uniform(-80, 80), rng.uniform(0, 6.3)
+        f = rng.uniform(1.0, 6.0)
+        img[..., c] = 128 + a * x + b * y + 30 * np.sin(2 * np.pi * f * (x + 0.5 * y) + p)
+    for _ in range(6):
+        y0, x0 = int(rng.integers(0, h)), int(rng.integers(0, w))
+        y1, x1 = y0 + int(rng.integers(1, max(2, h // 3))), x0 + int(rng.integers(1, max(2, w // 3)))
+        img[y0:y1, x0:x1, :] = rng.uniform(0, 255, 3)
+    img += rng.normal(0.0, 3.0, img.shape)
+    return np.clip(np.rint(img), 0, 255).astype(np.uint8)

@@ -126,3 +126,10 @@ def test_product_header_rejects_bad_streams():
     for bad in (b"", b"\xff\xd8", b"GIF89a....", b"\xff\xd8\xff\xd9"):
         with pytest.raises(VFilterError):
             jpeg_header(bad)
+
+
+def test_product_synthetic_scene_matches_oracle_generator():
+    """bench.py makes its JPEG-mode frames with vfilter.synthetic (it may not import the oracle)."""
+    from vfilter.synthetic import synthetic_scene
+    for seed, (h, w) in enumerate([(17, 13), (480, 640)]):
+        assert np.array_equal(synthetic_scene(seed, h, w), J.synthetic_scene(seed, h, w))
