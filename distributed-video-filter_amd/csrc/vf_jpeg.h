@@ -17,6 +17,7 @@ constexpr int kSubBits = 1024;  // bits per Huffman-decoding subsequence
 constexpr int kTile = 4096;     // bytes per (un)stuffing tile
 constexpr int kMaxPasses = 64;  // sync-pass flags kept on the device
 constexpr int kLook = 9;        // Huffman lookahead bits
+constexpr int kAcScratchWords = 52;  // per-block AC bit scratch (63 codes of <= 26 bits + EOB)
 
 // MCU geometry of one frame (libjpeg jdinput.c / jcmaster.c per-scan setup, restated)
 struct Geom {
@@ -111,9 +112,12 @@ hipError_t dec_color(const DecFrame *fr, int n, int max_w, int max_h, const uint
                      int bgr, int invert, hipStream_t s);
 
 hipError_t enc_fdct(const EncFrame *fr, int n, uint32_t max_blocks, const EncTables *tab, const uint8_t *pix,
-                    int16_t *coef, int bgr, int fastdct, hipStream_t s);
-hipError_t enc_huff(const EncFrame *fr, int n, uint32_t max_blocks, const EncTables *tab, const int16_t *coef,
-                    uint32_t *bits, const uint32_t *bitoff, uint8_t *stream, bool emit, hipStream_t s);
+                    int16_t *dcq, uint32_t *acbits, uint32_t *acscr, int bgr, int fastdct, hipStream_t s);
+hipError_t enc_len(const EncFrame *fr, int n, uint32_t max_blocks, const EncTables *tab, const int16_t *dcq,
+                   const uint32_t *acbits, uint32_t *bits, hipStream_t s);
+hipError_t enc_pack(const EncFrame *fr, int n, uint32_t max_blocks, const EncTables *tab, const int16_t *dcq,
+                    const uint32_t *acbits, const uint32_t *acscr, const uint32_t *bitoff, const uint32_t *total_bits,
+                    uint8_t *stream, hipStream_t s);
 hipError_t enc_ff_count(const EncFrame *fr, int n, uint32_t max_tiles, const uint32_t *total_bits,
                         const uint8_t *stream, uint32_t *tile_cnt, hipStream_t s);
 hipError_t enc_ff_write(const EncFrame *fr, int n, uint32_t max_tiles, const uint32_t *total_bits,

@@ -720,7 +720,9 @@ int Codec::prepare_encode(const int *ws, const int *hs, const uint64_t *img_offs
   CK(d_esegs_.ensure(sizeof(ScanSeg) * segs.size()));
   CK(d_etsum_.ensure(sizeof(uint32_t) * (t0 + 1)));
   CK(d_etotals_.ensure(sizeof(uint32_t) * segs.size()));
-  CK(d_ecoef_.ensure(blk * 128));
+  CK(d_dcq_.ensure(sizeof(int16_t) * blk));
+  CK(d_acbits_.ensure(sizeof(uint32_t) * blk));
+  CK(d_acscr_.ensure(sizeof(uint32_t) * kAcScratchWords * blk));
   CK(d_bits_.ensure(sizeof(uint32_t) * blk));
   CK(d_bitoff_.ensure(sizeof(uint32_t) * blk));
   CK(d_stream_.ensure(bits));
@@ -742,14 +744,14 @@ int Codec::run_encode(int bgr, bool fastdct, std::string *err) {
   const ScanSeg *segs = d_esegs_.as<ScanSeg>();
   const int n = en_;
   CK(hipEventRecord(ev_[6], s_));
-  CK(enc_fdct(fr, n, emax_blocks_, tab, d_pix_.as<uint8_t>(), d_ecoef_.as<int16_t>(), bgr, fastdct ? 1 : 0, s_));
-  CK(enc_huff(fr, n, emax_blocks_, tab, d_ecoef_.as<int16_t>(), d_bits_.as<uint32_t>(), nullptr, nullptr, false, s_));
+  CK(enc_fdct(fr, n, emax_blocks_, tab, d_pix_.as<uint8_t>(), d_dcq_.as<int16_t>(), d_acbits_.as<uint32_t>(),
+              d_acscr_.as<uint32_t>(), bgr, fastdct ? 1 : 0, s_));
+  CK(enc_len(fr, n, emax_blocks_, tab, d_dcq_.as<int16_t>(), d_acbits_.as<uint32_t>(), d_bits_.as<uint32_t>(), s_));
   uint32_t *total_bits = d_etotals_.as<uint32_t>();
   CK(scan_u32(segs, n, (emax_blocks_ + kScanTile - 1) / kScanTile, d_bits_.as<uint32_t>(), d_bitoff_.as<uint32_t>(),
               d_etsum_.as<uint32_t>(), total_bits, false, s_));
-  CK(hipMemsetAsync(d_stream_.p, 0, ebits_bytes_, s_));
-  CK(enc_huff(fr, n, emax_blocks_, tab, d_ecoef_.as<int16_t>(), nullptr, d_bitoff_.as<uint32_t>(),
-              d_stream_.as<uint8_t>(), true, s_));
+  CK(enc_pack(fr, n, emax_blocks_, tab, d_dcq_.as<int16_t>(), d_acbits_.as<uint32_t>(), d_acscr_.as<uint32_t>(),
+              d_bitoff_.as<uint32_t>(), total_bits, d_stream_.as<uint8_t>(), s_));
   CK(hipEventRecord(ev_[7], s_));
   CK(enc_ff_count(fr, n, emax_tiles_, total_bits, d_stream_.as<uint8_t>(), d_ffcnt_.as<uint32_t>(), s_));
   uint32_t *nff = d_etotals_.as<uint32_t>() + n;

@@ -810,25 +810,50 @@ __device__ __forceinline__ int ycc_comp(int k, int r, int g, int b) {  // jccolo
   return (32768 * r - 27439 * g - 5329 * b + (128 << 16) + 32767) >> 16;
 }
 
+constexpr uint32_t kAcWords = kAcScratchWords;
+
+// `size` (<= 32) bits at stream bit `pos` of an MSB-first word array in LDS
+__device__ __forceinline__ void lds_put(uint32_t *words, uint32_t pos, uint32_t bits, uint32_t size) {
+  if (!size) return;
+  const uint32_t w = pos >> 5, sh = pos & 31;
+  if (sh + size <= 32) {
+    atomicOr(words + w, bits << (32 - sh - size));
+  } else {
+    const uint32_t n2 = sh + size - 32;  // bits spilling into the next word
+    atomicOr(words + w, bits >> n2);
+    atomicOr(words + w + 1, bits << (32 - n2));
+  }
+}
+
 // 8 lanes per block.  A workgroup takes M = 32 / bpm whole MCUs and orders its 32 block
 // slots block-in-MCU-major (slot s -> block-in-MCU s / M of MCU s % M), so a wave's 8 blocks
 // are mostly one component and the luma / chroma sampling paths do not diverge in a wave.
+// After quantisation the 8 lanes Huffman-code the block's AC coefficients (jchuff.c
+// encode_one_block, AC part): lane r codes zigzag positions 8r..8r+7; every run of zeros is
+// read off the block's 64-bit nonzero mask (ZRL for each 16), lane offsets come from an
+// 8-lane scan, and the bits are OR-ed into an LDS image of the block's AC stream that is then
+// copied out.  Outputs per block: quantised DC, AC bit count, AC bits (MSB-first words).
 __global__ __launch_bounds__(256) void k_fdct(const EncFrame *fr, const EncTables *tab, const uint8_t *pix,
-                                              int16_t *coef, int bgr, int fastdct) {
+                                              int16_t *dcq, uint32_t *acbits, uint32_t *acscr, int bgr,
+                                              int fastdct) {
   const EncFrame &F = fr[blockIdx.y];
   const Geom &g = F.g;
   const uint32_t M = 32 / (uint32_t)g.bpm;
   if (blockIdx.x * M >= (uint32_t)g.nmcu) return;
   __shared__ int32_t ws[32][8][9];
   __shared__ int16_t qo[32][64];
+  __shared__ uint32_t acw[32][kAcWords];
   __shared__ uint16_t s_recip[2][64], s_corr[2][64];
   __shared__ int16_t s_shift[2][64];
+  __shared__ uint32_t s_ac[2][256];
   if (threadIdx.x < 128) {
     const int t = threadIdx.x >> 6, i = threadIdx.x & 63;
     s_recip[t][i] = tab->recip[t][i];
     s_corr[t][i] = tab->corr[t][i];
     s_shift[t][i] = tab->shift[t][i];
   }
+  for (int i = threadIdx.x; i < 512; i += 256) s_ac[i >> 8][i & 255] = tab->ac[i >> 8][i & 255];
+  for (int i = threadIdx.x; i < 32 * (int)kAcWords; i += 256) (&acw[0][0])[i] = 0;
   const uint32_t slot = threadIdx.x >> 3, r = threadIdx.x & 7;
   const uint32_t c = slot / M, mcu = blockIdx.x * M + slot % M;
   const uint32_t b = mcu * (uint32_t)g.bpm + c;
@@ -836,7 +861,7 @@ __global__ __launch_bounds__(256) void k_fdct(const EncFrame *fr, const EncTable
   bool real = false;
   if (c < (uint32_t)g.bpm && mcu < (uint32_t)g.nmcu) {
     block_pos(g, b, &k, &bx, &by);
-    real = bx < (uint32_t)g.wb[k] && by < (uint32_t)g.hb[k];  // dummy blocks are made by enc_huff
+    real = bx < (uint32_t)g.wb[k] && by < (uint32_t)g.hb[k];  // dummy blocks are made by k_len / k_pack
   }
   const uint8_t *img = pix + F.img_off;
   if (real) {  // pass 1: row r of the block's samples
@@ -879,13 +904,13 @@ __global__ __launch_bounds__(256) void k_fdct(const EncFrame *fr, const EncTable
     for (int j = 0; j < 8; ++j) ws[slot][r][j] = v[j];
   }
   __syncthreads();
+  const int t = k > 0;
   if (real) {  // pass 2: column r, quantised
     int32_t v[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) v[i] = ws[slot][i][r];
     if (fastdct) fdct_ifast_line(v);
     else fdct_islow_line(v, 1);
-    const int t = k > 0;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int n = i * 8 + r;
@@ -893,20 +918,81 @@ __global__ __launch_bounds__(256) void k_fdct(const EncFrame *fr, const EncTable
     }
   }
   __syncthreads();
-  if (real) {  // zigzag positions 8r .. 8r+7, one 16-byte store
-    int16_t o[8];
+  // AC Huffman coding; every lane of the wave takes part in the 8-lane shuffles
+  int vz[8];
+  uint32_t m8 = 0;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = qo[slot][kNat[r * 8 + j]];
-    *reinterpret_cast<uint4 *>(coef + (F.blk0 + b) * 64 + r * 8) = *reinterpret_cast<const uint4 *>(o);
+  for (int j = 0; j < 8; ++j) {
+    vz[j] = real ? qo[slot][kNat[r * 8 + j]] : 0;
+    if (vz[j] != 0 && (r | j) != 0) m8 |= 1u << j;
+  }
+  uint64_t mask = (uint64_t)m8 << (8 * r);
+  mask |= __shfl_xor(mask, 1, 8);
+  mask |= __shfl_xor(mask, 2, 8);
+  mask |= __shfl_xor(mask, 4, 8);
+  const uint64_t starts = mask | 1ull;  // the DC position starts the first run
+  const uint32_t zrl = s_ac[t][0xF0], eobc = s_ac[t][0x00];
+  const bool eob = mask == 0 || (63 - __clzll(mask)) < 63;
+  uint32_t nbits = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    if (!(m8 >> j & 1)) continue;
+    const int kk = 8 * (int)r + j;
+    const int prev = 63 - __clzll(starts & ((1ull << kk) - 1));
+    const int run = kk - prev - 1;
+    const uint32_t av = (uint32_t)(vz[j] < 0 ? -vz[j] : vz[j]);
+    const uint32_t nb = 32 - __clz(av);
+    nbits += (uint32_t)(run >> 4) * (zrl & 0xFF) + (s_ac[t][((run & 15) << 4) + nb] & 0xFF) + nb;
+  }
+  if (r == 7 && eob) nbits += eobc & 0xFF;
+  uint32_t incl = nbits;
+#pragma unroll
+  for (int off = 1; off < 8; off <<= 1) {
+    const uint32_t y = __shfl_up(incl, off, 8);
+    if ((int)r >= off) incl += y;
+  }
+  const uint32_t total = __shfl(incl, 7, 8);
+  if (real) {
+    uint32_t pos = incl - nbits;
+    uint32_t *aw = acw[slot];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (!(m8 >> j & 1)) continue;
+      const int kk = 8 * (int)r + j;
+      const int prev = 63 - __clzll(starts & ((1ull << kk) - 1));
+      int run = kk - prev - 1;
+      for (; run > 15; run -= 16) {
+        lds_put(aw, pos, zrl >> 8, zrl & 0xFF);
+        pos += zrl & 0xFF;
+      }
+      const int v = vz[j];
+      const uint32_t av = (uint32_t)(v < 0 ? -v : v);
+      const uint32_t nb = 32 - __clz(av);
+      const uint32_t e = s_ac[t][(run << 4) + nb];
+      const uint32_t code = ((e >> 8) << nb) | ((uint32_t)(v < 0 ? v - 1 : v) & ((1u << nb) - 1));
+      lds_put(aw, pos, code, (e & 0xFF) + nb);
+      pos += (e & 0xFF) + nb;
+    }
+    if (r == 7 && eob) lds_put(aw, pos, eobc >> 8, eobc & 0xFF);
+  }
+  __syncthreads();
+  if (real) {
+    const uint64_t gb = F.blk0 + b;
+    const uint32_t nw = (total + 31) >> 5;
+    for (uint32_t i = r; i < nw; i += 8) acscr[gb * kAcWords + i] = acw[slot][i];
+    if (r == 0) {
+      dcq[gb] = qo[slot][0];
+      acbits[gb] = total;
+    }
   }
 }
 
-// ---- encoder: Huffman ------------------------------------------------------------------------
+// ---- encoder: DC coding, bit offsets, packing --------------------------------------------------
 
-// DC of block-in-MCU c of MCU `mcu`, following jccoefct.c for dummy blocks: a dummy block at
-// the right edge takes its left neighbour's DC, a dummy row at the bottom the DC of the
-// component's last block in the row above (within the MCU).
-__device__ __forceinline__ int enc_dc_of(const Geom &g, const int16_t *coef, uint32_t mcu, uint32_t c) {
+// Quantised DC of block-in-MCU c of MCU `mcu`, following jccoefct.c for dummy blocks: a dummy
+// block at the right edge takes its left neighbour's DC, a dummy row at the bottom the DC of
+// the component's last block in the row above (within the MCU).
+__device__ __forceinline__ int enc_dc_of(const Geom &g, const int16_t *dcq, uint32_t mcu, uint32_t c) {
   const int k = g.bcomp[c];
   int xi = g.bxo[c], yi = g.byo[c];
   const int mx = (int)(mcu % (uint32_t)g.mcux), my = (int)(mcu / (uint32_t)g.mcux);
@@ -921,32 +1007,33 @@ __device__ __forceinline__ int enc_dc_of(const Geom &g, const int16_t *coef, uin
       xi -= 1;
       continue;
     }
-    const uint32_t cc = (uint32_t)(g.cfirst[k] + yi * g.mh[k] + xi);
-    return coef[((uint64_t)mcu * g.bpm + cc) * 64];
+    return dcq[(uint64_t)mcu * g.bpm + (uint32_t)(g.cfirst[k] + yi * g.mh[k] + xi)];
   }
 }
 
-template <bool EMIT>
-struct BitSink;
+// DC difference of block b (jchuff.c: diff to the previous block of the same component in
+// scan order) and whether b is a dummy edge block
+__device__ __forceinline__ int enc_dc_diff(const Geom &g, const int16_t *dcq, uint32_t b, bool *dummy) {
+  const uint32_t mcu = b / (uint32_t)g.bpm, c = b % (uint32_t)g.bpm;
+  const int k = g.bcomp[c];
+  const int dc = enc_dc_of(g, dcq, mcu, c);
+  int pred = 0;
+  if ((int)c > g.cfirst[k]) pred = enc_dc_of(g, dcq, mcu, c - 1);
+  else if (mcu > 0) pred = enc_dc_of(g, dcq, mcu - 1, (uint32_t)(g.cfirst[k] + g.mh[k] * g.mv[k] - 1));
+  const int mx = (int)(mcu % (uint32_t)g.mcux), my = (int)(mcu / (uint32_t)g.mcux);
+  *dummy = mx * g.mh[k] + g.bxo[c] >= g.wb[k] || my * g.mv[k] + g.byo[c] >= g.hb[k];
+  return dc - pred;
+}
 
-template <>
-struct BitSink<false> {
-  uint32_t total = 0;
-  __device__ __forceinline__ void put(uint32_t, uint32_t size) { total += size; }
-  __device__ __forceinline__ void finish() {}
-};
-
-template <>
-struct BitSink<true> {
+struct BitSink {  // MSB-first bits into big-endian words at a bit offset
   uint32_t *w;
   uint32_t wi;
   uint64_t acc;
   uint32_t n;
   bool first;
-  uint32_t total;
   __device__ __forceinline__ BitSink(uint32_t *words, uint32_t off)
-      : w(words), wi(off >> 5), acc(0), n(off & 31), first(true), total(0) {}
-  __device__ __forceinline__ void put(uint32_t code, uint32_t size) {
+      : w(words), wi(off >> 5), acc(0), n(off & 31), first(true) {}
+  __device__ __forceinline__ void put(uint32_t code, uint32_t size) {  // size <= 32
     acc = (acc << size) | code;
     n += size;
     if (n >= 32) {
@@ -964,85 +1051,60 @@ struct BitSink<true> {
   }
 };
 
-template <bool EMIT>
-__device__ __forceinline__ uint32_t encode_block(const Geom &g, const int16_t *cb, uint32_t b,
-                                                 const uint32_t (*dcT)[16], const uint32_t (*acT)[256],
-                                                 BitSink<EMIT> &out) {
-  const uint32_t mcu = b / (uint32_t)g.bpm, c = b % (uint32_t)g.bpm;
-  const int k = g.bcomp[c];
-  const int t = k > 0;
-  const int dc = enc_dc_of(g, cb, mcu, c);
-  int pred = 0;
-  if ((int)c > g.cfirst[k]) pred = enc_dc_of(g, cb, mcu, c - 1);
-  else if (mcu > 0) pred = enc_dc_of(g, cb, mcu - 1, (uint32_t)(g.cfirst[k] + g.mh[k] * g.mv[k] - 1));
-  const int mx = (int)(mcu % (uint32_t)g.mcux), my = (int)(mcu / (uint32_t)g.mcux);
-  const bool dummy = mx * g.mh[k] + g.bxo[c] >= g.wb[k] || my * g.mv[k] + g.byo[c] >= g.hb[k];
-  // DC difference (jchuff.c encode_one_block)
-  const int diff = dc - pred;
+__device__ __forceinline__ uint32_t dc_category(int diff) {
   const uint32_t a = (uint32_t)(diff < 0 ? -diff : diff);
-  const uint32_t nbits = a ? 32 - __clz(a) : 0;
-  uint32_t e = dcT[t][nbits];
-  out.put(e >> 8, e & 0xFF);
-  if (nbits) out.put((uint32_t)(diff < 0 ? diff - 1 : diff) & ((1u << nbits) - 1), nbits);
-  int run = 0;
-  if (!dummy) {
-    const uint4 *src = reinterpret_cast<const uint4 *>(cb + (uint64_t)b * 64);
-    for (int q = 0; q < 8; ++q) {
-      const uint4 raw = src[q];
-      const int16_t *vv = reinterpret_cast<const int16_t *>(&raw);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        if (q == 0 && j == 0) continue;
-        const int v = vv[j];
-        if (v == 0) {
-          ++run;
-          continue;
-        }
-        while (run > 15) {
-          e = acT[t][0xF0];
-          out.put(e >> 8, e & 0xFF);
-          run -= 16;
-        }
-        const uint32_t av = (uint32_t)(v < 0 ? -v : v);
-        const uint32_t nb = 32 - __clz(av);
-        e = acT[t][(run << 4) + nb];
-        out.put(e >> 8, e & 0xFF);
-        out.put((uint32_t)(v < 0 ? v - 1 : v) & ((1u << nb) - 1), nb);
-        run = 0;
-      }
-    }
-  } else {
-    run = 63;
-  }
-  if (run > 0) {
-    e = acT[t][0];
-    out.put(e >> 8, e & 0xFF);
-  }
-  return 0;
+  return a ? 32 - __clz(a) : 0;
 }
 
-template <bool EMIT>
-__global__ __launch_bounds__(256) void k_huff(const EncFrame *fr, const EncTables *tab, const int16_t *coef,
-                                              uint32_t *bits, const uint32_t *bitoff, uint8_t *stream) {
+// bits of every block: DC code + extra bits + AC bits (a dummy block's AC is one EOB)
+__global__ __launch_bounds__(256) void k_len(const EncFrame *fr, const EncTables *tab, const int16_t *dcq,
+                                             const uint32_t *acbits, uint32_t *bits) {
   const EncFrame &F = fr[blockIdx.y];
   const Geom &g = F.g;
-  if (blockIdx.x * 256 >= (uint32_t)g.nblocks) return;
-  __shared__ uint32_t sdc[2][16], sac[2][256];
-  for (int i = threadIdx.x; i < 512; i += 256) sac[i >> 8][i & 255] = tab->ac[i >> 8][i & 255];
-  if (threadIdx.x < 32) sdc[threadIdx.x >> 4][threadIdx.x & 15] = tab->dc[threadIdx.x >> 4][threadIdx.x & 15];
-  __syncthreads();
   const uint32_t b = blockIdx.x * 256 + threadIdx.x;
   if (b >= (uint32_t)g.nblocks) return;
-  const int16_t *cb = coef + F.blk0 * 64;
-  if (EMIT) {
-    BitSink<true> out(reinterpret_cast<uint32_t *>(stream + F.bits_off), bitoff[F.blk0 + b]);
-    encode_block<true>(g, cb, b, sdc, sac, out);
-    out.finish();
+  bool dummy;
+  const int diff = enc_dc_diff(g, dcq + F.blk0, b, &dummy);
+  const int t = g.bcomp[b % (uint32_t)g.bpm] > 0;
+  const uint32_t nb = dc_category(diff);
+  bits[F.blk0 + b] = (tab->dc[t][nb] & 0xFF) + nb + (dummy ? (tab->ac[t][0] & 0xFF) : acbits[F.blk0 + b]);
+}
+
+// every block writes its bits at its offset: DC code, extra bits, then its AC words
+__global__ __launch_bounds__(256) void k_pack(const EncFrame *fr, const EncTables *tab, const int16_t *dcq,
+                                              const uint32_t *acbits, const uint32_t *acscr, const uint32_t *bitoff,
+                                              uint8_t *stream) {
+  const EncFrame &F = fr[blockIdx.y];
+  const Geom &g = F.g;
+  const uint32_t b = blockIdx.x * 256 + threadIdx.x;
+  if (b >= (uint32_t)g.nblocks) return;
+  bool dummy;
+  const int diff = enc_dc_diff(g, dcq + F.blk0, b, &dummy);
+  const int t = g.bcomp[b % (uint32_t)g.bpm] > 0;
+  const uint32_t nb = dc_category(diff);
+  BitSink out(reinterpret_cast<uint32_t *>(stream + F.bits_off), bitoff[F.blk0 + b]);
+  const uint32_t e = tab->dc[t][nb];
+  out.put(e >> 8, e & 0xFF);
+  if (nb) out.put((uint32_t)(diff < 0 ? diff - 1 : diff) & ((1u << nb) - 1), nb);
+  if (dummy) {
+    const uint32_t eob = tab->ac[t][0];
+    out.put(eob >> 8, eob & 0xFF);
   } else {
-    BitSink<false> out;
-    encode_block<false>(g, cb, b, sdc, sac, out);
-    bits[F.blk0 + b] = out.total;
+    const uint64_t gb = F.blk0 + b;
+    const uint32_t n = acbits[gb];
+    const uint32_t *aw = acscr + gb * kAcWords;
+    for (uint32_t i = 0; i < (n >> 5); ++i) out.put(aw[i], 32);
+    if (n & 31) out.put(aw[n >> 5] >> (32 - (n & 31)), n & 31);
   }
+  out.finish();
+}
+
+// zero the words the packed stream of each frame will occupy (boundary words are OR-ed)
+__global__ __launch_bounds__(256) void k_zero_stream(const EncFrame *fr, const uint32_t *total_bits, uint8_t *stream) {
+  const EncFrame &F = fr[blockIdx.y];
+  const uint32_t nw = (total_bits[blockIdx.y] >> 5) + 2;
+  uint32_t *w = reinterpret_cast<uint32_t *>(stream + F.bits_off);
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < nw; i += gridDim.x * 256) w[i] = 0;
 }
 
 // ---- encoder: byte stuffing, header, EOI ------------------------------------------------------
@@ -1166,20 +1228,28 @@ hipError_t dec_color(const DecFrame *fr, int n, int max_w, int max_h, const uint
 }
 
 hipError_t enc_fdct(const EncFrame *fr, int n, uint32_t max_blocks, const EncTables *tab, const uint8_t *pix,
-                    int16_t *coef, int bgr, int fastdct, hipStream_t s) {
+                    int16_t *dcq, uint32_t *acbits, uint32_t *acscr, int bgr, int fastdct, hipStream_t s) {
   if (n <= 0 || !max_blocks) return hipSuccess;
   // a workgroup takes bpm * (32 / bpm) >= 27 blocks (bpm <= 10)
-  hipLaunchKernelGGL(k_fdct, dim3((max_blocks + 26) / 27, (unsigned)n), dim3(256), 0, s, fr, tab, pix, coef, bgr,
-                     fastdct);
+  hipLaunchKernelGGL(k_fdct, dim3((max_blocks + 26) / 27, (unsigned)n), dim3(256), 0, s, fr, tab, pix, dcq, acbits,
+                     acscr, bgr, fastdct);
   return hipGetLastError();
 }
 
-hipError_t enc_huff(const EncFrame *fr, int n, uint32_t max_blocks, const EncTables *tab, const int16_t *coef,
-                    uint32_t *bits, const uint32_t *bitoff, uint8_t *stream, bool emit, hipStream_t s) {
+hipError_t enc_len(const EncFrame *fr, int n, uint32_t max_blocks, const EncTables *tab, const int16_t *dcq,
+                   const uint32_t *acbits, uint32_t *bits, hipStream_t s) {
   if (n <= 0 || !max_blocks) return hipSuccess;
-  const dim3 g((max_blocks + 255) / 256, (unsigned)n);
-  if (emit) hipLaunchKernelGGL(k_huff<true>, g, dim3(256), 0, s, fr, tab, coef, bits, bitoff, stream);
-  else hipLaunchKernelGGL(k_huff<false>, g, dim3(256), 0, s, fr, tab, coef, bits, bitoff, stream);
+  hipLaunchKernelGGL(k_len, dim3((max_blocks + 255) / 256, (unsigned)n), dim3(256), 0, s, fr, tab, dcq, acbits, bits);
+  return hipGetLastError();
+}
+
+hipError_t enc_pack(const EncFrame *fr, int n, uint32_t max_blocks, const EncTables *tab, const int16_t *dcq,
+                    const uint32_t *acbits, const uint32_t *acscr, const uint32_t *bitoff, const uint32_t *total_bits,
+                    uint8_t *stream, hipStream_t s) {
+  if (n <= 0 || !max_blocks) return hipSuccess;
+  hipLaunchKernelGGL(k_zero_stream, dim3(64, (unsigned)n), dim3(256), 0, s, fr, total_bits, stream);
+  hipLaunchKernelGGL(k_pack, dim3((max_blocks + 255) / 256, (unsigned)n), dim3(256), 0, s, fr, tab, dcq, acbits,
+                     acscr, bitoff, stream);
   return hipGetLastError();
 }
 
