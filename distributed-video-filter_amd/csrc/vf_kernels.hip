@@ -111,6 +111,15 @@ const char *variant_name(int v) {
   return (v >= 0 && v < kVariantCount) ? names[v] : "?";
 }
 
+// Bodies above kSplitBytes are cut into equal sub-launches of at most kChunkBytes, issued
+// back to back on the stream.  Measured (profiles/r01_large_buffers.txt, tools/tune_invert
+// large): ONE grid-stride launch over 1.6-12.7 GB runs at 5.0-5.6 TB/s, the same bytes as
+// 192-256 MiB launches at 6.2-6.3 TB/s (64 MiB: 5.7, the grid is then half empty; 1 GiB:
+// 6.0).  Each sub-launch is 1.5-2 grid strides, so workgroups re-align at every launch
+// boundary instead of drifting apart over tens of strides.
+constexpr uint64_t kSplitBytes = 512ull << 20;
+constexpr uint64_t kChunkBytes = 256ull << 20;
+
 template <int U, bool NTL, bool NTS>
 static hipError_t launch_stream(const uint8_t *src, uint8_t *dst, size_t nbytes, int max_blocks,
                                 hipStream_t stream) {
@@ -120,15 +129,27 @@ static hipError_t launch_stream(const uint8_t *src, uint8_t *dst, size_t nbytes,
   const uint64_t rest = nbytes - h;
   const uint64_t n16 = rest >> 4;
   const uint32_t tail = (uint32_t)(rest & 15);
-  const uint64_t tiles = (n16 + (uint64_t)kBlock * U - 1) / ((uint64_t)kBlock * U);
-  uint64_t blocks = tiles ? tiles : 1;
-  if (blocks > (uint64_t)max_blocks) blocks = (uint64_t)max_blocks;
+  constexpr uint64_t TILE = (uint64_t)kBlock * U;  // vectors per tile
+  const uint64_t nchunks = (n16 << 4) > kSplitBytes ? ((n16 << 4) + kChunkBytes - 1) / kChunkBytes : 1;
+  // whole tiles per chunk; the last chunk takes the remainder (including any partial tile)
+  const uint64_t per = nchunks > 1 ? ((n16 + nchunks - 1) / nchunks + TILE - 1) / TILE * TILE : n16;
   const uint8_t *bs = src + h;
   uint8_t *bd = dst + h;
-  hipLaunchKernelGGL((invert_stream_kernel<U, NTL, NTS>), dim3((unsigned)blocks), dim3(kBlock), 0,
-                     stream, reinterpret_cast<const u32x4 *>(bs), reinterpret_cast<u32x4 *>(bd),
-                     n16, src, dst, h, bs + (n16 << 4), bd + (n16 << 4), tail);
-  return hipGetLastError();
+  for (uint64_t c0 = 0, k = 0; k == 0 || c0 < n16; c0 += per, ++k) {
+    const uint64_t m = (n16 - c0) < per ? (n16 - c0) : per;
+    const bool first = k == 0, last = c0 + m >= n16;
+    const uint64_t tiles = (m + TILE - 1) / TILE;
+    uint64_t blocks = tiles ? tiles : 1;
+    if (blocks > (uint64_t)max_blocks) blocks = (uint64_t)max_blocks;
+    hipLaunchKernelGGL((invert_stream_kernel<U, NTL, NTS>), dim3((unsigned)blocks), dim3(kBlock), 0,
+                       stream, reinterpret_cast<const u32x4 *>(bs) + c0,
+                       reinterpret_cast<u32x4 *>(bd) + c0, m, src, dst, first ? h : 0u,
+                       bs + (n16 << 4), bd + (n16 << 4), last ? tail : 0u);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    if (last) break;
+  }
+  return hipSuccess;
 }
 
 hipError_t launch_invert(const void *dsrc, void *ddst, size_t nbytes, const LaunchCfg &cfg,

@@ -117,6 +117,29 @@ def test_device_entry_alignment(vf_ctx, soff, doff):
         vf_ctx.free_device(dd)
 
 
+@pytest.mark.parametrize("soff,n", [(3, (600 << 20) + 77), (0, (512 << 20) + 16), (7, 1_300_000_009)])
+def test_device_split_launch_ragged(vf_ctx, soff, n):
+    """Bodies above 512 MiB are cut into <= 256 MiB sub-launches (vf_kernels.hip
+    launch_stream): the head goes with the first, the tail with the last; no byte outside
+    [dst, dst+n) is touched.  Checked against the oracle on the whole range."""
+    x = np.random.default_rng(n & 0xFFFF).integers(0, 256, n, dtype=np.uint8)
+    ds = vf_ctx.alloc_device(n + 64)
+    dd = vf_ctx.alloc_device(n + 64)
+    try:
+        vf_ctx.memset_device(dd, 0x5A, n + 64)
+        vf_ctx.upload(ds + soff, x, n)
+        vf_ctx.invert_device(ds + soff, dd + soff, n)
+        vf_ctx.sync()
+        y = np.empty(n + 64, np.uint8)
+        vf_ctx.download(y, dd, n + 64)
+        vf_ctx.sync()
+        assert np.array_equal(y[soff:soff + n], oracle.invert(x))
+        assert (y[:soff] == 0x5A).all() and (y[soff + n:] == 0x5A).all()
+    finally:
+        vf_ctx.free_device(ds)
+        vf_ctx.free_device(dd)
+
+
 def test_device_frames_descriptor_kernel(vf_ctx):
     shapes = [(480, 640), (1080, 1920), (2160, 3840), (17, 13), (480, 480)]
     frames = [oracle.synthetic_frame(40 + i, h, w) for i, (h, w) in enumerate(shapes)]
@@ -183,7 +206,7 @@ def test_errors_are_raised_not_swallowed(vf_ctx):
 
 
 def test_hbm_resident_sweep_point_batch256(vf_ctx):
-    """configs[4] smallest point: 256 x 1080p (1.59 GB) resident in HBM, one launch."""
+    """configs[4] smallest point: 256 x 1080p (1.59 GB) resident in HBM, one call (7 sub-launches)."""
     n_frames = 256
     total = n_frames * FB_1080
     seeds = [0, 1, 2, 3]

@@ -28,7 +28,7 @@ from vfilter.synthetic import SIZES, synthetic_frame  # noqa: E402
 PEAK = 8000.0
 
 
-def kernel_point(ctx, tag, h, w, batch, ring_min_bytes=2.4e9, steps=40):
+def kernel_point(ctx, tag, h, w, batch, ring_min_bytes=2.4e9, steps=40, warm=3, warm_ms=0.0, timed_ms=0.0):
     fb = h * w * 3
     bb = fb * batch
     nbuf = max(1, int(ring_min_bytes // (2 * bb)))
@@ -44,17 +44,27 @@ def kernel_point(ctx, tag, h, w, batch, ring_min_bytes=2.4e9, steps=40):
         dsts.append(d)
     ctx.sync()
     steps = max(4, min(steps, int(40 * 4e8 / (2 * bb)) + 4))
-    ctx.bench_device_ring(srcs, dsts, bb, 3)
+    # warm for at least warm_ms of kernel time (clocks and the fabric settle after the
+    # PCIe-bound upload phase), then time at least timed_ms
+    done_ms, est = 0.0, None
+    while True:
+        ms_w, _ = ctx.bench_device_ring(srcs, dsts, bb, warm)
+        done_ms += ms_w
+        est = ms_w / warm
+        if done_ms >= warm_ms:
+            break
+    steps = max(steps, int(timed_ms / est) + 1)
     region, _ = ctx.bench_device_ring(srcs, dsts, bb, steps)
-    _, iso = ctx.bench_device_ring(srcs, dsts, bb, min(steps, 10), per_launch=True)
+    _, iso = ctx.bench_device_ring(srcs, dsts, bb, max(min(steps, 40), 10), per_launch=True)
     for s, d in zip(srcs, dsts):
         ctx.free_device(s)
         ctx.free_device(d)
     ms = region / steps
     gbs = 2 * bb / (ms * 1e-3) / 1e9
     return {"kind": "kernel", "size": tag, "frame": [h, w, 3], "batch": batch, "bytes_in": bb,
-            "ring_buffers": nbuf, "steps": steps, "ms_per_launch": round(ms, 4),
+            "ring_buffers": nbuf, "steps": steps, "warm_ms": round(done_ms, 1), "ms_per_launch": round(ms, 4),
             "isolated_ms_median": round(float(np.median(iso)), 4),
+            "isolated_ms_min_max": [round(float(np.min(iso)), 4), round(float(np.max(iso)), 4)],
             "frames_per_s": round(batch / (ms * 1e-3), 1), "GBps": round(gbs, 1), "frac_of_peak": round(gbs / PEAK, 4)}
 
 
@@ -91,16 +101,22 @@ def main():
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "sweep.jsonl"))
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--e2e-only", action="store_true")
+    ap.add_argument("--c5-only", action="store_true", help="only the configs[4] large-batch points")
     ap.add_argument("--c5-point", type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument("--warm-ms", type=float, default=300.0, help="configs[4] points: min kernel ms of warmup")
+    ap.add_argument("--timed-ms", type=float, default=200.0, help="configs[4] points: min kernel ms timed")
     args = ap.parse_args()
     if args.c5_point:
         c = Context(0)
-        print(json.dumps(kernel_point(c, "1080p", 1080, 1920, args.c5_point, ring_min_bytes=0, steps=6)))
+        print(json.dumps(kernel_point(c, "1080p", 1080, 1920, args.c5_point, ring_min_bytes=0, steps=12,
+                                      warm=5, warm_ms=args.warm_ms, timed_ms=args.timed_ms)))
         c.close()
         return
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
     ctx = Context(0, max_frame_bytes=2160 * 3840 * 3, max_batch=4)
     points = [("480p", 32), ("480p", 256), ("1080p", 32), ("4k", 16), ("4k", 64)]
+    if args.c5_only:
+        points = []
     sweep = [256, 512, 1024] if args.quick else [256, 512, 1024, 2048, 4096]
     with open(args.out, "w") as f:
         def emit(r):
@@ -114,12 +130,13 @@ def main():
         # process: after many alloc/free cycles a multi-GB hipMalloc measured up to 20 % slower
         # (profiles/r01_large_buffers.txt), which a worker that allocates once never sees.
         for b in ([] if args.e2e_only else sweep):
-            r = subprocess.run([sys.executable, os.path.abspath(__file__), "--c5-point", str(b)],
+            r = subprocess.run([sys.executable, os.path.abspath(__file__), "--c5-point", str(b),
+                                "--warm-ms", str(args.warm_ms), "--timed-ms", str(args.timed_ms)],
                                capture_output=True, text=True, timeout=300)
             if r.returncode != 0:
                 raise RuntimeError(f"configs[4] point {b} failed: {r.stderr[-500:]}")
             emit(json.loads(r.stdout.strip().splitlines()[-1]))
-        for tag, b in (("480p", 32), ("1080p", 32), ("4k", 16)):
+        for tag, b in ((("480p", 32), ("1080p", 32), ("4k", 16)) if not args.c5_only else ()):
             h, w = SIZES[tag]
             emit(e2e_point(ctx, tag, h, w, b))
     ctx.close()

@@ -49,10 +49,9 @@ static const char *vname(int v) { return vf::variant_name(v); }
 
 // Large single-buffer experiment (configs[4]): one src of `bytes`, dst at several offsets
 // from a bigger allocation, and the same bytes as one launch vs sub-range launches.
-static int large_mode(size_t bytes, int reps) {
+static int large_mode(size_t bytes, int reps, size_t pad) {
   vf::LaunchCfg lc;
   uint8_t *src, *dst;
-  const size_t pad = (size_t)64 << 20;
   CK(hipMalloc(&src, bytes));
   CK(hipMalloc(&dst, bytes + pad));
   hipLaunchKernelGGL(fill_kernel, dim3(4096), dim3(256), 0, 0, src, bytes, 77u);
@@ -60,13 +59,15 @@ static int large_mode(size_t bytes, int reps) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  std::printf("large-buffer mode: %zu B, src %p dst %p (dst-src = %lld)\n", bytes, (void *)src,
-              (void *)dst, (long long)(dst - src));
+  std::printf("large-buffer mode: %zu B, dst alloc pad %zu, src %p dst %p (dst-src = %lld)\n", bytes, pad,
+              (void *)src, (void *)dst, (long long)(dst - src));
   const size_t offs[] = {0, 4096, 65536, (size_t)1 << 20, (size_t)2 << 20, (size_t)8 << 20,
                          (size_t)32 << 20};
-  const size_t subs[] = {0, (size_t)199065600, (size_t)1 << 30};
+  const size_t subs[] = {0, (size_t)64 << 20, (size_t)128 << 20, (size_t)192 << 20, (size_t)199065600,
+                         (size_t)256 << 20, (size_t)512 << 20, (size_t)1 << 30};
   for (size_t sub : subs) {
     for (size_t off : offs) {
+      if (off > pad) continue;  // dst + off + bytes must stay inside the dst allocation
       std::vector<double> v;
       for (int r = 0; r < reps; ++r) {
         CK(hipEventRecord(e0, 0));
@@ -89,7 +90,8 @@ static int large_mode(size_t bytes, int reps) {
 
 int main(int argc, char **argv) {
   if (argc > 2 && std::strcmp(argv[1], "large") == 0)
-    return large_mode(std::strtoull(argv[2], nullptr, 0), argc > 3 ? std::atoi(argv[3]) : 5);
+    return large_mode(std::strtoull(argv[2], nullptr, 0), argc > 3 ? std::atoi(argv[3]) : 5,
+                      (argc > 4 ? std::strtoull(argv[4], nullptr, 0) : 64) << 20);
   size_t batch = argc > 1 ? std::strtoull(argv[1], nullptr, 0) : (size_t)32 * 1920 * 1080 * 3;
   int ring = argc > 2 ? std::atoi(argv[2]) : 6;
   int rounds = argc > 3 ? std::atoi(argv[3]) : 7;
