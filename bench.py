@@ -19,6 +19,9 @@ Prints ONE JSON line on rank 0 (contract in the task statement), including
                 reported beside value, never as value.
   jpeg_mode     the reference's default use_jpeg=True path (decode -> invert -> encode) on 1080p
                 JPEGs: GPU-resident and host->host frames/s, with libjpeg-turbo on 1 core beside it.
+  distributor   configs[2] (4K, batch 16, frame-index shards, in-order reassembly) and configs[3]
+                (mixed 480p/1080p/4K stream, ordering overhead) through the distributor with one
+                worker process per GPU of this run: host->host frames/s, never the headline.
 """
 from __future__ import annotations
 
@@ -58,6 +61,8 @@ def parse():
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC traffic passes")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host->host end-to-end leg")
     ap.add_argument("--no-jpeg", action="store_true", help="skip the JPEG-mode leg (use_jpeg=True path)")
+    ap.add_argument("--no-distributor", action="store_true",
+                    help="skip the configs[2]/[3] distributor leg (worker process per GPU)")
     ap.add_argument("--probe", action="store_true", help=argparse.SUPPRESS)  # child under rocprofv3
     return ap.parse_args()
 
@@ -245,6 +250,50 @@ def cpu_baseline_jpeg(jpgs, seconds):
             "sample": f"{n} x 1080p JPEG frames ({dt:.1f} s) through libjpeg-turbo 2.1.2, 1 thread"}
 
 
+def distributor_leg(nworkers, ngpu, frames_scale=1.0, timeout_s=150):
+    """BASELINE.json configs[2] and configs[3] at this run's GPU count, host->host through the
+    whole fan-out: one Distributor (lossless, in-order reassembly, shared-memory ring) and one
+    `python -m vfilter.inverter` worker process per GPU (tools/pipeline_bench.py).
+      configs[2]  4K frames, batch 16, frame-index shards (policy "shard")
+      configs[3]  480p / 1080p / 4K interleaved 1:1:1, batch 16, credit-based pull (policy
+                  "pull"), reporting the ordering overhead (reorder wait, buffer depth)
+    Run by rank 0 as a child process group with a time limit, so a stuck worker cannot
+    outlive the bench; a failure is reported in the line, never raised."""
+    import signal
+    tool = os.path.join(ROOT, "tools", "pipeline_bench.py")
+    legs = {"configs[2]": ["--size", "4k", "--batch", "16", "--policy", "shard",
+                           "--frames", str(int(256 * nworkers * frames_scale))],
+            "configs[3]": ["--size", "mixed", "--batch", "16", "--policy", "pull",
+                           "--frames", str(int(384 * nworkers * frames_scale))]}
+    out = {}
+    for name, extra in legs.items():
+        cmd = [sys.executable, tool, "--workers", str(nworkers), "--gpus", str(ngpu), "--inflight", "2",
+               "--ring-slots", str(3 * 16 * nworkers)] + extra
+        t0 = time.time()
+        p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                             start_new_session=True)
+        try:
+            so, se = p.communicate(timeout=timeout_s)
+        except subprocess.TimeoutExpired:
+            os.killpg(p.pid, signal.SIGKILL)
+            p.communicate()
+            out[name] = {"error": f"timed out after {timeout_s} s"}
+            continue
+        lines = [ln for ln in so.splitlines() if ln.startswith("{")]
+        if p.returncode != 0 or not lines:
+            out[name] = {"error": f"rc={p.returncode}: {se[-300:]}"}
+            continue
+        r = json.loads(lines[-1])
+        keep = ("size", "workers", "gpus", "policy", "batch", "frames", "fps", "GBps_each_way",
+                "latency_ms_mean", "latency_ms_p99", "reorder_wait_mean_ms", "reorder_wait_max_ms",
+                "max_buffer_depth", "out_of_order_arrivals", "n_errors")
+        out[name] = {k: r[k] for k in keep if k in r}
+        out[name]["wall_s"] = round(time.time() - t0, 1)
+    out["note"] = ("host->host through distributor + shared-memory ring + one worker process per GPU; "
+                   "bound by host memory and PCIe, not HBM; never the headline value")
+    return out
+
+
 def main():
     args = parse()
     if args.probe:
@@ -332,6 +381,15 @@ def main():
         ctx.free_device(d)
     ctx.close()
 
+    fanout = None
+    if not args.no_distributor:
+        if rank == 0:
+            # one worker per rank; workers share GPUs only when rehearsing N ranks on fewer cards
+            fanout = distributor_leg(world, max(1, min(world, torch.cuda.device_count())))
+            log(f"distributor leg: {fanout}")
+        if world > 1:
+            dist.barrier()  # the other ranks idle (their GPUs serve the leg's workers)
+
     if rank == 0:
         frames = world * args.steps * args.batch
         line = {
@@ -365,6 +423,7 @@ def main():
             "cpu_baseline": cpu,
             "end_to_end": e2e,
             "jpeg_mode": jpeg,
+            "distributor": fanout,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
