@@ -224,10 +224,17 @@ def jpeg_mode(ctx, batch, iters=20):
     for _ in range(reps):
         tj.invert_batch(jpgs)
     h2h = (time.perf_counter() - t0) / reps
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(2) as ex:  # the worker's form (InverterWorker.submit_batch)
+        list(ex.map(lambda _: tj.invert_batch(jpgs), range(2)))
+        t0 = time.perf_counter()
+        list(ex.map(lambda _: tj.invert_batch(jpgs), range(10)))
+        h2h_pipe = (time.perf_counter() - t0) / 10
     return {"workload": f"1080p JPEG (q85 4:2:2) decode -> bitwise_not -> encode, batch {batch}",
             "gpu_resident_fps": round(batch / (ms / 1e3), 1), "gpu_resident_ms_per_batch": round(ms, 3),
             "stages_ms": {k: round(v, 4) for k, v in stages.items()},
             "host_to_host_fps": round(batch / h2h, 1),
+            "host_to_host_2threads_fps": round(batch / h2h_pipe, 1),
             "jpeg_bytes_mean": round(sum(len(j) for j in jpgs) / batch)}, jpgs
 
 

@@ -20,6 +20,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
+#include <condition_variable>
+#include <mutex>
 #include <new>
 #include <vector>
 
@@ -59,7 +62,13 @@ struct vf_ctx {
   // results of the last host->host job waited on (vf_elapsed_ms / vf_last_timeline)
   float last_kernel_ms = 0.f;
   std::vector<vf::ChunkTime> timeline;
-  vf::jpeg::Codec *jpeg = nullptr;  // created on first JPEG call
+  // JPEG codecs (created on first use, at most VF_JPEG_CODECS, default 2): each has its own
+  // stream and buffers, so JPEG calls from two host threads overlap one batch's host work
+  // (parse, staging, copy-out) with the other's GPU work.
+  std::mutex jpeg_mu;
+  std::condition_variable jpeg_cv;
+  std::vector<vf::jpeg::Codec *> jpeg_all, jpeg_free;
+  vf::jpeg::ComputeGate jpeg_gate;
 };
 
 namespace {
@@ -214,7 +223,7 @@ VF_EXPORT int vf_create(int device, size_t max_frame_bytes, int max_batch, vf_ct
 
 VF_EXPORT int vf_destroy(vf_ctx *ctx) {
   if (!ctx) return VF_OK;
-  delete ctx->jpeg;
+  for (vf::jpeg::Codec *c : ctx->jpeg_all) delete c;
   delete ctx->engine;  // finishes queued jobs first
   delete ctx;
   return VF_OK;
@@ -493,12 +502,41 @@ VF_EXPORT int vf_bench_device_ring(vf_ctx *ctx, void *const *srcs, void *const *
 
 namespace {
 
-int jpeg_codec(vf_ctx *ctx, vf::jpeg::Codec **out) {
-  if (!ctx->jpeg) {
-    ctx->jpeg = new (std::nothrow) vf::jpeg::Codec(ctx->device);
-    if (!ctx->jpeg) return set_err(ctx, VF_E_NOMEM, 0, "JPEG codec: out of host memory");
+// A codec leased to one call for its duration (blocks while all codecs are busy).
+class CodecLease {
+ public:
+  explicit CodecLease(vf_ctx *ctx) : ctx_(ctx) {
+    static const size_t kMax = std::max<size_t>(1, env_size("VF_JPEG_CODECS", 2));
+    std::unique_lock<std::mutex> lk(ctx->jpeg_mu);
+    ctx->jpeg_cv.wait(lk, [&] { return !ctx->jpeg_free.empty() || ctx->jpeg_all.size() < kMax; });
+    if (!ctx->jpeg_free.empty()) {
+      c_ = ctx->jpeg_free.back();
+      ctx->jpeg_free.pop_back();
+    } else {
+      c_ = new (std::nothrow) vf::jpeg::Codec(ctx->device, &ctx->jpeg_gate);
+      if (c_) ctx->jpeg_all.push_back(c_);
+    }
   }
-  *out = ctx->jpeg;
+  ~CodecLease() {
+    if (!c_) return;
+    {
+      std::lock_guard<std::mutex> lk(ctx_->jpeg_mu);
+      ctx_->jpeg_free.push_back(c_);
+    }
+    ctx_->jpeg_cv.notify_one();
+  }
+  CodecLease(const CodecLease &) = delete;
+  CodecLease &operator=(const CodecLease &) = delete;
+  vf::jpeg::Codec *get() const { return c_; }
+
+ private:
+  vf_ctx *ctx_;
+  vf::jpeg::Codec *c_ = nullptr;
+};
+
+int jpeg_codec(vf_ctx *ctx, const CodecLease &lease, vf::jpeg::Codec **out) {
+  if (!lease.get()) return set_err(ctx, VF_E_NOMEM, 0, "JPEG codec: out of host memory");
+  *out = lease.get();
   return VF_OK;
 }
 
@@ -529,8 +567,9 @@ VF_EXPORT int vf_jpeg_encode(vf_ctx *ctx, const uint8_t *const *imgs, const int 
   if (n < 0 || (n > 0 && (!imgs || !widths || !heights || !outs || !caps || !sizes)))
     return set_err(ctx, VF_E_INVALID, 0, "vf_jpeg_encode: bad arguments");
   if (n > 65535) return set_err(ctx, VF_E_INVALID, 0, "vf_jpeg_encode: at most 65535 frames per call");
+  CodecLease lease(ctx);
   vf::jpeg::Codec *c = nullptr;
-  int rc = jpeg_codec(ctx, &c);
+  int rc = jpeg_codec(ctx, lease, &c);
   if (rc) return rc;
   std::string err;
   rc = c->encode(imgs, widths, heights, n, pixel_format, quality, subsamp, flags, outs, caps, sizes, &err);
@@ -543,8 +582,9 @@ VF_EXPORT int vf_jpeg_decode(vf_ctx *ctx, const uint8_t *const *jpegs, const siz
   if (n < 0 || (n > 0 && (!jpegs || !jpeg_sizes || !outs || !caps)))
     return set_err(ctx, VF_E_INVALID, 0, "vf_jpeg_decode: bad arguments");
   if (n > 65535) return set_err(ctx, VF_E_INVALID, 0, "vf_jpeg_decode: at most 65535 frames per call");
+  CodecLease lease(ctx);
   vf::jpeg::Codec *c = nullptr;
-  int rc = jpeg_codec(ctx, &c);
+  int rc = jpeg_codec(ctx, lease, &c);
   if (rc) return rc;
   std::string err;
   rc = c->decode(jpegs, jpeg_sizes, n, pixel_format, flags, outs, caps, &err);
@@ -557,8 +597,9 @@ VF_EXPORT int vf_jpeg_invert(vf_ctx *ctx, const uint8_t *const *jpegs, const siz
   if (n < 0 || (n > 0 && (!jpegs || !jpeg_sizes || !outs || !caps || !sizes)))
     return set_err(ctx, VF_E_INVALID, 0, "vf_jpeg_invert: bad arguments");
   if (n > 65535) return set_err(ctx, VF_E_INVALID, 0, "vf_jpeg_invert: at most 65535 frames per call");
+  CodecLease lease(ctx);
   vf::jpeg::Codec *c = nullptr;
-  int rc = jpeg_codec(ctx, &c);
+  int rc = jpeg_codec(ctx, lease, &c);
   if (rc) return rc;
   std::string err;
   rc = c->invert(jpegs, jpeg_sizes, n, quality, subsamp, flags, outs, caps, sizes, &err);
@@ -570,8 +611,9 @@ VF_EXPORT int vf_jpeg_bench_invert(vf_ctx *ctx, const uint8_t *const *jpegs, con
   VF_CHECK_CTX(ctx);
   if (n <= 0 || n > 65535 || !jpegs || !jpeg_sizes || !ms || iters <= 0)
     return set_err(ctx, VF_E_INVALID, 0, "vf_jpeg_bench_invert: bad arguments");
+  CodecLease lease(ctx);
   vf::jpeg::Codec *c = nullptr;
-  int rc = jpeg_codec(ctx, &c);
+  int rc = jpeg_codec(ctx, lease, &c);
   if (rc) return rc;
   std::string err;
   rc = c->bench_invert(jpegs, jpeg_sizes, n, quality, subsamp, flags, iters, ms, stage_ms, &err);

@@ -3,7 +3,12 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "vf_jpeg.h"
@@ -45,12 +50,47 @@ struct HostBuf {
   ~HostBuf();
 };
 
+// A few persistent host threads for the per-frame host work of a batch (parsing, staging and
+// output copies): fn(i) for i in [0, n), indices handed out by an atomic counter; the caller
+// takes part and returns when every index is done.
+class TaskPool {
+ public:
+  explicit TaskPool(int nthreads);
+  ~TaskPool();
+  TaskPool(const TaskPool &) = delete;
+  TaskPool &operator=(const TaskPool &) = delete;
+  void run(int n, const std::function<void(int)> &fn);
+
+ private:
+  void loop();
+  void drain();
+  std::vector<std::thread> threads_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_cv_;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+  int active_ = 0;
+  int n_ = 0;
+  std::atomic<int> next_{0};
+  const std::function<void(int)> *fn_ = nullptr;
+};
+
+// Orders the GPU compute of the codecs of one context: a codec holds `mu` while it queues its
+// kernels, its stream first waits for `last` (the previous holder's kernels-done event) and
+// then publishes its own.  Kernels of two batches therefore never share the GPU (measured:
+// two 4K batches run concurrently took 12 ms each instead of 6), while one batch's host work
+// and copies still overlap the other's kernels.
+struct ComputeGate {
+  std::mutex mu;
+  hipEvent_t last = nullptr;
+};
+
 int header_info(const uint8_t *jpeg, size_t size, int *w, int *h, int *subsamp, int *colorspace, std::string *err);
 size_t buffer_size(int w, int h, int subsamp);
 
 class Codec {
  public:
-  explicit Codec(int device);
+  explicit Codec(int device, ComputeGate *gate = nullptr);
   ~Codec();
   Codec(const Codec &) = delete;
   Codec &operator=(const Codec &) = delete;
@@ -78,6 +118,7 @@ class Codec {
   int fetch_jpegs(uint8_t *const *outs, const size_t *caps, size_t *sizes, std::string *err);
 
   int device_;
+  ComputeGate *gate_;
   hipStream_t s_ = nullptr;
   hipEvent_t ev_[10] = {};
 
@@ -100,6 +141,7 @@ class Codec {
       d_out_, d_outsize_;
 
   HostBuf h_stage_, h_out_;
+  TaskPool pool_{4};
 };
 
 }  // namespace jpeg

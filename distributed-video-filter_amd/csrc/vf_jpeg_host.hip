@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -138,7 +139,10 @@ struct Parsed {
 };
 
 // jdmarker.c restated for baseline / extended sequential Huffman, one interleaved scan
-int parse(const uint8_t *b, size_t n, Parsed *P, std::string *err) {
+// Markers up to SOS.  With find_scan_end the entropy-coded segment's end is located too (the
+// first marker other than RSTn after SOS); memchr skips to each 0xFF (1 in ~256 bytes of
+// entropy data), so this costs a fraction of a byte-by-byte scan.  header_info does not need it.
+int parse(const uint8_t *b, size_t n, Parsed *P, std::string *err, bool find_scan_end = true) {
   auto fail = [&](const char *m) {
     *err = m;
     return -1;
@@ -215,8 +219,17 @@ int parse(const uint8_t *b, size_t n, Parsed *P, std::string *err) {
       if (s[1 + 2 * ns] != 0 || s[2 + 2 * ns] != 63 || s[3 + 2 * ns] != 0) return fail("not a baseline scan");
       P->scan_off = p + len;
       size_t q = P->scan_off;
+      if (!find_scan_end) q = n;
       while (q + 1 < n) {
-        if (b[q] == 0xFF && b[q + 1] != 0x00 && !(b[q + 1] >= 0xD0 && b[q + 1] <= 0xD7) && b[q + 1] != 0xFF) break;
+        const void *f = std::memchr(b + q, 0xFF, n - q);
+        if (!f) {
+          q = n;
+          break;
+        }
+        q = (size_t)(static_cast<const uint8_t *>(f) - b);
+        if (q + 1 >= n) break;
+        const uint8_t nx = b[q + 1];
+        if (nx != 0x00 && !(nx >= 0xD0 && nx <= 0xD7) && nx != 0xFF) break;
         ++q;
       }
       P->scan_end = q + 1 < n ? q : n;
@@ -438,7 +451,62 @@ HostBuf::~HostBuf() {
 
 // ---- codec -------------------------------------------------------------------------------------
 
-Codec::Codec(int device) : device_(device) {}
+TaskPool::TaskPool(int nthreads) {
+  for (int i = 1; i < nthreads; ++i) threads_.emplace_back([this] { loop(); });
+}
+
+TaskPool::~TaskPool() {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    stop_ = true;
+    ++gen_;
+  }
+  cv_.notify_all();
+  for (auto &t : threads_) t.join();
+}
+
+void TaskPool::drain() {
+  for (int i = next_.fetch_add(1); i < n_; i = next_.fetch_add(1)) (*fn_)(i);
+}
+
+void TaskPool::run(int n, const std::function<void(int)> &fn) {
+  if (n <= 1 || threads_.empty()) {
+    for (int i = 0; i < n; ++i) fn(i);
+    return;
+  }
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    fn_ = &fn;
+    n_ = n;
+    next_.store(0);
+    active_ = (int)threads_.size();
+    ++gen_;
+  }
+  cv_.notify_all();
+  drain();
+  std::unique_lock<std::mutex> lk(mu_);
+  done_cv_.wait(lk, [this] { return active_ == 0; });
+  fn_ = nullptr;
+}
+
+void TaskPool::loop() {
+  uint64_t seen = 0;
+  for (;;) {
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      cv_.wait(lk, [&] { return gen_ != seen; });
+      seen = gen_;
+      if (stop_) return;
+    }
+    drain();
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      if (--active_ == 0) done_cv_.notify_one();
+    }
+  }
+}
+
+Codec::Codec(int device, ComputeGate *gate) : device_(device), gate_(gate) {}
 
 Codec::~Codec() {
   (void)hipSetDevice(device_);
@@ -479,35 +547,45 @@ int Codec::prepare_decode(const uint8_t *const *jpegs, const size_t *sizes, int 
   uint32_t tiles = 0, subs = 0;
   dmax_tiles_ = dmax_sub_ = dmax_blocks_ = 0;
   dmax_w_ = dmax_h_ = 0;
-  for (int f = 0; f < n; ++f) {
+  // per frame, in parallel: markers, scan end, geometry and decode tables
+  std::vector<std::string> ferr((size_t)n);
+  pool_.run(n, [&](int f) {
     Parsed &P = parsed[(size_t)f];
-    if (!jpegs[f] || parse(jpegs[f], sizes[f], &P, err) != 0) {
-      if (!jpegs[f]) *err = "NULL JPEG buffer";
-      *err = "frame " + std::to_string(f) + ": " + *err;
-      return kJpeg;
+    std::string &e = ferr[(size_t)f];
+    if (!jpegs[f]) {
+      e = "NULL JPEG buffer";
+      return;
     }
+    if (parse(jpegs[f], sizes[f], &P, &e) != 0) return;
     if (P.restart) {
-      *err = "frame " + std::to_string(f) + ": restart intervals (DRI) are not supported by the GPU decoder yet";
-      return kJpeg;
+      e = "restart intervals (DRI) are not supported by the GPU decoder yet";
+      return;
     }
     DecFrame &F = dfr_[(size_t)f];
     if (!make_geom(P.w, P.h, P.ncomp, P.hs, P.vs, &F.g)) {
-      *err = "frame " + std::to_string(f) + ": unsupported sampling geometry";
-      return kJpeg;
+      e = "unsupported sampling geometry";
+      return;
     }
     for (int c = 0; c < P.ncomp; ++c) {
       std::memcpy(F.q[c], P.qt[P.tq[c]], sizeof F.q[c]);
       if (!decode_table(P.dcbits[P.td[c]], P.dcvals[P.td[c]], &F.dc[c]) ||
           !decode_table(P.acbits[P.ta[c]], P.acvals[P.ta[c]], &F.ac[c])) {
-        *err = "frame " + std::to_string(f) + ": bad Huffman table";
-        return kJpeg;
+        e = "bad Huffman table";
+        return;
       }
     }
     const size_t len = P.scan_end - P.scan_off;
-    if (len == 0 || len > (1u << 28)) {
-      *err = "frame " + std::to_string(f) + ": empty or oversized entropy-coded segment";
+    if (len == 0 || len > (1u << 28)) e = "empty or oversized entropy-coded segment";
+  });
+  for (int f = 0; f < n; ++f)
+    if (!ferr[(size_t)f].empty()) {
+      *err = "frame " + std::to_string(f) + ": " + ferr[(size_t)f];
       return kJpeg;
     }
+  for (int f = 0; f < n; ++f) {
+    const Parsed &P = parsed[(size_t)f];
+    DecFrame &F = dfr_[(size_t)f];
+    const size_t len = P.scan_end - P.scan_off;
     F.in_off = in_off;
     F.in_len = (uint32_t)len;
     F.ntiles = (uint32_t)((len + kTile - 1) / kTile);
@@ -559,10 +637,10 @@ int Codec::prepare_decode(const uint8_t *const *jpegs, const size_t *sizes, int 
     }
   // staging: inputs packed, then uploaded in one copy
   CK(h_stage_.ensure(in_off));
-  for (int f = 0; f < n; ++f) {
+  pool_.run(n, [&](int f) {
     const Parsed &P = parsed[(size_t)f];
     std::memcpy(h_stage_.as<uint8_t>() + dfr_[(size_t)f].in_off, jpegs[f] + P.scan_off, P.scan_end - P.scan_off);
-  }
+  });
   CK(hipSetDevice(device_));
   CK(d_in_.ensure(in_off));
   CK(d_dfr_.ensure(sizeof(DecFrame) * (size_t)n));
@@ -789,8 +867,16 @@ int Codec::fetch_jpegs(uint8_t *const *outs, const size_t *caps, size_t *sizes, 
                       hipMemcpyDeviceToHost, s_));
     off += align_up(sz[(size_t)f], 64);
   }
+  const auto ta = std::chrono::steady_clock::now();
   CK(hipStreamSynchronize(s_));
-  for (int f = 0; f < n; ++f) std::memcpy(outs[f], h_out_.as<uint8_t>() + offs[(size_t)f], sz[(size_t)f]);
+  const auto tb = std::chrono::steady_clock::now();
+  pool_.run(n, [&](int f) { std::memcpy(outs[f], h_out_.as<uint8_t>() + offs[(size_t)f], sz[(size_t)f]); });
+  if (std::getenv("VF_JPEG_TRACE")) {
+    const auto tc = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "[vf_jpeg]   fetch: d2h %.3f copy-out %.3f ms (%llu B)\n",
+                 std::chrono::duration<double, std::milli>(tb - ta).count(),
+                 std::chrono::duration<double, std::milli>(tc - tb).count(), (unsigned long long)total);
+  }
   return kOk;
 }
 
@@ -819,8 +905,9 @@ int Codec::encode(const uint8_t *const *imgs, const int *ws, const int *hs, int 
   if ((rc = prepare_encode(ws, hs, offs.data(), n, quality, subsamp, fast, err))) return rc;
   CK(h_stage_.ensure(pix));
   CK(d_pix_.ensure(pix));
-  for (int f = 0; f < n; ++f)
+  pool_.run(n, [&](int f) {
     std::memcpy(h_stage_.as<uint8_t>() + offs[(size_t)f], imgs[f], (size_t)ws[f] * hs[f] * 3);
+  });
   CK(hipMemcpyAsync(d_pix_.p, h_stage_.p, pix, hipMemcpyHostToDevice, s_));
   if ((rc = run_encode(pixel_format, fast, err))) return rc;
   return fetch_jpegs(outs, caps, sizes, err);
@@ -848,9 +935,10 @@ int Codec::decode(const uint8_t *const *jpegs, const size_t *jsizes, int n, int 
   CK(h_out_.ensure(dpix_bytes_));
   CK(hipMemcpyAsync(h_out_.p, d_pix_.p, dpix_bytes_, hipMemcpyDeviceToHost, s_));
   CK(hipStreamSynchronize(s_));
-  for (int f = 0; f < n; ++f)
+  pool_.run(n, [&](int f) {
     std::memcpy(outs[f], h_out_.as<uint8_t>() + dfr_[(size_t)f].out_off,
                 (size_t)dfr_[(size_t)f].g.w * dfr_[(size_t)f].g.h * 3);
+  });
   return kOk;
 }
 
@@ -859,7 +947,11 @@ int Codec::invert(const uint8_t *const *jpegs, const size_t *jsizes, int n, int 
   int rc = init(err);
   if (rc) return rc;
   if (n <= 0) return kOk;
+  static const bool trace = std::getenv("VF_JPEG_TRACE") != nullptr;
+  using clk = std::chrono::steady_clock;
+  const auto t0 = clk::now();
   if ((rc = prepare_decode(jpegs, jsizes, n, flags, err))) return rc;
+  const auto t1 = clk::now();
   std::vector<int> ws((size_t)n), hs((size_t)n);
   std::vector<uint64_t> offs((size_t)n);
   for (int f = 0; f < n; ++f) {
@@ -869,11 +961,34 @@ int Codec::invert(const uint8_t *const *jpegs, const size_t *jsizes, int n, int 
   }
   const bool fast = (flags & kFlagFastDct) != 0;
   if ((rc = prepare_encode(ws.data(), hs.data(), offs.data(), n, quality, subsamp, fast, err))) return rc;
-  // decode (BGR, inverted: cv2.bitwise_not, inverter.py:41) straight into the encoder's input
-  if ((rc = run_decode(1, true, err))) return rc;
-  if ((rc = run_encode(1, fast, err))) return rc;
+  const auto t2 = clk::now();
+  {
+    std::unique_lock<std::mutex> gl;
+    if (gate_) {
+      gl = std::unique_lock<std::mutex>(gate_->mu);
+      if (gate_->last) CK(hipStreamWaitEvent(s_, gate_->last, 0));
+    }
+    // decode (BGR, inverted: cv2.bitwise_not, inverter.py:41) straight into the encoder's input
+    if ((rc = run_decode(1, true, err))) return rc;
+    if ((rc = run_encode(1, fast, err))) return rc;
+    if (gate_) {
+      CK(hipEventRecord(ev_[9], s_));
+      gate_->last = ev_[9];
+    }
+  }
+  const auto t3 = clk::now();
   if ((rc = check_decode(err))) return rc;
-  return fetch_jpegs(outs, caps, sizes, err);
+  const auto t4 = clk::now();
+  rc = fetch_jpegs(outs, caps, sizes, err);
+  if (trace) {
+    const auto t5 = clk::now();
+    auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    static const clk::time_point origin = t0;
+    std::fprintf(stderr,
+                 "[vf_jpeg] invert codec %p n=%d at %.3f: prep_dec %.3f prep_enc %.3f queue %.3f wait %.3f fetch %.3f ms\n",
+                 (void *)this, n, ms(origin, t0), ms(t0, t1), ms(t1, t2), ms(t2, t3), ms(t3, t4), ms(t4, t5));
+  }
+  return rc;
 }
 
 int Codec::bench_invert(const uint8_t *const *jpegs, const size_t *jsizes, int n, int quality, int subsamp,
@@ -923,7 +1038,7 @@ int Codec::bench_invert(const uint8_t *const *jpegs, const size_t *jsizes, int n
 
 int header_info(const uint8_t *jpeg, size_t size, int *w, int *h, int *subsamp, int *colorspace, std::string *err) {
   Parsed P;
-  if (!jpeg || parse(jpeg, size, &P, err) != 0) {
+  if (!jpeg || parse(jpeg, size, &P, err, false) != 0) {
     if (!jpeg) *err = "NULL JPEG buffer";
     return kJpeg;
   }

@@ -301,6 +301,20 @@ class Context:
 
 
     # -- JPEG (default use_jpeg=True mode: inverter.py:32 -> :41 -> :44) -----------------------
+    def _out_arena(self, caps: Sequence[int]) -> list:
+        """Per-frame output windows (worst-case tjBufSize each) in one grow-only host arena
+        reused across calls: the encoder writes only the few hundred KB each JPEG needs, and
+        reused pages take no page faults.  Results are copied out (bytes) before returning."""
+        offs, tot = [], 0
+        for c in caps:
+            offs.append(tot)
+            tot += (int(c) + 63) & ~63
+        tls = self.__dict__.setdefault("_arena_tls", threading.local())  # one arena per calling thread
+        arena = getattr(tls, "arena", None)
+        if arena is None or arena.nbytes < tot:
+            arena = tls.arena = np.empty(tot, np.uint8)
+        return [arena[o:o + c] for o, c in zip(offs, caps)]
+
     @staticmethod
     def _ptrs(bufs):
         arrs = [b if isinstance(b, np.ndarray) else np.frombuffer(b, dtype=np.uint8) for b in bufs]
@@ -322,7 +336,7 @@ class Context:
         caps = [int(self._lib.vf_jpeg_buffer_size(a.shape[1], a.shape[0], subsamp)) for a in imgs]
         if not all(caps):
             raise ValueError("jpeg_encode: unsupported size or subsampling")
-        outs = [np.empty(c, np.uint8) for c in caps]
+        outs = self._out_arena(caps)
         _, oa = self._ptrs(outs)
         ca = (ctypes.c_size_t * n)(*caps)
         sz = (ctypes.c_size_t * n)()
@@ -358,7 +372,7 @@ class Context:
             caps.append(int(self._lib.vf_jpeg_buffer_size(w, h, subsamp)))
         if not all(caps):
             raise ValueError("jpeg_invert: unsupported size or subsampling")
-        outs = [np.empty(c, np.uint8) for c in caps]
+        outs = self._out_arena(caps)
         _, oa = self._ptrs(outs)
         js = (ctypes.c_size_t * n)(*[s.nbytes for s in srcs])
         ca = (ctypes.c_size_t * n)(*caps)

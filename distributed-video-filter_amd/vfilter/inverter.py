@@ -12,10 +12,12 @@ Raw frames: the reference reshapes every raw frame to 480x480x3 (inverter.py:34)
 any other size with a ValueError (worker.py:74-76).  The invert needs no shape, so any size
 is accepted here; the v1 wire format carries the shape when a producer provides it.
 
-JPEG (the reference default, ``use_jpeg=True``, inverter.py:10) needs PyTurboJPEG, which is
-not installed on this image; ``use_jpeg=True`` therefore raises at construction exactly as
-the reference does at import (``from turbojpeg import TurboJPEG``, inverter.py:7).  GPU JPEG
-is SURVEY §8f rank 4.
+JPEG (the reference default, ``use_jpeg=True``, inverter.py:10): ``vfilter.jpeg.TurboJPEG``
+(PyTurboJPEG's API on the gfx950 baseline-JPEG codec, bit-exact with libjpeg-turbo) replaces
+``turbojpeg.TurboJPEG`` (inverter.py:7,13).  A batch runs decode -> invert -> encode as one
+fused GPU pass; ``submit_batch`` hands it to one of two host threads, so one batch's host
+work (parse, staging, copy-out) overlaps the previous batch's GPU work (the library leases
+each call its own codec, stream and buffers).
 """
 from __future__ import annotations
 
@@ -46,6 +48,7 @@ class InverterWorker(Worker):
         # inverter.py:13 — TurboJPEG() with PyTurboJPEG's defaults, on this worker's GPU
         self.jpeg = TurboJPEG(ctx=self.ctx, tj_version=tj_version) if use_jpeg else None
         self._registered: List[int] = []
+        self._jpool = None  # executor for asynchronous JPEG batches (submit_batch)
         if install_signal_handlers:                                  # inverter.py:16-18
             signal.signal(signal.SIGINT, self._signal_handler)
             signal.signal(signal.SIGTERM, self._signal_handler)
@@ -107,7 +110,10 @@ class InverterWorker(Worker):
     def submit_batch(self, frames: Sequence, metas: Sequence[wire.FrameMeta], outs: Sequence):
         """Queue the batch with vf_invert_frames_async and return to receiving at once: the
         context's engine thread streams consecutive batches through the GPU back to back.
-        Ring frames (page-locked) are DMA'd in place; socket payloads are staged."""
+        Ring frames (page-locked) are DMA'd in place; socket payloads are staged.  JPEG
+        batches go to a 2-thread executor (fused decode -> invert -> encode per batch)."""
+        if self.jpeg and self.delay <= 0 and all(o is None for o in outs):
+            return ("jpeg", self._jpeg_pool().submit(self.process_batch, list(frames), metas, outs), len(frames))
         if self.jpeg or self.delay > 0:
             return super().submit_batch(frames, metas, outs)
         srcs, dsts = [], []
@@ -121,7 +127,21 @@ class InverterWorker(Worker):
             return ("done", [e] * len(frames), [])
         return ("gpu", ticket, srcs, dsts)  # srcs kept alive until the ticket completes
 
+    def _jpeg_pool(self):
+        if self._jpool is None:
+            from concurrent.futures import ThreadPoolExecutor
+            self._jpool = ThreadPoolExecutor(max_workers=2, thread_name_prefix="vf-jpeg")
+        return self._jpool
+
     def poll_batch(self, handle, block: bool):
+        if handle[0] == "jpeg":
+            fut = handle[1]
+            if not block and not fut.done():
+                return None
+            try:
+                return fut.result(), []
+            except Exception as e:
+                return [e] * handle[2], []
         if handle[0] != "gpu":
             return super().poll_batch(handle, block)
         _, ticket, _srcs, dsts = handle
@@ -150,6 +170,9 @@ class InverterWorker(Worker):
             except Exception:
                 pass
         self._registered.clear()
+        if self._jpool is not None:
+            self._jpool.shutdown(wait=True)
+            self._jpool = None
         super().close()
         self.ctx.close()
 
@@ -177,7 +200,9 @@ def main(argv=None):
     ap.add_argument("--delay", type=float, default=0.0,
                     help="Artificial processing delay in seconds (default: 0.0)")
     ap.add_argument("--host", default="localhost", help="distributor host (reference: hard-coded localhost)")
-    ap.add_argument("--jpeg", action="store_true", help="JPEG frames (needs PyTurboJPEG); default raw")
+    ap.add_argument("--raw", action="store_true",
+                    help="raw H x W x 3 frames (use_jpeg=False); default JPEG frames, as the reference CLI")
+    ap.add_argument("--jpeg", action="store_true", help=argparse.SUPPRESS)  # the default; kept for old scripts
     ap.add_argument("--device", type=int, default=None, help="GPU ordinal (default: VF_DEVICE / LOCAL_RANK / 0)")
     ap.add_argument("--batch", type=int, default=8, help="frames per request (protocol v1)")
     ap.add_argument("--inflight", type=int, default=2, help="batches in progress at once (protocol v1)")
@@ -187,7 +212,7 @@ def main(argv=None):
     ap.add_argument("--verbose", action="store_true")
     args = ap.parse_args(argv)
     worker = InverterWorker(args.host, args.distribute_port, args.collect_port, args.delay,
-                            use_jpeg=args.jpeg, device=args.device, batch=args.batch, inflight=args.inflight,
+                            use_jpeg=not args.raw, device=args.device, batch=args.batch, inflight=args.inflight,
                             protocol=args.protocol, transport=args.transport, verbose=args.verbose)
     try:
         worker.start()

@@ -99,4 +99,6 @@ class TurboJPEG:
 
     def invert_batch(self, jpeg_bufs: Sequence, quality: int = 85, jpeg_subsample: int = TJSAMP_422,
                      flags: int = 0) -> List[bytes]:
+        """One fused GPU pass over the batch (safe to call from several threads at once: each
+        call leases its own codec)."""
         return self.ctx.jpeg_invert(list(jpeg_bufs), quality, jpeg_subsample, self._enc_flags(flags, quality))

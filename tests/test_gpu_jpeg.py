@@ -119,3 +119,31 @@ def test_bad_streams_raise(tj):
         tj.decode(bytes(prog))
     # the context stays usable after errors
     assert np.array_equal(tj.decode(good), J.decode(good))
+
+
+def test_concurrent_calls_lease_separate_codecs(tj):
+    """Two host threads call invert_batch at once (what the JPEG worker's 2-thread submit
+    does): each call leases its own codec, stream and buffers, so both stay bit-exact."""
+    import threading
+    batches = [[J.encode(_img("scene", 10 * t + s, h, w)) for s in range(3)]
+               for t, (h, w) in enumerate([(1080, 1920), (480, 640), (130, 66), (720, 1280)])]
+    want = [[J.invert_jpeg(j) for j in b] for b in batches]
+    errors = []
+
+    def run(t):
+        try:
+            for it in range(4):
+                k = (t + it) % len(batches)
+                got = tj.invert_batch(batches[k])
+                if got != want[k]:
+                    errors.append(f"thread {t} iter {it} batch {k} differs")
+        except Exception as e:  # surfaced below
+            errors.append(repr(e))
+
+    ths = [threading.Thread(target=run, args=(t,)) for t in range(3)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join(120)
+    assert not any(th.is_alive() for th in ths)
+    assert not errors, errors[:3]

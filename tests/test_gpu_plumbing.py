@@ -120,9 +120,12 @@ def test_inverter_worker_jpeg_mode_matches_reference_path():
         assert bytes(w(jpg)) == want
         assert bytes(wd(jpg)) == want
         res = w.process_batch([jpg, small], [None, None], [None, None])
-        assert res[0] == want and res[1] == J.invert_jpeg(small)
+        assert bytes(res[0]) == want and bytes(res[1]) == J.invert_jpeg(small)
         bad = w.process_batch([jpg, b"\xff\xd8garbage"], [None, None], [None, None])
-        assert bad[0] == want and isinstance(bad[1], Exception)  # a bad frame fails alone
+        assert bytes(bad[0]) == want and isinstance(bad[1], Exception)  # a bad frame fails alone
+        h = w.submit_batch([jpg, small], [None, None], [None, None])  # the worker loop's async form
+        got, _ = w.poll_batch(h, block=True)
+        assert [bytes(g) for g in got] == [want, J.invert_jpeg(small)]
     finally:
         w.close()
         wd.close()

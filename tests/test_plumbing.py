@@ -202,6 +202,9 @@ def test_lossless_pull_ordered_two_workers():
     d = _dist(policy="pull", reassembly="ordered", queue_size=32)
     stop, procs = spawn_workers(2, d.distribute_port, d.collect_port, protocol="v1", batch=4)
     try:
+        t0 = time.time()
+        while d.num_workers() < 2 and time.time() - t0 < 60:  # pull: a late worker could get nothing
+            time.sleep(0.02)
         frames = _frames(80, [(120, 160), (97, 33), (480, 640)])
         th = threading.Thread(target=lambda: [d.add_frame_for_distribution(f) for f in frames])
         th.start()

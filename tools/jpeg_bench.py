@@ -6,7 +6,8 @@ Frames are synthetic camera-like scenes (oracle.jpeg.synthetic_scene), encoded o
 PyTurboJPEG defaults (q85, 4:2:2) as the app does (webcam_app.py:110).  Reported per size:
   gpu_resident   the fused GPU pass (vf_jpeg_bench_invert): inputs already in HBM; wall ms per
                  batch and per-stage ms (hipEvents), frames/s
-  host_to_host   vfilter.jpeg.TurboJPEG.invert_batch from Python bytes to Python bytes
+  host_to_host   vfilter.jpeg.TurboJPEG.invert_batch from Python bytes to Python bytes, one
+                 call at a time, and from 2 host threads (the JPEG worker's submit form)
   cpu_reference  libjpeg-turbo 2.1.2 (the codec under PyTurboJPEG; the image's libjpeg.so.8)
                  decode + np.bitwise_not + encode, 1 host core, per frame as the reference
   parity         GPU output == oracle.invert_jpeg for the first frame of each batch
@@ -56,6 +57,15 @@ def main():
         for _ in range(reps):
             tj.invert_batch(jpgs)
         h2h = (time.perf_counter() - t0) / reps
+        # the worker's form: batches handed to 2 host threads (InverterWorker.submit_batch),
+        # one batch's host work overlapping the other's GPU work
+        from concurrent.futures import ThreadPoolExecutor
+        with ThreadPoolExecutor(2) as ex:
+            list(ex.map(lambda _: tj.invert_batch(jpgs), range(2)))  # warm the second codec
+            preps = max(4, args.iters // 2)
+            t0 = time.perf_counter()
+            list(ex.map(lambda _: tj.invert_batch(jpgs), range(preps)))
+            h2h_pipe = (time.perf_counter() - t0) / preps
         # CPU reference: libjpeg-turbo per frame, 1 core
         ok, why = J.libjpeg_available()
         cpu = None
@@ -74,6 +84,7 @@ def main():
                "gpu_resident_ms_per_batch": round(ms, 3), "gpu_resident_fps": round(args.batch / (ms / 1e3), 1),
                "stages_ms": {k: round(v, 4) for k, v in stages.items()},
                "host_to_host_ms_per_batch": round(h2h * 1e3, 3), "host_to_host_fps": round(args.batch / h2h, 1),
+               "host_to_host_2threads_fps": round(args.batch / h2h_pipe, 1),
                "cpu_reference": cpu, "parity_vs_oracle": parity}
         print(json.dumps(rec), flush=True)
         if args.out:

@@ -72,7 +72,7 @@ def main():
     procs = []
     for i in range(args.workers):
         e = dict(env, VF_DEVICE=str(i % ngpu))
-        procs.append(subprocess.Popen([sys.executable, "-m", "vfilter.inverter", "--host", "127.0.0.1",
+        procs.append(subprocess.Popen([sys.executable, "-m", "vfilter.inverter", "--raw", "--host", "127.0.0.1",
                                        "--distribute-port", str(d.distribute_port), "--collect-port",
                                        str(d.collect_port), "--batch", str(args.batch), "--transport", "tcp",
                                        "--inflight", str(args.inflight)],
