@@ -13,7 +13,7 @@ namespace vf {
 namespace jpeg {
 
 constexpr int kMaxBpm = 10;     // blocks per MCU (T.81 B.2.3)
-constexpr int kSubBits = 1024;  // bits per Huffman-decoding subsequence
+constexpr int kSubBits = 256;  // bits per Huffman-decoding subsequence
 constexpr int kTile = 4096;     // bytes per (un)stuffing tile
 constexpr int kMaxPasses = 64;  // sync-pass flags kept on the device
 constexpr int kLook = 9;        // Huffman lookahead bits
@@ -102,7 +102,7 @@ hipError_t dec_unstuff_write(const DecFrame *fr, int n, uint32_t max_tiles, cons
                              const uint32_t *tile_off, const uint32_t *us_len, uint8_t *us, hipStream_t s);
 hipError_t dec_sync(const DecFrame *fr, int n, uint32_t max_sub, const uint8_t *us, const uint32_t *us_len,
                     const uint64_t *exit_in, uint64_t *exit_out, const uint32_t *cnt_in, uint32_t *cnt_out,
-                    uint64_t *used, uint32_t *changed, int pass, hipStream_t s);
+                    uint64_t *used, uint64_t *ck, uint32_t *ckrem, uint32_t *changed, int pass, hipStream_t s);
 hipError_t dec_write(const DecFrame *fr, int n, uint32_t max_sub, const uint8_t *us, const uint32_t *us_len,
                      const uint64_t *exits, const uint32_t *bstart, int16_t *coef, int32_t *dcseq,
                      hipStream_t s);

@@ -129,7 +129,7 @@ class Codec {
   int dmax_w_ = 0, dmax_h_ = 0;
   uint64_t dblocks_ = 0, dpix_bytes_ = 0;
   int sync_passes_ = 0;
-  DevBuf d_in_, d_dfr_, d_segs_, d_tile_, d_tsum_, d_totals_, d_us_, d_exit_[2], d_cnt_[2], d_used_, d_bstart_,
+  DevBuf d_in_, d_dfr_, d_segs_, d_tile_, d_tsum_, d_totals_, d_us_, d_exit_[2], d_cnt_[2], d_used_, d_ck_, d_ckrem_, d_bstart_,
       d_changed_, d_coef_, d_dcseq_, d_planes_, d_pix_;
 
   // encode layout

@@ -654,6 +654,8 @@ int Codec::prepare_decode(const uint8_t *const *jpegs, const size_t *sizes, int 
   CK(d_cnt_[0].ensure(sizeof(uint32_t) * subs));
   CK(d_cnt_[1].ensure(sizeof(uint32_t) * subs));
   CK(d_used_.ensure(sizeof(uint64_t) * subs));
+  CK(d_ck_.ensure(sizeof(uint64_t) * subs * (kSubBits / 64)));
+  CK(d_ckrem_.ensure(sizeof(uint32_t) * subs * (kSubBits / 64)));
   CK(d_bstart_.ensure(sizeof(uint32_t) * subs));
   CK(d_changed_.ensure(sizeof(uint32_t) * kMaxPasses));
   CK(d_coef_.ensure(blk * 128));
@@ -690,7 +692,8 @@ int Codec::run_decode(int bgr, bool invert, std::string *err) {
     const int a = pass & 1;
     CK(dec_sync(fr, n, dmax_sub_, d_us_.as<uint8_t>(), us_len, d_exit_[a ^ 1].as<uint64_t>(),
                 d_exit_[a].as<uint64_t>(), d_cnt_[a ^ 1].as<uint32_t>(), d_cnt_[a].as<uint32_t>(),
-                d_used_.as<uint64_t>(), d_changed_.as<uint32_t>() + (pass % kMaxPasses), pass > 0 ? 1 : 0, s_));
+                d_used_.as<uint64_t>(), d_ck_.as<uint64_t>(), d_ckrem_.as<uint32_t>(),
+                d_changed_.as<uint32_t>() + (pass % kMaxPasses), pass > 0 ? 1 : 0, s_));
     last = a;
     ++pass;
     if (pass < 2) continue;  // passes 0 and 1 are queued without a host round trip

@@ -258,18 +258,48 @@ __device__ __forceinline__ uint64_t pack_state(uint32_t pos, uint32_t z, uint32_
   return ((uint64_t)pos << 16) | (z << 8) | c;
 }
 
+// The frame geometry the Huffman loops need per symbol, in registers.  Geom lives in global
+// memory and is indexed by the per-lane block-in-MCU c, so reading g.bcomp[c] inside the loop
+// is a dependent vector memory load per symbol; here the component of c is a 2-bit field of
+// one register and the per-component values are picked with selects.
+struct HuffGeom {
+  uint32_t cpack;    // component of block-in-MCU c at bits 2c..2c+1
+  uint32_t bpm, nblocks;
+  uint32_t bpc[3];   // blocks of component k per MCU
+  uint32_t cfirst[3];
+  __device__ __forceinline__ explicit HuffGeom(const Geom &g) {
+    bpm = (uint32_t)g.bpm;
+    nblocks = (uint32_t)g.nblocks;
+    cpack = 0;
+    for (int j = 0; j < g.bpm; ++j) cpack |= (uint32_t)(g.bcomp[j] & 3) << (2 * j);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      bpc[k] = (uint32_t)(g.mh[k] * g.mv[k]);
+      cfirst[k] = (uint32_t)g.cfirst[k];
+    }
+  }
+  __device__ __forceinline__ uint32_t comp(uint32_t c) const { return (cpack >> (2 * c)) & 3; }
+  template <typename T>
+  __device__ __forceinline__ static T sel(const T *a, uint32_t k) { return k == 0 ? a[0] : k == 1 ? a[1] : a[2]; }
+};
+
 // Decode symbols from the reader's position until it reaches `end` (checked at symbol
 // boundaries).  State: z = next zigzag index of the current block (0 = DC next), c = its
 // block-in-MCU, blk = its block index (WRITE only), blocks = blocks completed.
 template <bool WRITE>
 __device__ __forceinline__ void decode_span(BitReader &br, uint32_t end, uint32_t &z, uint32_t &c,
-                                            uint32_t &blocks, const Geom &g, const HuffDec *dcT,
+                                            uint32_t &blocks, const HuffGeom &g, const HuffDec *dcT,
                                             const HuffDec *acT, uint32_t blk, int16_t *coef, int32_t *dcseq,
                                             const uint64_t *dcbase) {
+  uint64_t dcb[3] = {0, 0, 0};
+  if (WRITE) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) dcb[k] = dcbase[k];
+  }
   while (br.pos < end) {
-    if (WRITE && blk >= (uint32_t)g.nblocks) break;
+    if (WRITE && blk >= g.nblocks) break;
     br.refill();
-    const int k = g.bcomp[c];
+    const uint32_t k = g.comp(c);
     if (z == 0) {
       uint32_t s = huff_sym(br, dcT[k]);
       int v = 0;
@@ -279,8 +309,8 @@ __device__ __forceinline__ void decode_span(BitReader &br, uint32_t end, uint32_
         br.skip(s);
       }
       if (WRITE) {
-        const uint32_t mcu = blk / (uint32_t)g.bpm;
-        dcseq[dcbase[k] + (uint64_t)mcu * (g.mh[k] * g.mv[k]) + (c - g.cfirst[k])] = v;
+        const uint32_t mcu = blk / g.bpm;
+        dcseq[HuffGeom::sel(dcb, k) + (uint64_t)mcu * HuffGeom::sel(g.bpc, k) + (c - HuffGeom::sel(g.cfirst, k))] = v;
       }
       z = 1;
     } else {
@@ -300,7 +330,7 @@ __device__ __forceinline__ void decode_span(BitReader &br, uint32_t end, uint32_
     }
     if (z >= 64) {
       z = 0;
-      c = (c + 1 == (uint32_t)g.bpm) ? 0 : c + 1;
+      c = (c + 1 == g.bpm) ? 0 : c + 1;
       ++blocks;
       ++blk;
     }
@@ -315,49 +345,124 @@ __device__ __forceinline__ void load_tables(const DecFrame &F, HuffDec *tabs) {
   __syncthreads();
 }
 
+// One Huffman symbol of the sync decode (decode_span<false> without the outputs).
+__device__ __forceinline__ void sync_step(BitReader &br, uint32_t &z, uint32_t &c, uint32_t &blocks,
+                                          const HuffGeom &g, const HuffDec *dcT, const HuffDec *acT) {
+  br.refill();
+  const uint32_t k = g.comp(c);
+  if (z == 0) {
+    uint32_t s = huff_sym(br, dcT[k]);
+    if (s) br.skip(s > 16 ? 16 : s);
+    z = 1;
+  } else {
+    const uint32_t rs = huff_sym(br, acT[k]);
+    const uint32_t r = rs >> 4, s = rs & 15;
+    if (s) {
+      br.skip(s);
+      z += r + 1;
+    } else if (r == 15) {
+      z += 16;
+    } else {
+      z = 64;
+    }
+  }
+  if (z >= 64) {
+    z = 0;
+    c = (c + 1 == g.bpm) ? 0 : c + 1;
+    ++blocks;
+  }
+}
+
+// Checkpoints: kCk marks inside each subsequence, every kCkStep bits.  A decode records its
+// state (bit position, zigzag index, block-in-MCU) at the first symbol boundary at or past
+// each mark, and the number of blocks that trajectory completes from there to the
+// subsequence's end.  A later decode of the same subsequence from another entry that reaches
+// a mark in a recorded state has joined the recorded trajectory: its exit is the recorded
+// exit and its block count is its count so far plus the recorded remainder, so it stops
+// there.  The codes self-synchronise within a few symbols, so a re-decode usually stops at
+// the first mark.  Invariant: every valid checkpoint and the exit state describe one
+// trajectory (marks a decode did not reach from its entry are invalidated).
+constexpr int kCkStep = 64;
+constexpr int kCk = kSubBits / kCkStep - 1;
+constexpr uint64_t kNoCk = ~0ull;
+
 // One sync pass.  Every thread decodes its subsequence from its entry state; then, inside
 // the workgroup, a thread whose entry differs from its predecessor's current exit takes that
-// exit and decodes again, until the workgroup is consistent (usually one extra round, as
-// the codes self-synchronise).  Across workgroups the entry of a workgroup's first thread is
-// the previous pass's exit of its predecessor; a pass that changes no exit state means the
-// whole chain is consistent, and its counts were made from the final entry states.
+// exit and decodes again (up to the first checkpoint where it rejoins its previous decode),
+// until the workgroup is consistent.  Across workgroups the entry of a workgroup's first
+// thread is the previous pass's exit of its predecessor; a pass that changes no exit state
+// means the whole chain is consistent, and its counts were made from the final entry states.
 __global__ __launch_bounds__(256) void k_sync(const DecFrame *fr, const uint8_t *us, const uint32_t *us_len,
                                               const uint64_t *exit_in, uint64_t *exit_out, const uint32_t *cnt_in,
-                                              uint32_t *cnt_out, uint64_t *used, uint32_t *changed, int pass) {
+                                              uint32_t *cnt_out, uint64_t *used, uint64_t *ck, uint32_t *ckrem,
+                                              uint32_t *changed, int pass) {
   __shared__ HuffDec tabs[6];
   __shared__ uint64_t s_exit[256];
+  __shared__ uint64_t s_ck[kCk][256];
+  __shared__ uint32_t s_rem[kCk][256];
   const DecFrame &F = fr[blockIdx.y];
   if (blockIdx.x * 256 >= F.nsub_max) return;
   load_tables(F, tabs);
+  const HuffGeom hg(F.g);
   const uint32_t t = threadIdx.x;
   const uint32_t i = blockIdx.x * 256 + t;
   const uint32_t gi = F.sub0 + i;
   const uint32_t nbits = us_len[blockIdx.y] * 8u;
   const uint32_t nsub = (nbits + kSubBits - 1) / kSubBits;
   const bool live = i < nsub;
+  const uint32_t base = i * kSubBits;
   const uint32_t end = (i + 1 >= nsub) ? nbits : (i + 1) * kSubBits;
   uint64_t entry = 0, ex = pack_state(nbits, 0, 0);
   uint32_t cnt = 0;
-  bool need = false;
+  bool need = false, decoded = false;
   if (live) {
     if (i == 0) entry = 0;
-    else if (pass == 0) entry = pack_state(i * kSubBits, 0, 0);
+    else if (pass == 0) entry = pack_state(base, 0, 0);
     else entry = exit_in[gi - 1];
-    if (pass > 0 && entry == used[gi]) {  // same entry as last pass: same result
+#pragma unroll
+    for (int m = 0; m < kCk; ++m) {
+      s_ck[m][t] = pass > 0 ? ck[(uint64_t)gi * kCk + m] : kNoCk;
+      s_rem[m][t] = pass > 0 ? ckrem[(uint64_t)gi * kCk + m] : 0u;
+    }
+    if (pass > 0) {
       ex = exit_in[gi];
       cnt = cnt_in[gi];
+      need = entry != used[gi];  // same entry as last pass: same result
     } else {
       need = true;
     }
   }
   for (;;) {
     if (need) {
+      decoded = true;
       BitReader br;
       br.init(us + F.us_off, (uint32_t)(entry >> 16));
-      uint32_t z = (entry >> 8) & 0xFF, c = entry & 0xFF;
-      cnt = 0;
-      decode_span<false>(br, end, z, c, cnt, F.g, tabs, tabs + 3, 0, nullptr, nullptr, nullptr);
-      ex = pack_state(br.pos, z, c);
+      uint32_t z = (entry >> 8) & 0xFF, c = entry & 0xFF, n = 0;
+      int m = 0;
+      while (m < kCk && base + (uint32_t)(m + 1) * kCkStep <= br.pos) s_ck[m++][t] = kNoCk;
+      const int m0 = m;
+      int joined = -1;
+      while (br.pos < end) {
+        sync_step(br, z, c, n, hg, tabs, tabs + 3);
+        const uint32_t mk = base + (uint32_t)(m + 1) * kCkStep;
+        if (m < kCk && mk < end && br.pos >= mk) {
+          const uint64_t st = pack_state(br.pos, z, c);
+          if (s_ck[m][t] == st) {
+            joined = m;
+            break;
+          }
+          s_ck[m][t] = st;
+          s_rem[m][t] = n;  // blocks so far; turned into the remainder below
+          ++m;
+        }
+      }
+      if (joined >= 0) {
+        cnt = n + s_rem[joined][t];  // ex: the recorded trajectory's exit, unchanged
+      } else {
+        cnt = n;
+        ex = pack_state(br.pos, z, c);
+      }
+      for (int q = m0; q < m; ++q) s_rem[q][t] = cnt - s_rem[q][t];
     }
     s_exit[t] = ex;
     __syncthreads();
@@ -376,6 +481,13 @@ __global__ __launch_bounds__(256) void k_sync(const DecFrame *fr, const uint8_t 
     cnt_out[gi] = cnt;
     if (live) {
       used[gi] = entry;
+      if (decoded) {
+#pragma unroll
+        for (int m = 0; m < kCk; ++m) {
+          ck[(uint64_t)gi * kCk + m] = s_ck[m][t];
+          ckrem[(uint64_t)gi * kCk + m] = s_rem[m][t];
+        }
+      }
       if (pass == 0 || ex != exit_in[gi]) atomicOr(changed, 1u);
     }
   }
@@ -398,7 +510,7 @@ __global__ __launch_bounds__(256) void k_write(const DecFrame *fr, const uint8_t
   BitReader br;
   br.init(us + F.us_off, (uint32_t)(st >> 16));
   uint32_t z = (st >> 8) & 0xFF, c = st & 0xFF, blocks = 0;
-  decode_span<true>(br, end, z, c, blocks, F.g, tabs, tabs + 3, bstart[gi], coef + F.blk0 * 64, dcseq,
+  decode_span<true>(br, end, z, c, blocks, HuffGeom(F.g), tabs, tabs + 3, bstart[gi], coef + F.blk0 * 64, dcseq,
                     F.dcbase);
 }
 
@@ -1197,10 +1309,10 @@ hipError_t dec_unstuff_write(const DecFrame *fr, int n, uint32_t max_tiles, cons
 
 hipError_t dec_sync(const DecFrame *fr, int n, uint32_t max_sub, const uint8_t *us, const uint32_t *us_len,
                     const uint64_t *exit_in, uint64_t *exit_out, const uint32_t *cnt_in, uint32_t *cnt_out,
-                    uint64_t *used, uint32_t *changed, int pass, hipStream_t s) {
+                    uint64_t *used, uint64_t *ck, uint32_t *ckrem, uint32_t *changed, int pass, hipStream_t s) {
   if (n <= 0 || !max_sub) return hipSuccess;
   hipLaunchKernelGGL(k_sync, dim3((max_sub + 255) / 256, (unsigned)n), dim3(256), 0, s, fr, us, us_len, exit_in,
-                     exit_out, cnt_in, cnt_out, used, changed, pass);
+                     exit_out, cnt_in, cnt_out, used, ck, ckrem, changed, pass);
   return hipGetLastError();
 }
 
