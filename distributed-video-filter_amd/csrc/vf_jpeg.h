@@ -114,10 +114,10 @@ hipError_t dec_color(const DecFrame *fr, int n, int max_w, int max_h, const uint
 hipError_t enc_fdct(const EncFrame *fr, int n, uint32_t max_blocks, const EncTables *tab, const uint8_t *pix,
                     int16_t *dcq, uint32_t *acbits, uint32_t *acscr, int bgr, int fastdct, hipStream_t s);
 hipError_t enc_len(const EncFrame *fr, int n, uint32_t max_blocks, const EncTables *tab, const int16_t *dcq,
-                   const uint32_t *acbits, uint32_t *bits, hipStream_t s);
-hipError_t enc_pack(const EncFrame *fr, int n, uint32_t max_blocks, const EncTables *tab, const int16_t *dcq,
-                    const uint32_t *acbits, const uint32_t *acscr, const uint32_t *bitoff, const uint32_t *total_bits,
-                    uint8_t *stream, hipStream_t s);
+                   uint32_t *acbits, uint32_t *bits, uint32_t *pre, hipStream_t s);
+hipError_t enc_pack(const EncFrame *fr, int n, uint32_t max_blocks, const uint32_t *pre, const uint32_t *acbits,
+                    const uint32_t *acscr, const uint32_t *bitoff, const uint32_t *total_bits, uint8_t *stream,
+                    hipStream_t s);
 hipError_t enc_ff_count(const EncFrame *fr, int n, uint32_t max_tiles, const uint32_t *total_bits,
                         const uint8_t *stream, uint32_t *tile_cnt, hipStream_t s);
 hipError_t enc_ff_write(const EncFrame *fr, int n, uint32_t max_tiles, const uint32_t *total_bits,

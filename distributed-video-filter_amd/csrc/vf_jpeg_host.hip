@@ -708,6 +708,12 @@ int Codec::run_decode(int bgr, bool invert, std::string *err) {
     }
   }
   sync_passes_ = pass;
+  if (std::getenv("VF_JPEG_SYNC_STATS")) {
+    uint32_t st[4];
+    CK(hipMemcpy(st, d_changed_.as<uint32_t>() + kMaxPasses - 4, sizeof st, hipMemcpyDeviceToHost));
+    std::fprintf(stderr, "[vf_jpeg] sync: passes %d; rounds pass0 max %u sum %u, pass1 max %u sum %u (WGs %u)\n", pass,
+                 st[3], st[1], st[2], st[0], (dmax_sub_ + 255) / 256 * (uint32_t)n);
+  }
   CK(hipEventRecord(ev_[2], s_));
   // 3. block offsets of the subsequences, then the write pass
   uint32_t *blocks_total = d_totals_.as<uint32_t>() + n;
@@ -805,6 +811,7 @@ int Codec::prepare_encode(const int *ws, const int *hs, const uint64_t *img_offs
   CK(d_acbits_.ensure(sizeof(uint32_t) * blk));
   CK(d_acscr_.ensure(sizeof(uint32_t) * kAcScratchWords * blk));
   CK(d_bits_.ensure(sizeof(uint32_t) * blk));
+  CK(d_pre_.ensure(sizeof(uint32_t) * blk));
   CK(d_bitoff_.ensure(sizeof(uint32_t) * blk));
   CK(d_stream_.ensure(bits));
   CK(d_ffcnt_.ensure(sizeof(uint32_t) * tiles));
@@ -827,11 +834,12 @@ int Codec::run_encode(int bgr, bool fastdct, std::string *err) {
   CK(hipEventRecord(ev_[6], s_));
   CK(enc_fdct(fr, n, emax_blocks_, tab, d_pix_.as<uint8_t>(), d_dcq_.as<int16_t>(), d_acbits_.as<uint32_t>(),
               d_acscr_.as<uint32_t>(), bgr, fastdct ? 1 : 0, s_));
-  CK(enc_len(fr, n, emax_blocks_, tab, d_dcq_.as<int16_t>(), d_acbits_.as<uint32_t>(), d_bits_.as<uint32_t>(), s_));
+  CK(enc_len(fr, n, emax_blocks_, tab, d_dcq_.as<int16_t>(), d_acbits_.as<uint32_t>(), d_bits_.as<uint32_t>(),
+             d_pre_.as<uint32_t>(), s_));
   uint32_t *total_bits = d_etotals_.as<uint32_t>();
   CK(scan_u32(segs, n, (emax_blocks_ + kScanTile - 1) / kScanTile, d_bits_.as<uint32_t>(), d_bitoff_.as<uint32_t>(),
               d_etsum_.as<uint32_t>(), total_bits, false, s_));
-  CK(enc_pack(fr, n, emax_blocks_, tab, d_dcq_.as<int16_t>(), d_acbits_.as<uint32_t>(), d_acscr_.as<uint32_t>(),
+  CK(enc_pack(fr, n, emax_blocks_, d_pre_.as<uint32_t>(), d_acbits_.as<uint32_t>(), d_acscr_.as<uint32_t>(),
               d_bitoff_.as<uint32_t>(), total_bits, d_stream_.as<uint8_t>(), s_));
   CK(hipEventRecord(ev_[7], s_));
   CK(enc_ff_count(fr, n, emax_tiles_, total_bits, d_stream_.as<uint8_t>(), d_ffcnt_.as<uint32_t>(), s_));

@@ -385,6 +385,9 @@ __device__ __forceinline__ void sync_step(BitReader &br, uint32_t &z, uint32_t &
 constexpr int kCkStep = 64;
 constexpr int kCk = kSubBits / kCkStep - 1;
 constexpr uint64_t kNoCk = ~0ull;
+#ifndef VF_SYNC_STATS
+#define VF_SYNC_STATS 0
+#endif
 
 // One sync pass.  Every thread decodes its subsequence from its entry state; then, inside
 // the workgroup, a thread whose entry differs from its predecessor's current exit takes that
@@ -432,7 +435,9 @@ __global__ __launch_bounds__(256) void k_sync(const DecFrame *fr, const uint8_t 
       need = true;
     }
   }
+  uint32_t rounds = 0;
   for (;;) {
+    ++rounds;
     if (need) {
       decoded = true;
       BitReader br;
@@ -489,6 +494,10 @@ __global__ __launch_bounds__(256) void k_sync(const DecFrame *fr, const uint8_t 
         }
       }
       if (pass == 0 || ex != exit_in[gi]) atomicOr(changed, 1u);
+      if (VF_SYNC_STATS && t == 0) {  // debug: rounds histogram in the pass-flag tail
+        atomicMax(changed + (kMaxPasses - 1 - pass), rounds);
+        atomicAdd(changed + (kMaxPasses - 3 - pass), rounds);
+      }
     }
   }
 }
@@ -679,7 +688,9 @@ __global__ __launch_bounds__(256) void k_color(const DecFrame *fr, const uint8_t
   const int y = blockIdx.y, x0 = (blockIdx.x * 256 + threadIdx.x) * 8;
   if (y >= g.h || x0 >= g.w) return;
   int v[3][8];
-  for (int k = 0; k < g.ncomp; ++k) {
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    if (k >= g.ncomp) break;
     const uint8_t *p = planes + F.plane_off[k];
     const int pw = g.pw[k];
     const int he = g.maxh / g.hs[k], ve = g.maxv / g.vs[k];
@@ -922,6 +933,51 @@ __device__ __forceinline__ int ycc_comp(int k, int r, int g, int b) {  // jccolo
   return (32768 * r - 27439 * g - 5329 * b + (128 << 16) + 32767) >> 16;
 }
 
+// Component k of the 8 * H pixels of row py from px, summed in groups of H into v[0..7]
+// (assigned when `first`, else added: a second row of h2v2).  Edges replicated
+// (jccolor.c on expand_right_edge / expand_bottom_edge input).  4 pixels (3 dwords) at a
+// time, so at most 12 channel values are live instead of 3 * 8 * H.
+template <int H>
+__device__ __forceinline__ void line_acc(const uint8_t *img, int w, int h, int px, int py, bool bgr, int k,
+                                         int32_t v[8], bool first) {
+  py = py < h ? py : h - 1;
+  const uint8_t *row = img + (size_t)py * w * 3;
+  const uint8_t *src = row + (size_t)px * 3;
+  const bool fast = px + 8 * H <= w && ((uintptr_t)src & 3) == 0;
+#pragma unroll
+  for (int q = 0; q < 2 * H; ++q) {
+    int c[4];
+    if (fast) {
+      const uint32_t *s32 = reinterpret_cast<const uint32_t *>(src) + 3 * q;
+      const uint32_t w0 = s32[0], w1 = s32[1], w2 = s32[2];
+      const uint32_t wd[3] = {w0, w1, w2};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c0 = (int)((wd[(3 * j) / 4] >> (8 * ((3 * j) % 4))) & 0xFF);
+        const int c1 = (int)((wd[(3 * j + 1) / 4] >> (8 * ((3 * j + 1) % 4))) & 0xFF);
+        const int c2 = (int)((wd[(3 * j + 2) / 4] >> (8 * ((3 * j + 2) % 4))) & 0xFF);
+        c[j] = bgr ? ycc_comp(k, c2, c1, c0) : ycc_comp(k, c0, c1, c2);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        int x = px + 4 * q + j;
+        x = x < w ? x : w - 1;
+        const uint8_t *p = row + (size_t)x * 3;
+        c[j] = bgr ? ycc_comp(k, p[2], p[1], p[0]) : ycc_comp(k, p[0], p[1], p[2]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4 / H; ++j) {
+      const int o = q * (4 / H) + j;
+      int sum = 0;
+#pragma unroll
+      for (int e = 0; e < H; ++e) sum += c[j * H + e];
+      v[o] = first ? sum : v[o] + sum;
+    }
+  }
+}
+
 constexpr uint32_t kAcWords = kAcScratchWords;
 
 // `size` (<= 32) bits at stream bit `pos` of an MSB-first word array in LDS
@@ -981,28 +1037,18 @@ __global__ __launch_bounds__(256) void k_fdct(const EncFrame *fr, const EncTable
     const int real_rows = ((g.h + g.maxv - 1) / g.maxv) * g.vs[k];
     const int sy = min((int)(by * 8 + r), real_rows - 1);
     int32_t v[8];
-    if (he == 1 && ve == 1) {
-      int R[8], G[8], B[8];
-      load_rgb<8>(img, g.w, g.h, (int)bx * 8, sy, bgr, R, G, B);
+    if (ve == 1 && he <= 2) {  // he == 1: full-resolution line; he == 2: h2v1_downsample
+      if (he == 1) line_acc<1>(img, g.w, g.h, (int)bx * 8, sy, bgr, (int)k, v, true);
+      else line_acc<2>(img, g.w, g.h, (int)bx * 16, sy, bgr, (int)k, v, true);
+      if (he == 2) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = ycc_comp((int)k, R[j], G[j], B[j]);
-    } else if (he == 2 && ve == 1) {  // h2v1_downsample
-      int R[16], G[16], B[16];
-      load_rgb<16>(img, g.w, g.h, (int)bx * 16, sy, bgr, R, G, B);
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        v[j] = (ycc_comp((int)k, R[2 * j], G[2 * j], B[2 * j]) +
-                ycc_comp((int)k, R[2 * j + 1], G[2 * j + 1], B[2 * j + 1]) + (j & 1)) >> 1;
+        for (int j = 0; j < 8; ++j) v[j] = (v[j] + (j & 1)) >> 1;
+      }
     } else if (he == 2 && ve == 2) {  // h2v2_downsample
-      int R[16], G[16], B[16], R2[16], G2[16], B2[16];
-      load_rgb<16>(img, g.w, g.h, (int)bx * 16, 2 * sy, bgr, R, G, B);
-      load_rgb<16>(img, g.w, g.h, (int)bx * 16, 2 * sy + 1, bgr, R2, G2, B2);
+      line_acc<2>(img, g.w, g.h, (int)bx * 16, 2 * sy, bgr, (int)k, v, true);
+      line_acc<2>(img, g.w, g.h, (int)bx * 16, 2 * sy + 1, bgr, (int)k, v, false);
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
-        v[j] = (ycc_comp((int)k, R[2 * j], G[2 * j], B[2 * j]) +
-                ycc_comp((int)k, R[2 * j + 1], G[2 * j + 1], B[2 * j + 1]) +
-                ycc_comp((int)k, R2[2 * j], G2[2 * j], B2[2 * j]) +
-                ycc_comp((int)k, R2[2 * j + 1], G2[2 * j + 1], B2[2 * j + 1]) + 1 + (j & 1)) >> 2;
+      for (int j = 0; j < 8; ++j) v[j] = (v[j] + 1 + (j & 1)) >> 2;
     } else {
       const int ro = bgr ? 2 : 0, bo = 2 - ro;
 #pragma unroll
@@ -1168,9 +1214,13 @@ __device__ __forceinline__ uint32_t dc_category(int diff) {
   return a ? 32 - __clz(a) : 0;
 }
 
-// bits of every block: DC code + extra bits + AC bits (a dummy block's AC is one EOB)
+// bits of every block: DC code + extra bits + AC bits (a dummy block's AC is one EOB).  Also
+// leaves what k_pack needs without re-deriving the DC prediction: pre = (DC code and extra
+// bits << 5) | their length (<= 16 + 11 bits), and for a dummy block acbits = kDummyAc |
+// (EOB code << 5) | EOB length (k_fdct never writes a dummy block's acbits).
+constexpr uint32_t kDummyAc = 0x80000000u;
 __global__ __launch_bounds__(256) void k_len(const EncFrame *fr, const EncTables *tab, const int16_t *dcq,
-                                             const uint32_t *acbits, uint32_t *bits) {
+                                             uint32_t *acbits, uint32_t *bits, uint32_t *pre) {
   const EncFrame &F = fr[blockIdx.y];
   const Geom &g = F.g;
   const uint32_t b = blockIdx.x * 256 + threadIdx.x;
@@ -1179,34 +1229,43 @@ __global__ __launch_bounds__(256) void k_len(const EncFrame *fr, const EncTables
   const int diff = enc_dc_diff(g, dcq + F.blk0, b, &dummy);
   const int t = g.bcomp[b % (uint32_t)g.bpm] > 0;
   const uint32_t nb = dc_category(diff);
-  bits[F.blk0 + b] = (tab->dc[t][nb] & 0xFF) + nb + (dummy ? (tab->ac[t][0] & 0xFF) : acbits[F.blk0 + b]);
-}
-
-// every block writes its bits at its offset: DC code, extra bits, then its AC words
-__global__ __launch_bounds__(256) void k_pack(const EncFrame *fr, const EncTables *tab, const int16_t *dcq,
-                                              const uint32_t *acbits, const uint32_t *acscr, const uint32_t *bitoff,
-                                              uint8_t *stream) {
-  const EncFrame &F = fr[blockIdx.y];
-  const Geom &g = F.g;
-  const uint32_t b = blockIdx.x * 256 + threadIdx.x;
-  if (b >= (uint32_t)g.nblocks) return;
-  bool dummy;
-  const int diff = enc_dc_diff(g, dcq + F.blk0, b, &dummy);
-  const int t = g.bcomp[b % (uint32_t)g.bpm] > 0;
-  const uint32_t nb = dc_category(diff);
-  BitSink out(reinterpret_cast<uint32_t *>(stream + F.bits_off), bitoff[F.blk0 + b]);
   const uint32_t e = tab->dc[t][nb];
-  out.put(e >> 8, e & 0xFF);
-  if (nb) out.put((uint32_t)(diff < 0 ? diff - 1 : diff) & ((1u << nb) - 1), nb);
+  const uint32_t extra = nb ? ((uint32_t)(diff < 0 ? diff - 1 : diff) & ((1u << nb) - 1)) : 0u;
+  const uint64_t gb = F.blk0 + b;
+  pre[gb] = ((((e >> 8) << nb) | extra) << 5) | ((e & 0xFF) + nb);
+  uint32_t ac;
   if (dummy) {
     const uint32_t eob = tab->ac[t][0];
-    out.put(eob >> 8, eob & 0xFF);
+    acbits[gb] = kDummyAc | ((eob >> 8) << 5) | (eob & 0xFF);
+    ac = eob & 0xFF;
   } else {
-    const uint64_t gb = F.blk0 + b;
-    const uint32_t n = acbits[gb];
-    const uint32_t *aw = acscr + gb * kAcWords;
-    for (uint32_t i = 0; i < (n >> 5); ++i) out.put(aw[i], 32);
-    if (n & 31) out.put(aw[n >> 5] >> (32 - (n & 31)), n & 31);
+    ac = acbits[gb];
+  }
+  bits[gb] = (e & 0xFF) + nb + ac;
+}
+
+// every block writes its bits at its offset: DC code + extra bits (pre), then its AC words
+__global__ __launch_bounds__(256) void k_pack(const EncFrame *fr, const uint32_t *pre, const uint32_t *acbits,
+                                              const uint32_t *acscr, const uint32_t *bitoff, uint8_t *stream) {
+  const EncFrame &F = fr[blockIdx.y];
+  const uint32_t b = blockIdx.x * 256 + threadIdx.x;
+  if (b >= (uint32_t)F.g.nblocks) return;
+  const uint64_t gb = F.blk0 + b;
+  const uint32_t p = pre[gb], n = acbits[gb], off = bitoff[gb];
+  const uint32_t *aw = acscr + gb * kAcWords;
+  const uint32_t a0 = aw[0];  // issued with the other loads; unused by a dummy block
+  BitSink out(reinterpret_cast<uint32_t *>(stream + F.bits_off), off);
+  out.put(p >> 5, p & 31);
+  if (n & kDummyAc) {
+    out.put((n & ~kDummyAc) >> 5, n & 31);
+  } else if (n) {
+    if (n >= 32) {
+      out.put(a0, 32);
+      for (uint32_t i = 1; i < (n >> 5); ++i) out.put(aw[i], 32);
+      if (n & 31) out.put(aw[n >> 5] >> (32 - (n & 31)), n & 31);
+    } else {
+      out.put(a0 >> (32 - n), n);
+    }
   }
   out.finish();
 }
@@ -1349,19 +1408,20 @@ hipError_t enc_fdct(const EncFrame *fr, int n, uint32_t max_blocks, const EncTab
 }
 
 hipError_t enc_len(const EncFrame *fr, int n, uint32_t max_blocks, const EncTables *tab, const int16_t *dcq,
-                   const uint32_t *acbits, uint32_t *bits, hipStream_t s) {
+                   uint32_t *acbits, uint32_t *bits, uint32_t *pre, hipStream_t s) {
   if (n <= 0 || !max_blocks) return hipSuccess;
-  hipLaunchKernelGGL(k_len, dim3((max_blocks + 255) / 256, (unsigned)n), dim3(256), 0, s, fr, tab, dcq, acbits, bits);
+  hipLaunchKernelGGL(k_len, dim3((max_blocks + 255) / 256, (unsigned)n), dim3(256), 0, s, fr, tab, dcq, acbits, bits,
+                     pre);
   return hipGetLastError();
 }
 
-hipError_t enc_pack(const EncFrame *fr, int n, uint32_t max_blocks, const EncTables *tab, const int16_t *dcq,
-                    const uint32_t *acbits, const uint32_t *acscr, const uint32_t *bitoff, const uint32_t *total_bits,
-                    uint8_t *stream, hipStream_t s) {
+hipError_t enc_pack(const EncFrame *fr, int n, uint32_t max_blocks, const uint32_t *pre, const uint32_t *acbits,
+                    const uint32_t *acscr, const uint32_t *bitoff, const uint32_t *total_bits, uint8_t *stream,
+                    hipStream_t s) {
   if (n <= 0 || !max_blocks) return hipSuccess;
   hipLaunchKernelGGL(k_zero_stream, dim3(64, (unsigned)n), dim3(256), 0, s, fr, total_bits, stream);
-  hipLaunchKernelGGL(k_pack, dim3((max_blocks + 255) / 256, (unsigned)n), dim3(256), 0, s, fr, tab, dcq, acbits,
-                     acscr, bitoff, stream);
+  hipLaunchKernelGGL(k_pack, dim3((max_blocks + 255) / 256, (unsigned)n), dim3(256), 0, s, fr, pre, acbits, acscr,
+                     bitoff, stream);
   return hipGetLastError();
 }
 
