@@ -18,6 +18,8 @@ constexpr int kTile = 4096;     // bytes per (un)stuffing tile
 constexpr int kMaxPasses = 64;  // sync-pass flags kept on the device
 constexpr int kLook = 9;        // Huffman lookahead bits
 constexpr int kAcScratchWords = 52;  // per-block AC bit scratch (63 codes of <= 26 bits + EOB)
+constexpr int kCkStep = kSubBits / 8 < 64 ? 64 : kSubBits / 8;  // Huffman-sync checkpoint spacing (bits)
+constexpr int kCk = kSubBits / kCkStep - 1;                       // checkpoints per subsequence
 
 // MCU geometry of one frame (libjpeg jdinput.c / jcmaster.c per-scan setup, restated)
 struct Geom {
@@ -51,16 +53,30 @@ struct HuffDec {
   uint8_t vals[256];
 };
 
+// The same table for the synchronisation decoders, which only need how far each symbol moves:
+// sfast[next kLook bits] = (zigzag advance << 8) | (code length + extra bits) for codes of
+// <= kLook bits (advance 1 for a DC symbol, run + 1 for an AC coefficient, 16 for ZRL, 64 for
+// EOB), 0 for longer codes (decoded through maxcode / valoff / vals).
+struct HuffSync {
+  uint16_t sfast[1 << kLook];
+  int32_t maxcode[18];
+  int32_t valoff[18];
+  uint8_t vals[256];
+};
+
 struct DecFrame {
   Geom g;
   uint16_t q[3][64];       // dequantisation per component, natural order
   HuffDec dc[3], ac[3];    // per component (kept adjacent: loaded into LDS as one block)
+  HuffSync sdc[3], sac[3];  // the same, for the synchronisation decoders (adjacent too)
   uint64_t in_off;         // raw entropy-coded bytes in the batch input buffer (16-aligned)
   uint32_t in_len;
   uint32_t ntiles;         // kTile tiles over the raw bytes
   uint32_t tile0;          // first tile slot
   uint32_t sub0;           // first subsequence slot
   uint32_t nsub_max;       // subsequence slots (ceil(in_len * 8 / kSubBits))
+  uint32_t wg0, nwg;       // speculative sync: first workgroup slot, workgroups (spec_lanes)
+  uint64_t tr0;            // speculative sync: first trajectory slot (nwg * 256 per frame)
   uint32_t flags;          // bit 0: fancy upsampling allowed
   uint64_t us_off;         // unstuffed stream in the unstuffed buffer (16-aligned)
   uint64_t blk0;           // first block in the batch coefficient buffer
@@ -103,6 +119,35 @@ hipError_t dec_unstuff_write(const DecFrame *fr, int n, uint32_t max_tiles, cons
 hipError_t dec_sync(const DecFrame *fr, int n, uint32_t max_sub, const uint8_t *us, const uint32_t *us_len,
                     const uint64_t *exit_in, uint64_t *exit_out, const uint32_t *cnt_in, uint32_t *cnt_out,
                     uint64_t *used, uint64_t *ck, uint32_t *ckrem, uint32_t *changed, int pass, hipStream_t s);
+// Speculative sync (one pass, no host round trip): k_spec decodes every subsequence from
+// each possible block-in-MCU and links neighbouring subsequences, k_wglink links workgroups,
+// k_resolve / k_finalize pick each subsequence's true trajectory.  *unresolved != 0 after
+// the call means some link did not rejoin a trajectory: run the pass-based dec_sync instead.
+struct SpecBufs {
+  // per lane slot [tr0 + workgroup * 256 + subsequence-in-workgroup * lanes + lane]
+  uint64_t *tE;    // trajectory exit states
+  uint8_t *tG;     // walk with entry `lane`: trajectory at the subsequence (or kLinkNone)
+  uint64_t *tX;    //   its exit state
+  uint32_t *tXc;   //   its block count in the subsequence
+  uint64_t *pX;    // resolved prefix records (lane 0 slots)
+  uint32_t *pC;
+  // per workgroup [wg0 + workgroup] (x kSpecLanesMax where indexed by a lane)
+  uint8_t *wF;     // walk e: trajectory at the last subsequence (kLinkNone if explicit)
+  uint64_t *wck;   // checkpoints of each workgroup's first subsequence [(wg * 16 + c) * kCk + m]
+  uint32_t *wrem;  // blocks from each of them to that subsequence's end
+  uint8_t *wB;     // boundary link from the predecessor's last trajectory j
+  uint32_t *wBC;
+  uint64_t *wBX;
+  uint8_t *rE;     // resolved walk column
+  uint32_t *rK;    // resolved: prefix covers subsequences 0..rK
+  uint32_t *stats;  // diagnostics (VF_SYNC_STATS builds): [1] walker decodes [2] traced workgroups
+                    // [3] traced subsequences [4] link misses
+};
+constexpr int kSpecLanesMax = 16;
+inline uint32_t spec_lanes_host(int bpm) { return bpm <= 1 ? 1u : bpm <= 2 ? 2u : bpm <= 4 ? 4u : bpm <= 8 ? 8u : 16u; }
+hipError_t dec_sync_spec(const DecFrame *fr, int n, uint32_t max_wg, const uint8_t *us, const uint32_t *us_len,
+                         const SpecBufs &b, uint64_t *exit_out, uint32_t *cnt_out, uint32_t *unresolved,
+                         hipStream_t s);
 hipError_t dec_write(const DecFrame *fr, int n, uint32_t max_sub, const uint8_t *us, const uint32_t *us_len,
                      const uint64_t *exits, const uint32_t *bstart, int16_t *coef, int32_t *dcseq,
                      hipStream_t s);

@@ -200,14 +200,17 @@ __global__ __launch_bounds__(256) void k_unstuff_write(const DecFrame *fr, const
 // ---- decoder: Huffman ------------------------------------------------------------------------
 
 struct BitReader {
-  const uint32_t *w;
+  const uint32_t *w;  // words of the stream from word `woff` on (global memory or an LDS copy)
   uint64_t buf;  // next bits, left-aligned
   uint32_t nb;   // valid bits in buf
-  uint32_t wi;   // next word to load
+  uint32_t wi;   // next word to load (minus woff)
   uint32_t pos;  // bit position of the next unread bit
   __device__ __forceinline__ void init(const uint8_t *base, uint32_t p) {
-    w = reinterpret_cast<const uint32_t *>(base);
-    wi = p >> 5;
+    init_words(reinterpret_cast<const uint32_t *>(base), p, 0);
+  }
+  __device__ __forceinline__ void init_words(const uint32_t *words, uint32_t p, uint32_t woff) {
+    w = words;
+    wi = (p >> 5) - woff;
     buf = ((uint64_t)bswap32(w[wi]) << 32) | bswap32(w[wi + 1]);
     wi += 2;
     const uint32_t sk = p & 31;
@@ -345,32 +348,54 @@ __device__ __forceinline__ void load_tables(const DecFrame &F, HuffDec *tabs) {
   __syncthreads();
 }
 
-// One Huffman symbol of the sync decode (decode_span<false> without the outputs).
-__device__ __forceinline__ void sync_step(BitReader &br, uint32_t &z, uint32_t &c, uint32_t &blocks,
-                                          const HuffGeom &g, const HuffDec *dcT, const HuffDec *acT) {
-  br.refill();
-  const uint32_t k = g.comp(c);
-  if (z == 0) {
-    uint32_t s = huff_sym(br, dcT[k]);
-    if (s) br.skip(s > 16 ? 16 : s);
-    z = 1;
-  } else {
-    const uint32_t rs = huff_sym(br, acT[k]);
-    const uint32_t r = rs >> 4, s = rs & 15;
-    if (s) {
-      br.skip(s);
-      z += r + 1;
-    } else if (r == 15) {
-      z += 16;
-    } else {
-      z = 64;
+// (zigzag advance << 8) | bits of a symbol whose code is longer than kLook bits: jdhuff.c
+// jpeg_huff_decode's slow path (an unmatched code reads as symbol 0 after 16 bits)
+__device__ __noinline__ uint32_t sync_slow(const BitReader &br, const HuffSync &t, bool dc) {
+  const uint32_t c16 = br.peek(16);
+  uint32_t len = 16, sym = 0;
+  for (uint32_t l = kLook + 1; l <= 16; ++l) {
+    const int32_t c = (int32_t)(c16 >> (16 - l));
+    if (c <= t.maxcode[l]) {
+      sym = t.vals[(uint32_t)(c + t.valoff[l]) & 255];
+      len = l;
+      break;
     }
   }
+  uint32_t extra, adv;
+  if (dc) {
+    extra = sym > 16 ? 16 : sym;
+    adv = 1;
+  } else {
+    extra = sym & 15;
+    adv = extra ? (sym >> 4) + 1 : ((sym >> 4) == 15 ? 16 : 64);
+  }
+  return (adv << 8) | (len + extra);
+}
+
+// One Huffman symbol of the sync decode: the same bits and zigzag / block progression as
+// decode_span, through one combined lookup (HuffSync) instead of symbol + extra-bits steps.
+__device__ __forceinline__ void sync_step(BitReader &br, uint32_t &z, uint32_t &c, uint32_t &blocks,
+                                          const HuffGeom &g, const HuffSync *dcT, const HuffSync *acT) {
+  br.refill();
+  const uint32_t k = g.comp(c);
+  const HuffSync &T = z == 0 ? dcT[k] : acT[k];
+  uint32_t e = T.sfast[br.peek(kLook)];
+  if (!e) e = sync_slow(br, T, z == 0);
+  br.skip(e & 0xFF);
+  z += e >> 8;
   if (z >= 64) {
     z = 0;
     c = (c + 1 == g.bpm) ? 0 : c + 1;
     ++blocks;
   }
+}
+
+__device__ __forceinline__ void load_sync_tables(const DecFrame &F, HuffSync *tabs) {
+  const uint32_t *src = reinterpret_cast<const uint32_t *>(&F.sdc[0]);
+  uint32_t *dst = reinterpret_cast<uint32_t *>(tabs);
+  constexpr uint32_t nw = 6 * sizeof(HuffSync) / 4;
+  for (uint32_t j = threadIdx.x; j < nw; j += 256) dst[j] = src[j];
+  __syncthreads();
 }
 
 // Checkpoints: kCk marks inside each subsequence, every kCkStep bits.  A decode records its
@@ -382,8 +407,7 @@ __device__ __forceinline__ void sync_step(BitReader &br, uint32_t &z, uint32_t &
 // there.  The codes self-synchronise within a few symbols, so a re-decode usually stops at
 // the first mark.  Invariant: every valid checkpoint and the exit state describe one
 // trajectory (marks a decode did not reach from its entry are invalidated).
-constexpr int kCkStep = 64;
-constexpr int kCk = kSubBits / kCkStep - 1;
+
 constexpr uint64_t kNoCk = ~0ull;
 #ifndef VF_SYNC_STATS
 #define VF_SYNC_STATS 0
@@ -399,13 +423,13 @@ __global__ __launch_bounds__(256) void k_sync(const DecFrame *fr, const uint8_t 
                                               const uint64_t *exit_in, uint64_t *exit_out, const uint32_t *cnt_in,
                                               uint32_t *cnt_out, uint64_t *used, uint64_t *ck, uint32_t *ckrem,
                                               uint32_t *changed, int pass) {
-  __shared__ HuffDec tabs[6];
+  __shared__ HuffSync tabs[6];
   __shared__ uint64_t s_exit[256];
   __shared__ uint64_t s_ck[kCk][256];
   __shared__ uint32_t s_rem[kCk][256];
   const DecFrame &F = fr[blockIdx.y];
   if (blockIdx.x * 256 >= F.nsub_max) return;
-  load_tables(F, tabs);
+  load_sync_tables(F, tabs);
   const HuffGeom hg(F.g);
   const uint32_t t = threadIdx.x;
   const uint32_t i = blockIdx.x * 256 + t;
@@ -499,6 +523,367 @@ __global__ __launch_bounds__(256) void k_sync(const DecFrame *fr, const uint8_t 
         atomicAdd(changed + (kMaxPasses - 3 - pass), rounds);
       }
     }
+  }
+}
+
+// ---- decoder: speculative Huffman synchronisation ------------------------------------------
+//
+// The pass-based k_sync above needs a re-decode chain whenever a guessed entry state has the
+// wrong block-in-MCU c: bit positions and zigzag indices resynchronise within a few symbols,
+// but a wrong c selects the other component's tables and tends to survive, so corrections
+// travel one subsequence per round.  Here:
+//   k_spec    every subsequence is decoded from each possible c (bpm trajectories, one lane
+//             each: the extra work fills otherwise idle waves), checkpoints recorded; each
+//             trajectory of subsequence k-1 is linked to the trajectory of k its exit state
+//             rejoins (a short decode to the first matching checkpoint).  Then one lane per
+//             entry index e walks the workgroup: trajectory e of the first subsequence, the
+//             links after it, and, where a link rejoined nothing, an explicit state decoded
+//             on (the walker links it into the next subsequence itself).
+//   k_wglink  links the trajectories ending a workgroup into the next workgroup's first
+//             subsequence.
+//   k_resolve one lane per frame follows the true path across workgroups: entry e* of each
+//             workgroup from the previous one's walk, or, where the boundary link missed or a
+//             walk ended in an explicit state, by decoding on until the path rejoins a
+//             trajectory some walk column passes through (prefix records for the subsequences
+//             before that point).
+//   k_finalize writes exit state and block count per subsequence for the write pass.
+// Only a frame too long for k_resolve's tables, or a stream that never rejoins (corrupt
+// data), is reported unresolved; the caller then runs k_sync.
+
+__device__ __forceinline__ uint32_t spec_lanes(uint32_t bpm) {
+  return bpm <= 1 ? 1u : bpm <= 2 ? 2u : bpm <= 4 ? 4u : bpm <= 8 ? 8u : 16u;
+}
+constexpr uint32_t kSpecPadWords = 16;                                  // overshoot + lookahead
+constexpr uint32_t kSpecWords = 256 * (kSubBits / 32) + kSpecPadWords;  // NS <= 256 subsequences
+constexpr uint8_t kLinkNone = 0xF;  // rejoined no trajectory (explicit state follows)
+constexpr uint8_t kLinkLast = 0xE;  // the frame's last subsequence: decoded to the end
+
+// Decode from state X through subsequence [base, end); at each mark compare with the
+// checkpoints of trajectories 0..bpm-1 (ck(c, m), rem(c, m)).  Returns the trajectory joined,
+// or kLinkNone with *endst = the state at the first symbol boundary at/after `end`, or
+// kLinkLast (the frame's last subsequence, decoded to its end).  *count = blocks completed in
+// the subsequence along this path.
+template <typename CK, typename REM>
+__device__ __forceinline__ uint32_t spec_link(const uint32_t *words, uint32_t woff, uint64_t X, uint32_t base,
+                                              uint32_t end, bool last, const HuffGeom &hg, const HuffSync *tabs, CK ck,
+                                              REM rem, uint32_t *count, uint64_t *endst) {
+  BitReader br;
+  br.init_words(words, (uint32_t)(X >> 16), woff);
+  uint32_t z = (X >> 8) & 0xFF, c = X & 0xFF, n = 0;
+  int m = 0;
+  while (m < kCk && base + (uint32_t)(m + 1) * kCkStep <= br.pos) ++m;
+  while (br.pos < end) {
+    sync_step(br, z, c, n, hg, tabs, tabs + 3);
+    if (last) continue;
+    const uint32_t mk = base + (uint32_t)(m + 1) * kCkStep;
+    if (m < kCk && mk < end && br.pos >= mk) {
+      const uint64_t st = pack_state(br.pos, z, c);
+      for (uint32_t c2 = 0; c2 < hg.bpm; ++c2)
+        if (ck(c2, m) == st) {
+          *count = n + rem(c2, m);
+          return c2;
+        }
+      ++m;
+    }
+  }
+  *count = n;
+  *endst = pack_state(br.pos, z, c);
+  return last ? kLinkLast : kLinkNone;
+}
+
+__global__ __launch_bounds__(256) void k_spec(const DecFrame *fr, const uint8_t *us, const uint32_t *us_len,
+                                              SpecBufs B) {
+  __shared__ HuffSync tabs[6];
+  __shared__ uint64_t s_ck[kCk][256];
+  __shared__ uint32_t s_rem[kCk][256];
+  __shared__ uint64_t s_E[256];
+  __shared__ uint64_t s_X[256];
+  __shared__ uint32_t s_C[256];
+  __shared__ uint8_t s_M[256];
+  __shared__ uint32_t s_w[kSpecWords];
+  const DecFrame &F = fr[blockIdx.y];
+  if (blockIdx.x >= F.nwg) return;
+  const HuffGeom hg(F.g);
+  const uint32_t L = spec_lanes(hg.bpm), NS = 256 / L;
+  const uint32_t t = threadIdx.x, sl = t / L, c0 = t % L;
+  const uint32_t s = blockIdx.x * NS + sl;
+  const uint32_t nbits = us_len[blockIdx.y] * 8u, nsub = (nbits + kSubBits - 1) / kSubBits;
+  const bool live = c0 < hg.bpm && s < nsub;
+  const uint32_t base = s * kSubBits, end = (s + 1 >= nsub) ? nbits : (s + 1) * kSubBits;
+  const uint64_t g0 = F.tr0 + (uint64_t)blockIdx.x * 256, ti = g0 + t;
+  // the workgroup's stream words (every decode here stays within them, plus overshoot and
+  // lookahead), from the frame's padded unstuffed region
+  const uint32_t woff = blockIdx.x * NS * (kSubBits / 32);
+  const uint32_t fwords = (((F.in_len + 64) + 15) & ~15u) / 4;
+  const uint32_t *gw = reinterpret_cast<const uint32_t *>(us + F.us_off);
+  for (uint32_t i = t; i < NS * (kSubBits / 32) + kSpecPadWords; i += 256)
+    s_w[i] = woff + i < fwords ? gw[woff + i] : 0u;
+  load_sync_tables(F, tabs);  // its barrier also publishes s_w
+  // A: the trajectory of subsequence s from (base, z = 0, c = c0), checkpoints recorded
+  uint64_t E = 0;
+  uint32_t N = 0;
+#pragma unroll
+  for (int m = 0; m < kCk; ++m) s_ck[m][t] = kNoCk;
+  if (live) {
+    BitReader br;
+    br.init_words(s_w, base, woff);
+    uint32_t z = 0, c = c0, n = 0;
+    int m = 0;
+    while (br.pos < end) {
+      sync_step(br, z, c, n, hg, tabs, tabs + 3);
+      const uint32_t mk = base + (uint32_t)(m + 1) * kCkStep;
+      if (m < kCk && mk < end && br.pos >= mk) {
+        s_ck[m][t] = pack_state(br.pos, z, c);
+        s_rem[m][t] = n;
+        ++m;
+      }
+    }
+    for (int q = 0; q < m; ++q) s_rem[q][t] = n - s_rem[q][t];
+    E = pack_state(br.pos, z, c);
+    N = n;
+  }
+  s_E[t] = E;
+  __syncthreads();
+  if (live) {
+    B.tE[ti] = E;
+    if (sl == 0) {  // checkpoints of the first subsequence, for k_wglink
+      const uint64_t wb = ((uint64_t)(F.wg0 + blockIdx.x) * kSpecLanesMax + c0) * kCk;
+#pragma unroll
+      for (int m = 0; m < kCk; ++m) {
+        B.wck[wb + m] = s_ck[m][t];
+        B.wrem[wb + m] = s_rem[m][t];
+      }
+    }
+  }
+  // B: link trajectory c0 of s-1 into s
+  uint32_t M = kLinkNone, C = N;
+  uint64_t X = 0;
+  if (live && sl > 0) {
+    const uint32_t row = sl * L;
+    M = spec_link(s_w, woff, s_E[(sl - 1) * L + c0], base, end, s + 1 == nsub, hg, tabs,
+                  [&](uint32_t c2, int m) { return s_ck[m][row + c2]; },
+                  [&](uint32_t c2, int m) { return s_rem[m][row + c2]; }, &C, &X);
+    if (VF_SYNC_STATS && M == kLinkNone) atomicAdd(B.stats + 4, 1u);
+  }
+  s_M[t] = (uint8_t)M;
+  s_C[t] = C;
+  s_X[t] = X;
+  __syncthreads();
+  // C: one lane per entry index e walks the workgroup; walkers sit 256 / L lanes apart so
+  // their (divergent) explicit decodes run in different waves where possible
+  const uint32_t wsp = 256 / L, e = t / wsp;
+  if (t % wsp == 0 && e < hg.bpm && blockIdx.x * NS < nsub) {
+    uint32_t j = e;  // current trajectory, or kLinkNone while explicit
+    uint64_t st = s_E[e];
+    B.tG[g0 + e] = (uint8_t)e;
+    B.tX[g0 + e] = st;
+    B.tXc[g0 + e] = s_C[e];  // trajectory count (used for the frame's first subsequence)
+    for (uint32_t k = 1; k < NS && blockIdx.x * NS + k < nsub; ++k) {
+      const uint32_t sk = blockIdx.x * NS + k;
+      uint32_t cnt, M2;
+      uint64_t xe = 0;
+      if (j < hg.bpm) {
+        M2 = s_M[k * L + j];
+        cnt = s_C[k * L + j];
+        xe = s_X[k * L + j];
+      } else {  // explicit state: link it into subsequence k here
+        if (VF_SYNC_STATS) atomicAdd(B.stats + 1, 1u);
+        const uint32_t bk = sk * kSubBits, ek = (sk + 1 >= nsub) ? nbits : (sk + 1) * kSubBits;
+        const uint32_t row = k * L;
+        M2 = spec_link(s_w, woff, st, bk, ek, sk + 1 == nsub, hg, tabs,
+                       [&](uint32_t c2, int m) { return s_ck[m][row + c2]; },
+                       [&](uint32_t c2, int m) { return s_rem[m][row + c2]; }, &cnt, &xe);
+      }
+      if (M2 < hg.bpm) {
+        j = M2;
+        st = s_E[k * L + j];
+      } else {
+        j = M2;  // kLinkNone (explicit) or kLinkLast
+        st = xe;
+      }
+      B.tG[g0 + k * L + e] = (uint8_t)j;
+      B.tX[g0 + k * L + e] = st;
+      B.tXc[g0 + k * L + e] = cnt;
+      if (j == kLinkLast) break;
+    }
+    B.wF[(uint64_t)(F.wg0 + blockIdx.x) * kSpecLanesMax + e] = (uint8_t)(j < hg.bpm ? j : kLinkNone);
+  }
+}
+
+// Links across workgroup boundaries: trajectory j of the last subsequence of workgroup w-1
+// into the first subsequence of w.  16 boundaries per workgroup, one lane per j.
+__global__ __launch_bounds__(256) void k_wglink(const DecFrame *fr, const uint8_t *us, const uint32_t *us_len,
+                                                SpecBufs B) {
+  __shared__ HuffSync tabs[6];
+  const DecFrame &F = fr[blockIdx.y];
+  if (blockIdx.x * 16 >= F.nwg) return;
+  load_sync_tables(F, tabs);
+  const HuffGeom hg(F.g);
+  const uint32_t L = spec_lanes(hg.bpm), NS = 256 / L;
+  const uint32_t w = blockIdx.x * 16 + threadIdx.x / 16, j = threadIdx.x % 16;
+  const uint32_t nbits = us_len[blockIdx.y] * 8u, nsub = (nbits + kSubBits - 1) / kSubBits;
+  const uint32_t s = w * NS;
+  if (w == 0 || w >= F.nwg || j >= hg.bpm || s >= nsub) return;
+  const uint32_t base = s * kSubBits, end = (s + 1 >= nsub) ? nbits : (s + 1) * kSubBits;
+  const uint64_t X = B.tE[F.tr0 + (uint64_t)(w - 1) * 256 + (NS - 1) * L + j];
+  const uint64_t wc = (uint64_t)(F.wg0 + w) * kSpecLanesMax;
+  uint32_t C = 0;
+  uint64_t xe = 0;
+  const uint32_t M = spec_link(reinterpret_cast<const uint32_t *>(us + F.us_off), 0u, X, base, end, s + 1 == nsub,
+                               hg, tabs,
+                               [&](uint32_t c2, int m) { return B.wck[(wc + c2) * kCk + m]; },
+                               [&](uint32_t c2, int m) { return B.wrem[(wc + c2) * kCk + m]; }, &C, &xe);
+  const uint64_t wb = wc + j;
+  B.wB[wb] = (uint8_t)M;
+  B.wBC[wb] = C;
+  B.wBX[wb] = xe;
+}
+
+// The true path across the workgroups of a frame (one workgroup per frame).  Per workgroup w
+// it finds the walk column e* that is the path from subsequence kj + 1 on; subsequences
+// 0..kj get prefix records (exit state, count) in pX / pC.  The common case is two nibble
+// lookups in LDS (the boundary link from the trajectory ending w-1 rejoined trajectory e* of
+// w's first subsequence); where it did not, or the column ending w-1 was in an explicit
+// state, lane 0 decodes on until its exit state equals some column's exit (tX) there.
+constexpr uint32_t kResolveLds = 4096;  // workgroups per frame resolved here (else fallback)
+constexpr uint32_t kTraceWords = kSubBits / 32 + 6;  // one subsequence + overshoot + lookahead
+__device__ __forceinline__ uint32_t nib(uint64_t row, uint32_t i) { return (uint32_t)(row >> (4 * i)) & 0xF; }
+
+__global__ __launch_bounds__(256) void k_resolve(const DecFrame *fr, const uint8_t *us, const uint32_t *us_len,
+                                                 SpecBufs B, uint32_t *unresolved) {
+  __shared__ uint64_t sF[kResolveLds], sB[kResolveLds];
+  __shared__ uint8_t sE[kResolveLds], sK[kResolveLds], sJ[kResolveLds];
+  __shared__ HuffSync tabs[6];
+  __shared__ uint32_t s_tw[kTraceWords];
+  const DecFrame &F = fr[blockIdx.x];
+  const HuffGeom hg(F.g);
+  const uint32_t bpm = hg.bpm, L = spec_lanes(bpm), NS = 256 / L;
+  const uint32_t nbits = us_len[blockIdx.x] * 8u, nsub = (nbits + kSubBits - 1) / kSubBits;
+  const uint32_t nwg = min(F.nwg, (nsub + NS - 1) / NS);
+  if (nwg > kResolveLds) {
+    if (threadIdx.x == 0) atomicOr(unresolved, 1u);
+    return;
+  }
+  load_sync_tables(F, tabs);
+  for (uint32_t i = threadIdx.x; i < nwg; i += 256) {
+    uint64_t fr_ = 0, br_ = 0;
+    const uint64_t row = (uint64_t)(F.wg0 + i) * kSpecLanesMax;
+    for (uint32_t e = 0; e < bpm; ++e) {
+      fr_ |= (uint64_t)(B.wF[row + e] & 0xF) << (4 * e);
+      if (i > 0) br_ |= (uint64_t)(B.wB[row + e] & 0xF) << (4 * e);
+    }
+    sF[i] = fr_;
+    sB[i] = br_;
+  }
+  __syncthreads();
+  auto slot = [&](uint32_t w, uint32_t k, uint32_t lane) { return F.tr0 + (uint64_t)w * 256 + k * L + lane; };
+  const uint32_t fwords = (((F.in_len + 64) + 15) & ~15u) / 4;
+  const uint32_t *gw = reinterpret_cast<const uint32_t *>(us + F.us_off);
+  const uint8_t kTraced = 0xFF;  // sJ: the prefix was written by the tracer
+  if (threadIdx.x == 0) {
+    sE[0] = 0;
+    sK[0] = 0;
+    sJ[0] = kTraced;  // workgroup 0: frame start = trajectory 0 (records written below)
+    B.pX[slot(0, 0, 0)] = B.tX[slot(0, 0, 0)];
+    B.pC[slot(0, 0, 0)] = B.tXc[slot(0, 0, 0)];
+    uint32_t e = 0, kj = 0;
+    for (uint32_t w = 1; w < nwg; ++w) {
+      const uint32_t lastk = NS - 1;  // workgroup w-1 is full (only the frame's last one is not)
+      uint32_t jl = kLinkNone;
+      if (kj < lastk) jl = nib(sF[w - 1], e);
+      if (jl < bpm) {
+        const uint32_t jb = nib(sB[w], jl);
+        if (jb < bpm || jb == kLinkLast) {  // rejoined (or the frame's last subsequence)
+          sE[w] = (uint8_t)(jb < bpm ? jb : 0);
+          sK[w] = 0;
+          sJ[w] = (uint8_t)jl;
+          e = jb < bpm ? jb : 0;
+          kj = 0;
+          continue;
+        }
+      }
+      // trace from the explicit state at the end of w-1 (or after w's first subsequence)
+      if (VF_SYNC_STATS) atomicAdd(B.stats + 2, 1u);
+      uint64_t X;
+      uint32_t k = 0;
+      if (jl < bpm) {  // the boundary link decoded subsequence 0 without rejoining
+        const uint64_t wb = (uint64_t)(F.wg0 + w) * kSpecLanesMax + jl;
+        X = B.wBX[wb];
+        B.pX[slot(w, 0, 0)] = X;
+        B.pC[slot(w, 0, 0)] = B.wBC[wb];
+        k = 1;
+      } else {
+        X = kj < lastk ? B.tX[slot(w - 1, lastk, e)] : B.pX[slot(w - 1, lastk, 0)];
+      }
+      bool found = false;
+      for (; k < NS && w * NS + k < nsub; ++k) {
+        const uint32_t sk = w * NS + k;
+        const uint32_t ek = (sk + 1 >= nsub) ? nbits : (sk + 1) * kSubBits;
+        // the subsequence's words, fetched together (independent loads), then decoded from LDS
+        if (VF_SYNC_STATS) atomicAdd(B.stats + 3, 1u);
+        const uint32_t w0 = (uint32_t)(X >> 16) >> 5;
+        for (uint32_t q = 0; q < kTraceWords; ++q) s_tw[q] = w0 + q < fwords ? gw[w0 + q] : 0u;
+        BitReader br;
+        br.init_words(s_tw, (uint32_t)(X >> 16), w0);
+        uint32_t z = (X >> 8) & 0xFF, c = X & 0xFF, n = 0;
+        const uint32_t lim = min(ek, (w0 + kTraceWords - 3) * 32u);  // stays inside s_tw (binds only on corrupt data)
+        while (br.pos < lim) sync_step(br, z, c, n, hg, tabs, tabs + 3);
+        X = pack_state(br.pos, z, c);
+        B.pX[slot(w, k, 0)] = X;
+        B.pC[slot(w, k, 0)] = n;
+        if (sk + 1 == nsub) break;
+        for (uint32_t c2 = 0; c2 < bpm; ++c2)
+          if (B.tX[slot(w, k, c2)] == X) {  // the path is column c2 from here on
+            e = c2;
+            found = true;
+            break;
+          }
+        if (found) break;
+      }
+      sE[w] = (uint8_t)(found ? e : 0);
+      sK[w] = (uint8_t)(found ? k : NS - 1);
+      sJ[w] = kTraced;
+      kj = found ? k : NS - 1;
+    }
+  }
+  __syncthreads();
+  for (uint32_t w = threadIdx.x; w < nwg; w += 256) {
+    B.rE[F.wg0 + w] = sE[w];
+    B.rK[F.wg0 + w] = sK[w];
+    if (sJ[w] != kTraced) {  // rejoined at the boundary: prefix record of subsequence 0
+      const uint64_t wb = (uint64_t)(F.wg0 + w) * kSpecLanesMax + sJ[w];
+      B.pX[slot(w, 0, 0)] = sK[w] == 0 && nib(sB[w], sJ[w]) < bpm ? B.tE[slot(w, 0, sE[w])] : B.wBX[wb];
+      B.pC[slot(w, 0, 0)] = B.wBC[wb];
+    }
+  }
+}
+
+// Exit state and block count of every subsequence along the resolved path, in the layout
+// the write pass and the block-offset scan read (exit_out / cnt_out of k_sync).
+__global__ __launch_bounds__(256) void k_finalize(const DecFrame *fr, const uint32_t *us_len, SpecBufs B,
+                                                  uint64_t *exit_out, uint32_t *cnt_out) {
+  const DecFrame &F = fr[blockIdx.y];
+  if (blockIdx.x >= F.nwg) return;
+  const uint32_t bpm = (uint32_t)F.g.bpm, L = spec_lanes(bpm), NS = 256 / L;
+  const uint32_t nbits = us_len[blockIdx.y] * 8u, nsub = (nbits + kSubBits - 1) / kSubBits;
+  const uint32_t sl = threadIdx.x;
+  if (sl >= NS) return;
+  const uint32_t s = blockIdx.x * NS + sl;
+  if (s >= F.nsub_max) return;
+  const uint64_t gi = F.sub0 + s;
+  if (s >= nsub) {
+    exit_out[gi] = pack_state(nbits, 0, 0);
+    cnt_out[gi] = 0;
+    return;
+  }
+  const uint64_t g0 = F.tr0 + (uint64_t)blockIdx.x * 256;
+  const uint32_t kj = B.rK[F.wg0 + blockIdx.x], e = B.rE[F.wg0 + blockIdx.x];
+  if (sl <= kj) {
+    exit_out[gi] = B.pX[g0 + sl * L];
+    cnt_out[gi] = B.pC[g0 + sl * L];
+  } else {
+    exit_out[gi] = B.tX[g0 + sl * L + e];
+    cnt_out[gi] = B.tXc[g0 + sl * L + e];
   }
 }
 
@@ -608,23 +993,42 @@ __global__ __launch_bounds__(256) void k_idct(const DecFrame *fr, const int16_t 
   if (blockIdx.x * 32 >= (uint32_t)g.nblocks) return;
   __shared__ int32_t blkv[32][64];
   __shared__ int32_t ws[32][8][9];
-  const uint32_t slot = threadIdx.x >> 3, r = threadIdx.x & 7;
+  __shared__ int32_t s_q[3][64];     // dequantisation, natural order
+  __shared__ uint8_t s_nat[64];      // zigzag -> natural
+  __shared__ uint32_t s_pos[kMaxBpm];  // block-in-MCU -> component | x << 8 | y << 16 (blocks)
+  const uint32_t t = threadIdx.x;
+  if (t < 192) s_q[t >> 6][t & 63] = F.q[t >> 6][t & 63];
+  if (t < 64) s_nat[t] = kNat[t];
+  if (t < (uint32_t)g.bpm)
+    s_pos[t] = (uint32_t)g.bcomp[t] | ((uint32_t)g.bxo[t] << 8) | ((uint32_t)g.byo[t] << 16);
+  __syncthreads();
+  // per-component values, uniform: picked with selects, not per-lane global loads
+  const uint32_t mh[3] = {(uint32_t)g.mh[0], (uint32_t)g.mh[1], (uint32_t)g.mh[2]};
+  const uint32_t mv[3] = {(uint32_t)g.mv[0], (uint32_t)g.mv[1], (uint32_t)g.mv[2]};
+  const uint32_t cf[3] = {(uint32_t)g.cfirst[0], (uint32_t)g.cfirst[1], (uint32_t)g.cfirst[2]};
+  const uint64_t dcb[3] = {F.dcbase[0], F.dcbase[1], F.dcbase[2]};
+  const uint64_t po[3] = {F.plane_off[0], F.plane_off[1], F.plane_off[2]};
+  const uint32_t pw[3] = {(uint32_t)g.pw[0], (uint32_t)g.pw[1], (uint32_t)g.pw[2]};
+  const uint32_t slot = t >> 3, r = t & 7;
   const uint32_t b = blockIdx.x * 32 + slot;
   const bool valid = b < (uint32_t)g.nblocks;
-  uint32_t k = 0, bx = 0, by = 0;
+  const uint32_t mcu = b / (uint32_t)g.bpm, c = b - mcu * (uint32_t)g.bpm;
+  const uint32_t ps = valid ? s_pos[c] : 0u;
+  const uint32_t k = ps & 0xFF;
+  const uint32_t bx = (mcu % (uint32_t)g.mcux) * HuffGeom::sel(mh, k) + ((ps >> 8) & 0xFF);
+  const uint32_t by = (mcu / (uint32_t)g.mcux) * HuffGeom::sel(mv, k) + (ps >> 16);
   if (valid) {
-    block_pos(g, b, &k, &bx, &by);
     const uint4 raw = *reinterpret_cast<const uint4 *>(coef + (F.blk0 + b) * 64 + r * 8);
     const int16_t *v = reinterpret_cast<const int16_t *>(&raw);
+    int32_t dc = 0;
+    if (r == 0)
+      dc = dcseq[HuffGeom::sel(dcb, k) + (uint64_t)mcu * (HuffGeom::sel(mh, k) * HuffGeom::sel(mv, k)) +
+                 (c - HuffGeom::sel(cf, k))];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const uint32_t zz = r * 8 + j, n = kNat[zz];
-      int32_t x = v[j];
-      if (zz == 0) {
-        const uint32_t mcu = b / (uint32_t)g.bpm, c = b % (uint32_t)g.bpm;
-        x = (int16_t)dcseq[F.dcbase[k] + (uint64_t)mcu * (g.mh[k] * g.mv[k]) + (c - g.cfirst[k])];
-      }
-      blkv[slot][n] = x * (int32_t)F.q[k][n];
+      const uint32_t zz = r * 8 + j, n = s_nat[zz];
+      const int32_t x = zz == 0 ? (int32_t)(int16_t)dc : (int32_t)v[j];
+      blkv[slot][n] = x * s_q[k][n];
     }
   }
   __syncthreads();
@@ -648,7 +1052,7 @@ __global__ __launch_bounds__(256) void k_idct(const DecFrame *fr, const int16_t 
       lo |= idct_limit(out[i]) << (8 * i);
       hi |= idct_limit(out[i + 4]) << (8 * i);
     }
-    uint8_t *p = planes + F.plane_off[k] + (uint64_t)(by * 8 + r) * (uint32_t)g.pw[k] + bx * 8;
+    uint8_t *p = planes + HuffGeom::sel(po, k) + (uint64_t)(by * 8 + r) * HuffGeom::sel(pw, k) + bx * 8;
     *reinterpret_cast<uint2 *>(p) = make_uint2(lo, hi);
   }
 }
@@ -1372,6 +1776,17 @@ hipError_t dec_sync(const DecFrame *fr, int n, uint32_t max_sub, const uint8_t *
   if (n <= 0 || !max_sub) return hipSuccess;
   hipLaunchKernelGGL(k_sync, dim3((max_sub + 255) / 256, (unsigned)n), dim3(256), 0, s, fr, us, us_len, exit_in,
                      exit_out, cnt_in, cnt_out, used, ck, ckrem, changed, pass);
+  return hipGetLastError();
+}
+
+hipError_t dec_sync_spec(const DecFrame *fr, int n, uint32_t max_wg, const uint8_t *us, const uint32_t *us_len,
+                         const SpecBufs &b, uint64_t *exit_out, uint32_t *cnt_out, uint32_t *unresolved,
+                         hipStream_t s) {
+  if (n <= 0 || !max_wg) return hipSuccess;
+  hipLaunchKernelGGL(k_spec, dim3(max_wg, (unsigned)n), dim3(256), 0, s, fr, us, us_len, b);
+  hipLaunchKernelGGL(k_wglink, dim3((max_wg + 15) / 16, (unsigned)n), dim3(256), 0, s, fr, us, us_len, b);
+  hipLaunchKernelGGL(k_resolve, dim3((unsigned)n), dim3(256), 0, s, fr, us, us_len, b, unresolved);
+  hipLaunchKernelGGL(k_finalize, dim3(max_wg, (unsigned)n), dim3(256), 0, s, fr, us_len, b, exit_out, cnt_out);
   return hipGetLastError();
 }
 

@@ -147,3 +147,21 @@ def test_concurrent_calls_lease_separate_codecs(tj):
         th.join(120)
     assert not any(th.is_alive() for th in ths)
     assert not errors, errors[:3]
+
+
+@pytest.mark.parametrize("mode", ["spec", "pass"])
+@pytest.mark.parametrize("subsamp,quality", [(J.TJSAMP_420, 95), (J.TJSAMP_444, 90), (J.TJSAMP_422, 85)])
+def test_sync_modes_on_hard_content(tj, monkeypatch, mode, subsamp, quality):
+    """Both Huffman synchronisation paths (speculative trajectories + links, and the
+    pass-based chain) on content with long blocks (noise: links rejoin late, walkers and the
+    resolver decode explicit states) and a mixed batch, bit-exact with the oracle."""
+    monkeypatch.setenv("VF_JPEG_SYNC", mode)
+    rng = np.random.default_rng(quality)
+    imgs = [rng.integers(0, 256, (256, 320, 3), dtype=np.uint8),
+            _img("scene", 3, 480, 640),
+            np.clip(_img("scene", 4, 360, 200).astype(np.int16) + rng.integers(-40, 40, (360, 200, 3)), 0, 255)
+            .astype(np.uint8)]
+    jpgs = [J.encode(im, quality, J.TJPF_BGR, subsamp) for im in imgs]
+    got = tj.invert_batch(jpgs)
+    for g, j in zip(got, jpgs):
+        assert g == J.invert_jpeg(j)
