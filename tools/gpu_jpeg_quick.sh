@@ -8,4 +8,4 @@ timeout -k 10 200 python -u tools/jpeg_bench.py --sizes 480p,1080p,4k --batch 32
 python -c "
 import json
 for l in open('gpurun_out/jpeg_q.jsonl'):
-    d=json.loads(l); print(d['size'], d['gpu_resident_fps'], d['host_to_host_fps'], d['host_to_host_2threads_fps'], d['parity_vs_oracle'])"
+    d=json.loads(l); print(d['size'], d['gpu_resident_fps'], d['host_to_host_fps'], d['host_to_host_2threads_fps'], d['parity_vs_oracle'], d.get('stages_ms'))"
