@@ -14,7 +14,10 @@ Prints ONE JSON line on rank 0 (contract in the task statement), including
                 traffic = HBM bytes per launch from rocprofv3 PMC (FETCH_SIZE x 2 per the
                 gfx950 correction in MI355X_MICROARCH.md §HBM, + WRITE_SIZE), rank 0 at N=1
   cpu_baseline  the oracle's numpy restatement of inverter.py:41 (np.bitwise_not per frame,
-                a new array each call, like cv2.bitwise_not), 1 host core, ~10 s sample
+                a new array each call, like cv2.bitwise_not), 1 host core, ~10 s sample; plus
+                multi_process: the same arithmetic in up to 16 processes at once (BASELINE.md plan)
+  sizes         kernel-only frames/s and HBM fraction at 480p / 1080p / 4K on this run's GPUs
+                (north star: every size at 1/2/4/8 GPUs), same timing rules as the headline
   end_to_end    host->host rate through vf_invert_batch_host (pageable and pinned): PCIe-bound,
                 reported beside value, never as value.
   jpeg_mode     the reference's default use_jpeg=True path (decode -> invert -> encode) on 1080p
@@ -63,7 +66,11 @@ def parse():
     ap.add_argument("--no-jpeg", action="store_true", help="skip the JPEG-mode leg (use_jpeg=True path)")
     ap.add_argument("--no-distributor", action="store_true",
                     help="skip the configs[2]/[3] distributor leg (worker process per GPU)")
+    ap.add_argument("--no-sizes", action="store_true", help="skip the 480p / 1080p / 4K kernel leg")
+    ap.add_argument("--cpu-procs", type=int, default=16,
+                    help="processes of the multi-process CPU baseline (capped by the CPU affinity; 0 = skip)")
     ap.add_argument("--probe", action="store_true", help=argparse.SUPPRESS)  # child under rocprofv3
+    ap.add_argument("--cpu-worker", type=float, default=0.0, help=argparse.SUPPRESS)  # cpu_baseline_multi child
     return ap.parse_args()
 
 
@@ -71,23 +78,24 @@ def parse():
 # device ring
 # ---------------------------------------------------------------------------------------
 
-def make_ring(ctx, batch, ring_gb, np, rank=0, world=1):
+def make_ring(ctx, batch, ring_gb, np, rank=0, world=1, hw=(H, W), distinct=97):
     """Ring slot k of this rank holds the frames of global batch k*world + rank (its
     frame-index shard, vfilter.sharding); step s processes slot s % nbuf, i.e. the frames
     of global batch s*world + rank up to the ring's reuse of synthetic content."""
     from vfilter import sharding
     from vfilter.synthetic import synthetic_frame
-    batch_bytes = batch * FRAME_BYTES
+    fb = hw[0] * hw[1] * C
+    batch_bytes = batch * fb
     nbuf = max(2, int(ring_gb * 1e9 // (2 * batch_bytes)))
     cache = {}
     host = np.empty(batch_bytes, np.uint8)
     srcs, dsts = [], []
     for k in range(nbuf):
         for j, i in enumerate(sharding.batch_frames(sharding.batch_of_step(k, rank, world), batch)):
-            seed = sharding.synthetic_seed(i)
+            seed = sharding.synthetic_seed(i, distinct)
             if seed not in cache:
-                cache[seed] = synthetic_frame(seed, H, W).reshape(-1)
-            host[j * FRAME_BYTES:(j + 1) * FRAME_BYTES] = cache[seed]
+                cache[seed] = synthetic_frame(seed, hw[0], hw[1]).reshape(-1)
+            host[j * fb:(j + 1) * fb] = cache[seed]
         s, d = ctx.alloc_device(batch_bytes), ctx.alloc_device(batch_bytes)
         ctx.upload(s, host, batch_bytes)
         ctx.sync()  # host buffer is reused for the next slot
@@ -103,9 +111,6 @@ def probe(args):
     ctx = Context(0)
     srcs, dsts, batch_bytes, _ = make_ring(ctx, args.batch, args.ring_gb, np)
     ctx.bench_device_ring(srcs, dsts, batch_bytes, args.steps)
-    for s, d in zip(srcs, dsts):
-        ctx.free_device(s)
-        ctx.free_device(d)
     ctx.close()
 
 
@@ -161,6 +166,74 @@ def cpu_baseline(host_batch, batch, seconds, np):
     return {"value": round(n / dt, 2), "unit": "frames/s", "cores": 1, "kind": "port",
             "sample": f"{n} x 1080p frames ({dt:.1f} s), np.bitwise_not per frame "
                       f"(oracle restatement of cv2.bitwise_not, inverter.py:41), 1 thread"}
+
+
+def cpu_worker(seconds):
+    """Child of cpu_baseline_multi: one process, np.bitwise_not(x, out=y) over a contiguous
+    1080p batch of 32 (BASELINE.md's CPU-baseline plan) for `seconds`; prints frames done."""
+    import numpy as np
+    x = np.random.default_rng(os.getpid() % 97).integers(0, 256, (32, H, W, C), dtype=np.uint8)
+    y = np.empty_like(x)
+    n = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        np.bitwise_not(x, out=y)
+        n += len(x)
+    print(json.dumps({"frames": n, "seconds": time.perf_counter() - t0}), flush=True)
+
+
+def cpu_baseline_multi(seconds, procs):
+    """BASELINE.md plan (ii): the reference's filter arithmetic on `procs` host processes at
+    once (the reference scales by worker processes, distributor.py:229-241), each over its
+    own contiguous 1080p batch.  Started as child processes (fresh interpreters, no GPU)."""
+    cmd = [sys.executable, os.path.abspath(__file__), "--cpu-worker", str(seconds)]
+    ps = [subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True) for _ in range(procs)]
+    rate = 0.0
+    for p in ps:
+        so, _ = p.communicate(timeout=seconds + 120)
+        r = json.loads([ln for ln in so.splitlines() if ln.startswith("{")][-1])
+        rate += r["frames"] / r["seconds"]
+    return {"value": round(rate, 1), "unit": "frames/s", "cores": procs, "kind": "port",
+            "GBps_r_plus_w": round(rate * 2 * FRAME_BYTES / 1e9, 1),
+            "sample": f"{procs} processes x {seconds:.0f} s of np.bitwise_not(x, out=y) over a 32-frame "
+                      f"1080p batch each (oracle arithmetic of inverter.py:41)"}
+
+
+def resolution_leg(ctx, np, rank, world, steps, barrier_sync, reduce_max):
+    """North star: kernel-only throughput at 480p, 1080p and 4K on this run's GPUs, as
+    whole-job frames/s and as a fraction of the HBM roofline.  Same timing rules as the
+    headline (warmup, barrier + sync on both sides, max over ranks; hipEvent mean per launch
+    for the roofline); batches of ~200-400 MB per launch so no size is launch-bound."""
+    out = {}
+    for name, (hh, ww), batch in (("480p", (480, 640), 256), ("1080p", (H, W), 32), ("4k", (2160, 3840), 16)):
+        srcs, dsts, bb, _ = make_ring(ctx, batch, 2.4, np, rank, world, hw=(hh, ww), distinct=8)
+        # warm until a call costs what its kernels cost: the first calls over a fresh ring carry
+        # ~8-17 ms of one-off host-side latency (first touch of new allocations)
+        for _ in range(5):
+            tw = time.perf_counter()
+            wr, _ = ctx.bench_device_ring(srcs, dsts, bb, 10)
+            tw = time.perf_counter() - tw
+            if tw * 1e3 < 1.2 * wr + 0.5:
+                break
+        barrier_sync()
+        t0 = time.perf_counter()
+        region_ms, _ = ctx.bench_device_ring(srcs, dsts, bb, steps)
+        tc = time.perf_counter() - t0
+        ctx.sync()
+        barrier_sync()
+        elapsed = reduce_max(time.perf_counter() - t0)
+        log(f"sizes {name}: warmup call {tw * 1e3:.2f} ms (region {wr:.2f}), timed call {tc * 1e3:.2f} ms "
+            f"(region {region_ms:.2f}), wall {elapsed * 1e3:.2f} ms")
+        mean_ms = reduce_max(region_ms / steps)
+        for s_, d_ in zip(srcs, dsts):
+            ctx.free_device(s_)
+            ctx.free_device(d_)
+        gbs = 2.0 * bb / (mean_ms * 1e-3) / 1e9
+        out[name] = {"frame": [hh, ww, C], "batch_per_rank": batch, "steps": steps,
+                     "fps": round(world * steps * batch / elapsed, 1),
+                     "kernel_GBps_per_gpu": round(gbs, 1), "frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 4)}
+    out["note"] = "kernel-only, HBM-resident, whole job over all ranks; GB/s = slowest rank's mean launch"
+    return out
 
 
 def end_to_end(ctx, host_batch, batch, np, reps=8):
@@ -305,6 +378,8 @@ def main():
     args = parse()
     if args.probe:
         return probe(args)
+    if args.cpu_worker:
+        return cpu_worker(args.cpu_worker)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -357,15 +432,26 @@ def main():
     # untimed: isolated per-launch durations (event pair around each launch) for reference
     _, isolated = ctx.bench_device_ring(srcs, dsts, batch_bytes, min(args.steps, 60), per_launch=True)
 
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64,
-                         device="cuda" if (have_gpu and backend == "nccl") else "cpu")
+    def reduce_max(x):
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device="cuda" if (have_gpu and backend == "nccl") else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        return float(t.item())
+
+    elapsed = reduce_max(elapsed)
 
     # average launch duration over the timed region (includes the ~1-2 us kernel boundaries)
     mean_ms = region_ms / args.steps if args.steps else float("nan")
     achieved = 2.0 * batch_bytes / (mean_ms * 1e-3) / 1e9
+    for s_, d_ in zip(srcs, dsts):  # the sizes leg needs the HBM
+        ctx.free_device(s_)
+        ctx.free_device(d_)
+    sizes = None
+    if not args.no_sizes:
+        sizes = resolution_leg(ctx, np, rank, world, 100, barrier_sync, reduce_max)
+        if rank == 0:
+            log(f"sizes: {sizes}")
     e2e = None
     cpu = None
     if rank == 0 and not args.no_e2e:
@@ -378,14 +464,14 @@ def main():
         log(f"jpeg mode: {jpeg}")
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         cpu = cpu_baseline(host_batch, args.batch, args.cpu_seconds, np)
+        procs = min(args.cpu_procs, len(os.sched_getaffinity(0)))
+        if procs > 1:
+            cpu["multi_process"] = cpu_baseline_multi(min(5.0, args.cpu_seconds), procs)
         log(f"cpu baseline: {cpu}")
         if jpeg is not None:
             jpeg["cpu_reference"] = cpu_baseline_jpeg(jpgs, min(5.0, args.cpu_seconds))
             log(f"jpeg cpu reference: {jpeg['cpu_reference']}")
 
-    for s, d in zip(srcs, dsts):
-        ctx.free_device(s)
-        ctx.free_device(d)
     ctx.close()
 
     fanout = None
@@ -428,6 +514,7 @@ def main():
                          "isolated_launch_ms_median": round(float(np.median(isolated)), 5),
                          "traffic_detail": traffic_detail},
             "cpu_baseline": cpu,
+            "sizes": sizes,
             "end_to_end": e2e,
             "jpeg_mode": jpeg,
             "distributor": fanout,

@@ -1441,6 +1441,12 @@ __global__ __launch_bounds__(256) void k_fdct(const EncFrame *fr, const EncTable
     const int real_rows = ((g.h + g.maxv - 1) / g.maxv) * g.vs[k];
     const int sy = min((int)(by * 8 + r), real_rows - 1);
     int32_t v[8];
+#ifdef VF_ABL_NOPIX
+    if (true) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (int)((bx * 8 + j + sy * 3 + k) & 255);
+    } else
+#endif
     if (ve == 1 && he <= 2) {  // he == 1: full-resolution line; he == 2: h2v1_downsample
       if (he == 1) line_acc<1>(img, g.w, g.h, (int)bx * 8, sy, bgr, (int)k, v, true);
       else line_acc<2>(img, g.w, g.h, (int)bx * 16, sy, bgr, (int)k, v, true);
@@ -1480,6 +1486,14 @@ __global__ __launch_bounds__(256) void k_fdct(const EncFrame *fr, const EncTable
     }
   }
   __syncthreads();
+#ifdef VF_ABL_NOAC
+  if (real && r == 0) {
+    const uint64_t gb = F.blk0 + b;
+    dcq[gb] = qo[slot][0];
+    acbits[gb] = (uint32_t)qo[slot][1] & 1;
+  }
+  return;
+#endif
   // AC Huffman coding; every lane of the wave takes part in the 8-lane shuffles
   int vz[8];
   uint32_t m8 = 0;
