@@ -15,7 +15,8 @@ Prints ONE JSON line on rank 0 (contract in the task statement), including
                 gfx950 correction in MI355X_MICROARCH.md §HBM, + WRITE_SIZE), rank 0 at N=1
   cpu_baseline  the oracle's numpy restatement of inverter.py:41 (np.bitwise_not per frame,
                 a new array each call, like cv2.bitwise_not), 1 host core, ~10 s sample; plus
-                multi_process: the same arithmetic in up to 16 processes at once (BASELINE.md plan)
+                multi_process: the same arithmetic in up to 16 processes at once (BASELINE.md plan),
+                process_scaling_fps: 1, 2, 4, 8 and 16 processes; sizes: 1 core at 480p and 4K
   sizes         kernel-only frames/s and HBM fraction at 480p / 1080p / 4K on this run's GPUs
                 (north star: every size at 1/2/4/8 GPUs), same timing rules as the headline
   end_to_end    host->host rate through vf_invert_batch_host (pageable and pinned): PCIe-bound,
@@ -166,6 +167,25 @@ def cpu_baseline(host_batch, batch, seconds, np):
     return {"value": round(n / dt, 2), "unit": "frames/s", "cores": 1, "kind": "port",
             "sample": f"{n} x 1080p frames ({dt:.1f} s), np.bitwise_not per frame "
                       f"(oracle restatement of cv2.bitwise_not, inverter.py:41), 1 thread"}
+
+
+def cpu_baseline_sizes(seconds, np):
+    """The same 1-core oracle baseline at 480p and 4K (north star: every size is reported next
+    to the reference CPU path), `seconds` per size."""
+    from oracle import oracle
+    from vfilter.synthetic import synthetic_frame
+    out = {}
+    for name, (hh, ww) in (("480p", (480, 640)), ("4k", (2160, 3840))):
+        frames = [synthetic_frame(s, hh, ww) for s in range(4)]
+        n = 0
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < seconds:
+            oracle.invert(frames[n % 4])
+            n += 1
+        dt = time.perf_counter() - t0
+        out[name] = {"value": round(n / dt, 2), "unit": "frames/s", "cores": 1, "kind": "port",
+                     "sample": f"{n} x {name} frames ({dt:.1f} s), np.bitwise_not per frame, 1 thread"}
+    return out
 
 
 def cpu_worker(seconds):
@@ -467,6 +487,15 @@ def main():
         procs = min(args.cpu_procs, len(os.sched_getaffinity(0)))
         if procs > 1:
             cpu["multi_process"] = cpu_baseline_multi(min(5.0, args.cpu_seconds), procs)
+            # BASELINE.md plan: 1, 2, 4, ... processes, to show where host memory saturates
+            series = {}
+            p_ = 1
+            while p_ < procs:
+                series[str(p_)] = cpu_baseline_multi(min(2.0, args.cpu_seconds), p_)["value"]
+                p_ *= 2
+            series[str(procs)] = cpu["multi_process"]["value"]
+            cpu["process_scaling_fps"] = series
+        cpu["sizes"] = cpu_baseline_sizes(min(3.0, args.cpu_seconds), np)
         log(f"cpu baseline: {cpu}")
         if jpeg is not None:
             jpeg["cpu_reference"] = cpu_baseline_jpeg(jpgs, min(5.0, args.cpu_seconds))
