@@ -903,7 +903,7 @@ int Codec::prepare_encode(const int *ws, const int *hs, const uint64_t *img_offs
   CK(d_etotals_.ensure(sizeof(uint32_t) * segs.size()));
   CK(d_dcq_.ensure(sizeof(int16_t) * blk));
   CK(d_acbits_.ensure(sizeof(uint32_t) * blk));
-  CK(d_acscr_.ensure(sizeof(uint32_t) * kAcScratchWords * blk));
+  CK(d_acscr_.ensure(sizeof(uint32_t) * kAcScratchWords * ((blk + 63) & ~(size_t)63)));  // whole 64-block groups
   CK(d_bits_.ensure(sizeof(uint32_t) * blk));
   CK(d_pre_.ensure(sizeof(uint32_t) * blk));
   CK(d_bitoff_.ensure(sizeof(uint32_t) * blk));

@@ -1384,27 +1384,58 @@ __device__ __forceinline__ void line_acc(const uint8_t *img, int w, int h, int p
 
 constexpr uint32_t kAcWords = kAcScratchWords;
 
-// `size` (<= 32) bits at stream bit `pos` of an MSB-first word array in LDS
-__device__ __forceinline__ void lds_put(uint32_t *words, uint32_t pos, uint32_t bits, uint32_t size) {
-  if (!size) return;
-  const uint32_t w = pos >> 5, sh = pos & 31;
-  if (sh + size <= 32) {
-    atomicOr(words + w, bits << (32 - sh - size));
-  } else {
-    const uint32_t n2 = sh + size - 32;  // bits spilling into the next word
-    atomicOr(words + w, bits >> n2);
-    atomicOr(words + w + 1, bits << (32 - n2));
-  }
+// AC scratch layout: blocks in groups of 64, word i of the 64 blocks of a group contiguous,
+// so k_pack's one-thread-per-block reads of word i are one 256-B span per wave instead of
+// 64 lines 208 B apart (the host rounds the allocation up to whole groups).
+__device__ __forceinline__ uint64_t acs_idx(uint64_t gb, uint32_t i) {
+  return (gb >> 6) * (64ull * kAcWords) + (uint64_t)i * 64 + (gb & 63);
 }
+
+// MSB-first bits of one lane into an LDS word image, from bit `pos` on.  Words the lane
+// shares with its neighbours (its first and its last) are OR-ed; the words in between are
+// the lane's alone and are stored.  The image is zeroed beforehand.
+struct LdsBits {
+  uint32_t *w;
+  uint32_t wi, n;
+  uint64_t acc;
+  bool first;
+  __device__ __forceinline__ LdsBits(uint32_t *words, uint32_t pos)
+      : w(words), wi(pos >> 5), n(pos & 31), acc(0), first(true) {}
+  __device__ __forceinline__ void put(uint32_t bits, uint32_t size) {  // size <= 32
+    acc = (acc << size) | bits;
+    n += size;
+    if (n >= 32) {
+      n -= 32;
+      const uint32_t v = (uint32_t)(acc >> n);
+      if (first) atomicOr(w + wi, v);
+      else w[wi] = v;
+      first = false;
+      ++wi;
+      acc &= n ? ((1ull << n) - 1) : 0ull;
+    }
+  }
+  __device__ __forceinline__ void finish() {
+    if (n) atomicOr(w + wi, (uint32_t)(acc << (32 - n)));
+  }
+};
+
+// natural (row-major) index -> zigzag position (inverse of kNat)
+__constant__ uint8_t kZig[64] = {0,  1,  5,  6,  14, 15, 27, 28, 2,  4,  7,  13, 16, 26, 29, 42,
+                                 3,  8,  12, 17, 25, 30, 41, 43, 9,  11, 18, 24, 31, 40, 44, 53,
+                                 10, 19, 23, 32, 39, 45, 52, 54, 20, 22, 33, 38, 46, 51, 55, 60,
+                                 21, 34, 37, 47, 50, 56, 59, 61, 35, 36, 48, 49, 57, 58, 62, 63};
 
 // 8 lanes per block.  A workgroup takes M = 32 / bpm whole MCUs and orders its 32 block
 // slots block-in-MCU-major (slot s -> block-in-MCU s / M of MCU s % M), so a wave's 8 blocks
 // are mostly one component and the luma / chroma sampling paths do not diverge in a wave.
 // After quantisation the 8 lanes Huffman-code the block's AC coefficients (jchuff.c
-// encode_one_block, AC part): lane r codes zigzag positions 8r..8r+7; every run of zeros is
-// read off the block's 64-bit nonzero mask (ZRL for each 16), lane offsets come from an
-// 8-lane scan, and the bits are OR-ed into an LDS image of the block's AC stream that is then
-// copied out.  Outputs per block: quantised DC, AC bit count, AC bits (MSB-first words).
+// encode_one_block, AC part): the quantised block sits in LDS in zigzag order, so lane r
+// reads zigzag positions 8r..8r+7 with one 16-B load.  Each lane finds the run before each of
+// its coefficients from a running "previous nonzero" position (seeded from the block's 64-bit
+// nonzero mask; ZRL for each 16), looks each code up once and keeps it in registers, takes
+// its offset from an 8-lane scan of the lanes' bit counts, and writes its bits through a
+// register accumulator into an LDS image of the block's AC stream that is then copied out.
+// Outputs per block: quantised DC, AC bit count, AC bits (MSB-first words).
 __global__ __launch_bounds__(256) void k_fdct(const EncFrame *fr, const EncTables *tab, const uint8_t *pix,
                                               int16_t *dcq, uint32_t *acbits, uint32_t *acscr, int bgr,
                                               int fastdct) {
@@ -1418,6 +1449,8 @@ __global__ __launch_bounds__(256) void k_fdct(const EncFrame *fr, const EncTable
   __shared__ uint16_t s_recip[2][64], s_corr[2][64];
   __shared__ int16_t s_shift[2][64];
   __shared__ uint32_t s_ac[2][256];
+  __shared__ uint8_t s_zig[64];
+  if (threadIdx.x < 64) s_zig[threadIdx.x] = kZig[threadIdx.x];
   if (threadIdx.x < 128) {
     const int t = threadIdx.x >> 6, i = threadIdx.x & 63;
     s_recip[t][i] = tab->recip[t][i];
@@ -1482,7 +1515,7 @@ __global__ __launch_bounds__(256) void k_fdct(const EncFrame *fr, const EncTable
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int n = i * 8 + r;
-      qo[slot][n] = quantize(v[i], s_recip[t][n], s_corr[t][n], s_shift[t][n]);
+      qo[slot][s_zig[n]] = quantize(v[i], s_recip[t][n], s_corr[t][n], s_shift[t][n]);
     }
   }
   __syncthreads();
@@ -1496,29 +1529,41 @@ __global__ __launch_bounds__(256) void k_fdct(const EncFrame *fr, const EncTable
 #endif
   // AC Huffman coding; every lane of the wave takes part in the 8-lane shuffles
   int vz[8];
+  {
+    const uint4 q4 = real ? *reinterpret_cast<const uint4 *>(&qo[slot][r * 8]) : make_uint4(0, 0, 0, 0);
+    const uint32_t qw[4] = {q4.x, q4.y, q4.z, q4.w};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) vz[j] = (int)(int16_t)(qw[j >> 1] >> (16 * (j & 1)));
+  }
   uint32_t m8 = 0;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    vz[j] = real ? qo[slot][kNat[r * 8 + j]] : 0;
+  for (int j = 0; j < 8; ++j)
     if (vz[j] != 0 && (r | j) != 0) m8 |= 1u << j;
-  }
   uint64_t mask = (uint64_t)m8 << (8 * r);
   mask |= __shfl_xor(mask, 1, 8);
   mask |= __shfl_xor(mask, 2, 8);
   mask |= __shfl_xor(mask, 4, 8);
-  const uint64_t starts = mask | 1ull;  // the DC position starts the first run
   const uint32_t zrl = s_ac[t][0xF0], eobc = s_ac[t][0x00];
+  const uint32_t zlen = zrl & 0xFF;
   const bool eob = mask == 0 || (63 - __clzll(mask)) < 63;
+  // the last nonzero position before this lane's first (the DC position starts the first run)
+  int prev = r ? 63 - __clzll((mask | 1ull) & ((1ull << (8 * r)) - 1)) : 0;
+  uint32_t code[8], clen[8], nzr[8];
   uint32_t nbits = 0;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    if (!(m8 >> j & 1)) continue;
+    const bool nz = (m8 >> j) & 1;
     const int kk = 8 * (int)r + j;
-    const int prev = 63 - __clzll(starts & ((1ull << kk) - 1));
     const int run = kk - prev - 1;
-    const uint32_t av = (uint32_t)(vz[j] < 0 ? -vz[j] : vz[j]);
+    const int v = vz[j];
+    const uint32_t av = (uint32_t)(v < 0 ? -v : v);
     const uint32_t nb = 32 - __clz(av);
-    nbits += (uint32_t)(run >> 4) * (zrl & 0xFF) + (s_ac[t][((run & 15) << 4) + nb] & 0xFF) + nb;
+    const uint32_t e = s_ac[t][((run & 15) << 4) + (nb & 15)];
+    code[j] = ((e >> 8) << nb) | ((uint32_t)(v < 0 ? v - 1 : v) & ((1u << nb) - 1));
+    clen[j] = nz ? (e & 0xFF) + nb : 0u;
+    nzr[j] = nz ? (uint32_t)(run >> 4) : 0u;
+    nbits += nzr[j] * zlen + clen[j];
+    prev = nz ? kk : prev;
   }
   if (r == 7 && eob) nbits += eobc & 0xFF;
   uint32_t incl = nbits;
@@ -1528,34 +1573,21 @@ __global__ __launch_bounds__(256) void k_fdct(const EncFrame *fr, const EncTable
     if ((int)r >= off) incl += y;
   }
   const uint32_t total = __shfl(incl, 7, 8);
-  if (real) {
-    uint32_t pos = incl - nbits;
-    uint32_t *aw = acw[slot];
+  if (real && nbits) {
+    LdsBits out(acw[slot], incl - nbits);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      if (!(m8 >> j & 1)) continue;
-      const int kk = 8 * (int)r + j;
-      const int prev = 63 - __clzll(starts & ((1ull << kk) - 1));
-      int run = kk - prev - 1;
-      for (; run > 15; run -= 16) {
-        lds_put(aw, pos, zrl >> 8, zrl & 0xFF);
-        pos += zrl & 0xFF;
-      }
-      const int v = vz[j];
-      const uint32_t av = (uint32_t)(v < 0 ? -v : v);
-      const uint32_t nb = 32 - __clz(av);
-      const uint32_t e = s_ac[t][(run << 4) + nb];
-      const uint32_t code = ((e >> 8) << nb) | ((uint32_t)(v < 0 ? v - 1 : v) & ((1u << nb) - 1));
-      lds_put(aw, pos, code, (e & 0xFF) + nb);
-      pos += (e & 0xFF) + nb;
+      for (uint32_t z = nzr[j]; z; --z) out.put(zrl >> 8, zlen);
+      if (clen[j]) out.put(code[j], clen[j]);
     }
-    if (r == 7 && eob) lds_put(aw, pos, eobc >> 8, eobc & 0xFF);
+    if (r == 7 && eob) out.put(eobc >> 8, eobc & 0xFF);
+    out.finish();
   }
   __syncthreads();
   if (real) {
     const uint64_t gb = F.blk0 + b;
     const uint32_t nw = (total + 31) >> 5;
-    for (uint32_t i = r; i < nw; i += 8) acscr[gb * kAcWords + i] = acw[slot][i];
+    for (uint32_t i = r; i < nw; i += 8) acscr[acs_idx(gb, i)] = acw[slot][i];
     if (r == 0) {
       dcq[gb] = qo[slot][0];
       acbits[gb] = total;
@@ -1670,7 +1702,7 @@ __global__ __launch_bounds__(256) void k_pack(const EncFrame *fr, const uint32_t
   if (b >= (uint32_t)F.g.nblocks) return;
   const uint64_t gb = F.blk0 + b;
   const uint32_t p = pre[gb], n = acbits[gb], off = bitoff[gb];
-  const uint32_t *aw = acscr + gb * kAcWords;
+  const uint32_t *aw = acscr + acs_idx(gb, 0);  // word i at aw[64 * i]
   const uint32_t a0 = aw[0];  // issued with the other loads; unused by a dummy block
   BitSink out(reinterpret_cast<uint32_t *>(stream + F.bits_off), off);
   out.put(p >> 5, p & 31);
@@ -1679,8 +1711,8 @@ __global__ __launch_bounds__(256) void k_pack(const EncFrame *fr, const uint32_t
   } else if (n) {
     if (n >= 32) {
       out.put(a0, 32);
-      for (uint32_t i = 1; i < (n >> 5); ++i) out.put(aw[i], 32);
-      if (n & 31) out.put(aw[n >> 5] >> (32 - (n & 31)), n & 31);
+      for (uint32_t i = 1; i < (n >> 5); ++i) out.put(aw[64 * i], 32);
+      if (n & 31) out.put(aw[64 * (n >> 5)] >> (32 - (n & 31)), n & 31);
     } else {
       out.put(a0 >> (32 - n), n);
     }
