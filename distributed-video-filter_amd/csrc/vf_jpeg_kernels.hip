@@ -991,7 +991,7 @@ __global__ __launch_bounds__(256) void k_idct(const DecFrame *fr, const int16_t 
   const DecFrame &F = fr[blockIdx.y];
   const Geom &g = F.g;
   if (blockIdx.x * 32 >= (uint32_t)g.nblocks) return;
-  __shared__ int32_t blkv[32][64];
+  __shared__ int32_t blkv[32][72];  // rows padded to 72: a wave's 8 column reads hit 64 banks
   __shared__ int32_t ws[32][8][9];
   __shared__ int32_t s_q[3][64];     // dequantisation, natural order
   __shared__ uint8_t s_nat[64];      // zigzag -> natural
