@@ -45,8 +45,15 @@ struct EncTables {
   uint32_t ac[2][256];  // (code << 8) | size by run/size symbol
 };
 
+// Codes longer than kLook bits: lim[i] = (maxcode[l] + 1) << (16 - l) for l = kLook + 1 + i,
+// running maximum over i (lim[7] unused).  The length of the code starting the next 16 bits
+// c16 is kLook + 1 + #{i : c16 >= lim[i]} (17 = no code: jdhuff.c's corrupt-data case), the
+// same as jdhuff.c jpeg_huff_decode's length-by-length maxcode walk, in one 32-B LDS read.
+static_assert(kLook == 9, "lim[] holds code lengths 10..16");
+
 // Huffman decoding table: jdhuff.c derived table plus a kLook-bit lookahead
 struct HuffDec {
+  alignas(16) uint32_t lim[8];
   uint16_t fast[1 << kLook];  // (length << 8) | symbol for codes of <= kLook bits, else 0
   int32_t maxcode[18];
   int32_t valoff[18];
@@ -58,6 +65,7 @@ struct HuffDec {
 // <= kLook bits (advance 1 for a DC symbol, run + 1 for an AC coefficient, 16 for ZRL, 64 for
 // EOB), 0 for longer codes (decoded through maxcode / valoff / vals).
 struct HuffSync {
+  alignas(16) uint32_t lim[8];
   uint16_t sfast[1 << kLook];
   int32_t maxcode[18];
   int32_t valoff[18];

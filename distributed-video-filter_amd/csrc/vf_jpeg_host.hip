@@ -125,11 +125,20 @@ bool decode_table(const uint8_t bits[17], const uint8_t *vals, HuffDec *t) {
     code <<= 1;
   }
   t->maxcode[17] = 0xFFFFF;
+  uint32_t run = 0;
+  for (int i = 0; i < 7; ++i) {
+    const int l = kLook + 1 + i;
+    const uint32_t v = t->maxcode[l] < 0 ? 0u : (uint32_t)(t->maxcode[l] + 1) << (16 - l);
+    run = v > run ? v : run;
+    t->lim[i] = run;
+  }
+  t->lim[7] = 0xFFFFFFFFu;
   return true;
 }
 
 // jdhuff.c decode semantics folded into one lookup for the sync decoders (see HuffSync)
 void sync_table(const HuffDec &t, bool dc, HuffSync *s) {
+  std::memcpy(s->lim, t.lim, sizeof s->lim);
   std::memcpy(s->maxcode, t.maxcode, sizeof s->maxcode);
   std::memcpy(s->valoff, t.valoff, sizeof s->valoff);
   std::memcpy(s->vals, t.vals, sizeof s->vals);
@@ -711,7 +720,7 @@ int Codec::prepare_decode(const uint8_t *const *jpegs, const size_t *sizes, int 
     CK(d_wBX_.ensure(sizeof(uint64_t) * wl));
     CK(d_rE_.ensure(wgs));
     CK(d_rK_.ensure(sizeof(uint32_t) * wgs));
-    CK(d_unres_.ensure(sizeof(uint32_t) * 8));
+    CK(d_unres_.ensure(sizeof(uint32_t) * 16));
   }
   CK(d_changed_.ensure(sizeof(uint32_t) * kMaxPasses));
   CK(d_coef_.ensure(blk * 128));
@@ -761,7 +770,7 @@ int Codec::run_decode(int bgr, bool invert, std::string *err) {
                 d_pX_.as<uint64_t>(), d_pC_.as<uint32_t>(), d_wF_.as<uint8_t>(), d_wck_.as<uint64_t>(),
                 d_wrem_.as<uint32_t>(), d_wB_.as<uint8_t>(), d_wBC_.as<uint32_t>(), d_wBX_.as<uint64_t>(),
                 d_rE_.as<uint8_t>(), d_rK_.as<uint32_t>(), d_unres_.as<uint32_t>()};
-    CK(hipMemsetAsync(d_unres_.p, 0, sizeof(uint32_t) * 8, s_));
+    CK(hipMemsetAsync(d_unres_.p, 0, sizeof(uint32_t) * 16, s_));
     CK(dec_sync_spec(fr, n, dmax_wg_, d_us_.as<uint8_t>(), us_len, sb, d_exit_[0].as<uint64_t>(),
                      d_cnt_[0].as<uint32_t>(), d_unres_.as<uint32_t>(), s_));
     uint32_t unres = 1;
@@ -771,11 +780,14 @@ int Codec::run_decode(int bgr, bool invert, std::string *err) {
     ++spec_calls_;
     if (unres) ++spec_fallbacks_;
     if (std::getenv("VF_JPEG_SYNC_STATS")) {
-      uint32_t st[8];
+      uint32_t st[16];
       CK(hipMemcpy(st, d_unres_.p, sizeof st, hipMemcpyDeviceToHost));
+      std::fprintf(stderr, "[vf_jpeg] k_spec kcycles summed over workgroups, from start: part A %u, part B %u, "
+                   "walkers end %u (x bpm)\n", st[8], st[9], st[10]);
       std::fprintf(stderr, "[vf_jpeg] spec: unresolved %u walker decodes %u traced workgroups %u traced subsequences "
-                   "%u link misses %u (workgroups %u, subsequences %u)\n", st[0], st[1], st[2], st[3], st[4],
-                   dmax_wg_ * (uint32_t)n, dmax_sub_ * (uint32_t)n);
+                   "%u link misses %u (workgroups %u, subsequences %u); k_resolve kcycles summed over frames: "
+                   "trace %u walk %u\n", st[0], st[1], st[2], st[3], st[4],
+                   dmax_wg_ * (uint32_t)n, dmax_sub_ * (uint32_t)n, st[5], st[6]);
     }
   }
   if (flag) CK(hipMemsetAsync(d_changed_.p, 0, sizeof(uint32_t) * kMaxPasses, s_));

@@ -232,21 +232,26 @@ struct BitReader {
   }
 };
 
+// Length of a code longer than kLook bits starting the 16 bits c16 (17: none, see HuffDec.lim)
+__device__ __forceinline__ uint32_t long_code_len(uint32_t c16, const uint32_t *lim) {
+  const uint4 a = *reinterpret_cast<const uint4 *>(lim);
+  const uint4 b = *reinterpret_cast<const uint4 *>(lim + 4);
+  return kLook + 1 + (c16 >= a.x) + (c16 >= a.y) + (c16 >= a.z) + (c16 >= a.w) + (c16 >= b.x) + (c16 >= b.y) +
+         (c16 >= b.z);
+}
+
 // jdhuff.c jpeg_huff_decode with a kLook-bit first level
 __device__ __forceinline__ uint32_t huff_sym(BitReader &br, const HuffDec &t) {
   const uint32_t e = t.fast[br.peek(kLook)];
   uint32_t len = e >> 8, sym = e & 0xFF;
   if (len == 0) {
     const uint32_t c16 = br.peek(16);
-    len = 16;
-    sym = 0;  // corrupt code: jdhuff.c returns 0
-    for (uint32_t l = kLook + 1; l <= 16; ++l) {
-      const int32_t c = (int32_t)(c16 >> (16 - l));
-      if (c <= t.maxcode[l]) {
-        sym = t.vals[(uint32_t)(c + t.valoff[l]) & 255];
-        len = l;
-        break;
-      }
+    len = long_code_len(c16, t.lim);
+    if (len > 16) {
+      len = 16;
+      sym = 0;  // corrupt code: jdhuff.c returns 0
+    } else {
+      sym = t.vals[(uint32_t)((int32_t)(c16 >> (16 - len)) + t.valoff[len]) & 255];
     }
   }
   br.skip(len);
@@ -350,17 +355,11 @@ __device__ __forceinline__ void load_tables(const DecFrame &F, HuffDec *tabs) {
 
 // (zigzag advance << 8) | bits of a symbol whose code is longer than kLook bits: jdhuff.c
 // jpeg_huff_decode's slow path (an unmatched code reads as symbol 0 after 16 bits)
-__device__ __noinline__ uint32_t sync_slow(const BitReader &br, const HuffSync &t, bool dc) {
+__device__ __forceinline__ uint32_t sync_slow(const BitReader &br, const HuffSync &t, bool dc) {
   const uint32_t c16 = br.peek(16);
-  uint32_t len = 16, sym = 0;
-  for (uint32_t l = kLook + 1; l <= 16; ++l) {
-    const int32_t c = (int32_t)(c16 >> (16 - l));
-    if (c <= t.maxcode[l]) {
-      sym = t.vals[(uint32_t)(c + t.valoff[l]) & 255];
-      len = l;
-      break;
-    }
-  }
+  uint32_t len = long_code_len(c16, t.lim), sym = 0;
+  if (len > 16) len = 16;  // corrupt code: symbol 0
+  else sym = t.vals[(uint32_t)((int32_t)(c16 >> (16 - len)) + t.valoff[len]) & 255];
   uint32_t extra, adv;
   if (dc) {
     extra = sym > 16 ? 16 : sym;
@@ -603,6 +602,7 @@ __global__ __launch_bounds__(256) void k_spec(const DecFrame *fr, const uint8_t 
   __shared__ uint32_t s_w[kSpecWords];
   const DecFrame &F = fr[blockIdx.y];
   if (blockIdx.x >= F.nwg) return;
+  const long long c_start = VF_SYNC_STATS ? clock64() : 0;
   const HuffGeom hg(F.g);
   const uint32_t L = spec_lanes(hg.bpm), NS = 256 / L;
   const uint32_t t = threadIdx.x, sl = t / L, c0 = t % L;
@@ -644,6 +644,7 @@ __global__ __launch_bounds__(256) void k_spec(const DecFrame *fr, const uint8_t 
   }
   s_E[t] = E;
   __syncthreads();
+  if (VF_SYNC_STATS && t == 0) atomicAdd(B.stats + 8, (uint32_t)((clock64() - c_start) >> 10));
   if (live) {
     B.tE[ti] = E;
     if (sl == 0) {  // checkpoints of the first subsequence, for k_wglink
@@ -669,6 +670,7 @@ __global__ __launch_bounds__(256) void k_spec(const DecFrame *fr, const uint8_t 
   s_C[t] = C;
   s_X[t] = X;
   __syncthreads();
+  if (VF_SYNC_STATS && t == 0) atomicAdd(B.stats + 9, (uint32_t)((clock64() - c_start) >> 10));
   // C: one lane per entry index e walks the workgroup; walkers sit 256 / L lanes apart so
   // their (divergent) explicit decodes run in different waves where possible
   const uint32_t wsp = 256 / L, e = t / wsp;
@@ -707,6 +709,7 @@ __global__ __launch_bounds__(256) void k_spec(const DecFrame *fr, const uint8_t 
       if (j == kLinkLast) break;
     }
     B.wF[(uint64_t)(F.wg0 + blockIdx.x) * kSpecLanesMax + e] = (uint8_t)(j < hg.bpm ? j : kLinkNone);
+    if (VF_SYNC_STATS) atomicAdd(B.stats + 10, (uint32_t)((clock64() - c_start) >> 10));
   }
 }
 
@@ -781,6 +784,7 @@ __global__ __launch_bounds__(256) void k_resolve(const DecFrame *fr, const uint8
   const uint32_t *gw = reinterpret_cast<const uint32_t *>(us + F.us_off);
   const uint8_t kTraced = 0xFF;  // sJ: the prefix was written by the tracer
   if (threadIdx.x == 0) {
+    long long c_loop = VF_SYNC_STATS ? clock64() : 0, c_trace = 0;
     sE[0] = 0;
     sK[0] = 0;
     sJ[0] = kTraced;  // workgroup 0: frame start = trajectory 0 (records written below)
@@ -804,6 +808,7 @@ __global__ __launch_bounds__(256) void k_resolve(const DecFrame *fr, const uint8
       }
       // trace from the explicit state at the end of w-1 (or after w's first subsequence)
       if (VF_SYNC_STATS) atomicAdd(B.stats + 2, 1u);
+      const long long c_t0 = VF_SYNC_STATS ? clock64() : 0;
       uint64_t X;
       uint32_t k = 0;
       if (jl < bpm) {  // the boundary link decoded subsequence 0 without rejoining
@@ -844,6 +849,11 @@ __global__ __launch_bounds__(256) void k_resolve(const DecFrame *fr, const uint8
       sK[w] = (uint8_t)(found ? k : NS - 1);
       sJ[w] = kTraced;
       kj = found ? k : NS - 1;
+      if (VF_SYNC_STATS) c_trace += clock64() - c_t0;
+    }
+    if (VF_SYNC_STATS) {  // shader-clock kcycles: the trace path, the whole walk
+      atomicAdd(B.stats + 5, (uint32_t)(c_trace >> 10));
+      atomicAdd(B.stats + 6, (uint32_t)((clock64() - c_loop) >> 10));
     }
   }
   __syncthreads();
