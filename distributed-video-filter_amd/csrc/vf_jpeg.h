@@ -16,7 +16,10 @@ constexpr int kMaxBpm = 10;     // blocks per MCU (T.81 B.2.3)
 constexpr int kSubBits = 256;  // bits per Huffman-decoding subsequence
 constexpr int kTile = 4096;     // bytes per (un)stuffing tile
 constexpr int kMaxPasses = 64;  // sync-pass flags kept on the device
-constexpr int kLook = 9;        // Huffman lookahead bits
+#ifndef VF_KLOOK
+#define VF_KLOOK 9
+#endif
+constexpr int kLook = VF_KLOOK;        // Huffman lookahead bits
 constexpr int kAcScratchWords = 52;  // per-block AC bit scratch (63 codes of <= 26 bits + EOB)
 constexpr int kCkStep = kSubBits / 8 < 64 ? 64 : kSubBits / 8;  // Huffman-sync checkpoint spacing (bits)
 constexpr int kCk = kSubBits / kCkStep - 1;                       // checkpoints per subsequence
@@ -49,7 +52,7 @@ struct EncTables {
 // running maximum over i (lim[7] unused).  The length of the code starting the next 16 bits
 // c16 is kLook + 1 + #{i : c16 >= lim[i]} (17 = no code: jdhuff.c's corrupt-data case), the
 // same as jdhuff.c jpeg_huff_decode's length-by-length maxcode walk, in one 32-B LDS read.
-static_assert(kLook == 9, "lim[] holds code lengths 10..16");
+static_assert(kLook >= 9 && kLook <= 15, "lim[] holds code lengths kLook + 1 .. 16 (at most 7)");
 
 // Huffman decoding table: jdhuff.c derived table plus a kLook-bit lookahead
 struct HuffDec {

@@ -126,13 +126,16 @@ bool decode_table(const uint8_t bits[17], const uint8_t *vals, HuffDec *t) {
   }
   t->maxcode[17] = 0xFFFFF;
   uint32_t run = 0;
-  for (int i = 0; i < 7; ++i) {
+  for (int i = 0; i < 8; ++i) {
     const int l = kLook + 1 + i;
+    if (l > 16) {  // no such length: never counted
+      t->lim[i] = 0xFFFFFFFFu;
+      continue;
+    }
     const uint32_t v = t->maxcode[l] < 0 ? 0u : (uint32_t)(t->maxcode[l] + 1) << (16 - l);
     run = v > run ? v : run;
     t->lim[i] = run;
   }
-  t->lim[7] = 0xFFFFFFFFu;
   return true;
 }
 
