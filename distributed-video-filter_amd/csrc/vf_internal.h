@@ -34,7 +34,9 @@ enum Variant : int {
   kVariantU2 = 7,
   kVariantU8 = 8,
   kVariantU1 = 9,
-  kVariantCount = 10,
+  kVariantU4NTChunk = 10,  // contiguous tiles per workgroup instead of grid-stride (tuning)
+  kVariantU8NTChunk = 11,
+  kVariantCount = 12,
 };
 
 const char *variant_name(int v);

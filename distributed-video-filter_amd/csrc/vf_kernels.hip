@@ -36,15 +36,21 @@ __device__ __forceinline__ void st16(u32x4 *p, u32x4 v) {
 }
 
 // Body: n16 aligned 16-B vectors at src/dst.  Head/tail: up to 15 bytes each, bytewise.
-template <int U, bool NTL, bool NTS>
+// CHUNK (tuning variant): block b takes the contiguous tiles [b * tpb, (b + 1) * tpb)
+// instead of striding over the grid.
+template <int U, bool NTL, bool NTS, bool CHUNK = false>
 __global__ __launch_bounds__(kBlock) void invert_stream_kernel(
     const u32x4 *__restrict__ src, u32x4 *__restrict__ dst, uint64_t n16,
     const uint8_t *__restrict__ hsrc, uint8_t *__restrict__ hdst, uint32_t head,
-    const uint8_t *__restrict__ tsrc, uint8_t *__restrict__ tdst, uint32_t tail) {
+    const uint8_t *__restrict__ tsrc, uint8_t *__restrict__ tdst, uint32_t tail, uint64_t tpb) {
   constexpr uint64_t TILE = (uint64_t)kBlock * U;
-  const uint64_t stride = (uint64_t)gridDim.x * TILE;
+  const uint64_t stride = CHUNK ? TILE : (uint64_t)gridDim.x * TILE;
   const uint32_t t = threadIdx.x;
-  uint64_t t0 = (uint64_t)blockIdx.x * TILE;  // wave-uniform tile start
+  uint64_t t0 = (uint64_t)blockIdx.x * (CHUNK ? tpb : 1) * TILE;  // wave-uniform tile start
+  if (CHUNK) {
+    const uint64_t e = t0 + tpb * TILE;
+    n16 = e < n16 ? e : n16;
+  }
   for (; t0 + TILE <= n16; t0 += stride) {
     const u32x4 *s = src + t0 + t;
     u32x4 *d = dst + t0 + t;
@@ -107,7 +113,8 @@ __global__ __launch_bounds__(kBlock) void invert_frames_kernel(const uint8_t *co
 
 const char *variant_name(int v) {
   static const char *names[kVariantCount] = {"u4-nt", "u2-nt", "u8-nt", "u1-nt", "u4-ntl",
-                                             "u4-nts", "u4", "u2", "u8", "u1"};
+                                             "u4-nts", "u4", "u2", "u8", "u1", "u4-nt-chunk",
+                                             "u8-nt-chunk"};
   return (v >= 0 && v < kVariantCount) ? names[v] : "?";
 }
 
@@ -120,7 +127,7 @@ const char *variant_name(int v) {
 constexpr uint64_t kSplitBytes = 512ull << 20;
 constexpr uint64_t kChunkBytes = 256ull << 20;
 
-template <int U, bool NTL, bool NTS>
+template <int U, bool NTL, bool NTS, bool CHUNK = false>
 static hipError_t launch_stream(const uint8_t *src, uint8_t *dst, size_t nbytes, int max_blocks,
                                 hipStream_t stream) {
   // Split [src, src+n) into head (bytes until 16-B alignment), body (whole vectors) and tail.
@@ -141,10 +148,12 @@ static hipError_t launch_stream(const uint8_t *src, uint8_t *dst, size_t nbytes,
     const uint64_t tiles = (m + TILE - 1) / TILE;
     uint64_t blocks = tiles ? tiles : 1;
     if (blocks > (uint64_t)max_blocks) blocks = (uint64_t)max_blocks;
-    hipLaunchKernelGGL((invert_stream_kernel<U, NTL, NTS>), dim3((unsigned)blocks), dim3(kBlock), 0,
+    const uint64_t tpb = (tiles + blocks - 1) / blocks;  // CHUNK: tiles per block
+    if (CHUNK && tpb) blocks = (tiles + tpb - 1) / tpb;
+    hipLaunchKernelGGL((invert_stream_kernel<U, NTL, NTS, CHUNK>), dim3((unsigned)blocks), dim3(kBlock), 0,
                        stream, reinterpret_cast<const u32x4 *>(bs) + c0,
                        reinterpret_cast<u32x4 *>(bd) + c0, m, src, dst, first ? h : 0u,
-                       bs + (n16 << 4), bd + (n16 << 4), last ? tail : 0u);
+                       bs + (n16 << 4), bd + (n16 << 4), last ? tail : 0u, tpb);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (last) break;
@@ -176,6 +185,8 @@ hipError_t launch_invert(const void *dsrc, void *ddst, size_t nbytes, const Laun
     case kVariantU2: return launch_stream<2, false, false>(s, d, nbytes, mb, stream);
     case kVariantU8: return launch_stream<8, false, false>(s, d, nbytes, mb, stream);
     case kVariantU1: return launch_stream<1, false, false>(s, d, nbytes, mb, stream);
+    case kVariantU4NTChunk: return launch_stream<4, true, true, true>(s, d, nbytes, mb, stream);
+    case kVariantU8NTChunk: return launch_stream<8, true, true, true>(s, d, nbytes, mb, stream);
     default: return hipErrorInvalidValue;
   }
 }
