@@ -143,9 +143,10 @@ class Codec {
   uint32_t emax_blocks_ = 0, emax_tiles_ = 0;
   uint64_t eblocks_ = 0, ebits_bytes_ = 0;
   DevBuf d_efr_, d_etab_, d_hdr_, d_esegs_, d_etsum_, d_etotals_, d_dcq_, d_acbits_, d_acscr_, d_bits_, d_pre_, d_bitoff_, d_stream_, d_ffcnt_,
-      d_out_, d_outsize_;
+      d_out_, d_outsize_, d_pack_;
 
-  HostBuf h_stage_, h_out_;
+  HostBuf h_stage_, h_out_, h_flag_;  // h_flag_: the speculative sync's unresolved flag
+  bool spec_check_ = false;           // run_decode queued that flag's read; check_decode tests it
   TaskPool pool_{4};
 };
 

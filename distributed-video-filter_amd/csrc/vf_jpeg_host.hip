@@ -776,12 +776,14 @@ int Codec::run_decode(int bgr, bool invert, std::string *err) {
     CK(hipMemsetAsync(d_unres_.p, 0, sizeof(uint32_t) * 16, s_));
     CK(dec_sync_spec(fr, n, dmax_wg_, d_us_.as<uint8_t>(), us_len, sb, d_exit_[0].as<uint64_t>(),
                      d_cnt_[0].as<uint32_t>(), d_unres_.as<uint32_t>(), s_));
-    uint32_t unres = 1;
-    CK(hipMemcpyAsync(&unres, d_unres_.p, sizeof unres, hipMemcpyDeviceToHost, s_));
-    CK(hipStreamSynchronize(s_));
-    if (!unres) flag = 0;  // resolved: exits / counts are in slot 0
+    // k_resolve reports a frame unresolved only when it has more workgroups than it stages,
+    // which prepare_decode already excludes (spec_ok_), so the rest is queued without a host
+    // round trip; the flag is read at check_decode's synchronisation and turned into an error.
+    CK(h_flag_.ensure(64));
+    CK(hipMemcpyAsync(h_flag_.p, d_unres_.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s_));
+    spec_check_ = true;
+    flag = 0;  // exits / counts are in slot 0
     ++spec_calls_;
-    if (unres) ++spec_fallbacks_;
     if (std::getenv("VF_JPEG_SYNC_STATS")) {
       uint32_t st[16];
       CK(hipMemcpy(st, d_unres_.p, sizeof st, hipMemcpyDeviceToHost));
@@ -849,6 +851,14 @@ int Codec::check_decode(std::string *err) {
   CK(hipMemcpyAsync(tot.data(), d_totals_.as<uint32_t>() + dn_, sizeof(uint32_t) * (size_t)dn_,
                     hipMemcpyDeviceToHost, s_));
   CK(hipStreamSynchronize(s_));
+  if (spec_check_) {
+    spec_check_ = false;
+    if (*h_flag_.as<uint32_t>()) {
+      ++spec_fallbacks_;
+      *err = "speculative Huffman synchronisation left a frame unresolved";
+      return kJpeg;
+    }
+  }
   for (int f = 0; f < dn_; ++f)
     if (tot[(size_t)f] < (uint32_t)dfr_[(size_t)f].g.nblocks) {
       *err = "frame " + std::to_string(f) + ": entropy-coded data ends after " + std::to_string(tot[(size_t)f]) +
@@ -925,6 +935,7 @@ int Codec::prepare_encode(const int *ws, const int *hs, const uint64_t *img_offs
   CK(d_stream_.ensure(bits));
   CK(d_ffcnt_.ensure(sizeof(uint32_t) * tiles));
   CK(d_out_.ensure(out));
+  CK(d_pack_.ensure(out));
   CK(d_outsize_.ensure(sizeof(uint64_t) * (size_t)n));
   // small tables go through pageable memcpy (synchronous w.r.t. the host buffers)
   CK(hipMemcpyAsync(d_efr_.p, efr_.data(), sizeof(EncFrame) * (size_t)n, hipMemcpyHostToDevice, s_));
@@ -957,6 +968,7 @@ int Codec::run_encode(int bgr, bool fastdct, std::string *err) {
               d_ffcnt_.as<uint32_t>(), d_etsum_.as<uint32_t>(), nff, false, s_));
   CK(enc_ff_write(fr, n, emax_tiles_, total_bits, d_stream_.as<uint8_t>(), d_ffcnt_.as<uint32_t>(), nff,
                   d_hdr_.as<uint8_t>(), d_out_.as<uint8_t>(), d_outsize_.as<uint64_t>(), s_));
+  CK(enc_compact(fr, n, d_outsize_.as<uint64_t>(), d_out_.as<uint8_t>(), d_pack_.as<uint8_t>(), s_));
   CK(hipEventRecord(ev_[8], s_));
   return kOk;
 }
@@ -981,12 +993,11 @@ int Codec::fetch_jpegs(uint8_t *const *outs, const size_t *caps, size_t *sizes, 
   CK(h_out_.ensure(total));
   uint64_t off = 0;
   std::vector<uint64_t> offs((size_t)n);
-  for (int f = 0; f < n; ++f) {
+  for (int f = 0; f < n; ++f) {  // k_compact's layout
     offs[(size_t)f] = off;
-    CK(hipMemcpyAsync(h_out_.as<uint8_t>() + off, d_out_.as<uint8_t>() + efr_[(size_t)f].out_off, sz[(size_t)f],
-                      hipMemcpyDeviceToHost, s_));
     off += align_up(sz[(size_t)f], 64);
   }
+  CK(hipMemcpyAsync(h_out_.p, d_pack_.p, total, hipMemcpyDeviceToHost, s_));
   const auto ta = std::chrono::steady_clock::now();
   CK(hipStreamSynchronize(s_));
   const auto tb = std::chrono::steady_clock::now();

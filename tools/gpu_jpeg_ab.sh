@@ -14,4 +14,4 @@ python -c "
 import json
 for v in ('head','new'):
     for l in open('gpurun_out/ab_%s.jsonl'%v):
-        d=json.loads(l); print(v, d['size'], d['gpu_resident_fps'], d['parity_vs_oracle'], d.get('stages_ms'))"
+        d=json.loads(l); print(v, d['size'], d['gpu_resident_fps'], 'h2h', d.get('host_to_host_fps'), d.get('host_to_host_2threads_fps'), d['parity_vs_oracle'], d.get('stages_ms'))"
