@@ -1095,12 +1095,9 @@ __device__ __forceinline__ uint32_t clamp255(int v) { return (uint32_t)(v < 0 ? 
 // 8 horizontally adjacent output pixels per thread: one 8-byte load per full-size plane,
 // the chroma samples they need (+1 neighbour each side) for 2x horizontal subsampling, and
 // three 8-byte stores of interleaved output when the row is 8-byte aligned.
-__global__ __launch_bounds__(256) void k_color(const DecFrame *fr, const uint8_t *planes, uint8_t *pix, int bgr,
-                                               int invert) {
-  const DecFrame &F = fr[blockIdx.z];
-  const Geom &g = F.g;
-  const int y = blockIdx.y, x0 = (blockIdx.x * 256 + threadIdx.x) * 8;
-  if (y >= g.h || x0 >= g.w) return;
+// The 8 output pixels of row y from x0 (24 bytes of interleaved output in o).
+__device__ __forceinline__ void color8(const DecFrame &F, const Geom &g, const uint8_t *__restrict__ planes, int y,
+                                       int x0, int bgr, int invert, uint8_t o[24]) {
   int v[3][8];
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
@@ -1154,7 +1151,6 @@ __global__ __launch_bounds__(256) void k_color(const DecFrame *fr, const uint8_t
         v[k][j] = up_sample(p, pw, dw, dh, he, ve, fancy && he <= 2 && ve <= 2, min(x0 + j, g.w - 1), y);
     }
   }
-  uint8_t o[24];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     uint32_t r, gg, b;
@@ -1175,6 +1171,10 @@ __global__ __launch_bounds__(256) void k_color(const DecFrame *fr, const uint8_t
     o[3 * j + 1] = (uint8_t)gg;
     o[3 * j + 2] = (uint8_t)(bgr ? r : b);
   }
+}
+
+__device__ __forceinline__ void color8_store(const DecFrame &F, const Geom &g, uint8_t *__restrict__ pix, int y,
+                                             int x0, const uint8_t o[24]) {
   uint8_t *dst = pix + F.out_off + ((size_t)y * g.w + x0) * 3;
   if (x0 + 8 <= g.w && ((uintptr_t)dst & 7) == 0) {
     uint2 *d2 = reinterpret_cast<uint2 *>(dst);
@@ -1192,6 +1192,22 @@ __global__ __launch_bounds__(256) void k_color(const DecFrame *fr, const uint8_t
     const int n = min(8, g.w - x0) * 3;
     for (int j = 0; j < n; ++j) dst[j] = o[j];
   }
+}
+
+// Two rows per workgroup: both rows' plane loads are issued before either row is stored (the
+// kernel is bound by load latency per wave; one short row per workgroup left it exposed).
+__global__ __launch_bounds__(256) void k_color(const DecFrame *fr, const uint8_t *__restrict__ planes,
+                                               uint8_t *__restrict__ pix, int bgr, int invert) {
+  const DecFrame &F = fr[blockIdx.z];
+  const Geom &g = F.g;
+  const int y0 = blockIdx.y * 2, x0 = (blockIdx.x * 256 + threadIdx.x) * 8;
+  if (y0 >= g.h || x0 >= g.w) return;
+  const bool two = y0 + 1 < g.h;
+  uint8_t o0[24], o1[24];
+  color8(F, g, planes, y0, x0, bgr, invert, o0);
+  color8(F, g, planes, two ? y0 + 1 : y0, x0, bgr, invert, o1);
+  color8_store(F, g, pix, y0, x0, o0);
+  if (two) color8_store(F, g, pix, y0 + 1, x0, o1);
 }
 
 // ---- encoder: colour + downsampling + FDCT + quantisation -----------------------------------
@@ -1885,7 +1901,7 @@ hipError_t dec_idct(const DecFrame *fr, int n, uint32_t max_blocks, const int16_
 hipError_t dec_color(const DecFrame *fr, int n, int max_w, int max_h, const uint8_t *planes, uint8_t *pix, int bgr,
                      int invert, hipStream_t s) {
   if (n <= 0 || max_w <= 0 || max_h <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_color, dim3((unsigned)((max_w + 2047) / 2048), (unsigned)max_h, (unsigned)n), dim3(256), 0, s,
+  hipLaunchKernelGGL(k_color, dim3((unsigned)((max_w + 2047) / 2048), (unsigned)((max_h + 1) / 2), (unsigned)n), dim3(256), 0, s,
                      fr, planes, pix, bgr, invert);
   return hipGetLastError();
 }
