@@ -1794,16 +1794,25 @@ __device__ __forceinline__ uint32_t ff_bytes(const uint8_t *s, uint32_t nbytes, 
 
 __global__ __launch_bounds__(256) void k_ff_count(const EncFrame *fr, const uint32_t *total_bits,
                                                   const uint8_t *stream, uint32_t *cnt) {
+  // Grid-stride over the frame's worst-case tiles: the stream fills only the first few (a
+  // 1080p q85 frame ~45 of ~1,500), so one workgroup per tile launched ~48 k workgroups per
+  // batch that mostly wrote a zero.  Tiles past the stream's end get their zero count here.
   const EncFrame &F = fr[blockIdx.y];
-  if (blockIdx.x >= F.ntiles_max) return;
   __shared__ uint32_t sh[4];
   const uint32_t tb = total_bits[blockIdx.y], nbytes = (tb + 7) >> 3;
-  uint8_t bytes[16];
-  const uint32_t i0 = blockIdx.x * kTile + threadIdx.x * 16;
-  const uint32_t n = i0 < nbytes ? ff_bytes(stream + F.bits_off, nbytes, tb, i0, bytes) : 0;
-  uint32_t tot;
-  (void)wg_excl_scan(n, sh, &tot);
-  if (threadIdx.x == 0) cnt[F.tile0 + blockIdx.x] = tot;
+  for (uint32_t t = blockIdx.x; t < F.ntiles_max; t += gridDim.x) {  // t is uniform
+    if (t * kTile < nbytes) {
+      uint8_t bytes[16];
+      const uint32_t i0 = t * kTile + threadIdx.x * 16;
+      const uint32_t n = i0 < nbytes ? ff_bytes(stream + F.bits_off, nbytes, tb, i0, bytes) : 0;
+      uint32_t tot;
+      (void)wg_excl_scan(n, sh, &tot);
+      if (threadIdx.x == 0) cnt[F.tile0 + t] = tot;
+      __syncthreads();  // sh is reused by the next tile's scan
+    } else if (threadIdx.x == 0) {
+      cnt[F.tile0 + t] = 0;
+    }
+  }
 }
 
 __global__ __launch_bounds__(256) void k_ff_write(const EncFrame *fr, const uint32_t *total_bits,
@@ -1812,26 +1821,28 @@ __global__ __launch_bounds__(256) void k_ff_write(const EncFrame *fr, const uint
   const EncFrame &F = fr[blockIdx.y];
   const uint32_t tb = total_bits[blockIdx.y], nbytes = (tb + 7) >> 3;
   const uint32_t ntiles = (nbytes + kTile - 1) / kTile;
-  if (blockIdx.x >= ntiles) return;
   __shared__ uint32_t sh[4];
   uint8_t *o = out + F.out_off;
-  if (blockIdx.x == 0)
-    for (uint32_t j = threadIdx.x; j < F.hdr_len; j += 256) o[j] = hdr[F.hdr_off + j];
-  uint8_t bytes[16];
-  const uint32_t i0 = blockIdx.x * kTile + threadIdx.x * 16;
-  const uint32_t n = i0 < nbytes ? ff_bytes(stream + F.bits_off, nbytes, tb, i0, bytes) : 0;
-  uint32_t tot;
-  uint64_t pos = (uint64_t)F.hdr_len + i0 + off[F.tile0 + blockIdx.x] + wg_excl_scan(n, sh, &tot);
-  for (int j = 0; j < 16; ++j) {
-    if (i0 + j >= nbytes) break;
-    o[pos++] = bytes[j];
-    if (bytes[j] == 0xFF) o[pos++] = 0;
-  }
-  if (blockIdx.x == ntiles - 1 && threadIdx.x == 0) {
-    const uint64_t size = (uint64_t)F.hdr_len + nbytes + nff[blockIdx.y] + 2;
-    o[size - 2] = 0xFF;
-    o[size - 1] = 0xD9;
-    out_size[blockIdx.y] = size;
+  for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {  // grid-stride over the stream's tiles
+    if (t == 0)
+      for (uint32_t j = threadIdx.x; j < F.hdr_len; j += 256) o[j] = hdr[F.hdr_off + j];
+    uint8_t bytes[16];
+    const uint32_t i0 = t * kTile + threadIdx.x * 16;
+    const uint32_t n = i0 < nbytes ? ff_bytes(stream + F.bits_off, nbytes, tb, i0, bytes) : 0;
+    uint32_t tot;
+    uint64_t pos = (uint64_t)F.hdr_len + i0 + off[F.tile0 + t] + wg_excl_scan(n, sh, &tot);
+    for (int j = 0; j < 16; ++j) {
+      if (i0 + j >= nbytes) break;
+      o[pos++] = bytes[j];
+      if (bytes[j] == 0xFF) o[pos++] = 0;
+    }
+    if (t == ntiles - 1 && threadIdx.x == 0) {
+      const uint64_t size = (uint64_t)F.hdr_len + nbytes + nff[blockIdx.y] + 2;
+      o[size - 2] = 0xFF;
+      o[size - 1] = 0xD9;
+      out_size[blockIdx.y] = size;
+    }
+    __syncthreads();  // sh is reused by the next tile's scan
   }
 }
 
@@ -1933,10 +1944,13 @@ hipError_t enc_pack(const EncFrame *fr, int n, uint32_t max_blocks, const uint32
   return hipGetLastError();
 }
 
+constexpr uint32_t kFFGrid = 64;  // stuffing workgroups per frame (grid-stride over tiles)
+
 hipError_t enc_ff_count(const EncFrame *fr, int n, uint32_t max_tiles, const uint32_t *total_bits,
                         const uint8_t *stream, uint32_t *tile_cnt, hipStream_t s) {
   if (n <= 0 || !max_tiles) return hipSuccess;
-  hipLaunchKernelGGL(k_ff_count, dim3(max_tiles, (unsigned)n), dim3(256), 0, s, fr, total_bits, stream, tile_cnt);
+  hipLaunchKernelGGL(k_ff_count, dim3(max_tiles < kFFGrid ? max_tiles : kFFGrid, (unsigned)n), dim3(256), 0, s, fr,
+                     total_bits, stream, tile_cnt);
   return hipGetLastError();
 }
 
@@ -1944,8 +1958,8 @@ hipError_t enc_ff_write(const EncFrame *fr, int n, uint32_t max_tiles, const uin
                         const uint8_t *stream, const uint32_t *tile_off, const uint32_t *nff, const uint8_t *hdr,
                         uint8_t *out, uint64_t *out_size, hipStream_t s) {
   if (n <= 0 || !max_tiles) return hipSuccess;
-  hipLaunchKernelGGL(k_ff_write, dim3(max_tiles, (unsigned)n), dim3(256), 0, s, fr, total_bits, stream, tile_off,
-                     nff, hdr, out, out_size);
+  hipLaunchKernelGGL(k_ff_write, dim3(max_tiles < kFFGrid ? max_tiles : kFFGrid, (unsigned)n), dim3(256), 0, s, fr,
+                     total_bits, stream, tile_off, nff, hdr, out, out_size);
   return hipGetLastError();
 }
 
