@@ -84,6 +84,19 @@ def test_invert_is_decode_not_encode(tj):
     assert tj.invert(jpgs[0]) == got[0]
 
 
+@pytest.mark.parametrize("out_ss", [0, 1, 2, 3, 4])
+def test_invert_samplings_and_edges(tj, out_ss):
+    """invert_batch for every output sampling over a batch of every input sampling, sizes
+    that are not whole MCUs (right / bottom edge replication), both upsamplings and both
+    forward DCTs."""
+    jpgs = [J.encode(_img("scene" if i % 2 else "noise", 200 + i, h, w), 80, J.TJPF_BGR, i % 5)
+            for i, (h, w) in enumerate(SIZES + [(31, 45), (480, 641), (23, 100)])]
+    for flags in (0, TJFLAG_FASTUPSAMPLE | TJFLAG_FASTDCT):
+        got = tj.invert_batch(jpgs, 85, out_ss, flags)
+        for g, j in zip(got, jpgs):
+            assert g == J.invert_jpeg(j, 85, out_ss, flags), (len(j), out_ss, flags)
+
+
 def test_invert_1080p_batch(tj):
     jpgs = [J.encode(_img("scene", s, 1080, 1920)) for s in range(3)]
     for g, j in zip(tj.invert_batch(jpgs), jpgs):
