@@ -995,14 +995,33 @@ __device__ __forceinline__ void block_pos(const Geom &g, uint32_t b, uint32_t *k
   *by = (mcu / (uint32_t)g.mcux) * (uint32_t)g.mv[*k] + (uint32_t)g.byo[c];
 }
 
-// 8 lanes per block, 32 blocks per workgroup
+// Measured (tools/gpu_jpeg_variants.sh, profiles/r01_jpeg_idct_variants.txt; dc + idct ms at
+// 1080p / 4K): 1 block per lane group with separate LDS for the two passes 0.200 / 0.73 (the
+// earlier kernel); aliased 0.202 / 0.74; 2 blocks not aliased 0.21 / 0.76; 2 blocks aliased
+// 0.170 / 0.61; 3 aliased 0.197 / 0.71; 4 aliased 0.205 / 0.74.
+#ifndef VF_IDCT_NB
+#define VF_IDCT_NB 2
+#endif
+#ifndef VF_IDCT_ALIAS
+#define VF_IDCT_ALIAS 1
+#endif
+constexpr int kIdctNb = VF_IDCT_NB;         // blocks per 8-lane group
+constexpr int kIdctBlocks = 32 * kIdctNb;   // blocks per workgroup
+
+// 8 lanes per block, kIdctNb blocks per 8-lane group: both blocks' coefficient loads are issued
+// before either is transformed, and the column pass's output reuses the block's LDS row (one
+// more barrier, half the LDS: 18.4 KB per workgroup for 64 blocks)
 __global__ __launch_bounds__(256) void k_idct(const DecFrame *fr, const int16_t *coef, const int32_t *dcseq,
                                               uint8_t *planes) {
   const DecFrame &F = fr[blockIdx.y];
   const Geom &g = F.g;
-  if (blockIdx.x * 32 >= (uint32_t)g.nblocks) return;
-  __shared__ int32_t blkv[32][72];  // rows padded to 72: a wave's 8 column reads hit 64 banks
-  __shared__ int32_t ws[32][8][9];
+  if (blockIdx.x * kIdctBlocks >= (uint32_t)g.nblocks) return;
+  __shared__ int32_t blkv[kIdctBlocks][72];  // rows padded to 72: a wave's 8 column reads hit 64 banks
+#if VF_IDCT_ALIAS
+  int32_t(*wsb)[72] = blkv;                 // column-pass output reuses the block's row after a barrier
+#else
+  __shared__ int32_t wsb[kIdctBlocks][72];  // [8][9] per block
+#endif
   __shared__ int32_t s_q[3][64];     // dequantisation, natural order
   __shared__ uint8_t s_nat[64];      // zigzag -> natural
   __shared__ uint32_t s_pos[kMaxBpm];  // block-in-MCU -> component | x << 8 | y << 16 (blocks)
@@ -1020,41 +1039,67 @@ __global__ __launch_bounds__(256) void k_idct(const DecFrame *fr, const int16_t 
   const uint64_t po[3] = {F.plane_off[0], F.plane_off[1], F.plane_off[2]};
   const uint32_t pw[3] = {(uint32_t)g.pw[0], (uint32_t)g.pw[1], (uint32_t)g.pw[2]};
   const uint32_t slot = t >> 3, r = t & 7;
-  const uint32_t b = blockIdx.x * 32 + slot;
-  const bool valid = b < (uint32_t)g.nblocks;
-  const uint32_t mcu = b / (uint32_t)g.bpm, c = b - mcu * (uint32_t)g.bpm;
-  const uint32_t ps = valid ? s_pos[c] : 0u;
-  const uint32_t k = ps & 0xFF;
-  const uint32_t bx = (mcu % (uint32_t)g.mcux) * HuffGeom::sel(mh, k) + ((ps >> 8) & 0xFF);
-  const uint32_t by = (mcu / (uint32_t)g.mcux) * HuffGeom::sel(mv, k) + (ps >> 16);
-  if (valid) {
-    const uint4 raw = *reinterpret_cast<const uint4 *>(coef + (F.blk0 + b) * 64 + r * 8);
-    const int16_t *v = reinterpret_cast<const int16_t *>(&raw);
-    int32_t dc = 0;
-    if (r == 0)
-      dc = dcseq[HuffGeom::sel(dcb, k) + (uint64_t)mcu * (HuffGeom::sel(mh, k) * HuffGeom::sel(mv, k)) +
-                 (c - HuffGeom::sel(cf, k))];
+  bool valid[kIdctNb];
+  uint32_t kk[kIdctNb], bxs[kIdctNb], bys[kIdctNb];
+  uint4 raw[kIdctNb];
+  int32_t dc[kIdctNb];
+#pragma unroll
+  for (int h = 0; h < kIdctNb; ++h) {
+    const uint32_t b = blockIdx.x * kIdctBlocks + h * 32 + slot;
+    valid[h] = b < (uint32_t)g.nblocks;
+    const uint32_t mcu = b / (uint32_t)g.bpm, c = b - mcu * (uint32_t)g.bpm;
+    const uint32_t ps = valid[h] ? s_pos[c] : 0u;
+    const uint32_t k = ps & 0xFF;
+    kk[h] = k;
+    bxs[h] = (mcu % (uint32_t)g.mcux) * HuffGeom::sel(mh, k) + ((ps >> 8) & 0xFF);
+    bys[h] = (mcu / (uint32_t)g.mcux) * HuffGeom::sel(mv, k) + (ps >> 16);
+    raw[h] = make_uint4(0, 0, 0, 0);
+    dc[h] = 0;
+    if (valid[h]) {
+      raw[h] = *reinterpret_cast<const uint4 *>(coef + (F.blk0 + b) * 64 + r * 8);
+      if (r == 0)
+        dc[h] = dcseq[HuffGeom::sel(dcb, k) + (uint64_t)mcu * (HuffGeom::sel(mh, k) * HuffGeom::sel(mv, k)) +
+                      (c - HuffGeom::sel(cf, k))];
+    }
+  }
+#pragma unroll
+  for (int h = 0; h < kIdctNb; ++h) {
+    if (!valid[h]) continue;
+    const uint32_t qw[4] = {raw[h].x, raw[h].y, raw[h].z, raw[h].w};
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const uint32_t zz = r * 8 + j, n = s_nat[zz];
-      const int32_t x = zz == 0 ? (int32_t)(int16_t)dc : (int32_t)v[j];
-      blkv[slot][n] = x * s_q[k][n];
+      const int32_t v = (int32_t)(int16_t)(qw[j >> 1] >> (16 * (j & 1)));
+      const int32_t x = zz == 0 ? (int32_t)(int16_t)dc[h] : v;
+      blkv[h * 32 + slot][n] = x * s_q[kk[h]][n];
     }
   }
   __syncthreads();
-  if (valid) {  // pass 1: column r
-    int32_t in[8], out[8];
+  int32_t col[kIdctNb][8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) in[i] = blkv[slot][i * 8 + r];
-    idct_line(in, out, 11);
+  for (int h = 0; h < kIdctNb; ++h) {  // pass 1: column r
+    if (!valid[h]) continue;
+    int32_t in[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) ws[slot][i][r] = out[i];
+    for (int i = 0; i < 8; ++i) in[i] = blkv[h * 32 + slot][i * 8 + r];
+    idct_line(in, col[h], 11);
+  }
+#if VF_IDCT_ALIAS
+  __syncthreads();
+#endif
+#pragma unroll
+  for (int h = 0; h < kIdctNb; ++h) {
+    if (!valid[h]) continue;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) wsb[h * 32 + slot][i * 9 + r] = col[h][i];
   }
   __syncthreads();
-  if (valid) {  // pass 2: row r
+#pragma unroll
+  for (int h = 0; h < kIdctNb; ++h) {  // pass 2: row r
+    if (!valid[h]) continue;
     int32_t in[8], out[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) in[i] = ws[slot][r][i];
+    for (int i = 0; i < 8; ++i) in[i] = wsb[h * 32 + slot][r * 9 + i];
     idct_line(in, out, 18);
     uint32_t lo = 0, hi = 0;
 #pragma unroll
@@ -1062,7 +1107,8 @@ __global__ __launch_bounds__(256) void k_idct(const DecFrame *fr, const int16_t 
       lo |= idct_limit(out[i]) << (8 * i);
       hi |= idct_limit(out[i + 4]) << (8 * i);
     }
-    uint8_t *p = planes + HuffGeom::sel(po, k) + (uint64_t)(by * 8 + r) * HuffGeom::sel(pw, k) + bx * 8;
+    const uint32_t k = kk[h];
+    uint8_t *p = planes + HuffGeom::sel(po, k) + (uint64_t)(bys[h] * 8 + r) * HuffGeom::sel(pw, k) + bxs[h] * 8;
     *reinterpret_cast<uint2 *>(p) = make_uint2(lo, hi);
   }
 }
@@ -1905,7 +1951,8 @@ hipError_t dec_write(const DecFrame *fr, int n, uint32_t max_sub, const uint8_t 
 hipError_t dec_idct(const DecFrame *fr, int n, uint32_t max_blocks, const int16_t *coef, const int32_t *dcseq,
                     uint8_t *planes, hipStream_t s) {
   if (n <= 0 || !max_blocks) return hipSuccess;
-  hipLaunchKernelGGL(k_idct, dim3((max_blocks + 31) / 32, (unsigned)n), dim3(256), 0, s, fr, coef, dcseq, planes);
+  hipLaunchKernelGGL(k_idct, dim3((max_blocks + kIdctBlocks - 1) / kIdctBlocks, (unsigned)n), dim3(256), 0, s, fr,
+                     coef, dcseq, planes);
   return hipGetLastError();
 }
 
