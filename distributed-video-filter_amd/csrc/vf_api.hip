@@ -59,6 +59,7 @@ struct vf_ctx {
   vf::Engine *engine = nullptr;
   int hip = 0;
   char msg[512] = "no error";
+  std::mutex err_mu;  // msg / hip: JPEG calls on one context may fail on two threads at once
   // results of the last host->host job waited on (vf_elapsed_ms / vf_last_timeline)
   float last_kernel_ms = 0.f;
   std::vector<vf::ChunkTime> timeline;
@@ -83,6 +84,7 @@ int set_err(vf_ctx *ctx, int status, int hip, const char *fmt, ...) {
   t.hip = hip;
   std::snprintf(t.msg, sizeof t.msg, "%s", buf);
   if (ctx) {
+    std::lock_guard<std::mutex> lk(ctx->err_mu);
     ctx->hip = hip;
     std::snprintf(ctx->msg, sizeof ctx->msg, "%s", buf);
   }
@@ -174,6 +176,19 @@ VF_EXPORT int vf_device_count(int *out_count) {
     n = 0;
   }
   *out_count = n;
+  return VF_OK;
+}
+
+VF_EXPORT int vf_device_pci_bus_id(int device, char *buf, int len) {
+  if (!buf || len < 13) return set_err(nullptr, VF_E_INVALID, 0, "vf_device_pci_bus_id: buffer too small");
+  buf[0] = 0;
+  int ndev = 0;
+  vf_device_count(&ndev);
+  if (device < 0 || device >= ndev)
+    return set_err(nullptr, VF_E_NODEVICE, 0, "vf_device_pci_bus_id: device %d not available (%d visible)",
+                   device, ndev);
+  hipError_t e = hipDeviceGetPCIBusId(buf, len, device);
+  if (e != hipSuccess) return fail_hip(nullptr, e, "hipDeviceGetPCIBusId", __LINE__);
   return VF_OK;
 }
 

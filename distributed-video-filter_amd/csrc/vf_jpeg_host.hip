@@ -101,8 +101,11 @@ void code_table(const uint8_t bits[17], const uint8_t *vals, uint32_t *out, int 
   }
 }
 
-// jdhuff.c jpeg_make_d_derived_tbl + a kLook-bit lookahead
-bool decode_table(const uint8_t bits[17], const uint8_t *vals, HuffDec *t) {
+// jdhuff.c jpeg_make_d_derived_tbl + a kLook-bit lookahead.  Rejects what jdhuff.c rejects
+// with JERR_BAD_HUFF_TABLE: more than 256 symbols, a code that does not fit its length or is
+// all ones (code + 1 >= 2^l; checked per code, BEFORE the lookahead write it would overrun),
+// and DC symbols above 15.
+bool decode_table(const uint8_t bits[17], const uint8_t *vals, bool dc, HuffDec *t) {
   std::memset(t, 0, sizeof *t);
   int p = 0;
   uint32_t code = 0;
@@ -111,6 +114,8 @@ bool decode_table(const uint8_t bits[17], const uint8_t *vals, HuffDec *t) {
       t->valoff[l] = p - (int32_t)code;
       for (int i = 0; i < bits[l]; ++i, ++p, ++code) {
         if (p >= 256) return false;
+        if (code + 1 >= (1u << l)) return false;  // over-subscribed, or the all-ones code
+        if (dc && vals[p] > 15) return false;
         t->vals[p] = vals[p];
         if (l <= kLook) {
           const uint32_t base = code << (kLook - l);
@@ -118,7 +123,6 @@ bool decode_table(const uint8_t bits[17], const uint8_t *vals, HuffDec *t) {
         }
       }
       t->maxcode[l] = (int32_t)code - 1;
-      if (code > (1u << l)) return false;  // over-subscribed table
     } else {
       t->maxcode[l] = -1;
     }
@@ -606,8 +610,8 @@ int Codec::prepare_decode(const uint8_t *const *jpegs, const size_t *sizes, int 
     }
     for (int c = 0; c < P.ncomp; ++c) {
       std::memcpy(F.q[c], P.qt[P.tq[c]], sizeof F.q[c]);
-      if (!decode_table(P.dcbits[P.td[c]], P.dcvals[P.td[c]], &F.dc[c]) ||
-          !decode_table(P.acbits[P.ta[c]], P.acvals[P.ta[c]], &F.ac[c])) {
+      if (!decode_table(P.dcbits[P.td[c]], P.dcvals[P.td[c]], true, &F.dc[c]) ||
+          !decode_table(P.acbits[P.ta[c]], P.acvals[P.ta[c]], false, &F.ac[c])) {
         e = "bad Huffman table";
         return;
       }

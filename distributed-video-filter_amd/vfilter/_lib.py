@@ -38,6 +38,7 @@ SIGNATURES = {
     "vf_get_abi_version": (ctypes.c_int, []),
     "vf_status_string": (ctypes.c_char_p, [ctypes.c_int]),
     "vf_device_count": (ctypes.c_int, [_c_int_p]),
+    "vf_device_pci_bus_id": (ctypes.c_int, [ctypes.c_int, ctypes.c_char_p, ctypes.c_int]),
     "vf_create": (ctypes.c_int, [ctypes.c_int, _sz, ctypes.c_int, ctypes.POINTER(_vp)]),
     "vf_destroy": (ctypes.c_int, [_vp]),
     "vf_last_error": (ctypes.c_char_p, [_vp]),
@@ -125,6 +126,16 @@ def device_count() -> int:
     return n.value
 
 
+def device_pci_bus_id(device: int) -> str:
+    """PCI address ("dddd:bb:dd.f") of HIP device ``device``."""
+    lib = load_library()
+    buf = ctypes.create_string_buffer(64)
+    st = lib.vf_device_pci_bus_id(int(device), buf, 64)
+    if st != VF_OK:
+        raise VFilterError(lib.vf_last_error(None).decode(), st, lib.vf_last_hip_error(None))
+    return buf.value.decode()
+
+
 def _addr(a) -> int:
     """Address of a numpy array / writable buffer / int pointer."""
     if isinstance(a, int):
@@ -153,9 +164,10 @@ class Context:
 
     # -- plumbing -----------------------------------------------------------------------
     def _check(self, st: int) -> None:
+        # the calling thread's own error record: JPEG calls may fail on two threads at once
+        # on one context, and the context's record holds whichever failed last
         if st != VF_OK:
-            raise VFilterError(self._lib.vf_last_error(self._ctx).decode(), st,
-                               self._lib.vf_last_hip_error(self._ctx))
+            raise VFilterError(self._lib.vf_last_error(None).decode(), st, self._lib.vf_last_hip_error(None))
 
     @property
     def handle(self) -> int:

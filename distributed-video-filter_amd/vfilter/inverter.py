@@ -81,8 +81,10 @@ class InverterWorker(Worker):
 
     # -- a dispatched batch: one gathered device call ------------------------------------
     def process_batch(self, frames: Sequence, metas: Sequence[wire.FrameMeta], outs: Sequence) -> List:
-        if self.jpeg and self.delay <= 0 and all(o is None for o in outs):
-            try:  # the whole batch in one fused GPU pass
+        if self.jpeg and self.delay <= 0:
+            # the whole batch in one fused GPU pass; results are JPEGs of their own size (the
+            # loop puts ring frames' results into their slots, see Worker._finish_job)
+            try:
                 return self.jpeg.invert_batch(list(frames))
             except Exception:  # retry frame by frame so a bad frame fails alone (worker.py:74-76)
                 return super().process_batch(frames, metas, outs)
@@ -112,7 +114,7 @@ class InverterWorker(Worker):
         context's engine thread streams consecutive batches through the GPU back to back.
         Ring frames (page-locked) are DMA'd in place; socket payloads are staged.  JPEG
         batches go to a 2-thread executor (fused decode -> invert -> encode per batch)."""
-        if self.jpeg and self.delay <= 0 and all(o is None for o in outs):
+        if self.jpeg and self.delay <= 0:
             return ("jpeg", self._jpeg_pool().submit(self.process_batch, list(frames), metas, outs), len(frames))
         if self.jpeg or self.delay > 0:
             return super().submit_batch(frames, metas, outs)

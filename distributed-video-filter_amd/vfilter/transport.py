@@ -136,6 +136,8 @@ class _Listener:
                 conn.close()
             except OSError:
                 pass
+            if not self._closed:
+                self.inbox.put((pid, None))  # disconnect notice (ZeroMQ gives none; see RouterEnd.recv)
 
     def poll(self, timeout_ms: int) -> bool:
         if not self.inbox.empty():
@@ -251,7 +253,9 @@ class RouterEnd:
     def poll(self, timeout_ms: int) -> bool:
         return bool(self.sock.poll(timeout_ms))
 
-    def recv(self) -> Tuple[bytes, List[bytes]]:
+    def recv(self) -> Tuple[bytes, Optional[List[bytes]]]:
+        """(peer, parts); parts is None when "tcp" saw the peer disconnect (the distributor
+        then re-queues that worker's frames at once instead of waiting for their deadline)."""
         if self.kind == "zmq":
             parts = self.sock.recv_multipart(self._zmq.NOBLOCK)
             return parts[0], parts[1:]
@@ -292,7 +296,7 @@ class PullEnd:
         if self.kind == "zmq":
             return self.sock.recv_multipart(self._zmq.NOBLOCK)
         got = self.sock.recv(0)
-        if got is None:
+        if got is None or got[1] is None:  # nothing, or a PUSH peer's disconnect notice
             raise BlockingIOError
         return got[1]
 

@@ -10,16 +10,20 @@ v0 — the reference's own messages, byte for byte:
 
 v1 — shape-carrying and batched.  Every v1 message starts with a
 tag part that can never be a decimal index string, so a v1 peer can always tell v0 from v1:
-  request  ["READY1", json{"credit": k, "shm": bool}]
+  request  ["READY1", json{"credit": k, "shm": bool, "wid": worker id, "numa": node of its GPU}]
   dispatch ["FRAMES1", json{"frames": [{"index": i, "shape": [h, w, c] | null, "nbytes": n,
                                         "slot": s | null}, ...],
                              "ring": {"name": shm name, "slot_bytes": n} (if any slot)},
             frame_0, ..., frame_{k-1}]
            (frames whose "slot" is set travel in the shared-memory ring and have no part)
-  result   ["RESULT1", json{"pid": p, "frames": [{"index", "shape", "nbytes", "slot",
-                                                 "start", "end", "error"}...],
+  result   ["RESULT1", json{"pid": p, "wid": worker id, "frames": [{"index", "shape", "nbytes",
+                                                 "slot", "start", "end", "error"}...],
                             "spans": [{"name", "begin", "end", "bytes"}...] (GPU timeline)},
             out_0, ...]
+  "wid" ties a result to the request stream it answers (the distributor tracks every dispatched
+  frame per worker, re-queues a lost worker's frames and frees their ring slots); "numa" lets
+  the distributor place the worker's ring slice on its GPU's NUMA node.  A result's "nbytes" is
+  the RESULT's length (a JPEG differs from its input's).
 A worker run with protocol v0 against the reference distributor sends "READY" and reads 2
 parts; this build's distributor answers a bare "READY" with a v0 dispatch.  Either side of the reference can
 therefore be swapped for this build's independently.
@@ -66,6 +70,8 @@ class Request:
     version: int
     credit: int = 1
     shm: bool = False
+    wid: Optional[str] = None
+    numa: Optional[int] = None
 
 
 @dataclass
@@ -82,6 +88,7 @@ class Result:
     metas: List[FrameMeta]
     payloads: List[Optional[bytes]] = field(default_factory=list)
     version: int = 1
+    wid: Optional[str] = None
     # GPU spans of the batch: [{"name": "H2D"|"kernel"|"D2H", "begin": t, "end": t, "bytes": n}]
     # (wall-clock seconds, like start/end), for the distributor's Perfetto export
     spans: List[dict] = field(default_factory=list)
@@ -89,10 +96,16 @@ class Result:
 
 # ---- requests -------------------------------------------------------------------------
 
-def encode_request(credit: int = 1, shm: bool = False, version: int = 1) -> List[bytes]:
+def encode_request(credit: int = 1, shm: bool = False, version: int = 1, wid: Optional[str] = None,
+                   numa: Optional[int] = None) -> List[bytes]:
     if version == 0:
         return [READY_V0]
-    return [READY_V1, json.dumps({"credit": int(credit), "shm": bool(shm)}).encode()]
+    d = {"credit": int(credit), "shm": bool(shm)}
+    if wid is not None:
+        d["wid"] = str(wid)
+    if numa is not None:
+        d["numa"] = int(numa)
+    return [READY_V1, json.dumps(d).encode()]
 
 
 def decode_request(parts: Sequence[bytes]) -> Optional[Request]:
@@ -103,7 +116,10 @@ def decode_request(parts: Sequence[bytes]) -> Optional[Request]:
         return Request(version=0)
     if tag == READY_V1 and len(parts) >= 2:
         d = json.loads(bytes(parts[1]))
-        return Request(version=1, credit=max(1, int(d.get("credit", 1))), shm=bool(d.get("shm", False)))
+        numa = d.get("numa")
+        return Request(version=1, credit=max(1, int(d.get("credit", 1))), shm=bool(d.get("shm", False)),
+                       wid=None if d.get("wid") is None else str(d["wid"]),
+                       numa=None if numa is None else int(numa))
     return None
 
 
@@ -142,8 +158,11 @@ def encode_result_v0(index: int, pid, start: float, end: float, frame) -> List:
     return [str(index).encode(), str(pid).encode(), str(start).encode(), str(end).encode(), frame]
 
 
-def encode_result(pid, metas: Sequence[FrameMeta], payloads: Sequence, spans: Optional[List[dict]] = None) -> List:
+def encode_result(pid, metas: Sequence[FrameMeta], payloads: Sequence, spans: Optional[List[dict]] = None,
+                  wid: Optional[str] = None) -> List:
     d = {"pid": str(pid), "frames": [m.to_json() for m in metas]}
+    if wid is not None:
+        d["wid"] = str(wid)
     if spans:
         d["spans"] = spans
     head = json.dumps(d).encode()
@@ -162,4 +181,5 @@ def decode_result(parts: Sequence) -> Result:
     metas = [FrameMeta.from_json(x) for x in d["frames"]]
     it = iter(parts[2:])
     payloads = [None if (m.slot is not None or m.error is not None) else next(it) for m in metas]
-    return Result(str(d["pid"]), metas, payloads, version=1, spans=list(d.get("spans", [])))
+    return Result(str(d["pid"]), metas, payloads, version=1, spans=list(d.get("spans", [])),
+                  wid=None if d.get("wid") is None else str(d["wid"]))

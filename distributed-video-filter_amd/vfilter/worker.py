@@ -32,6 +32,13 @@ from . import wire
 from .shm import FrameRing
 
 
+def _same_buffer(r, o) -> bool:
+    """True when result ``r`` is the ring output view ``o`` (written in place)."""
+    if o is None or not isinstance(r, np.ndarray):
+        return False
+    return r.nbytes == o.nbytes and (r.nbytes == 0 or r.ctypes.data == o.ctypes.data)
+
+
 class Worker:
     def __init__(self, host: str = "localhost", distribute_port: int = 5555, collect_port: int = 5556, *,
                  transport: str = "auto", protocol: str = "v1", batch: int = 1, depth: int = 0,
@@ -69,16 +76,19 @@ class Worker:
         raise NotImplementedError("Subclasses must implement __call__ method")
 
     def process_batch(self, frames: Sequence, metas: Sequence[wire.FrameMeta], outs: Sequence) -> List:
-        """Filter a batch.  ``outs[i]`` is a writable buffer for frame i's result when the
-        frame lives in the shared-memory ring, else None.  Returns, per frame, the result
-        (bytes-like; ignored where ``outs[i]`` was given and filled in place) or an
-        Exception instance for a frame that failed.  Default: the plugin, frame by frame."""
+        """Filter a batch.  ``outs[i]`` is a writable buffer of the input's size for frame i's
+        result when the frame lives in the shared-memory ring, else None.  Returns, per frame,
+        the result or an Exception instance for a frame that failed.  A result written in
+        place is returned as ``outs[i]`` itself; any other bytes-like result (e.g. a JPEG,
+        whose size differs from its input's) is copied into the slot's output half by the
+        loop when it fits, else sent as a socket payload.  Default: the plugin, frame by frame."""
         results = []
         for f, o in zip(frames, outs):
             try:
                 r = self(f)
-                if o is not None:
+                if o is not None and memoryview(r).nbytes == o.nbytes:
                     o[:] = np.frombuffer(r, dtype=np.uint8)
+                    r = o  # in place; a result of another size goes back as its own buffer
                 results.append(r)
             except Exception as e:  # worker.py:74-76
                 results.append(e)
@@ -197,26 +207,38 @@ class Worker:
                 outs.append(None)
         if self.verbose:
             print(f"Processing frames {[m.index for m in d.metas]}")
-        return d, start_time, self.submit_batch(frames, d.metas, outs)
+        return d, start_time, self.submit_batch(frames, d.metas, outs), ring, outs
 
     def _finish_job(self, job, block: bool) -> bool:
-        d, start_time, handle = job
+        d, start_time, handle, ring, outs = job
         got = self.poll_batch(handle, block)
         if got is None:
             return False
         results, spans = got
         end_time = time.time()
         metas, payloads = [], []
-        for m, r in zip(d.metas, results):
+        for m, r, o in zip(d.metas, results, outs):
             om = wire.FrameMeta(index=m.index, nbytes=m.nbytes, shape=m.shape, slot=m.slot,
                                 start=start_time, end=end_time)
+            payload = None
             if isinstance(r, Exception):
                 om.error = f"{type(r).__name__}: {r}"
                 self.errors += 1
                 print(f"Error in worker: frame {m.index}: {r}")
-                payloads.append(None)
-            else:
-                payloads.append(None if m.slot is not None else r)
+            elif m.slot is None:
+                payload = r
+            elif not _same_buffer(r, o):
+                # a result of its own size (JPEG): into the slot's output half when it fits,
+                # else back over the socket; either way the result carries its length
+                rb = np.frombuffer(r, dtype=np.uint8)
+                om.nbytes = rb.nbytes
+                om.shape = None
+                if rb.nbytes <= ring.slot_bytes:
+                    ring.out_view(m.slot, rb.nbytes)[:] = rb
+                else:
+                    om.slot = None
+                    payload = r
+            payloads.append(payload)
             metas.append(om)
         self.collect_socket.send(wire.encode_result(self.process_id, metas, payloads, spans))
         self.frames_processed += len(metas)

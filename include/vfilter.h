@@ -61,6 +61,12 @@ const char *vf_status_string(int status);
 /* Number of visible HIP devices (0 when there is no GPU; never fails for that). */
 int vf_device_count(int *out_count);
 
+/* PCI address of HIP device `device` ("dddd:bb:dd.f", from hipDeviceGetPCIBusId) in `buf`
+ * (`len` >= 13 bytes).  The host side reads the device's NUMA node from sysfs with it and
+ * places that GPU worker's shared-memory frame ring on the node (the reference's workers keep
+ * no host buffers of their own: frames arrive in pyzmq messages, worker.py:50-51). */
+int vf_device_pci_bus_id(int device, char *buf, int len);
+
 /* Create a context on `device`.  Allocates the pinned host staging ring and device slot
  * buffers used by the host->host entry points (VF_SLOTS slots, default 4, each of
  * min(`max_frame_bytes` x `max_batch`, 16 MiB) bytes; VF_SLOT_BYTES overrides, clamped to
@@ -71,7 +77,10 @@ int vf_create(int device, size_t max_frame_bytes, int max_batch, vf_ctx **out);
 /* Destroy a context (NULL is allowed).  Synchronises its streams first. */
 int vf_destroy(vf_ctx *ctx);
 
-/* Last error message of `ctx`, or of the calling thread when ctx is NULL.  Never NULL. */
+/* Last error message of `ctx`, or of the calling thread when ctx is NULL.  Never NULL.
+ * Every failing call also records its message for the calling thread, so a caller that
+ * shares one context between threads (JPEG calls lease separate codecs) should read
+ * vf_last_error(NULL) on the thread that saw the failure. */
 const char *vf_last_error(const vf_ctx *ctx);
 
 /* Last hipError_t recorded by `ctx` (0 if none), or by the calling thread when ctx is NULL. */

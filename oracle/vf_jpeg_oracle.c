@@ -621,8 +621,9 @@ typedef struct {
   int defined;
 } dec_huff_t;
 
-/* jdhuff.c jpeg_make_d_derived_tbl (canonical decode part) */
-static int make_dec_table(const uint8_t bits[17], const uint8_t *vals, int nvals, dec_huff_t *t) {
+/* jdhuff.c jpeg_make_d_derived_tbl (canonical decode part; a DC table's symbols must be
+ * 0..15, as jdhuff.c's isDC check requires) */
+static int make_dec_table(const uint8_t bits[17], const uint8_t *vals, int nvals, int dc, dec_huff_t *t) {
   uint8_t huffsize[257];
   uint32_t huffcode[257];
   int p = 0;
@@ -632,6 +633,9 @@ static int make_dec_table(const uint8_t bits[17], const uint8_t *vals, int nvals
       huffsize[p++] = (uint8_t)l;
     }
   if (p != nvals) return -1;
+  if (dc)
+    for (int i = 0; i < nvals; ++i)
+      if (vals[i] > 15) return -1;
   huffsize[p] = 0;
   uint32_t code = 0;
   int si = huffsize[0];
@@ -957,12 +961,12 @@ int vfo_jpeg_decode(const uint8_t *jpg, size_t n, int pixel_format, int fast_ups
     int cnt = 0;
     for (int l = 1; l <= 16; ++l) cnt += info.dc_bits[info.td[c]][l];
     if (!dct[info.td[c]].defined &&
-        make_dec_table(info.dc_bits[info.td[c]], info.dc_vals[info.td[c]], cnt, &dct[info.td[c]]))
+        make_dec_table(info.dc_bits[info.td[c]], info.dc_vals[info.td[c]], cnt, 1, &dct[info.td[c]]))
       return VFO_JE_BAD;
     cnt = 0;
     for (int l = 1; l <= 16; ++l) cnt += info.ac_bits[info.ta[c]][l];
     if (!act[info.ta[c]].defined &&
-        make_dec_table(info.ac_bits[info.ta[c]], info.ac_vals[info.ta[c]], cnt, &act[info.ta[c]]))
+        make_dec_table(info.ac_bits[info.ta[c]], info.ac_vals[info.ta[c]], cnt, 0, &act[info.ta[c]]))
       return VFO_JE_BAD;
   }
   /* component planes (whole blocks of the interleaved MCU grid) */

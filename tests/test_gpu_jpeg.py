@@ -134,6 +134,23 @@ def test_bad_streams_raise(tj):
     assert np.array_equal(tj.decode(good), J.decode(good))
 
 
+def test_bad_huffman_tables_raise(tj):
+    """Tables libjpeg-turbo's jdhuff.c refuses (pinned in test_jpeg_oracle.py): over-subscribed
+    lengths (255 one-bit codes used to overrun the 1 KiB lookahead table), all-ones codes and
+    DC symbols above 15 -> VF_E_JPEG from decode, invert and a batch (only the bad frame)."""
+    from _jpeg_craft import bad_tables, tables_of, with_table
+    good = J.encode(_img("scene", 3, 48, 64))
+    for seg in tables_of(good).values():
+        assert np.array_equal(tj.decode(with_table(good, seg)), J.decode(good))
+    for name, seg in bad_tables():
+        bad = with_table(good, seg)
+        with pytest.raises(VFilterError):
+            tj.decode(bad)
+        with pytest.raises(VFilterError):
+            tj.invert(bad)
+    assert tj.invert(good) == J.invert_jpeg(good)
+
+
 def test_concurrent_calls_lease_separate_codecs(tj):
     """Two host threads call invert_batch at once (what the JPEG worker's 2-thread submit
     does): each call leases its own codec, stream and buffers, so both stay bit-exact."""

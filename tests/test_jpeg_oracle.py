@@ -133,3 +133,25 @@ def test_product_synthetic_scene_matches_oracle_generator():
     from vfilter.synthetic import synthetic_scene
     for seed, (h, w) in enumerate([(17, 13), (480, 640)]):
         assert np.array_equal(synthetic_scene(seed, h, w), J.synthetic_scene(seed, h, w))
+
+
+def test_bad_huffman_tables_rejected_like_libjpeg():
+    """Malformed DHT tables (tests/_jpeg_craft.py) are refused by libjpeg-turbo 2.1.2's
+    jdhuff.c (JERR_BAD_HUFF_TABLE) and by the oracle; re-inserting the stream's own tables
+    (a legal redefinition) still decodes identically in both.  The GPU codec is held to the
+    same cases in tests/test_gpu_jpeg.py."""
+    from _jpeg_craft import bad_tables, tables_of, with_table
+    good = J.encode(_img("scene", 3, 48, 64))
+    want = J.decode(good)
+    for seg in tables_of(good).values():
+        same = with_table(good, seg)
+        assert np.array_equal(J.decode(same), want)
+        if LIBJPEG:
+            assert np.array_equal(J.libjpeg_decode(same), want)
+    for name, seg in bad_tables():
+        bad = with_table(good, seg)
+        with pytest.raises(ValueError):
+            J.decode(bad)
+        if LIBJPEG:
+            with pytest.raises(RuntimeError):
+                J.libjpeg_decode(bad)
