@@ -15,7 +15,7 @@ all: lib oracle
 lib: $(LIB)
 
 SRCS := $(CSRC)/vf_kernels.hip $(CSRC)/vf_engine.hip $(CSRC)/vf_api.hip $(CSRC)/vf_jpeg_kernels.hip $(CSRC)/vf_jpeg_host.hip
-HDRS := $(CSRC)/vf_internal.h $(CSRC)/vf_jpeg.h $(CSRC)/vf_jpeg_codec.h include/vfilter.h
+HDRS := $(CSRC)/vf_internal.h $(CSRC)/vf_stream.h $(CSRC)/vf_jpeg.h $(CSRC)/vf_jpeg_codec.h include/vfilter.h
 
 $(LIB): $(SRCS) $(HDRS)
 	$(HIPCC) $(HIPFLAGS) $(LDFLAGS) -pthread $(SRCS) -o $@
@@ -28,7 +28,7 @@ tools: tools/tune_invert tools/pcie_probe
 tools/pcie_probe: tools/pcie_probe.hip
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 $< -o $@
 
-tools/tune_invert: tools/tune_invert.hip $(CSRC)/vf_kernels.hip $(CSRC)/vf_internal.h
+tools/tune_invert: tools/tune_invert.hip $(CSRC)/vf_kernels.hip $(CSRC)/vf_internal.h $(CSRC)/vf_stream.h
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -Iinclude -I$(CSRC) tools/tune_invert.hip $(CSRC)/vf_kernels.hip -o $@
 
 clean:

@@ -212,8 +212,6 @@ VF_EXPORT int vf_create(int device, size_t max_frame_bytes, int max_batch, vf_ct
   if (!ctx) return set_err(nullptr, VF_E_NOMEM, 0, "vf_create: out of host memory");
   ctx->device = device;
   ctx->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
-  ctx->cfg.variant = (int)env_size("VF_VARIANT", (size_t)vf::kVariantU4NT);
-  if (ctx->cfg.variant < 0 || ctx->cfg.variant >= vf::kVariantCount) ctx->cfg.variant = vf::kVariantU4NT;
   ctx->cfg.max_blocks = (int)env_size("VF_MAX_BLOCKS", (size_t)ctx->num_cus * 32);
   if (ctx->cfg.max_blocks < 1) ctx->cfg.max_blocks = ctx->num_cus * 32;
   const int nslots = (int)std::min<size_t>(kMaxSlots, std::max<size_t>(2, env_size("VF_SLOTS", 4)));
@@ -528,7 +526,8 @@ class CodecLease {
       c_ = ctx->jpeg_free.back();
       ctx->jpeg_free.pop_back();
     } else {
-      c_ = new (std::nothrow) vf::jpeg::Codec(ctx->device, &ctx->jpeg_gate);
+      static const bool gated = env_size("VF_JPEG_GATE", 1) != 0;
+      c_ = new (std::nothrow) vf::jpeg::Codec(ctx->device, gated ? &ctx->jpeg_gate : nullptr);
       if (c_) ctx->jpeg_all.push_back(c_);
     }
   }

@@ -41,12 +41,6 @@ namespace jpeg {
 
 namespace {
 
-// zigzag position -> natural (row-major) index (jutils.c jpeg_natural_order)
-__constant__ uint8_t kNat[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
-                                 12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
-                                 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
-                                 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
-
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
 // ---- workgroup scans (256 threads = 4 waves of 64) -----------------------------------------
@@ -999,37 +993,46 @@ __device__ __forceinline__ void block_pos(const Geom &g, uint32_t b, uint32_t *k
 // 1080p / 4K): 1 block per lane group with separate LDS for the two passes 0.200 / 0.73 (the
 // earlier kernel); aliased 0.202 / 0.74; 2 blocks not aliased 0.21 / 0.76; 2 blocks aliased
 // 0.170 / 0.61; 3 aliased 0.197 / 0.71; 4 aliased 0.205 / 0.74.
-#ifndef VF_IDCT_NB
-#define VF_IDCT_NB 2
-#endif
-#ifndef VF_IDCT_ALIAS
-#define VF_IDCT_ALIAS 1
-#endif
-constexpr int kIdctNb = VF_IDCT_NB;         // blocks per 8-lane group
+constexpr int kIdctNb = 2;                  // blocks per 8-lane group
 constexpr int kIdctBlocks = 32 * kIdctNb;   // blocks per workgroup
+
+// LDS placement of a block's coefficients, conflict-free for both accesses of k_idct.  Lane r
+// holds zigzag positions 8r..8r+7 (one 16-B load) and stores them; in pass 1 it reads column r.
+// A block's row is 72 dwords (8 mod 32), so a 32-lane half (4 blocks x 8 lanes) is free of
+// conflicts when, for every store j and every read i, the 8 lanes' dwords differ mod 8.
+// Natural position n = 8i + c sits at dword 8i + g(n), where g permutes each natural row and
+// also each zigzag class {zigzag 8r + j : r} -- an 8-edge-colouring of the 8-regular bipartite
+// graph rows x zigzag-classes (one edge per position; König).  The zigzag store of the
+// natural-order scatter it replaces cost 16 extra LDS cycles per block pair and wave, the
+// mixed-component dequantisation reads 32 (SQ_LDS_BANK_CONFLICT 3.98e8 per 1080p batch,
+// profiles/r01_jpeg_pmc_sq.txt).
+__constant__ uint8_t kIdctPos[64] = {  // zigzag index -> dword of the block row (8 * row + g)
+    1,  0,  9,  17, 8,  3,  2,  11, 16, 25, 32, 27, 19, 10, 5,  4,  12, 18, 26, 34, 42, 48,
+    40, 33, 29, 21, 14, 7,  6,  13, 20, 24, 35, 46, 51, 56, 57, 49, 41, 38, 31, 23, 15, 22,
+    28, 36, 43, 50, 58, 59, 52, 44, 37, 30, 39, 45, 54, 60, 61, 53, 47, 55, 62, 63};
+__constant__ uint32_t kIdctCol[8] = {  // column c: nibble i = g(8i + c)
+    0x00201111u, 0x13023000u, 0x21612333u, 0x32135222u, 0x44360545u, 0x56447464u, 0x65554757u, 0x77776676u};
 
 // 8 lanes per block, kIdctNb blocks per 8-lane group: both blocks' coefficient loads are issued
 // before either is transformed, and the column pass's output reuses the block's LDS row (one
-// more barrier, half the LDS: 18.4 KB per workgroup for 64 blocks)
+// more barrier, half the LDS: 18.4 KB per workgroup for 64 blocks).  Dequantisation happens
+// on pass 1's reads, as in jidctint.c (DEQUANTIZE(inptr[DCTSIZE*k], quantptr[DCTSIZE*k])).
 __global__ __launch_bounds__(256) void k_idct(const DecFrame *fr, const int16_t *coef, const int32_t *dcseq,
                                               uint8_t *planes) {
   const DecFrame &F = fr[blockIdx.y];
   const Geom &g = F.g;
   if (blockIdx.x * kIdctBlocks >= (uint32_t)g.nblocks) return;
-  __shared__ int32_t blkv[kIdctBlocks][72];  // rows padded to 72: a wave's 8 column reads hit 64 banks
-#if VF_IDCT_ALIAS
-  int32_t(*wsb)[72] = blkv;                 // column-pass output reuses the block's row after a barrier
-#else
-  __shared__ int32_t wsb[kIdctBlocks][72];  // [8][9] per block
-#endif
-  __shared__ int32_t s_q[3][64];     // dequantisation, natural order
-  __shared__ uint8_t s_nat[64];      // zigzag -> natural
-  __shared__ uint32_t s_pos[kMaxBpm];  // block-in-MCU -> component | x << 8 | y << 16 (blocks)
+  __shared__ int32_t blkv[kIdctBlocks][72];  // coefficients (kIdctPos), then the column pass's [8][9]
+  __shared__ int32_t s_q[3][72];     // dequantisation, natural order; rows 8 mod 32 dwords apart
+  __shared__ uint8_t s_pos[64];      // kIdctPos
+  __shared__ uint32_t s_col[8];      // kIdctCol
+  __shared__ uint32_t s_geo[kMaxBpm];  // block-in-MCU -> component | x << 8 | y << 16 (blocks)
   const uint32_t t = threadIdx.x;
   if (t < 192) s_q[t >> 6][t & 63] = F.q[t >> 6][t & 63];
-  if (t < 64) s_nat[t] = kNat[t];
+  if (t < 64) s_pos[t] = kIdctPos[t];
+  if (t < 8) s_col[t] = kIdctCol[t];
   if (t < (uint32_t)g.bpm)
-    s_pos[t] = (uint32_t)g.bcomp[t] | ((uint32_t)g.bxo[t] << 8) | ((uint32_t)g.byo[t] << 16);
+    s_geo[t] = (uint32_t)g.bcomp[t] | ((uint32_t)g.bxo[t] << 8) | ((uint32_t)g.byo[t] << 16);
   __syncthreads();
   // per-component values, uniform: picked with selects, not per-lane global loads
   const uint32_t mh[3] = {(uint32_t)g.mh[0], (uint32_t)g.mh[1], (uint32_t)g.mh[2]};
@@ -1048,7 +1051,7 @@ __global__ __launch_bounds__(256) void k_idct(const DecFrame *fr, const int16_t 
     const uint32_t b = blockIdx.x * kIdctBlocks + h * 32 + slot;
     valid[h] = b < (uint32_t)g.nblocks;
     const uint32_t mcu = b / (uint32_t)g.bpm, c = b - mcu * (uint32_t)g.bpm;
-    const uint32_t ps = valid[h] ? s_pos[c] : 0u;
+    const uint32_t ps = valid[h] ? s_geo[c] : 0u;
     const uint32_t k = ps & 0xFF;
     kk[h] = k;
     bxs[h] = (mcu % (uint32_t)g.mcux) * HuffGeom::sel(mh, k) + ((ps >> 8) & 0xFF);
@@ -1062,36 +1065,36 @@ __global__ __launch_bounds__(256) void k_idct(const DecFrame *fr, const int16_t 
                       (c - HuffGeom::sel(cf, k))];
     }
   }
+  const uint2 pos8 = *reinterpret_cast<const uint2 *>(&s_pos[r * 8]);  // this lane's 8 store dwords
+  const uint32_t colg = s_col[r];
 #pragma unroll
   for (int h = 0; h < kIdctNb; ++h) {
     if (!valid[h]) continue;
     const uint32_t qw[4] = {raw[h].x, raw[h].y, raw[h].z, raw[h].w};
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const uint32_t zz = r * 8 + j, n = s_nat[zz];
       const int32_t v = (int32_t)(int16_t)(qw[j >> 1] >> (16 * (j & 1)));
-      const int32_t x = zz == 0 ? (int32_t)(int16_t)dc[h] : v;
-      blkv[h * 32 + slot][n] = x * s_q[kk[h]][n];
+      const uint32_t at = ((j < 4 ? pos8.x : pos8.y) >> (8 * (j & 3))) & 0xFF;
+      blkv[h * 32 + slot][at] = (r == 0 && j == 0) ? (int32_t)(int16_t)dc[h] : v;
     }
   }
   __syncthreads();
   int32_t col[kIdctNb][8];
 #pragma unroll
-  for (int h = 0; h < kIdctNb; ++h) {  // pass 1: column r
+  for (int h = 0; h < kIdctNb; ++h) {  // pass 1: column r, dequantised
     if (!valid[h]) continue;
     int32_t in[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) in[i] = blkv[h * 32 + slot][i * 8 + r];
+    for (int i = 0; i < 8; ++i)
+      in[i] = blkv[h * 32 + slot][i * 8 + ((colg >> (4 * i)) & 7)] * s_q[kk[h]][i * 8 + r];
     idct_line(in, col[h], 11);
   }
-#if VF_IDCT_ALIAS
   __syncthreads();
-#endif
 #pragma unroll
   for (int h = 0; h < kIdctNb; ++h) {
     if (!valid[h]) continue;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) wsb[h * 32 + slot][i * 9 + r] = col[h][i];
+    for (int i = 0; i < 8; ++i) blkv[h * 32 + slot][i * 9 + r] = col[h][i];
   }
   __syncthreads();
 #pragma unroll
@@ -1099,7 +1102,7 @@ __global__ __launch_bounds__(256) void k_idct(const DecFrame *fr, const int16_t 
     if (!valid[h]) continue;
     int32_t in[8], out[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) in[i] = wsb[h * 32 + slot][r * 9 + i];
+    for (int i = 0; i < 8; ++i) in[i] = blkv[h * 32 + slot][r * 9 + i];
     idct_line(in, out, 18);
     uint32_t lo = 0, hi = 0;
 #pragma unroll
@@ -1491,11 +1494,22 @@ struct LdsBits {
   }
 };
 
-// natural (row-major) index -> zigzag position (inverse of kNat)
+// natural (row-major) index -> zigzag position (inverse of jutils.c jpeg_natural_order)
 __constant__ uint8_t kZig[64] = {0,  1,  5,  6,  14, 15, 27, 28, 2,  4,  7,  13, 16, 26, 29, 42,
                                  3,  8,  12, 17, 25, 30, 41, 43, 9,  11, 18, 24, 31, 40, 44, 53,
                                  10, 19, 23, 32, 39, 45, 52, 54, 20, 22, 33, 38, 46, 51, 55, 60,
                                  21, 34, 37, 47, 50, 56, 59, 61, 35, 36, 48, 49, 57, 58, 62, 63};
+
+// Position of zigzag coefficient zz in a block's row of qo: its 16-B octet (zz / 8, the AC
+// coder's one ds_read_b128 per lane) is XOR-ed with (0, 5, 2, 7)[slot % 4].  The row is 32
+// dwords (0 mod 32), so unswizzled, the 4 blocks of a 32-lane half store every 16-bit
+// coefficient to the same banks: 48 extra LDS cycles per wave over pass 2's eight scattered
+// stores; swizzled, 12 (searched exhaustively over per-slot octet XORs that keep the b128
+// reads conflict-free; SQ_LDS_BANK_CONFLICT 3.45e8 per 1080p batch before,
+// profiles/r01_jpeg_pmc_sq.txt).
+__device__ __forceinline__ uint32_t qo_at(uint32_t slot, uint32_t zz) {
+  return (((zz >> 3) ^ ((0x7250u >> (4 * (slot & 3))) & 7)) << 3) | (zz & 7);
+}
 
 // 8 lanes per block.  A workgroup takes M = 32 / bpm whole MCUs and orders its 32 block
 // slots block-in-MCU-major (slot s -> block-in-MCU s / M of MCU s % M), so a wave's 8 blocks
@@ -1546,12 +1560,6 @@ __global__ __launch_bounds__(256) void k_fdct(const EncFrame *fr, const EncTable
     const int real_rows = ((g.h + g.maxv - 1) / g.maxv) * g.vs[k];
     const int sy = min((int)(by * 8 + r), real_rows - 1);
     int32_t v[8];
-#ifdef VF_ABL_NOPIX
-    if (true) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = (int)((bx * 8 + j + sy * 3 + k) & 255);
-    } else
-#endif
     if (ve == 1 && he <= 2) {  // he == 1: full-resolution line; he == 2: h2v1_downsample
       if (he == 1) line_acc<1>(img, g.w, g.h, (int)bx * 8, sy, bgr, (int)k, v, true);
       else line_acc<2>(img, g.w, g.h, (int)bx * 16, sy, bgr, (int)k, v, true);
@@ -1587,22 +1595,14 @@ __global__ __launch_bounds__(256) void k_fdct(const EncFrame *fr, const EncTable
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int n = i * 8 + r;
-      qo[slot][s_zig[n]] = quantize(v[i], s_recip[t][n], s_corr[t][n], s_shift[t][n]);
+      qo[slot][qo_at(slot, s_zig[n])] = quantize(v[i], s_recip[t][n], s_corr[t][n], s_shift[t][n]);
     }
   }
   __syncthreads();
-#ifdef VF_ABL_NOAC
-  if (real && r == 0) {
-    const uint64_t gb = F.blk0 + b;
-    dcq[gb] = qo[slot][0];
-    acbits[gb] = (uint32_t)qo[slot][1] & 1;
-  }
-  return;
-#endif
   // AC Huffman coding; every lane of the wave takes part in the 8-lane shuffles
   int vz[8];
   {
-    const uint4 q4 = real ? *reinterpret_cast<const uint4 *>(&qo[slot][r * 8]) : make_uint4(0, 0, 0, 0);
+    const uint4 q4 = real ? *reinterpret_cast<const uint4 *>(&qo[slot][qo_at(slot, r * 8)]) : make_uint4(0, 0, 0, 0);
     const uint32_t qw[4] = {q4.x, q4.y, q4.z, q4.w};
 #pragma unroll
     for (int j = 0; j < 8; ++j) vz[j] = (int)(int16_t)(qw[j >> 1] >> (16 * (j & 1)));
@@ -1661,7 +1661,7 @@ __global__ __launch_bounds__(256) void k_fdct(const EncFrame *fr, const EncTable
     const uint32_t nw = (total + 31) >> 5;
     for (uint32_t i = r; i < nw; i += 8) acscr[acs_idx(gb, i)] = acw[slot][i];
     if (r == 0) {
-      dcq[gb] = qo[slot][0];
+      dcq[gb] = qo[slot][qo_at(slot, 0)];
       acbits[gb] = total;
     }
   }

@@ -17,12 +17,27 @@ Additions for GPU workers (keyword-only):
                    worker's credit (contiguous index runs -> contiguous device batches); ingest
                    blocks instead of dropping when ``queue_size`` frames are waiting.
   policy="shard"   lossless, deterministic: index chunk c = [c*shard_chunk, (c+1)*shard_chunk)
-                   goes to the (c % shard_workers)-th worker to register — frame-index sharding
-                   across 1/2/4/8 GPUs.
+                   goes to shard c % shard_workers; shard k belongs to the k-th worker to
+                   register — frame-index sharding across 1/2/4/8 GPUs.
   reassembly="ordered"  every result released exactly once in index order
                    (``get_next_frame``), with ordering-overhead statistics.
   ring_slots>0     same-node shared-memory data plane (``vfilter.shm``): frames are written once
                    into a ring slot and only slot numbers travel on the sockets.
+                   ring_layout="per_worker" (default for pull/shard): every worker gets its own
+                   slice of ``ring_slots`` slots, bound to the NUMA node of its GPU
+                   (``vfilter.numa``); it page-locks only that slice.  A frame is written into
+                   the slice of the worker that will filter it (shard: the shard's owner; pull:
+                   the worker with the most free slots, so a slower worker gets fewer frames).
+                   ring_layout="shared": one ring every worker maps (the latest policy's).
+Worker loss (lossless policies).  Every dispatched frame is tracked per worker.  A worker
+whose oldest outstanding batch is older than ``batch_timeout`` seconds, or whose connection
+closes (tcp transport), is evicted: its frames are re-queued to the others (copied into their
+slices), its shards move to a spare or to the least-loaded live worker, and a frame that has
+been dispatched ``max_attempts`` times is counted lost (``OrderedBuffer.mark_lost``), so
+``get_next_frame`` never waits forever.  A result that still arrives from an evicted worker is
+a duplicate and is dropped; its ring slot is kept out of use until then.  An evicted worker
+that asks again is taken back and re-takes its home shard.  (The reference tolerates workers
+coming and going through READY and loses a failed frame, worker.py:74-76.)
 All shared state sits behind one lock (the reference relies on the GIL).
 """
 from __future__ import annotations
@@ -37,6 +52,7 @@ from typing import Deque, Dict, List, Optional
 
 import numpy as np
 
+from . import numa
 from . import transport as tp
 from . import wire
 from .reorder import DisplayBuffer, OrderedBuffer
@@ -45,23 +61,49 @@ from .shm import FrameRing
 
 
 class _Peer:
-    __slots__ = ("pid", "version", "requests", "frames_sent", "results", "errors", "shard")
+    __slots__ = ("pid", "version", "wid", "requests", "frames_sent", "results", "errors", "home_shard", "shm",
+                 "numa", "slice", "queue", "inflight", "quarantine", "batches", "alive", "gone", "evictions",
+                 "order")
 
-    def __init__(self, pid: bytes, version: int):
+    def __init__(self, pid: bytes, req: wire.Request, order: int):
         self.pid = pid
-        self.version = version
+        self.version = req.version
+        self.wid = req.wid
+        self.shm = bool(req.shm)
+        self.numa = req.numa
+        self.order = order                    # registration order
         self.requests: Deque[int] = collections.deque()  # credits of outstanding requests
         self.frames_sent = 0
         self.results = 0
         self.errors = 0
-        self.shard: Optional[int] = None
+        self.home_shard: Optional[int] = None
+        self.slice: Optional[int] = None      # ring slice (per_worker layout)
+        self.queue: Deque[dict] = collections.deque()   # pull + per_worker: frames in this slice
+        self.inflight: Dict[int, dict] = {}   # index -> dispatched copy awaiting its result
+        self.quarantine: Dict[int, dict] = {}  # copies dispatched before an eviction
+        self.batches: Deque[list] = collections.deque()  # [t_dispatch, {indices}] oldest first
+        self.alive = True
+        self.gone = False                     # connection closed: no result can come any more
+        self.evictions = 0
+
+
+class _Slice:
+    __slots__ = ("ring", "free", "numa", "bound", "owner")
+
+    def __init__(self, ring: FrameRing, node: Optional[int], bound: bool, owner: Optional[bytes]):
+        self.ring = ring
+        self.free: List[int] = list(range(ring.nslots - 1, -1, -1))
+        self.numa = node
+        self.bound = bound
+        self.owner = owner
 
 
 class Distributor:
     def __init__(self, distribute_port: int = 5555, collect_port: int = 5556, frame_delay: int = 5,
                  enable_trace_export: bool = False, *, policy: str = "latest", reassembly: str = "display",
                  transport: str = "auto", host: str = "*", queue_size: int = 10, frame_buffer_size: int = 50,
-                 ring_slots: int = 0, ring_slot_bytes: int = 0, shard_workers: int = 0, shard_chunk: int = 1,
+                 ring_slots: int = 0, ring_slot_bytes: int = 0, ring_layout: str = "auto", shard_workers: int = 0,
+                 shard_chunk: int = 1, batch_timeout: float = 30.0, max_attempts: int = 3,
                  trace_file: str = "webcam_frame_timing.pftrace", verbose: bool = True, zero_copy: bool = False):
         if zero_copy and (ring_slots < 1 or reassembly != "ordered"):
             raise ValueError("zero_copy needs ring_slots > 0 and reassembly='ordered'")
@@ -72,6 +114,12 @@ class Distributor:
             raise ValueError("reassembly must be display | ordered")
         if policy == "shard" and shard_workers < 1:
             raise ValueError("policy='shard' needs shard_workers >= 1")
+        if ring_layout == "auto":
+            ring_layout = "shared" if policy == "latest" else "per_worker"
+        if ring_layout not in ("shared", "per_worker"):
+            raise ValueError("ring_layout must be auto | shared | per_worker")
+        if ring_layout == "per_worker" and policy == "latest":
+            raise ValueError("the latest policy serves any worker from one slot: use ring_layout='shared'")
         self.policy = policy
         self.reassembly = reassembly
         self.verbose = verbose
@@ -80,11 +128,14 @@ class Distributor:
         self.frame_index_counter = 0
         self.last_frame_sent = -1                   # distributor.py:17
         self.current_frame_data: Optional[dict] = None
-        self._pending: Deque[dict] = collections.deque()   # lossless policies
+        self._pending: Deque[dict] = collections.deque()   # pull without per-worker slices
         self._shard_pending: Dict[int, Deque[dict]] = collections.defaultdict(collections.deque)
+        self._orphans: Deque[dict] = collections.deque()   # pull + per_worker, no live worker
         self.queue_size = queue_size
         self.shard_workers = shard_workers
         self.shard_chunk = max(1, shard_chunk)
+        self.batch_timeout = float(batch_timeout)
+        self.max_attempts = max(1, int(max_attempts))
         # reassembly (distributor.py:19-24)
         self._display = DisplayBuffer(frame_delay, frame_buffer_size)
         self._ordered = OrderedBuffer(0)
@@ -98,13 +149,23 @@ class Distributor:
         self.collect_socket = tp.PullEnd(self.transport, host, collect_port, self._zctx)
         self.distribute_port = self.distribute_socket.port
         self.collect_port = self.collect_socket.port
-        # shared-memory ring
-        self.ring: Optional[FrameRing] = None
+        # shared-memory ring: slices of ring_slots slots; global slot id = slice * ring_slots + k
+        self.ring_slots = int(ring_slots)
+        self.ring_slot_bytes = int(ring_slot_bytes)
+        self.ring_layout = ring_layout if ring_slots > 0 else None
+        self._slices: List[_Slice] = []
+        self.ring: Optional[FrameRing] = None       # the shared ring (ring_layout="shared")
         if ring_slots > 0:
             if ring_slot_bytes < 1:
                 raise ValueError("ring_slots needs ring_slot_bytes (largest frame)")
-            self.ring = FrameRing(ring_slots, ring_slot_bytes)
-        self._slot_of: Dict[int, int] = {}
+            if ring_layout == "shared":
+                self.ring = FrameRing(ring_slots, ring_slot_bytes)
+                self._slices.append(_Slice(self.ring, None, False, None))
+        self._reserved: Dict[int, Optional[int]] = {}   # reserved slot -> its frame index (per_worker)
+        self._clone_src: Dict[int, dict] = {}   # quarantined slot -> re-queued copy reading from it
+        self._held: Dict[int, int] = {}         # zero_copy: index -> slot of its released result
+        self._copies: Dict[int, int] = {}       # index -> copies queued or in flight
+        self._settled = set()                   # indices delivered/lost while copies remain
         # tracing (distributor.py:37-40)
         self.enable_trace_export = enable_trace_export
         self.frame_timings: List[dict] = []
@@ -112,8 +173,16 @@ class Distributor:
         self.trace_file = trace_file
         # peers and counters
         self._peers: Dict[bytes, _Peer] = {}
-        self._shard_owner: Dict[int, bytes] = {}
+        self._by_wid: Dict[str, _Peer] = {}
+        self._shard_home: Dict[int, bytes] = {}   # shard -> the worker it belongs to
+        self._shard_owner: Dict[int, bytes] = {}  # shard -> the worker serving it now
+        self._rr = 0
         self.frames_dropped = 0
+        self.frames_lost = 0
+        self.frames_requeued = 0
+        self.duplicates = 0
+        self.evictions = 0
+        self.departures = 0
         self.results_received = 0
         self.result_errors = 0
         # threads (distributor.py:42-51)
@@ -162,9 +231,10 @@ class Distributor:
         self.collect_socket.close()
         if self._zctx is not None:
             self._zctx.term()
-        if self.ring is not None:
-            self.ring.close()
-            self.ring = None
+        for sl in self._slices:
+            sl.ring.close()
+        self._slices = []
+        self.ring = None
         if self.verbose:
             print("ZeroMQ connections closed" if self.transport == "zmq" else "Connections closed")
             print("Frame reordering statistics:")
@@ -238,6 +308,38 @@ class Distributor:
                                     "duration_ms": dur * 1000}})
         return ev
 
+    def trace_summary(self) -> dict:
+        """The statistics the reference prints after an export (distributor.py:151-171): the
+        mean interval between capture instants and the mean worker processing span.  GPU spans
+        are summarised per stage beside them (bytes and GB/s)."""
+        out: dict = {}
+        inst = [t for t in self.frame_timings if t["event_ph"] == "i"]
+        comp = [t for t in self.frame_timings if t["event_ph"] == "X"]
+        if len(inst) > 1:
+            ts = [t["timestamp"] for t in inst]
+            iv = [ts[i + 1] - ts[i] for i in range(len(ts) - 1)]
+            avg = sum(iv) / len(iv)
+            out["avg_capture_interval_ms"] = avg * 1000
+            out["capture_fps"] = (1 / avg) if avg > 0 else float("inf")
+        if comp:
+            ds = [t["end_time"] - t["begin_time"] for t in comp]
+            avg = sum(ds) / len(ds)
+            out["avg_processing_ms"] = avg * 1000
+            out["processing_fps"] = (1 / avg) if avg > 0 else float("inf")
+            out["frames_processed"] = len(comp)
+        gpu: Dict[str, dict] = {}
+        for t in self.frame_timings:
+            if t["event_ph"] == "G":
+                g = gpu.setdefault(t["name"], {"spans": 0, "seconds": 0.0, "bytes": 0})
+                g["spans"] += 1
+                g["seconds"] += max(0.0, t["end_time"] - t["begin_time"])
+                g["bytes"] += int(t["bytes"])
+        for g in gpu.values():
+            g["GBps"] = g["bytes"] / g["seconds"] / 1e9 if g["seconds"] > 0 else None
+        if gpu:
+            out["gpu"] = gpu
+        return out
+
     def export_perfetto_trace(self):
         if not self.enable_trace_export:
             print("Trace export is disabled")
@@ -249,6 +351,58 @@ class Distributor:
             json.dump({"traceEvents": self.trace_events()}, f)
         print(f"Perfetto trace exported to: {self.trace_file}")
         print(f"Total frames logged: {len(self.frame_timings)}")
+        s = self.trace_summary()                    # distributor.py:151-171
+        if "avg_capture_interval_ms" in s:
+            print(f"Average frame capture interval: {s['avg_capture_interval_ms']:.2f}ms")
+            print(f"Frame capture rate: {s['capture_fps']:.1f} FPS")
+        if "avg_processing_ms" in s:
+            print(f"Average processing duration: {s['avg_processing_ms']:.2f}ms")
+            print(f"Processing rate: {s['processing_fps']:.1f} FPS")
+            print(f"Total frames processed: {s['frames_processed']}")
+        for name, g in s.get("gpu", {}).items():
+            rate = f", {g['GBps']:.1f} GB/s" if g["GBps"] else ""
+            print(f"GPU {name}: {g['spans']} spans, {g['seconds'] * 1000:.2f}ms, {g['bytes']} bytes{rate}")
+
+    # ---- ring slots -----------------------------------------------------------------------
+    def in_view(self, slot: int, nbytes: int) -> np.ndarray:
+        """Input half of ring slot ``slot`` (a global slot id)."""
+        sid, k = divmod(slot, self.ring_slots)
+        return self._slices[sid].ring.in_view(k, nbytes)
+
+    def out_view(self, slot: int, nbytes: int) -> np.ndarray:
+        sid, k = divmod(slot, self.ring_slots)
+        return self._slices[sid].ring.out_view(k, nbytes)
+
+    frame_view = in_view
+
+    def free_slots(self) -> int:
+        with self._lock:
+            return sum(len(sl.free) for sl in self._slices)
+
+    def total_slots(self) -> int:
+        with self._lock:
+            return len(self._slices) * self.ring_slots
+
+    def _alloc_slot(self, sid: int) -> Optional[int]:
+        sl = self._slices[sid]
+        return sid * self.ring_slots + sl.free.pop() if sl.free else None
+
+    def _free_slot(self, slot: Optional[int]) -> None:
+        if slot is None or not self._slices:
+            return
+        clone = self._clone_src.pop(slot, None)
+        if clone is not None and clone.get("slot") is None:
+            clone["slot"], clone["src_slot"] = slot, None  # the re-queued copy now owns it
+            return
+        sid, k = divmod(slot, self.ring_slots)
+        self._slices[sid].free.append(k)
+        self._cv.notify_all()
+
+    def _make_slice(self, p: _Peer) -> None:
+        ring = FrameRing(self.ring_slots, self.ring_slot_bytes)
+        bound = numa.bind(ring.base_address, ring.nbytes, p.numa) if p.numa is not None else False
+        self._slices.append(_Slice(ring, p.numa, bound, p.pid))
+        p.slice = len(self._slices) - 1
 
     # ---- ingest (distributor.py:173-203) -------------------------------------------------
     def add_frame_for_distribution(self, frame, timestamp=None, shape=None, block: bool = True) -> int:
@@ -261,64 +415,119 @@ class Distributor:
             shape = list(frame.shape) if shape is None else shape
             frame = np.ascontiguousarray(frame)
         nbytes = frame.nbytes if isinstance(frame, np.ndarray) else len(frame)
-        slot = None
-        if self.ring is not None:
+        if self._slices or self.ring_layout == "per_worker":
             slot = self.reserve_frame(nbytes, block)
             if slot is None:
                 return -1
-            self.ring.in_view(slot, nbytes)[:] = np.frombuffer(frame, dtype=np.uint8) \
-                if not isinstance(frame, np.ndarray) else frame.reshape(-1).view(np.uint8)
-        return self._enqueue(None if slot is not None else frame, nbytes, shape, slot, timestamp, block)
+            src = frame.reshape(-1).view(np.uint8) if isinstance(frame, np.ndarray) else \
+                np.frombuffer(frame, dtype=np.uint8)
+            self.in_view(slot, nbytes)[:] = src
+            return self.commit_frame(slot, nbytes, shape, timestamp, block)
+        return self._enqueue(frame, nbytes, shape, None, timestamp, block)
 
     # ---- zero-copy ingest (ring mode) ------------------------------------------------------
     def reserve_frame(self, nbytes: int, block: bool = True) -> Optional[int]:
         """Reserve a ring slot for a frame of ``nbytes``; fill ``frame_view(slot, nbytes)`` in
-        place (e.g. decode or capture straight into it), then ``commit_frame``.  Returns None
-        when no slot is free and ``block`` is False."""
-        if self.ring is None:
+        place (e.g. decode or capture straight into it), then ``commit_frame`` (or
+        ``cancel_frame``).  Returns None when no slot is free and ``block`` is False.  With
+        per-worker slices the frame's index is fixed here (it decides the slice)."""
+        if self.ring_layout is None:
             raise RuntimeError("reserve_frame needs ring_slots > 0")
-        if nbytes > self.ring.slot_bytes:
-            raise ValueError(f"frame of {nbytes} B exceeds ring slot of {self.ring.slot_bytes} B")
-        slot = self.ring.acquire(timeout=None if (block and self.policy != "latest") else 0)
-        if slot is None and self.policy == "latest":
-            slot = self._evict_oldest_queued_slot()
-        return slot
-
-    def frame_view(self, slot: int, nbytes: int) -> np.ndarray:
-        return self.ring.in_view(slot, nbytes)
+        if nbytes > self.ring_slot_bytes:
+            raise ValueError(f"frame of {nbytes} B exceeds ring slot of {self.ring_slot_bytes} B")
+        with self._cv:
+            while True:
+                if self.ring_layout == "shared":
+                    slot = self._alloc_slot(0)
+                    if slot is None and self.policy == "latest":
+                        slot = self._evict_oldest_queued_slot()
+                    if slot is not None:
+                        self._reserved[slot] = None
+                        return slot
+                elif self.policy == "latest" or self._waiting() < self.queue_size:
+                    idx = self.frame_index_counter
+                    p = self._target_peer(idx)
+                    if p is not None:
+                        slot = self._alloc_slot(p.slice)
+                        if slot is not None:
+                            self.frame_index_counter += 1
+                            self._reserved[slot] = idx
+                            return slot
+                if not block or not self.running:
+                    return None
+                self._cv.wait(0.05)
 
     def commit_frame(self, slot: int, nbytes: int, shape=None, timestamp=None, block: bool = True) -> int:
         """Queue the frame written into ``slot``; returns its index (as add_frame_for_distribution)."""
         return self._enqueue(None, nbytes, shape, slot, time.time() if timestamp is None else timestamp, block)
 
+    def cancel_frame(self, slot: int) -> None:
+        """Give back a reserved slot that will not be committed (its index, if one was fixed at
+        reservation, is counted lost so the in-order consumer does not wait for it)."""
+        with self._cv:
+            idx = self._reserved.pop(slot, None)
+            self._free_slot(slot)
+            if idx is not None:
+                self._lose(idx)
+
+    def _target_peer(self, idx: int) -> Optional[_Peer]:
+        """The worker whose slice frame ``idx`` goes into (per_worker layout)."""
+        if self.policy == "shard":
+            pid = self._shard_owner.get(chunk_owner(idx, self.shard_chunk, self.shard_workers))
+            p = self._peers.get(pid) if pid is not None else None
+            return p if p is not None and p.alive and p.slice is not None else None
+        live = [p for p in self._peers.values() if p.alive and p.slice is not None
+                and self._slices[p.slice].free]
+        if not live:
+            return None
+        most = max(len(self._slices[p.slice].free) for p in live)
+        best = [p for p in live if len(self._slices[p.slice].free) == most]
+        self._rr += 1
+        return best[self._rr % len(best)]
+
     def _enqueue(self, frame, nbytes: int, shape, slot: Optional[int], timestamp: float, block: bool) -> int:
         with self._cv:
-            frame_index = self.frame_index_counter          # distributor.py:179-180
-            self.frame_index_counter += 1
-            item = {"frame": None if slot is not None else frame, "frame_index": frame_index,
-                    "timestamp": timestamp, "nbytes": nbytes, "shape": shape, "slot": slot}
-            if slot is not None:
-                self._slot_of[frame_index] = slot
+            idx = self._reserved.pop(slot, None) if slot is not None else None
+            if idx is None:
+                if self.policy != "latest":
+                    # wait for room BEFORE taking an index: a rejected frame must not leave a
+                    # hole in the index sequence (the ordered consumer would wait for it)
+                    while block and self.running and self._waiting() >= self.queue_size:
+                        self._cv.wait(0.05)
+                    if self._waiting() >= self.queue_size:
+                        self._free_slot(slot)
+                        return -1
+                idx = self.frame_index_counter          # distributor.py:179-180
+                self.frame_index_counter += 1
+            item = {"frame": None if slot is not None else frame, "frame_index": idx, "timestamp": timestamp,
+                    "nbytes": nbytes, "shape": shape, "slot": slot, "src_slot": None, "attempts": 0}
+            self._copies[idx] = 1
             if self.policy == "latest":
                 self._ingest_latest(item)
             else:
-                while block and self.running and self._waiting() >= self.queue_size:
-                    self._cv.wait(0.05)
-                if not block and self._waiting() >= self.queue_size:
-                    if slot is not None:
-                        self._free_slot(frame_index)
-                    return -1
-                if self.policy == "pull":
-                    self._pending.append(item)
-                else:
-                    self._shard_pending[chunk_owner(frame_index, self.shard_chunk, self.shard_workers)].append(item)
+                self._lane_for(item).append(item)
                 self._cv.notify_all()
-            self.log_frame_timing(frame_index, timestamp, "frame_captured")
-        return frame_index
+            self.log_frame_timing(idx, timestamp, "frame_captured")
+        return idx
+
+    def _lane_for(self, item: dict) -> Deque[dict]:
+        """Queue a (re-)queued frame waits in."""
+        if self.policy == "shard":
+            return self._shard_pending[chunk_owner(item["frame_index"], self.shard_chunk, self.shard_workers)]
+        if self.ring_layout != "per_worker":
+            return self._pending
+        if item["slot"] is not None:
+            owner = self._peers.get(self._slices[item["slot"] // self.ring_slots].owner)
+            if owner is not None and owner.alive:
+                return owner.queue
+        live = [p for p in self._peers.values() if p.alive and p.slice is not None]
+        if not live:
+            return self._orphans
+        return min(live, key=lambda p: (len(p.queue) + len(p.inflight), p.order)).queue
 
     def _waiting(self) -> int:
         if self.policy == "pull":
-            return len(self._pending)
+            return len(self._pending) + len(self._orphans) + sum(len(p.queue) for p in self._peers.values())
         return sum(len(q) for q in self._shard_pending.values())
 
     def _ingest_latest(self, item):
@@ -336,73 +545,163 @@ class Distributor:
                 if self.verbose:
                     print(f"Frame {item['frame_index']} dropped due to queue overflow")
 
-    def _drop(self, item):
+    def _drop(self, item, keep_slot: bool = False) -> Optional[int]:
+        """A frame the latest policy discards (queue overflow, or overwritten in the dispatch
+        slot before any worker took it).  Returns its slot when ``keep_slot``."""
         self.frames_dropped += 1
-        if item.get("slot") is not None:
-            self._free_slot(item["frame_index"])
+        slot = item.get("slot")
+        if not keep_slot:
+            self._free_slot(slot)
+        self._copy_done(item["frame_index"])
+        if self.reassembly == "ordered":
+            self._ordered.mark_lost(item["frame_index"])
+            self._released.extend(self._ordered.pop_ready())
+            self._cv.notify_all()
+        return slot if keep_slot else None
 
     def _evict_oldest_queued_slot(self) -> Optional[int]:
-        with self._lock:
-            try:
-                old = self.frame_queue.get_nowait()
-            except queue.Empty:
-                return None
-            self.frames_dropped += 1
-            s = self._slot_of.pop(old["frame_index"], None)
-            return s
+        try:
+            old = self.frame_queue.get_nowait()
+        except queue.Empty:
+            return None
+        return self._drop(old, keep_slot=True)
 
-    def _free_slot(self, index: int):
-        s = self._slot_of.pop(index, None)
-        if s is not None and self.ring is not None:
-            self.ring.release(s)
+    # ---- copies and losses -----------------------------------------------------------------
+    def _copy_done(self, idx: int) -> None:
+        n = self._copies.get(idx, 0) - 1
+        if n > 0:
+            self._copies[idx] = n
+        else:
+            self._copies.pop(idx, None)
+            self._settled.discard(idx)
+
+    def _settle(self, idx: int) -> None:
+        if self._copies.get(idx, 0) > 0:
+            self._settled.add(idx)
+
+    def _lose(self, idx: int) -> None:
+        self.frames_lost += 1
+        self._settle(idx)
+        if self.reassembly == "ordered":
+            self._ordered.mark_lost(idx)
+            self._released.extend(self._ordered.pop_ready())
+        self._cv.notify_all()
 
     # ---- dispatch (distributor.py:205-251) ------------------------------------------------
     def handle_distribute_requests(self):
         poll_ms = 10 if self.policy == "latest" else 1
         while self.running:
             try:
-                if self.policy == "latest":
-                    try:                                      # distributor.py:210-221
-                        item = self.frame_queue.get_nowait()
-                        with self._lock:
-                            prev = self.current_frame_data
-                            self.current_frame_data = item
-                            if prev is not None and prev["frame_index"] > self.last_frame_sent:
-                                self._drop(prev)  # overwritten before any READY took it
-                    except queue.Empty:
-                        pass
-                if self.distribute_socket.poll(poll_ms):
-                    pid, parts = self.distribute_socket.recv()
-                    req = wire.decode_request(parts)
-                    if req is not None:
-                        self._on_request(pid, req)
-                self._serve_waiting()
+                self.dispatch_step(poll_ms)
             except BlockingIOError:
                 continue
             except Exception as e:
                 print(f"Error handling distribute request: {e}")
                 continue
 
-    def _peer(self, pid: bytes, version: int) -> _Peer:
-        p = self._peers.get(pid)
-        if p is None:
-            p = self._peers[pid] = _Peer(pid, version)
-            if self.policy == "shard":
-                k = len(self._shard_owner)
-                if k < self.shard_workers:
-                    self._shard_owner[k] = pid
-                    p.shard = k
-        return p
+    def dispatch_step(self, poll_ms: int = 0) -> None:
+        """One iteration of the dispatch loop (distributor.py:209-248): move at most one queued
+        frame into the latest-wins slot, poll the dispatch socket for ``poll_ms`` and answer
+        what arrived, evict workers past their deadline, serve outstanding requests."""
+        if self.policy == "latest":
+            try:                                          # distributor.py:210-221
+                item = self.frame_queue.get_nowait()
+                with self._lock:
+                    prev = self.current_frame_data
+                    self.current_frame_data = item
+                    if prev is not None and prev["frame_index"] > self.last_frame_sent:
+                        self._drop(prev)  # overwritten before any READY took it
+            except queue.Empty:
+                pass
+        if self.distribute_socket.poll(poll_ms):
+            pid, parts = self.distribute_socket.recv()
+            if parts is None:
+                with self._cv:
+                    p = self._peers.get(pid)
+                    if p is not None:
+                        self._evict(p, "connection closed", gone=True)
+            else:
+                req = wire.decode_request(parts)
+                if req is not None:
+                    self._on_request(pid, req)
+        self._check_deadlines()
+        self._serve_waiting()
 
     def _on_request(self, pid: bytes, req: wire.Request):
-        with self._lock:
-            p = self._peer(pid, req.version)
+        with self._cv:
+            p = self._peers.get(pid)
+            if p is None:
+                p = self._register(pid, req)
+                if p is None:
+                    return
+            elif not p.alive and not p.gone:
+                self._revive(p)
             if req.version == 0 and self.policy == "latest":
                 self._serve_latest_v0(p)                      # distributor.py:229-241
                 return
             if req.version == 0 and len(p.requests) >= 2:
                 return  # a reference worker re-sends READY every 10 ms; keep at most 2
             p.requests.append(req.credit)
+
+    def _register(self, pid: bytes, req: wire.Request) -> Optional[_Peer]:
+        p = _Peer(pid, req, len(self._peers))
+        if self.ring_layout == "per_worker":
+            try:
+                self._make_slice(p)
+            except (MemoryError, OSError) as e:
+                print(f"Distributor: no ring slice for worker {pid.hex()}: {e}")
+                return None
+        self._peers[pid] = p
+        if p.wid:
+            self._by_wid[p.wid] = p
+        if self.policy == "shard":
+            self._rebalance_shards()
+        elif self._orphans:
+            self._relane(list(self._orphans))
+            self._orphans.clear()
+        self._cv.notify_all()
+        return p
+
+    def _revive(self, p: _Peer) -> None:
+        """An evicted worker asked again: take it back; it re-takes its home shard."""
+        p.alive = True
+        if self.verbose:
+            print(f"Distributor: worker {p.pid.hex()} is back")
+        if self.policy == "shard" and p.home_shard is not None:
+            other = self._peers.get(self._shard_home.get(p.home_shard))
+            if other is not None and other is not p:
+                other.home_shard = None
+            self._shard_home[p.home_shard] = p.pid
+            self._rebalance_shards()
+        self._cv.notify_all()
+
+    def _rebalance_shards(self) -> None:
+        """Shard k is served by its home worker while that one is alive; an orphaned shard is
+        adopted (as home) by a live worker that has none, else served by the live worker with
+        the fewest shards."""
+        live = sorted((p for p in self._peers.values() if p.alive), key=lambda p: p.order)
+        for k in range(self.shard_workers):
+            home = self._peers.get(self._shard_home.get(k))
+            if home is None or not home.alive:
+                spare = next((p for p in live if p.home_shard is None), None)
+                if spare is not None:
+                    if home is not None:
+                        home.home_shard = None
+                    spare.home_shard = k
+                    self._shard_home[k] = spare.pid
+                    home = spare
+            if home is not None and home.alive:
+                self._shard_owner[k] = home.pid
+                continue
+            cur = self._peers.get(self._shard_owner.get(k))
+            if cur is not None and cur.alive:
+                continue
+            if live:
+                load = collections.Counter(self._shard_owner.get(j) for j in range(self.shard_workers)
+                                           if j != k)
+                self._shard_owner[k] = min(live, key=lambda p: (load[p.pid], p.order)).pid
+            else:
+                self._shard_owner.pop(k, None)
 
     def _serve_latest_v0(self, p: _Peer):
         cur = self.current_frame_data
@@ -413,13 +712,19 @@ class Distributor:
     def _serve_waiting(self):
         with self._lock:
             for p in list(self._peers.values()):
-                while p.requests:
+                while p.alive and p.requests:
                     items = self._take(p, p.requests[0])
                     if not items:
                         break
                     p.requests.popleft()
                     if not self._send(p, items):
+                        self._unsend(p, items)
                         break
+
+    def _lanes_of(self, p: _Peer) -> List[Deque[dict]]:
+        if self.policy == "pull":
+            return [p.queue] if self.ring_layout == "per_worker" else [self._pending]
+        return [self._shard_pending[k] for k in range(self.shard_workers) if self._shard_owner.get(k) == p.pid]
 
     def _take(self, p: _Peer, credit: int) -> List[dict]:
         if self.policy == "latest":
@@ -428,34 +733,173 @@ class Distributor:
                 self.last_frame_sent = cur["frame_index"]
                 return [cur]
             return []
-        src = self._pending if self.policy == "pull" else (
-            self._shard_pending.get(p.shard) if p.shard is not None else None)
-        if not src:
-            return []
         if p.version == 0:
             credit = 1
-        out = []
-        while src and len(out) < credit:
-            out.append(src.popleft())
-        self._cv.notify_all()  # ingest may be waiting for room
+        lanes = [ln for ln in self._lanes_of(p) if ln]
+        if not lanes:
+            return []
+        out: List[dict] = []
+        taken = set()
+        # lowest indices first; a copy that must move into this worker's slice but finds no
+        # free slot there is skipped, not waited on (the slots may be held by the frames
+        # queued behind it)
+        for it in sorted((it for ln in lanes for it in ln), key=lambda x: x["frame_index"]):
+            if len(out) >= credit:
+                break
+            if it["frame_index"] in self._settled:  # delivered from another copy
+                self._release_copy(it)
+                taken.add(id(it))
+                continue
+            if self._place(it, p):
+                out.append(it)
+                taken.add(id(it))
+        if taken:
+            for ln in lanes:
+                keep = [it for it in ln if id(it) not in taken]
+                if len(keep) != len(ln):
+                    ln.clear()
+                    ln.extend(keep)
+            self._cv.notify_all()  # ingest may be waiting for room
         return out
+
+    def _place(self, it: dict, p: _Peer) -> bool:
+        """Make sure frame copy ``it`` sits in a slot ``p`` can read (its own slice, or any
+        slot of the shared ring for a copy that does not own one yet)."""
+        if self.ring_layout is None:
+            return True
+        sid = 0 if self.ring_layout == "shared" else p.slice
+        slot = it["slot"]
+        if slot is None and it["src_slot"] is None:
+            return True  # travels as a socket payload
+        if slot is not None and (self.ring_layout == "shared" or slot // self.ring_slots == sid):
+            return True
+        new = self._alloc_slot(sid)
+        if new is None:
+            return False
+        src = slot if slot is not None else it["src_slot"]
+        self.in_view(new, it["nbytes"])[:] = self.in_view(src, it["nbytes"])
+        if slot is not None:
+            self._free_slot(slot)
+        else:
+            self._clone_src.pop(src, None)
+        it["slot"], it["src_slot"] = new, None
+        return True
+
+    def _release_copy(self, it: dict) -> None:
+        """A queued copy that will not be dispatched (its frame is settled)."""
+        if it.get("slot") is not None:
+            self._free_slot(it["slot"])
+        elif it.get("src_slot") is not None:
+            self._clone_src.pop(it["src_slot"], None)
+        self._copy_done(it["frame_index"])
 
     def _send(self, p: _Peer, items: List[dict]) -> bool:
         if p.version == 0:
             it = items[0]
-            payload = it["frame"] if it["slot"] is None else \
-                bytes(self.ring.in_view(it["slot"], it["nbytes"]))
+            payload = it["frame"] if it["slot"] is None else bytes(self.in_view(it["slot"], it["nbytes"]))
             ok = self.distribute_socket.send(p.pid, wire.encode_dispatch_v0(it["frame_index"], payload))
         else:
-            metas = [wire.FrameMeta(index=it["frame_index"], nbytes=it["nbytes"], shape=it["shape"],
-                                    slot=it["slot"]) for it in items]
             ring = None
-            if any(m.slot is not None for m in metas):
-                ring = {"name": self.ring.name, "slot_bytes": self.ring.slot_bytes}
-            ok = self.distribute_socket.send(p.pid, wire.encode_dispatch(metas, [it["frame"] for it in items], ring))
+            use_ring = p.shm and any(it["slot"] is not None for it in items)
+            if use_ring:
+                sid = items[0]["slot"] // self.ring_slots
+                ring = {"name": self._slices[sid].ring.name, "slot_bytes": self._slices[sid].ring.slot_bytes}
+            metas, payloads = [], []
+            for it in items:
+                in_ring = use_ring and it["slot"] is not None
+                metas.append(wire.FrameMeta(index=it["frame_index"], nbytes=it["nbytes"], shape=it["shape"],
+                                            slot=it["slot"] % self.ring_slots if in_ring else None))
+                payloads.append(None if in_ring else (it["frame"] if it["slot"] is None else
+                                                      bytes(self.in_view(it["slot"], it["nbytes"]))))
+            ok = self.distribute_socket.send(p.pid, wire.encode_dispatch(metas, payloads, ring))
         if ok:
             p.frames_sent += len(items)
+            batch = [time.monotonic(), set()]
+            for it in items:
+                it["attempts"] += 1
+                it["_batch"] = batch
+                p.inflight[it["frame_index"]] = it
+                batch[1].add(it["frame_index"])
+            p.batches.append(batch)
         return ok
+
+    def _unsend(self, p: _Peer, items: List[dict]) -> None:
+        """The transport refused a dispatch (the worker is gone): back to the queues."""
+        if self.policy == "latest":
+            for it in items:
+                self._drop(it)
+        else:
+            self._relane(items)
+        self._evict(p, "dispatch refused (worker disconnected)", gone=True)
+
+    def _relane(self, items: List[dict]) -> None:
+        """Put frame copies back at the front of their queues, in index order."""
+        by_lane: Dict[int, list] = {}
+        lanes: Dict[int, Deque[dict]] = {}
+        for it in items:
+            ln = self._lane_for(it)
+            lanes[id(ln)] = ln
+            by_lane.setdefault(id(ln), []).append(it)
+        for key, its in by_lane.items():
+            ln = lanes[key]
+            merged = sorted(its + list(ln), key=lambda x: x["frame_index"])
+            ln.clear()
+            ln.extend(merged)
+        self._cv.notify_all()
+
+    # ---- worker loss -----------------------------------------------------------------------
+    def _check_deadlines(self) -> None:
+        if self.batch_timeout <= 0:
+            return
+        now = time.monotonic()
+        with self._cv:
+            for p in list(self._peers.values()):
+                if p.alive and p.batches and now - p.batches[0][0] > self.batch_timeout:
+                    self._evict(p, f"no result within {self.batch_timeout:g} s")
+
+    def _evict(self, p: _Peer, reason: str, gone: bool = False) -> None:
+        """Take ``p`` out of service: re-queue (or lose, after ``max_attempts``) what it holds."""
+        was_alive = p.alive
+        p.alive = False
+        p.gone = p.gone or gone
+        p.requests.clear()
+        if was_alive and gone and not p.inflight and not p.queue:
+            self.departures += 1            # left with nothing outstanding
+        elif was_alive:
+            p.evictions += 1
+            self.evictions += 1
+            if self.verbose:
+                print(f"Distributor: worker {p.pid.hex()} evicted ({reason}); "
+                      f"{len(p.inflight)} frames in flight re-queued")
+        requeue = []
+        for idx in sorted(p.inflight):
+            it = p.inflight[idx]
+            it.pop("_batch", None)
+            p.quarantine[idx] = it          # its slot stays out of use until a result frees it
+            if self.policy == "latest" or it["attempts"] >= self.max_attempts:
+                self._lose(idx)
+                continue
+            clone = dict(it, slot=None, src_slot=it["slot"])
+            if it["slot"] is not None:
+                self._clone_src[it["slot"]] = clone
+            self._copies[idx] = self._copies.get(idx, 0) + 1
+            self.frames_requeued += 1
+            requeue.append(clone)
+        p.inflight.clear()
+        p.batches.clear()
+        if p.queue:
+            requeue.extend(p.queue)
+            p.queue.clear()
+        if self.policy == "shard":
+            self._rebalance_shards()
+        if requeue:
+            self._relane(requeue)
+        if p.gone:  # nothing can come back from it: its quarantined slots are free again
+            for it in p.quarantine.values():
+                self._free_slot(it.get("slot"))
+                self._copy_done(it["frame_index"])
+            p.quarantine.clear()
+        self._cv.notify_all()
 
     # ---- collect (distributor.py:253-289) ------------------------------------------------
     def check_inverter_output(self):
@@ -470,38 +914,75 @@ class Distributor:
                 print(f"Error receiving inverted frame: {e}")
                 continue
 
+    def _find_copy(self, p: Optional[_Peer], idx: int):
+        """(worker, dispatched copy) of a result; the worker's copy leaves its in-flight set."""
+        cands = [p] if p is not None else list(self._peers.values())
+        for q in cands:
+            it = q.inflight.pop(idx, None)
+            if it is not None:
+                b = it.pop("_batch", None)
+                if b is not None:
+                    b[1].discard(idx)
+                while q.batches and not q.batches[0][1]:
+                    q.batches.popleft()
+                return q, it
+            it = q.quarantine.pop(idx, None)
+            if it is not None:
+                return q, it
+        return None, None
+
     def _on_result(self, res: wire.Result):
         pid_val = int(res.pid) if res.pid.isdigit() else res.pid
         for sp in res.spans:
             self.log_gpu_span(sp.get("name", "?"), float(sp["begin"]), float(sp["end"]), pid_val,
                               int(sp.get("bytes", 0)))
+        with self._cv:
+            sender = self._by_wid.get(res.wid) if res.wid else None
         for m, payload in zip(res.metas, res.payloads):
-            self.log_frame_complete_timing(m.index, m.start, m.end, "frame_inverted_received",
-                                           int(res.pid) if res.pid.isdigit() else res.pid)
-            if m.error is not None:
-                with self._cv:
+            self.log_frame_complete_timing(m.index, m.start, m.end, "frame_inverted_received", pid_val)
+            with self._cv:
+                q, it = self._find_copy(sender, m.index)
+                slot = it.get("slot") if it is not None else None
+                if q is not None:
+                    q.results += 1
+                    if m.error is not None:
+                        q.errors += 1
+                tracked = it is not None
+                if tracked and m.index in self._settled:    # a re-queued frame's second result
+                    self.duplicates += 1
+                    self._free_slot(slot)
+                    self._copy_done(m.index)
+                    continue
+                if tracked:
+                    self._copy_done(m.index)
+                    self._settle(m.index)
+                if m.error is not None:
                     self.result_errors += 1
-                    self._free_slot(m.index)
+                    self._free_slot(slot)
                     if self.reassembly == "ordered":
                         self._ordered.mark_lost(m.index)
                         self._released.extend(self._ordered.pop_ready())
                         self._cv.notify_all()
-                continue
-            if m.slot is not None:
-                # zero-copy: hand out the slot's output half; the consumer releases it
-                data = self.ring.out_view(m.slot, m.nbytes) if self.zero_copy else \
-                    bytes(self.ring.out_view(m.slot, m.nbytes))
-            else:
-                data = payload
-            with self._cv:
-                if not (self.zero_copy and m.slot is not None):
-                    self._free_slot(m.index)
+                    continue
+                if m.slot is not None and slot is None:
+                    continue  # a ring result with no dispatch record: nothing to read it from
+                keep = self.zero_copy and m.slot is not None
+                if m.slot is not None:
+                    view = self.out_view(slot, m.nbytes)
+                    data = view if keep else bytes(view)
+                else:
+                    data = payload
+                if keep:
+                    self._held[m.index] = slot
+                else:
+                    self._free_slot(slot)
                 self.results_received += 1
                 if self.reassembly == "display":
                     self._display.receive(m.index, data, res.pid, m.start, m.end)
                 else:
                     self._ordered.push(m.index, data, {"process_id": res.pid, "start_time": m.start,
-                                                       "end_time": m.end, "shape": m.shape, "slot": m.slot})
+                                                       "end_time": m.end, "shape": m.shape,
+                                                       "slot": slot if keep else None})
                     self._released.extend(self._ordered.pop_ready())
                 self._cv.notify_all()
 
@@ -543,17 +1024,31 @@ class Distributor:
     def release_frame(self, index: int) -> None:
         """zero_copy: return frame ``index``'s ring slot once its result view is consumed."""
         with self._cv:
-            self._free_slot(index)
+            self._free_slot(self._held.pop(index, None))
 
     def num_workers(self) -> int:
         with self._lock:
-            return len(self._peers)
+            return sum(1 for p in self._peers.values() if p.alive)
 
     def ordering_stats(self) -> dict:
         with self._lock:
             s = self._ordered.stats()
             s.update({"frames_dropped": self.frames_dropped, "results_received": self.results_received,
-                      "result_errors": self.result_errors,
-                      "workers": {p.pid.hex(): {"sent": p.frames_sent, "shard": p.shard}
+                      "result_errors": self.result_errors, "frames_lost": self.frames_lost,
+                      "frames_requeued": self.frames_requeued, "duplicates": self.duplicates,
+                      "evictions": self.evictions, "departures": self.departures,
+                      "workers": {p.pid.hex(): {"sent": p.frames_sent, "results": p.results, "alive": p.alive,
+                                                "home_shard": p.home_shard,
+                                                "shards": sorted(k for k, o in self._shard_owner.items()
+                                                                 if o == p.pid),
+                                                "in_flight": len(p.inflight), "evictions": p.evictions,
+                                                "slice": self._slice_info(p.slice)}
                                   for p in self._peers.values()}})
             return s
+
+    def _slice_info(self, sid: Optional[int]) -> Optional[dict]:
+        if sid is None:
+            return None
+        sl = self._slices[sid]
+        return {"name": sl.ring.name, "bytes": sl.ring.nbytes, "numa": sl.numa, "numa_bound": sl.bound,
+                "free": len(sl.free)}

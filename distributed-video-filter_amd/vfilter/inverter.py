@@ -157,9 +157,14 @@ class InverterWorker(Worker):
         spans = gpu_spans(self.ctx.last_timeline(), t_end - ms / 1e3) if ms >= 0 else []
         return dsts, spans
 
+    def numa_node(self):
+        from .numa import gpu_numa_node
+        return gpu_numa_node(self.device)
+
     def on_ring_attached(self, ring) -> None:
-        """Page-lock the whole shared-memory ring once: the slot pipeline then DMAs straight
-        from the input halves and into the output halves (no staging copy)."""
+        """Page-lock the ring (this worker's own slice, with the distributor's per-worker
+        layout) once: the slot pipeline then DMAs straight from the input halves and into the
+        output halves (no staging copy)."""
         try:
             self._registered.append(self.ctx.host_register(ring.buf, ring.nbytes))
         except Exception as e:  # still correct through staging, just slower

@@ -41,8 +41,7 @@ class FrameRing:
             self.shm = shared_memory.SharedMemory(create=True, size=size)
             self.owner = True
         else:
-            self.shm = shared_memory.SharedMemory(name=name)
-            _untrack(self.shm)
+            self.shm = _attach(name)
             self.owner = False
             self.slot_bytes = slot_bytes
             self.nslots = self.shm.size // (2 * slot_bytes)
@@ -111,11 +110,19 @@ def shm_free_bytes() -> Optional[int]:
         return None
 
 
-def _untrack(shm: shared_memory.SharedMemory) -> None:
-    """An attaching process must not unlink the owner's segment at exit (CPython registers
-    every attach with the resource tracker; bpo-38119)."""
-    try:
-        from multiprocessing import resource_tracker
-        resource_tracker.unregister(shm._name, "shared_memory")  # type: ignore[attr-defined]
-    except Exception:
-        pass
+_attach_lock = threading.Lock()
+
+
+def _attach(name: str) -> shared_memory.SharedMemory:
+    """Map the owner's segment without registering it with the resource tracker: CPython
+    registers every attach and would unlink the owner's segment when this process exits
+    (bpo-38119); unregistering afterwards instead removes the owner's own registration when
+    the tracker is shared (multiprocessing "spawn" children share their parent's)."""
+    from multiprocessing import resource_tracker
+    with _attach_lock:
+        reg = resource_tracker.register
+        resource_tracker.register = lambda *a, **k: None
+        try:
+            return shared_memory.SharedMemory(name=name)
+        finally:
+            resource_tracker.register = reg

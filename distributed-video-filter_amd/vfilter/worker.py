@@ -67,6 +67,7 @@ class Worker:
         self._ring_lock = threading.Lock()
         self._ring: Optional[FrameRing] = None
         self._ring_name: Optional[str] = None
+        self.wid = f"{self.process_id}-{id(self):x}"  # ties results to this loop's requests
         if verbose:
             print(f"Worker started on ports {distribute_port} (request) and {collect_port} (send)")
             print(f"Process ID: {self.process_id}")
@@ -96,6 +97,11 @@ class Worker:
 
     def on_ring_attached(self, ring: FrameRing) -> None:
         """Hook: a GPU worker page-locks the ring here."""
+
+    def numa_node(self) -> Optional[int]:
+        """Hook: NUMA node the distributor should place this worker's ring slice on (a GPU
+        worker returns its GPU's node)."""
+        return None
 
     # -- loop --------------------------------------------------------------------------
     def start(self, max_frames: Optional[int] = None):
@@ -240,7 +246,12 @@ class Worker:
                     payload = r
             payloads.append(payload)
             metas.append(om)
-        self.collect_socket.send(wire.encode_result(self.process_id, metas, payloads, spans))
+        try:
+            self.collect_socket.send(wire.encode_result(self.process_id, metas, payloads, spans, wid=self.wid))
+        except Exception as e:  # the distributor re-queues frames whose result never arrives
+            self.errors += 1
+            print(f"Error in worker: could not send results {[m.index for m in metas]}: {e}")
+            return True
         self.frames_processed += len(metas)
         return True
 
@@ -251,25 +262,34 @@ class Worker:
         arrival order."""
         outstanding = 0
         jobs: "collections.deque" = collections.deque()
+        numa = self.numa_node()
         while self.running and (max_frames is None or self.frames_processed < max_frames):
-            while outstanding < self.depth:
-                self.dealer_socket.send(wire.encode_request(self.batch, shm=True))
-                outstanding += 1
-            while jobs and self._finish_job(jobs[0], block=len(jobs) >= self.inflight):
-                jobs.popleft()
-            if len(jobs) >= self.inflight:
-                continue
-            if not self.dealer_socket.poll(1 if jobs else 10):
-                continue
-            parts = self.dealer_socket.recv()
-            start_time = time.time()
             try:
-                d = wire.decode_dispatch(parts)
-            except Exception as e:
-                print(f"Error in worker: bad dispatch message: {e}")
-                continue
-            if d.version == 1:
-                outstanding -= 1
-            jobs.append(self._start_job(d, start_time))
+                while outstanding < self.depth:
+                    self.dealer_socket.send(wire.encode_request(self.batch, shm=True, wid=self.wid, numa=numa))
+                    outstanding += 1
+                while jobs and self._finish_job(jobs[0], block=len(jobs) >= self.inflight):
+                    jobs.popleft()
+                if len(jobs) >= self.inflight:
+                    continue
+                if not self.dealer_socket.poll(1 if jobs else 10):
+                    continue
+                parts = self.dealer_socket.recv()
+                start_time = time.time()
+                try:
+                    d = wire.decode_dispatch(parts)
+                except Exception as e:
+                    print(f"Error in worker: bad dispatch message: {e}")
+                    continue
+                if d.version == 1:
+                    outstanding -= 1
+                jobs.append(self._start_job(d, start_time))
+            except Exception as e:  # worker.py:74-76: report and keep serving
+                self.errors += 1
+                print(f"Error in worker: {type(e).__name__}: {e}")
+                time.sleep(0.01)
         while jobs:  # finish what was accepted before stopping
-            self._finish_job(jobs.popleft(), block=True)
+            try:
+                self._finish_job(jobs.popleft(), block=True)
+            except Exception as e:
+                print(f"Error in worker: {type(e).__name__}: {e}")

@@ -18,9 +18,24 @@ from vfilter.worker import Worker  # noqa: E402
 
 
 class OracleWorker(Worker):
+    delay = 0.0
+
     def __call__(self, frame):
         from oracle import oracle
+        if self.delay > 0:
+            import time
+            time.sleep(self.delay)
         return oracle.invert_bytes(frame)
+
+
+class ResizingWorker(OracleWorker):
+    """A plugin whose result size differs from its input's, like a re-encoded JPEG: the
+    inverted bytes plus a 7-byte trailer, or half of them for frames of 64 bytes or less."""
+
+    def __call__(self, frame):
+        from oracle import oracle
+        x = oracle.invert_bytes(frame)
+        return x[: len(x) // 2] if len(x) <= 64 else x + b"trailer"
 
 
 def _watch(stop_event, worker):
@@ -36,7 +51,9 @@ def run_worker(dport, cport, stop_event, protocol="v1", batch=4, transport="tcp"
                            install_signal_handlers=False, batch=batch, protocol=protocol,
                            transport=transport)
     else:
-        w = OracleWorker("127.0.0.1", dport, cport, batch=batch, protocol=protocol, transport=transport)
+        cls = ResizingWorker if kind == "resizing" else OracleWorker
+        w = cls("127.0.0.1", dport, cport, batch=batch, protocol=protocol, transport=transport)
+        w.delay = delay
     threading.Thread(target=_watch, args=(stop_event, w), daemon=True).start()
     try:
         w.start()
@@ -44,18 +61,32 @@ def run_worker(dport, cport, stop_event, protocol="v1", batch=4, transport="tcp"
         w.close()
 
 
+class _Stops:
+    """One stop event per worker process: setting an event a killed process was waiting on
+    would block forever (multiprocessing's Condition waits for the sleeper to acknowledge)."""
+
+    def __init__(self, events):
+        self.events = events
+
+    def set_for(self, procs):
+        for ev, p in zip(self.events, procs):
+            if p.is_alive():
+                ev.set()
+
+
 def spawn_workers(n, dport, cport, **kw):
     import multiprocessing as mp
     ctx = mp.get_context("spawn")
-    stop = ctx.Event()
-    procs = [ctx.Process(target=run_worker, args=(dport, cport, stop), kwargs=kw, daemon=True) for _ in range(n)]
+    stops = _Stops([ctx.Event() for _ in range(n)])
+    procs = [ctx.Process(target=run_worker, args=(dport, cport, ev), kwargs=kw, daemon=True)
+             for ev in stops.events]
     for p in procs:
         p.start()
-    return stop, procs
+    return stops, procs
 
 
 def stop_workers(stop, procs, timeout=10.0):
-    stop.set()
+    stop.set_for(procs)
     for p in procs:
         p.join(timeout)
         if p.is_alive():

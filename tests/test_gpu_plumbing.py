@@ -36,35 +36,63 @@ def _run(d, frames, n_workers, batch, timeout=60):
         stop_workers(stop, procs)
 
 
-@pytest.mark.timeout(180)
-def test_config3_4k_batch16_sharded_in_order_ring():
-    d = Distributor(0, 0, policy="shard", reassembly="ordered", shard_workers=2, shard_chunk=16,
-                    queue_size=64, ring_slots=24, ring_slot_bytes=2160 * 3840 * 3, transport="tcp",
-                    host="127.0.0.1", verbose=False)
+def _sharded_4k(nworkers, nframes, ring_slots):
+    """configs[2]: 4K frames, batch 16, frame-index shards of 16 over ``nworkers`` GPU worker
+    processes (all on this box's one GPU), each with its own ring slice; in-order release,
+    bit-exact, chunk c served by the owner of shard c % nworkers, every slot returned."""
+    d = Distributor(0, 0, policy="shard", reassembly="ordered", shard_workers=nworkers, shard_chunk=16,
+                    queue_size=2 * 16 * nworkers, ring_slots=ring_slots, ring_slot_bytes=2160 * 3840 * 3,
+                    transport="tcp", host="127.0.0.1", verbose=False)
     d.start()
     try:
-        frames = [oracle.synthetic_frame(i % 4, 2160, 3840) for i in range(64)]
-        stop, procs = spawn_workers(2, d.distribute_port, d.collect_port, protocol="v1", batch=16, kind="gpu")
+        base = [oracle.synthetic_frame(s, 2160, 3840) for s in range(4)]
+        want = [oracle.invert(b).reshape(-1) for b in base]
+        stop, procs = spawn_workers(nworkers, d.distribute_port, d.collect_port, protocol="v1", batch=16,
+                                    kind="gpu")
         try:
-            time.sleep(3.0)  # both workers register (GPU context creation) before frames flow
-            th = threading.Thread(target=lambda: [d.add_frame_for_distribution(f) for f in frames])
+            t0 = time.time()
+            while d.num_workers() < nworkers:  # every shard's home worker registered
+                assert time.time() - t0 < 90, f"{d.num_workers()} of {nworkers} workers registered"
+                assert all(p.is_alive() for p in procs), "a worker process died"
+                time.sleep(0.05)
+            th = threading.Thread(target=lambda: [d.add_frame_for_distribution(base[i % 4]) for i in range(nframes)])
             th.start()
             owners = []
-            for i in range(len(frames)):
+            for i in range(nframes):
                 item = d.get_next_frame(timeout=60)
                 assert item is not None, d.ordering_stats()
                 idx, data, info = item
                 assert idx == i
-                assert np.array_equal(np.frombuffer(data, np.uint8), oracle.invert(frames[i]).reshape(-1))
+                assert np.array_equal(np.frombuffer(data, np.uint8), want[i % 4]), i
                 owners.append(info["process_id"])
             th.join()
         finally:
             stop_workers(stop, procs)
-        chunks = [set(owners[c * 16:(c + 1) * 16]) for c in range(4)]
-        assert all(len(c) == 1 for c in chunks) and chunks[0] != chunks[1] and chunks[0] == chunks[2]
-        assert d.ring.free_slots() == 24
+        nchunks = nframes // 16
+        chunks = [set(owners[c * 16:(c + 1) * 16]) for c in range(nchunks)]
+        assert all(len(c) == 1 for c in chunks)
+        owner = [next(iter(c)) for c in chunks]
+        assert len(set(owner[:nworkers])) == nworkers       # one shard per worker
+        assert all(owner[c] == owner[c % nworkers] for c in range(nchunks))  # chunk_owner(i, 16, N)
+        st = d.ordering_stats()
+        assert st["released"] == nframes and st["lost"] == 0 and st["evictions"] == 0
+        assert d.free_slots() == d.total_slots() == nworkers * ring_slots
+        return st
     finally:
         d.cleanup()
+
+
+@pytest.mark.timeout(180)
+def test_config3_4k_batch16_sharded_in_order_ring():
+    _sharded_4k(2, 64, 24)
+
+
+@pytest.mark.timeout(240)
+def test_config2_4k_batch16_eight_way_shard_one_card():
+    """BASELINE configs[2]'s fan-out width: 8 worker processes (on the box's one GPU), 8
+    frame-index shards, 160 frames (10 chunks of 16) through 8 per-worker ring slices."""
+    st = _sharded_4k(8, 160, 16)
+    assert len(st["workers"]) == 8
 
 
 @pytest.mark.timeout(180)
@@ -129,6 +157,36 @@ def test_inverter_worker_jpeg_mode_matches_reference_path():
     finally:
         w.close()
         wd.close()
+
+
+@pytest.mark.timeout(180)
+def test_jpeg_mode_through_ring_in_order():
+    """JPEG frames (the reference default) through the shared-memory ring: each result is a
+    JPEG of its own size, written into the slot's output half (or sent back over the socket
+    when it does not fit) and read with its own length."""
+    from oracle import jpeg as J
+    jpgs = [J.encode(J.synthetic_scene(i, 480, 640) if i % 3 else
+                     np.random.default_rng(i).integers(0, 256, (96, 128, 3), dtype=np.uint8), 85)
+            for i in range(24)]
+    slot = max(len(j) for j in jpgs)
+    d = Distributor(0, 0, policy="pull", reassembly="ordered", queue_size=16, ring_slots=8, ring_slot_bytes=slot,
+                    transport="tcp", host="127.0.0.1", verbose=False)
+    d.start()
+    stop, procs = spawn_workers(2, d.distribute_port, d.collect_port, protocol="v1", batch=4, kind="gpu",
+                                use_jpeg=True)
+    try:
+        th = threading.Thread(target=lambda: [d.add_frame_for_distribution(j) for j in jpgs])
+        th.start()
+        for i in range(len(jpgs)):
+            item = d.get_next_frame(timeout=60)
+            assert item is not None, d.ordering_stats()
+            assert item[0] == i and bytes(item[1]) == J.invert_jpeg(jpgs[i]), i
+        th.join()
+        assert d.free_slots() == d.total_slots()
+        assert d.ordering_stats()["result_errors"] == 0
+    finally:
+        stop_workers(stop, procs)
+        d.cleanup()
 
 
 @pytest.mark.timeout(180)

@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""Host->host JPEG invert (the worker's use_jpeg=True path) in the forms the worker could use,
+one size per run, each in a fresh process so codec settings (read at codec creation) apply:
+  1thread      one invert_batch call at a time
+  2threads     two host threads, each call leasing its own codec (kernels ordered by the
+               context's compute gate)
+  2threads_nogate   the same with VF_JPEG_GATE=0 (kernels of the two codecs may overlap)
+Prints one JSON line per mode.  VF_JPEG_TRACE=1 adds the library's per-call phase times.
+  python tools/jpeg_modes.py 1080p [mode]"""
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "distributed-video-filter_amd")]
+
+SIZES = {"480p": (480, 640), "1080p": (1080, 1920), "4k": (2160, 3840)}
+
+
+def run(size, mode, batch=32, reps=12):
+    from vfilter import Context
+    from vfilter.jpeg import TurboJPEG
+    from vfilter.synthetic import synthetic_scene
+    h, w = SIZES[size]
+    ctx = Context(0)
+    tj = TurboJPEG(ctx=ctx)
+    jpgs = tj.encode_batch([synthetic_scene(s, h, w) for s in range(8)])
+    jpgs = [jpgs[i % 8] for i in range(batch)]
+    if mode == "1thread":
+        for _ in range(3):
+            tj.invert_batch(jpgs)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            tj.invert_batch(jpgs)
+        dt = time.perf_counter() - t0
+    else:
+        from concurrent.futures import ThreadPoolExecutor
+        with ThreadPoolExecutor(2) as ex:
+            list(ex.map(lambda _: tj.invert_batch(jpgs), range(4)))
+            t0 = time.perf_counter()
+            list(ex.map(lambda _: tj.invert_batch(jpgs), range(reps)))
+            dt = time.perf_counter() - t0
+    ms, stages = ctx.jpeg_bench_invert(jpgs, 85, 1, 0, iters=10)
+    print(json.dumps({"size": size, "mode": mode, "batch": batch, "fps": round(reps * batch / dt, 1),
+                      "ms_per_batch": round(dt / reps * 1e3, 3), "gpu_resident_ms": round(ms, 3)}), flush=True)
+    ctx.close()
+
+
+if __name__ == "__main__":
+    size = sys.argv[1] if len(sys.argv) > 1 else "1080p"
+    if len(sys.argv) > 2:
+        run(size, sys.argv[2])
+    else:
+        for mode in ("1thread", "2threads", "2threads_nogate"):
+            env = dict(os.environ)
+            if mode == "2threads_nogate":
+                env["VF_JPEG_GATE"] = "0"
+            subprocess.run([sys.executable, __file__, size, mode], env=env, check=True, timeout=300)

@@ -4,18 +4,20 @@ over N workers, in-order reassembly) and configs[3] (mixed 480p/1080p/4K stream,
 overhead), host->host through the whole fan-out.
 
 One Distributor (lossless ``shard`` or ``pull`` policy, ``ordered`` reassembly, shared-memory
-ring, zero-copy in and out) feeds N ``python -m vfilter.inverter`` worker processes, worker i
-on GPU i % G.  Each worker page-locks the ring, so frames go ring -> GPU -> ring by DMA.
+ring with one slice per worker on its GPU's NUMA node, zero-copy in and out) feeds N
+``python -m vfilter.inverter`` worker processes, worker i on GPU i % G.  Each worker page-locks
+its own slice, so frames go slice -> GPU -> slice by DMA.
 Reported: delivered frames/s in index order, GB/s each way, per-frame latency (commit ->
 in-order release), reorder wait and buffer depth.
 
   python tools/pipeline_bench.py --workers 2 --size 4k --batch 16 --frames 512
   python tools/pipeline_bench.py --workers 2 --size mixed --policy pull
 
-Producer modes: ``resident`` (default) — ring slots are filled once with random bytes and
-frames are committed without a host copy, isolating distribution + PCIe + kernel +
-reassembly; ``copy`` — each frame is copied into its slot from a pre-generated frame (what a
-producer that cannot decode straight into the ring pays).
+Producer modes: ``copy`` (default) — each frame is copied into its slot from a pre-generated
+frame (what a producer that cannot decode straight into the ring pays); ``resident`` — ring
+slots are filled once with random bytes and frames are committed without a host copy,
+isolating distribution + PCIe + kernel + reassembly.  Every ``--verify-every``-th frame is
+checked in full against its input; the others on their first and last 4 KiB.
 """
 import argparse
 import json
@@ -45,9 +47,10 @@ def main():
     ap.add_argument("--frames", type=int, default=512)
     ap.add_argument("--batch", type=int, default=16)
     ap.add_argument("--policy", default="shard", choices=("shard", "pull"))
-    ap.add_argument("--producer", default="resident", choices=("resident", "copy"))
-    ap.add_argument("--ring-slots", type=int, default=0, help="0 = 4 batches per worker, capped by /dev/shm")
-    ap.add_argument("--verify-every", type=int, default=64)
+    ap.add_argument("--producer", default="copy", choices=("resident", "copy"))
+    ap.add_argument("--ring-slots", type=int, default=0,
+                    help="slots per worker slice (0 = 3 batches, capped by /dev/shm)")
+    ap.add_argument("--verify-every", type=int, default=8)
     ap.add_argument("--inflight", type=int, default=2, help="batches in progress per worker")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
@@ -55,17 +58,17 @@ def main():
     shapes = [SIZES["480p"], SIZES["1080p"], SIZES["4k"]] if args.size == "mixed" else [SIZES[args.size]]
     fbytes = [h * w * 3 for h, w in shapes]
     slot_bytes = max(fbytes)
-    slots = args.ring_slots or 4 * args.batch * args.workers
+    slots = args.ring_slots or 3 * args.batch
     free = shm_free_bytes()
     if free is not None:
-        slots = max(2 * args.batch, min(slots, int(free * 0.6) // (2 * slot_bytes)))
+        slots = max(2 * args.batch, min(slots, int(free * 0.6) // (2 * slot_bytes * args.workers)))
     ngpu = args.gpus
     if ngpu <= 0:
         from vfilter import device_count
         ngpu = max(1, device_count())
 
     d = Distributor(0, 0, policy=args.policy, reassembly="ordered", transport="tcp", host="127.0.0.1",
-                    queue_size=4 * args.batch * args.workers, ring_slots=slots, ring_slot_bytes=slot_bytes,
+                    queue_size=3 * args.batch * args.workers, ring_slots=slots, ring_slot_bytes=slot_bytes,
                     shard_workers=args.workers, shard_chunk=args.batch, zero_copy=True, verbose=False)
     d.start()
     env = dict(os.environ, PYTHONPATH=PKG + os.pathsep + os.environ.get("PYTHONPATH", ""))
@@ -88,11 +91,12 @@ def main():
 
         rng = np.random.default_rng(0)
         # resident content: each slot's input half holds random bytes once
-        for s in range(slots):
-            d.ring.in_view(s, slot_bytes)[:] = rng.integers(0, 256, slot_bytes, dtype=np.uint8)
+        if args.producer == "resident":
+            for s in range(d.total_slots()):
+                d.in_view(s, slot_bytes)[:] = rng.integers(0, 256, slot_bytes, dtype=np.uint8)
         pregen = [rng.integers(0, 256, fb, dtype=np.uint8) for fb in fbytes]
-        # warmup: every worker maps and page-locks the ring on its first batch (hipHostRegister
-        # of the whole ring, ~0.15 s per GB) -- a one-off start-up cost kept out of the timing
+        # warmup: every worker maps and page-locks its slice on its first batch (hipHostRegister,
+        # ~0.15 s per GB) -- a one-off start-up cost kept out of the timing
         warm = 2 * args.batch * args.workers * len(shapes)
         n = args.frames
         commit_t = np.zeros(warm + n)
@@ -126,11 +130,12 @@ def main():
             idx, view, info = item
             if idx != i:
                 errors.append(f"order: got {idx} expected {i}")
-            src = d.ring.in_view(info["slot"], view.nbytes)
+            src = d.in_view(info["slot"], view.nbytes)
             if i % args.verify_every == 0:
-                ok = np.array_equal(view, np.bitwise_not(src))  # sanity check of the sample
+                ok = np.array_equal(view, np.bitwise_not(src))
             else:
-                ok = np.array_equal(view[:4096], np.bitwise_not(src[:4096]))
+                ok = np.array_equal(view[:4096], np.bitwise_not(src[:4096])) and \
+                    np.array_equal(view[-4096:], np.bitwise_not(src[-4096:]))
             if not ok:
                 errors.append(f"frame {i} differs")
             if i >= warm:
@@ -143,10 +148,14 @@ def main():
         lat = (release_t[warm:] - commit_t[warm:]) * 1e3
         st = d.ordering_stats()
         st["max_depth"] = max(st["max_depth"], d_stats0["max_depth"])
+        slices = [w["slice"] for w in st["workers"].values() if w["slice"]]
         result = {"kind": "pipeline", "size": args.size, "workers": args.workers, "gpus": min(ngpu, args.workers),
                   "inflight_per_worker": args.inflight,
                   "policy": args.policy, "producer": args.producer, "batch": args.batch, "frames": n,
-                  "ring_slots": slots, "fps": round(n / el, 1), "GBps_each_way": round(total_bytes / el / 1e9, 2),
+                  "ring_slots_per_worker": slots, "verify_full_every": args.verify_every,
+                  "slice_bytes_per_worker": slices[0]["bytes"] if slices else None,
+                  "slice_numa": [sl["numa"] for sl in slices], "slice_numa_bound": [sl["numa_bound"] for sl in slices],
+                  "evictions": st["evictions"], "frames_lost": st["frames_lost"], "fps": round(n / el, 1), "GBps_each_way": round(total_bytes / el / 1e9, 2),
                   "latency_ms_mean": round(float(lat.mean()), 3), "latency_ms_p99": round(float(np.percentile(lat, 99)), 3),
                   "reorder_wait_mean_ms": round(st["reorder_wait_mean_ms"], 3),
                   "reorder_wait_max_ms": round(st["reorder_wait_max_ms"], 3), "max_buffer_depth": st["max_depth"],

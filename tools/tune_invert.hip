@@ -16,6 +16,37 @@
 #include <vector>
 
 #include "vf_internal.h"
+#include "vf_stream.h"
+
+// The variants (the library ships U4-NT, vf_kernels.hip).  Un = n independent 16-B loads in
+// flight per lane; NT = nontemporal loads and stores, NTL / NTS = on one side only; CHUNK =
+// contiguous tiles per workgroup instead of grid-stride.
+enum { kU4NT, kU2NT, kU8NT, kU1NT, kU4NTL, kU4NTS, kU4, kU2, kU8, kU1, kU4NTChunk, kU8NTChunk, kVariantCount };
+
+static const char *vname(int v) {
+  static const char *names[kVariantCount] = {"u4-nt", "u2-nt", "u8-nt", "u1-nt", "u4-ntl", "u4-nts",
+                                             "u4",    "u2",    "u8",    "u1",    "u4-nt-chunk", "u8-nt-chunk"};
+  return (v >= 0 && v < kVariantCount) ? names[v] : "?";
+}
+
+static hipError_t launch_variant(int v, const uint8_t *s, uint8_t *d, size_t n, int mb, hipStream_t st) {
+  using vf::launch_stream;
+  switch (v) {
+    case kU4NT: return launch_stream<4, true, true>(s, d, n, mb, st);
+    case kU2NT: return launch_stream<2, true, true>(s, d, n, mb, st);
+    case kU8NT: return launch_stream<8, true, true>(s, d, n, mb, st);
+    case kU1NT: return launch_stream<1, true, true>(s, d, n, mb, st);
+    case kU4NTL: return launch_stream<4, true, false>(s, d, n, mb, st);
+    case kU4NTS: return launch_stream<4, false, true>(s, d, n, mb, st);
+    case kU4: return launch_stream<4, false, false>(s, d, n, mb, st);
+    case kU2: return launch_stream<2, false, false>(s, d, n, mb, st);
+    case kU8: return launch_stream<8, false, false>(s, d, n, mb, st);
+    case kU1: return launch_stream<1, false, false>(s, d, n, mb, st);
+    case kU4NTChunk: return launch_stream<4, true, true, true>(s, d, n, mb, st);
+    case kU8NTChunk: return launch_stream<8, true, true, true>(s, d, n, mb, st);
+    default: return hipErrorInvalidValue;
+  }
+}
 
 #define CK(x)                                                                       \
   do {                                                                              \
@@ -44,8 +75,6 @@ __global__ void check_kernel(const uint8_t *a, const uint8_t *b, size_t n, int *
   for (; i < n; i += stride)
     if ((uint8_t)~a[i] != b[i]) atomicAdd(bad, 1);
 }
-
-static const char *vname(int v) { return vf::variant_name(v); }
 
 // Large single-buffer experiment (configs[4]): one src of `bytes`, dst at several offsets
 // from a bigger allocation, and the same bytes as one launch vs sub-range launches.
@@ -115,18 +144,15 @@ int main(int argc, char **argv) {
   std::vector<Cfg> cfgs;
   const int mults[] = {2, 4, 8, 16, 32, 1 << 20};  // blocks per CU cap; huge = one tile per block
   const char *only = std::getenv("TUNE_VARIANTS");  // e.g. "0,1,2"
-  for (int v = 0; v < vf::kVariantCount; ++v) {
+  for (int v = 0; v < kVariantCount; ++v) {
     if (only && !std::strstr(only, std::to_string(v).c_str())) continue;
     for (int m : mults) cfgs.push_back({v, (int)std::min<long>((long)cus * m, 1 << 30)});
   }
 
   // correctness of every variant (unaligned tail exercised with batch - 7 bytes)
   for (const Cfg &c : cfgs) {
-    vf::LaunchCfg lc;
-    lc.variant = c.variant;
-    lc.max_blocks = c.blocks;
     CK(hipMemset(dst[0], 0, batch));
-    CK(vf::launch_invert(src[0] + 3, dst[0] + 3, batch - 7, lc, 0));
+    CK(launch_variant(c.variant, src[0] + 3, dst[0] + 3, batch - 7, c.blocks, 0));
     CK(hipMemset(bad, 0, sizeof(int)));
     hipLaunchKernelGGL(check_kernel, dim3(4096), dim3(256), 0, 0, src[0] + 3, dst[0] + 3,
                        batch - 7, bad);
@@ -146,14 +172,12 @@ int main(int argc, char **argv) {
   int slot = 0;
   for (int rd = 0; rd < rounds; ++rd) {
     for (size_t ci = 0; ci < cfgs.size(); ++ci) {
-      vf::LaunchCfg lc;
-      lc.variant = cfgs[ci].variant;
-      lc.max_blocks = cfgs[ci].blocks;
-      CK(vf::launch_invert(src[slot], dst[slot], batch, lc, 0));  // warm
+      const int v = cfgs[ci].variant, mb = cfgs[ci].blocks;
+      CK(launch_variant(v, src[slot], dst[slot], batch, mb, 0));  // warm
       slot = (slot + 1) % ring;
       CK(hipEventRecord(e0, 0));
       for (int l = 0; l < launches; ++l) {
-        CK(vf::launch_invert(src[slot], dst[slot], batch, lc, 0));
+        CK(launch_variant(v, src[slot], dst[slot], batch, mb, 0));
         slot = (slot + 1) % ring;
       }
       CK(hipEventRecord(e1, 0));
