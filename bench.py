@@ -109,15 +109,16 @@ def probe(args):
     """Child of rocprofv3 --pmc: launch the same kernel on the same ring, nothing else."""
     import numpy as np
     from vfilter import Context
-    ctx = Context(0)
+    ctx = Context(int(os.environ.get("VF_DEVICE", "0")))
     srcs, dsts, batch_bytes, _ = make_ring(ctx, args.batch, args.ring_gb, np)
     ctx.bench_device_ring(srcs, dsts, batch_bytes, args.steps)
     ctx.close()
 
 
-def pmc_traffic(args):
+def pmc_traffic(args, device=0):
     """HBM bytes per launch from two separate rocprofv3 --pmc passes (FETCH_SIZE needs 3 TCC
-    slots and WRITE_SIZE 2, so they cannot share a pass).  Returns (bytes, detail) or (None, why)."""
+    slots and WRITE_SIZE 2, so they cannot share a pass), on rank 0's GPU.  Returns (bytes,
+    detail) or (None, why)."""
     rp = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
     if not os.path.exists(rp):
         return None, "rocprofv3 not found"
@@ -127,7 +128,7 @@ def pmc_traffic(args):
         cmd = ["timeout", "-s", "KILL", "90", rp, "--pmc", ctr, "--output-format", "csv", "-d", out,
                "-o", "pmc", "--", sys.executable, os.path.abspath(__file__), "--probe",
                "--steps", "20", "--batch", str(args.batch), "--ring-gb", str(args.ring_gb)]
-        r = subprocess.run(cmd, capture_output=True, text=True)
+        r = subprocess.run(cmd, capture_output=True, text=True, env=dict(os.environ, VF_DEVICE=str(device)))
         files = glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True)
         if r.returncode != 0 or not files:
             shutil.rmtree(out, ignore_errors=True)
@@ -256,7 +257,7 @@ def resolution_leg(ctx, np, rank, world, steps, barrier_sync, reduce_max):
     return out
 
 
-def end_to_end(ctx, host_batch, batch, np, reps=8):
+def end_to_end(ctx, host_batch, batch, np, reps=16):
     """Host->host frames/s (PCIe-inclusive): one synchronous vf_invert_batch_host call per
     batch from pageable numpy memory and from pinned memory, and the worker's pipelined form
     (vf_invert_frames_async, two batches in flight, pinned) that keeps the engine busy across
@@ -318,16 +319,31 @@ def jpeg_mode(ctx, batch, iters=20):
         tj.invert_batch(jpgs)
     h2h = (time.perf_counter() - t0) / reps
     from concurrent.futures import ThreadPoolExecutor
-    with ThreadPoolExecutor(2) as ex:  # the worker's form (InverterWorker.submit_batch)
+    with ThreadPoolExecutor(2) as ex:  # two host threads, one call each at a time
         list(ex.map(lambda _: tj.invert_batch(jpgs), range(2)))
         t0 = time.perf_counter()
         list(ex.map(lambda _: tj.invert_batch(jpgs), range(10)))
         h2h_pipe = (time.perf_counter() - t0) / 10
+    # the worker's form (InverterWorker.submit_batch): one thread, two batches in flight
+    for _ in range(2):  # warm both codecs (a codec's first batch allocates its buffers)
+        a, b = tj.invert_batch_submit(jpgs), tj.invert_batch_submit(jpgs)
+        tj.invert_batch_result(a)
+        tj.invert_batch_result(b)
+    t0 = time.perf_counter()
+    q = [tj.invert_batch_submit(jpgs)]
+    for _ in range(19):
+        q.append(tj.invert_batch_submit(jpgs))
+        tj.invert_batch_result(q.pop(0))
+    tj.invert_batch_result(q.pop(0))
+    h2h_async = (time.perf_counter() - t0) / 20
     return {"workload": f"1080p JPEG (q85 4:2:2) decode -> bitwise_not -> encode, batch {batch}",
             "gpu_resident_fps": round(batch / (ms / 1e3), 1), "gpu_resident_ms_per_batch": round(ms, 3),
             "stages_ms": {k: round(v, 4) for k, v in stages.items()},
             "host_to_host_fps": round(batch / h2h, 1),
             "host_to_host_2threads_fps": round(batch / h2h_pipe, 1),
+            "host_to_host_worker_fps": round(batch / h2h_async, 1),
+            "host_to_host_note": "1 call at a time | 2 host threads | the worker's form: 1 thread, 2 batches "
+                                 "in flight (vf_jpeg_invert_submit / _wait / _fetch)",
             "jpeg_bytes_mean": round(sum(len(j) for j in jpgs) / batch)}, jpgs
 
 
@@ -350,25 +366,36 @@ def cpu_baseline_jpeg(jpgs, seconds):
             "sample": f"{n} x 1080p JPEG frames ({dt:.1f} s) through libjpeg-turbo 2.1.2, 1 thread"}
 
 
-def distributor_leg(nworkers, ngpu, frames_scale=1.0, timeout_s=150):
+def distributor_leg(nworkers, ngpu, host_gbps=None, pcie_gbps=None, frames_scale=1.0, timeout_s=150):
     """BASELINE.json configs[2] and configs[3] at this run's GPU count, host->host through the
-    whole fan-out: one Distributor (lossless, in-order reassembly, shared-memory ring) and one
-    `python -m vfilter.inverter` worker process per GPU (tools/pipeline_bench.py).
-      configs[2]  4K frames, batch 16, frame-index shards (policy "shard")
-      configs[3]  480p / 1080p / 4K interleaved 1:1:1, batch 16, credit-based pull (policy
-                  "pull"), reporting the ordering overhead (reorder wait, buffer depth)
-    Run by rank 0 as a child process group with a time limit, so a stuck worker cannot
-    outlive the bench; a failure is reported in the line, never raised."""
+    whole fan-out: one Distributor (lossless, in-order reassembly, one NUMA-bound shared-memory
+    ring slice per worker) and one `python -m vfilter.inverter` worker process per GPU
+    (tools/pipeline_bench.py).
+      configs[2]           4K frames, batch 16, frame-index shards (policy "shard"); the
+                           producer copies every frame into its slot ("copy")
+      configs[2]_resident  the same with frames committed in place (no producer copy)
+      configs[3]           480p / 1080p / 4K interleaved 1:1:1, batch 16, pull policy,
+                           producer copy, reporting the ordering overhead
+    Every 8th frame is verified in full, the others on their first and last 4 KiB.  Beside each
+    leg: the ceilings for this many GPUs — PCIe (the pinned pipelined rate measured in
+    end_to_end, each way, per GPU) and host DRAM (the host's measured r+w bandwidth from the
+    multi-process CPU baseline over the host bytes each frame costs: producer copy read+write,
+    H2D read, D2H write, verification reads).  Run by rank 0 as a child process group with a
+    time limit, so a stuck worker cannot outlive the bench; a failure is reported in the line,
+    never raised."""
     import signal
     tool = os.path.join(ROOT, "tools", "pipeline_bench.py")
-    legs = {"configs[2]": ["--size", "4k", "--batch", "16", "--policy", "shard",
-                           "--frames", str(int(256 * nworkers * frames_scale))],
-            "configs[3]": ["--size", "mixed", "--batch", "16", "--policy", "pull",
-                           "--frames", str(int(384 * nworkers * frames_scale))]}
+    k4 = 2160 * 3840 * 3
+    legs = {"configs[2]": (["--size", "4k", "--batch", "16", "--policy", "shard", "--producer", "copy",
+                            "--frames", str(int(256 * nworkers * frames_scale))], k4, 4.25),
+            "configs[2]_resident": (["--size", "4k", "--batch", "16", "--policy", "shard", "--producer",
+                                     "resident", "--frames", str(int(256 * nworkers * frames_scale))], k4, 2.25),
+            "configs[3]": (["--size", "mixed", "--batch", "16", "--policy", "pull", "--producer", "copy",
+                            "--frames", str(int(384 * nworkers * frames_scale))],
+                           (640 * 480 + 1920 * 1080 + 3840 * 2160) * 3 // 3, 4.25)}
     out = {}
-    for name, extra in legs.items():
-        cmd = [sys.executable, tool, "--workers", str(nworkers), "--gpus", str(ngpu), "--inflight", "2",
-               "--ring-slots", str(3 * 16 * nworkers)] + extra
+    for name, (extra, fbytes, host_x) in legs.items():
+        cmd = [sys.executable, tool, "--workers", str(nworkers), "--gpus", str(ngpu), "--inflight", "2"] + extra
         t0 = time.time()
         p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
                              start_new_session=True)
@@ -384,13 +411,24 @@ def distributor_leg(nworkers, ngpu, frames_scale=1.0, timeout_s=150):
             out[name] = {"error": f"rc={p.returncode}: {se[-300:]}"}
             continue
         r = json.loads(lines[-1])
-        keep = ("size", "workers", "gpus", "policy", "batch", "frames", "fps", "GBps_each_way",
+        keep = ("size", "workers", "gpus", "policy", "producer", "batch", "frames", "fps", "GBps_each_way",
                 "latency_ms_mean", "latency_ms_p99", "reorder_wait_mean_ms", "reorder_wait_max_ms",
-                "max_buffer_depth", "out_of_order_arrivals", "n_errors")
-        out[name] = {k: r[k] for k in keep if k in r}
-        out[name]["wall_s"] = round(time.time() - t0, 1)
-    out["note"] = ("host->host through distributor + shared-memory ring + one worker process per GPU; "
-                   "bound by host memory and PCIe, not HBM; never the headline value")
+                "max_buffer_depth", "out_of_order_arrivals", "n_errors", "verify_full_every",
+                "slice_bytes_per_worker", "slice_numa", "slice_numa_bound", "evictions", "frames_lost")
+        leg = {k: r[k] for k in keep if k in r}
+        leg["fps_per_gpu"] = round(r["fps"] / max(1, min(ngpu, nworkers)), 1)
+        ceil = {"frame_bytes_mean": fbytes, "host_bytes_per_frame": f"{host_x} x frame"}
+        if pcie_gbps:
+            ceil["pcie_fps"] = round(min(ngpu, nworkers) * pcie_gbps * 1e9 / fbytes, 1)
+        if host_gbps:
+            ceil["host_dram_fps"] = round(host_gbps * 1e9 / (host_x * fbytes), 1)
+        leg["ceilings"] = ceil
+        leg["wall_s"] = round(time.time() - t0, 1)
+        out[name] = leg
+    out["note"] = ("host->host through distributor + per-worker shared-memory ring slices + one worker process "
+                   "per GPU; bound by host memory and PCIe, not HBM; never the headline value. ceilings: pcie = "
+                   "GPUs x end_to_end.pinned_pipelined GB/s each way / frame bytes; host_dram = the multi-process "
+                   "CPU baseline's r+w GB/s / host bytes per frame")
     return out
 
 
@@ -406,27 +444,33 @@ def main():
     if world != args.gpus:
         log(f"note: WORLD_SIZE={world} but --gpus {args.gpus}; using WORLD_SIZE")
 
-    # PMC passes run before this process touches the GPU (the profiler child owns it).
-    traffic, traffic_detail = None, "skipped"
-    if rank == 0 and world == 1 and not args.no_traffic:
-        t0 = time.time()
-        traffic, traffic_detail = pmc_traffic(args)
-        log(f"pmc traffic: {traffic} ({traffic_detail}) in {time.time() - t0:.1f}s")
-
     import numpy as np
     import torch
     import torch.distributed as dist
     from vfilter import Context
 
-    have_gpu = torch.cuda.is_available()
     # one GPU per rank (LOCAL_RANK); VF_DEVICE + BENCH_DIST_BACKEND=gloo rehearse N ranks on
     # one card (the timing barrier is the only cross-rank operation, so gloo is enough)
     device = int(os.environ.get("VF_DEVICE", local_rank))
+    have_gpu = torch.cuda.device_count() > 0  # counts devices without initialising HIP
     backend = os.environ.get("BENCH_DIST_BACKEND") or ("nccl" if have_gpu else "gloo")
-    if have_gpu:
-        torch.cuda.set_device(device)
+    cpu_group = None
     if world > 1:
         dist.init_process_group(backend, rank=rank, world_size=world)
+        cpu_group = dist.new_group(backend="gloo")  # host-only barrier before any GPU work
+
+    # PMC passes run before ANY rank touches a GPU: rank 0's profiler child owns rank 0's GPU
+    # (the others wait on a host-only barrier, so nothing else runs on the card being counted)
+    traffic, traffic_detail = None, "skipped"
+    if rank == 0 and not args.no_traffic:
+        t0 = time.time()
+        traffic, traffic_detail = pmc_traffic(args, device)
+        log(f"pmc traffic: {traffic} ({traffic_detail}) in {time.time() - t0:.1f}s")
+    if world > 1:
+        dist.barrier(group=cpu_group)
+    have_gpu = torch.cuda.is_available()
+    if have_gpu:
+        torch.cuda.set_device(device)
 
     def barrier_sync():
         if have_gpu:
@@ -482,20 +526,24 @@ def main():
     if rank == 0 and not args.no_jpeg:
         jpeg, jpgs = jpeg_mode(ctx, args.batch)
         log(f"jpeg mode: {jpeg}")
-    if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        cpu = cpu_baseline(host_batch, args.batch, args.cpu_seconds, np)
+    if rank == 0 and args.cpu_seconds > 0:
+        # after every timed region (the other ranks wait at the distributor leg's barrier); at
+        # N > 1 a shorter sample without the process-count series keeps the run bounded
+        full = world == 1
+        cpu = cpu_baseline(host_batch, args.batch, args.cpu_seconds if full else min(3.0, args.cpu_seconds), np)
         procs = min(args.cpu_procs, len(os.sched_getaffinity(0)))
         if procs > 1:
-            cpu["multi_process"] = cpu_baseline_multi(min(5.0, args.cpu_seconds), procs)
-            # BASELINE.md plan: 1, 2, 4, ... processes, to show where host memory saturates
-            series = {}
-            p_ = 1
-            while p_ < procs:
-                series[str(p_)] = cpu_baseline_multi(min(2.0, args.cpu_seconds), p_)["value"]
-                p_ *= 2
-            series[str(procs)] = cpu["multi_process"]["value"]
-            cpu["process_scaling_fps"] = series
-        cpu["sizes"] = cpu_baseline_sizes(min(3.0, args.cpu_seconds), np)
+            cpu["multi_process"] = cpu_baseline_multi(min(5.0 if full else 2.0, args.cpu_seconds), procs)
+            if full:  # BASELINE.md plan: 1, 2, 4, ... processes, to show where host memory saturates
+                series = {}
+                p_ = 1
+                while p_ < procs:
+                    series[str(p_)] = cpu_baseline_multi(min(2.0, args.cpu_seconds), p_)["value"]
+                    p_ *= 2
+                series[str(procs)] = cpu["multi_process"]["value"]
+                cpu["process_scaling_fps"] = series
+        if full:
+            cpu["sizes"] = cpu_baseline_sizes(min(3.0, args.cpu_seconds), np)
         log(f"cpu baseline: {cpu}")
         if jpeg is not None:
             jpeg["cpu_reference"] = cpu_baseline_jpeg(jpgs, min(5.0, args.cpu_seconds))
@@ -507,7 +555,9 @@ def main():
     if not args.no_distributor:
         if rank == 0:
             # one worker per rank; workers share GPUs only when rehearsing N ranks on fewer cards
-            fanout = distributor_leg(world, max(1, min(world, torch.cuda.device_count())))
+            host_gbps = (cpu or {}).get("multi_process", {}).get("GBps_r_plus_w")
+            pcie_gbps = (e2e or {}).get("pinned_pipelined_GBps_each_way")
+            fanout = distributor_leg(world, max(1, min(world, torch.cuda.device_count())), host_gbps, pcie_gbps)
             log(f"distributor leg: {fanout}")
         if world > 1:
             dist.barrier()  # the other ranks idle (their GPUs serve the leg's workers)

@@ -22,6 +22,7 @@
 #include <cstring>
 #include <algorithm>
 #include <condition_variable>
+#include <map>
 #include <mutex>
 #include <new>
 #include <vector>
@@ -70,6 +71,9 @@ struct vf_ctx {
   std::condition_variable jpeg_cv;
   std::vector<vf::jpeg::Codec *> jpeg_all, jpeg_free;
   vf::jpeg::ComputeGate jpeg_gate;
+  // submitted vf_jpeg_invert_submit batches: ticket -> the codec that holds it until fetched
+  std::map<uint64_t, vf::jpeg::Codec *> jpeg_jobs;
+  uint64_t jpeg_next_ticket = 1;
 };
 
 namespace {
@@ -236,7 +240,7 @@ VF_EXPORT int vf_create(int device, size_t max_frame_bytes, int max_batch, vf_ct
 
 VF_EXPORT int vf_destroy(vf_ctx *ctx) {
   if (!ctx) return VF_OK;
-  for (vf::jpeg::Codec *c : ctx->jpeg_all) delete c;
+  for (vf::jpeg::Codec *c : ctx->jpeg_all) delete c;  // each synchronises its stream first
   delete ctx->engine;  // finishes queued jobs first
   delete ctx;
   return VF_OK;
@@ -533,6 +537,7 @@ class CodecLease {
   }
   ~CodecLease() {
     if (!c_) return;
+    c_->quiesce();  // a failed call may have left work queued (no-op after a success)
     {
       std::lock_guard<std::mutex> lk(ctx_->jpeg_mu);
       ctx_->jpeg_free.push_back(c_);
@@ -547,6 +552,50 @@ class CodecLease {
   vf_ctx *ctx_;
   vf::jpeg::Codec *c_ = nullptr;
 };
+
+// A codec for an asynchronous batch: never blocks (the caller thread may be the one that would
+// fetch the batches holding the others); a new codec when none is free, up to kMaxJpegJobs.
+constexpr size_t kMaxJpegJobs = 8;
+vf::jpeg::Codec *lease_nowait(vf_ctx *ctx) {
+  std::lock_guard<std::mutex> lk(ctx->jpeg_mu);
+  if (!ctx->jpeg_free.empty()) {
+    vf::jpeg::Codec *c = ctx->jpeg_free.back();
+    ctx->jpeg_free.pop_back();
+    return c;
+  }
+  if (ctx->jpeg_all.size() >= kMaxJpegJobs) return nullptr;
+  static const bool gated = env_size("VF_JPEG_GATE", 1) != 0;
+  vf::jpeg::Codec *c = new (std::nothrow) vf::jpeg::Codec(ctx->device, gated ? &ctx->jpeg_gate : nullptr);
+  if (c) ctx->jpeg_all.push_back(c);
+  return c;
+}
+
+void give_back(vf_ctx *ctx, vf::jpeg::Codec *c) {
+  {
+    std::lock_guard<std::mutex> lk(ctx->jpeg_mu);
+    ctx->jpeg_free.push_back(c);
+  }
+  ctx->jpeg_cv.notify_one();
+}
+
+vf::jpeg::Codec *job_codec(vf_ctx *ctx, uint64_t ticket) {
+  std::lock_guard<std::mutex> lk(ctx->jpeg_mu);
+  auto it = ctx->jpeg_jobs.find(ticket);
+  return it == ctx->jpeg_jobs.end() ? nullptr : it->second;
+}
+
+void end_job(vf_ctx *ctx, uint64_t ticket) {
+  vf::jpeg::Codec *c = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(ctx->jpeg_mu);
+    auto it = ctx->jpeg_jobs.find(ticket);
+    if (it == ctx->jpeg_jobs.end()) return;
+    c = it->second;
+    ctx->jpeg_jobs.erase(it);
+  }
+  c->quiesce();
+  give_back(ctx, c);
+}
 
 int jpeg_codec(vf_ctx *ctx, const CodecLease &lease, vf::jpeg::Codec **out) {
   if (!lease.get()) return set_err(ctx, VF_E_NOMEM, 0, "JPEG codec: out of host memory");
@@ -618,6 +667,66 @@ VF_EXPORT int vf_jpeg_invert(vf_ctx *ctx, const uint8_t *const *jpegs, const siz
   std::string err;
   rc = c->invert(jpegs, jpeg_sizes, n, quality, subsamp, flags, outs, caps, sizes, &err);
   return jpeg_status(ctx, rc, "vf_jpeg_invert: " + err);
+}
+
+VF_EXPORT int vf_jpeg_invert_submit(vf_ctx *ctx, const uint8_t *const *jpegs, const size_t *jpeg_sizes, int n,
+                                    int quality, int subsamp, int flags, uint64_t *ticket) {
+  VF_CHECK_CTX(ctx);
+  if (!ticket || n <= 0 || n > 65535 || !jpegs || !jpeg_sizes)
+    return set_err(ctx, VF_E_INVALID, 0, "vf_jpeg_invert_submit: bad arguments");
+  *ticket = 0;
+  vf::jpeg::Codec *c = lease_nowait(ctx);
+  if (!c)
+    return set_err(ctx, VF_E_INVALID, 0, "vf_jpeg_invert_submit: %zu batches already in flight; fetch one first",
+                   kMaxJpegJobs);
+  std::string err;
+  const int rc = c->submit_invert(jpegs, jpeg_sizes, n, quality, subsamp, flags, &err);
+  if (rc != VF_OK) {
+    c->quiesce();  // a submit that failed after queueing work must not hand the codec on mid-flight
+    give_back(ctx, c);
+    return jpeg_status(ctx, rc, "vf_jpeg_invert_submit: " + err);
+  }
+  std::lock_guard<std::mutex> lk(ctx->jpeg_mu);
+  *ticket = ctx->jpeg_next_ticket++;
+  ctx->jpeg_jobs[*ticket] = c;
+  return VF_OK;
+}
+
+VF_EXPORT int vf_jpeg_invert_query(vf_ctx *ctx, uint64_t ticket, int *done) {
+  VF_CHECK_CTX(ctx);
+  vf::jpeg::Codec *c = job_codec(ctx, ticket);
+  if (!c || !done) return set_err(ctx, VF_E_INVALID, 0, "vf_jpeg_invert_query: unknown ticket %llu",
+                                  (unsigned long long)ticket);
+  *done = c->done_invert() ? 1 : 0;
+  return VF_OK;
+}
+
+VF_EXPORT int vf_jpeg_invert_wait(vf_ctx *ctx, uint64_t ticket, size_t *total) {
+  VF_CHECK_CTX(ctx);
+  vf::jpeg::Codec *c = job_codec(ctx, ticket);
+  if (!c || !total) return set_err(ctx, VF_E_INVALID, 0, "vf_jpeg_invert_wait: unknown ticket %llu",
+                                   (unsigned long long)ticket);
+  std::string err;
+  const int rc = c->wait_invert(total, &err);
+  if (rc != VF_OK) end_job(ctx, ticket);  // a failed batch is over: its codec is free again
+  return jpeg_status(ctx, rc, "vf_jpeg_invert_wait: " + err);
+}
+
+VF_EXPORT int vf_jpeg_invert_fetch(vf_ctx *ctx, uint64_t ticket, uint8_t *out, size_t cap, size_t *sizes,
+                                   size_t *offsets) {
+  VF_CHECK_CTX(ctx);
+  vf::jpeg::Codec *c = job_codec(ctx, ticket);
+  if (!c) return set_err(ctx, VF_E_INVALID, 0, "vf_jpeg_invert_fetch: unknown ticket %llu", (unsigned long long)ticket);
+  std::string err;
+  int rc = VF_OK;
+  if (!c->waited()) {  // fetch without wait: wait here (out == NULL just releases the batch)
+    size_t total = 0;
+    rc = c->wait_invert(&total, &err);
+  }
+  if (rc == VF_OK) rc = c->fetch_invert(out, cap, sizes, offsets, &err);
+  if (rc == VF_E_INVALID && out && cap) return jpeg_status(ctx, rc, "vf_jpeg_invert_fetch: " + err);  // retry with room
+  end_job(ctx, ticket);
+  return jpeg_status(ctx, rc, "vf_jpeg_invert_fetch: " + err);
 }
 
 VF_EXPORT int vf_jpeg_bench_invert(vf_ctx *ctx, const uint8_t *const *jpegs, const size_t *jpeg_sizes, int n,

@@ -106,6 +106,7 @@ class Engine {
     std::vector<Seg> segs;
     bool direct = true;  // every byte page-locked: DMA straight from/to the caller
     size_t total = 0, chunk = 0;
+    size_t queued = 0;            // bytes put into slots so far
     size_t seg = 0, seg_off = 0;  // fill cursor
     int chunks_submitted = 0, chunks_done = 0;
     bool started = false, all_submitted = false;
@@ -125,6 +126,7 @@ class Engine {
   static constexpr size_t kMaxResults = 1024;
 
   void run();
+  size_t chunk_size(const Job &job) const;
   bool step_fill();
   bool step_d2h();
   bool step_retire();

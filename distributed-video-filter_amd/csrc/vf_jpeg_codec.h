@@ -102,6 +102,20 @@ class Codec {
              uint8_t *const *outs, const size_t *caps, std::string *err);
   int invert(const uint8_t *const *jpegs, const size_t *sizes, int n, int quality, int subsamp, int flags,
              uint8_t *const *outs, const size_t *caps, size_t *out_sizes, std::string *err);
+  // invert() in three steps, so one host thread can keep batches of two codecs in flight:
+  // submit_invert returns once everything is queued (inputs staged: the caller's buffers may go);
+  // done_invert never blocks; wait_invert blocks and gives the packed output size; fetch_invert
+  // copies the packed outputs (frame f at offs[f], sizes[f] bytes; out may be NULL).
+  int submit_invert(const uint8_t *const *jpegs, const size_t *sizes, int n, int quality, int subsamp, int flags,
+                    std::string *err);
+  bool done_invert();
+  int wait_invert(size_t *total, std::string *err);
+  int fetch_invert(uint8_t *out, size_t cap, size_t *sizes, size_t *offs, std::string *err);
+  uint64_t fetch_refills() const { return fetch_refills_; }
+  bool waited() const { return waited_; }
+  // wait for anything still queued on the codec's stream (after a failed call, before the codec
+  // and its pinned buffers go to the next caller)
+  void quiesce();
   // the device part of invert() `iters` times on resident inputs; mean wall ms per iteration,
   // stage_ms[0..6] = unstuff, sync, write, dc+idct, colour, fdct+huffman, stuffing; [7] = passes
   int bench_invert(const uint8_t *const *jpegs, const size_t *sizes, int n, int quality, int subsamp, int flags,
@@ -111,16 +125,20 @@ class Codec {
   int init(std::string *err);
   int prepare_decode(const uint8_t *const *jpegs, const size_t *sizes, int n, int flags, std::string *err);
   int run_decode(int bgr, bool invert, std::string *err);
+  int queue_decode_check(std::string *err);
   int check_decode(std::string *err);
   int prepare_encode(const int *ws, const int *hs, const uint64_t *img_offs, int n, int quality, int subsamp,
                      bool fastdct, std::string *err);
   int run_encode(int bgr, bool fastdct, std::string *err);
-  int fetch_jpegs(uint8_t *const *outs, const size_t *caps, size_t *sizes, std::string *err);
+  int queue_fetch(uint64_t guess, std::string *err);
+  int finish_fetch(std::string *err);
+  int copy_out(uint8_t *const *outs, const size_t *caps, size_t *sizes, std::string *err);
 
   int device_;
   ComputeGate *gate_;
   hipStream_t s_ = nullptr;
   hipEvent_t ev_[10] = {};
+  hipEvent_t done_ = nullptr;  // the last call's downloads have landed
 
   // decode layout
   std::vector<DecFrame> dfr_;
@@ -146,6 +164,10 @@ class Codec {
       d_out_, d_outsize_, d_pack_;
 
   HostBuf h_stage_, h_out_, h_flag_;  // h_flag_: the speculative sync's unresolved flag
+  HostBuf h_ddesc_, h_edesc_, h_meta_;  // pinned descriptor uploads; block totals + output sizes
+  uint64_t guess_ = 0, out_total_ = 0, fetch_refills_ = 0;
+  bool waited_ = false;
+  std::vector<uint64_t> out_sizes_, out_offs_;
   bool spec_check_ = false;           // run_decode queued that flag's read; check_decode tests it
   TaskPool pool_{4};
 };

@@ -556,6 +556,7 @@ Codec::~Codec() {
   }
   for (hipEvent_t e : ev_)
     if (e) (void)hipEventDestroy(e);
+  if (done_) (void)hipEventDestroy(done_);
 }
 
 #define CK(call)                                                                          \
@@ -572,6 +573,7 @@ int Codec::init(std::string *err) {
   CK(hipSetDevice(device_));
   CK(hipStreamCreateWithFlags(&s_, hipStreamNonBlocking));
   for (hipEvent_t &e : ev_) CK(hipEventCreate(&e));
+  CK(hipEventCreateWithFlags(&done_, hipEventDisableTiming));
   return kOk;
 }
 
@@ -734,11 +736,16 @@ int Codec::prepare_decode(const uint8_t *const *jpegs, const size_t *sizes, int 
   CK(d_dcseq_.ensure(sizeof(int32_t) * (dcoff + 1)));
   CK(d_planes_.ensure(plane));
   CK(d_pix_.ensure(pix));
+  // descriptors go through pinned memory too, so every upload stays asynchronous and nothing
+  // waits for the GPU before the kernels are queued (the pinned buffers are reused only by the
+  // codec's next call, which starts after this one has synchronised)
+  const size_t dsz = sizeof(DecFrame) * (size_t)n, ssz = sizeof(ScanSeg) * segs.size();
+  CK(h_ddesc_.ensure(dsz + ssz));
+  std::memcpy(h_ddesc_.as<uint8_t>(), dfr_.data(), dsz);
+  std::memcpy(h_ddesc_.as<uint8_t>() + dsz, segs.data(), ssz);
   CK(hipMemcpyAsync(d_in_.p, h_stage_.p, in_off, hipMemcpyHostToDevice, s_));
-  CK(hipMemcpyAsync(d_dfr_.p, dfr_.data(), sizeof(DecFrame) * (size_t)n, hipMemcpyHostToDevice, s_));
-  CK(hipMemcpyAsync(d_segs_.p, segs.data(), sizeof(ScanSeg) * segs.size(), hipMemcpyHostToDevice, s_));
-  // the pinned staging buffer is reused below: make sure the upload has consumed it
-  CK(hipStreamSynchronize(s_));
+  CK(hipMemcpyAsync(d_dfr_.p, h_ddesc_.p, dsz, hipMemcpyHostToDevice, s_));
+  CK(hipMemcpyAsync(d_segs_.p, h_ddesc_.as<uint8_t>() + dsz, ssz, hipMemcpyHostToDevice, s_));
   return kOk;
 }
 
@@ -849,12 +856,17 @@ int Codec::run_decode(int bgr, bool invert, std::string *err) {
   return kOk;
 }
 
-// Check that every frame decoded all its blocks (reads the totals written by run_decode).
-int Codec::check_decode(std::string *err) {
-  std::vector<uint32_t> tot((size_t)dn_);
-  CK(hipMemcpyAsync(tot.data(), d_totals_.as<uint32_t>() + dn_, sizeof(uint32_t) * (size_t)dn_,
+// Queue the D2H of every frame's decoded block count (written by run_decode) into pinned memory.
+int Codec::queue_decode_check(std::string *err) {
+  CK(h_meta_.ensure(sizeof(uint64_t) * (size_t)dn_ * 2 + 64));
+  CK(hipMemcpyAsync(h_meta_.p, d_totals_.as<uint32_t>() + dn_, sizeof(uint32_t) * (size_t)dn_,
                     hipMemcpyDeviceToHost, s_));
-  CK(hipStreamSynchronize(s_));
+  return kOk;
+}
+
+// Check that every frame decoded all its blocks (after queue_decode_check and a synchronisation).
+int Codec::check_decode(std::string *err) {
+  const uint32_t *tot = h_meta_.as<uint32_t>();
   if (spec_check_) {
     spec_check_ = false;
     if (*h_flag_.as<uint32_t>()) {
@@ -941,12 +953,20 @@ int Codec::prepare_encode(const int *ws, const int *hs, const uint64_t *img_offs
   CK(d_out_.ensure(out));
   CK(d_pack_.ensure(out));
   CK(d_outsize_.ensure(sizeof(uint64_t) * (size_t)n));
-  // small tables go through pageable memcpy (synchronous w.r.t. the host buffers)
-  CK(hipMemcpyAsync(d_efr_.p, efr_.data(), sizeof(EncFrame) * (size_t)n, hipMemcpyHostToDevice, s_));
-  CK(hipMemcpyAsync(d_etab_.p, &tab, sizeof tab, hipMemcpyHostToDevice, s_));
-  CK(hipMemcpyAsync(d_hdr_.p, hdr.data(), hdr.size(), hipMemcpyHostToDevice, s_));
-  CK(hipMemcpyAsync(d_esegs_.p, segs.data(), sizeof(ScanSeg) * segs.size(), hipMemcpyHostToDevice, s_));
-  CK(hipStreamSynchronize(s_));
+  // frame descriptors, tables, headers and scan segments: one pinned blob, asynchronous uploads
+  const size_t fsz = sizeof(EncFrame) * (size_t)n, ssz = sizeof(ScanSeg) * segs.size();
+  const size_t o_tab = align_up(fsz, 256), o_hdr = o_tab + align_up(sizeof tab, 256),
+               o_seg = o_hdr + align_up(hdr.size(), 256);
+  CK(h_edesc_.ensure(o_seg + ssz));
+  uint8_t *hb = h_edesc_.as<uint8_t>();
+  std::memcpy(hb, efr_.data(), fsz);
+  std::memcpy(hb + o_tab, &tab, sizeof tab);
+  std::memcpy(hb + o_hdr, hdr.data(), hdr.size());
+  std::memcpy(hb + o_seg, segs.data(), ssz);
+  CK(hipMemcpyAsync(d_efr_.p, hb, fsz, hipMemcpyHostToDevice, s_));
+  CK(hipMemcpyAsync(d_etab_.p, hb + o_tab, sizeof tab, hipMemcpyHostToDevice, s_));
+  CK(hipMemcpyAsync(d_hdr_.p, hb + o_hdr, hdr.size(), hipMemcpyHostToDevice, s_));
+  CK(hipMemcpyAsync(d_esegs_.p, hb + o_seg, ssz, hipMemcpyHostToDevice, s_));
   return kOk;
 }
 
@@ -977,40 +997,48 @@ int Codec::run_encode(int bgr, bool fastdct, std::string *err) {
   return kOk;
 }
 
-// Sizes -> caps check -> D2H of every JPEG into the caller's buffers.
-int Codec::fetch_jpegs(uint8_t *const *outs, const size_t *caps, size_t *sizes, std::string *err) {
+// Queue, behind the encode kernels: the D2H of every output size, and of the first `guess`
+// bytes of the packed outputs (k_compact's layout: frames 64-B aligned, back to back), guessed
+// from the inputs' sizes, so the common case needs no second round trip; then the done event.
+int Codec::queue_fetch(uint64_t guess, std::string *err) {
   const int n = en_;
-  std::vector<uint64_t> sz((size_t)n);
-  CK(hipMemcpyAsync(sz.data(), d_outsize_.p, sizeof(uint64_t) * (size_t)n, hipMemcpyDeviceToHost, s_));
-  CK(hipStreamSynchronize(s_));
+  CK(h_meta_.ensure(sizeof(uint64_t) * (size_t)n * 2 + 64));
+  uint64_t *sz = h_meta_.as<uint64_t>() + n;  // [0, n) u32 block totals, then the sizes
+  CK(hipMemcpyAsync(sz, d_outsize_.p, sizeof(uint64_t) * (size_t)n, hipMemcpyDeviceToHost, s_));
+  guess = std::min<uint64_t>(guess, d_pack_.cap);
+  CK(h_out_.ensure(guess));
+  guess_ = guess;
+  if (guess) CK(hipMemcpyAsync(h_out_.p, d_pack_.p, guess, hipMemcpyDeviceToHost, s_));
+  CK(hipEventRecord(done_, s_));
+  return kOk;
+}
+
+// After done_: the packed layout (sizes, offsets, total) and, when the guess fell short, the
+// rest of the outputs (one more round trip).
+int Codec::finish_fetch(std::string *err) {
+  const int n = en_;
+  const uint64_t *sz = h_meta_.as<uint64_t>() + n;
+  out_sizes_.resize((size_t)n);
+  out_offs_.resize((size_t)n);
   uint64_t total = 0;
   for (int f = 0; f < n; ++f) {
-    sizes[f] = (size_t)sz[(size_t)f];
-    total += align_up(sz[(size_t)f], 64);
+    out_sizes_[(size_t)f] = sz[f];
+    out_offs_[(size_t)f] = total;
+    total += align_up(sz[f], 64);
   }
-  for (int f = 0; f < n; ++f)
-    if (sz[(size_t)f] > caps[f] || !outs[f]) {
-      *err = "frame " + std::to_string(f) + ": output buffer of " + std::to_string(caps[f]) +
-             " bytes is too small for the " + std::to_string(sz[(size_t)f]) + "-byte JPEG";
-      return kInvalid;
+  out_total_ = total;
+  if (total > guess_) {
+    ++fetch_refills_;
+    if (total > h_out_.cap) {  // grow, keeping what already arrived
+      HostBuf bigger;
+      CK(bigger.ensure(total));
+      std::memcpy(bigger.p, h_out_.p, guess_);
+      std::swap(bigger.p, h_out_.p);
+      std::swap(bigger.cap, h_out_.cap);
     }
-  CK(h_out_.ensure(total));
-  uint64_t off = 0;
-  std::vector<uint64_t> offs((size_t)n);
-  for (int f = 0; f < n; ++f) {  // k_compact's layout
-    offs[(size_t)f] = off;
-    off += align_up(sz[(size_t)f], 64);
-  }
-  CK(hipMemcpyAsync(h_out_.p, d_pack_.p, total, hipMemcpyDeviceToHost, s_));
-  const auto ta = std::chrono::steady_clock::now();
-  CK(hipStreamSynchronize(s_));
-  const auto tb = std::chrono::steady_clock::now();
-  pool_.run(n, [&](int f) { std::memcpy(outs[f], h_out_.as<uint8_t>() + offs[(size_t)f], sz[(size_t)f]); });
-  if (std::getenv("VF_JPEG_TRACE")) {
-    const auto tc = std::chrono::steady_clock::now();
-    std::fprintf(stderr, "[vf_jpeg]   fetch: d2h %.3f copy-out %.3f ms (%llu B)\n",
-                 std::chrono::duration<double, std::milli>(tb - ta).count(),
-                 std::chrono::duration<double, std::milli>(tc - tb).count(), (unsigned long long)total);
+    CK(hipMemcpyAsync(h_out_.as<uint8_t>() + guess_, d_pack_.as<uint8_t>() + guess_, total - guess_,
+                      hipMemcpyDeviceToHost, s_));
+    CK(hipStreamSynchronize(s_));
   }
   return kOk;
 }
@@ -1045,7 +1073,29 @@ int Codec::encode(const uint8_t *const *imgs, const int *ws, const int *hs, int 
   });
   CK(hipMemcpyAsync(d_pix_.p, h_stage_.p, pix, hipMemcpyHostToDevice, s_));
   if ((rc = run_encode(pixel_format, fast, err))) return rc;
-  return fetch_jpegs(outs, caps, sizes, err);
+  uint64_t guess = 0;
+  for (int f = 0; f < n; ++f) guess += align_up((size_t)ws[f] * hs[f] / 4 + 8192, 64);
+  if ((rc = queue_fetch(guess, err))) return rc;
+  CK(hipEventSynchronize(done_));
+  if ((rc = finish_fetch(err))) return rc;
+  return copy_out(outs, caps, sizes, err);
+}
+
+// Per-frame copies of the fetched packed outputs into the caller's buffers (caps checked).
+int Codec::copy_out(uint8_t *const *outs, const size_t *caps, size_t *sizes, std::string *err) {
+  const int n = en_;
+  for (int f = 0; f < n; ++f) {
+    sizes[f] = (size_t)out_sizes_[(size_t)f];
+    if (out_sizes_[(size_t)f] > caps[f] || !outs[f]) {
+      *err = "frame " + std::to_string(f) + ": output buffer of " + std::to_string(caps[f]) +
+             " bytes is too small for the " + std::to_string(out_sizes_[(size_t)f]) + "-byte JPEG";
+      return kInvalid;
+    }
+  }
+  pool_.run(n, [&](int f) {
+    std::memcpy(outs[f], h_out_.as<uint8_t>() + out_offs_[(size_t)f], out_sizes_[(size_t)f]);
+  });
+  return kOk;
 }
 
 int Codec::decode(const uint8_t *const *jpegs, const size_t *jsizes, int n, int pixel_format, int flags,
@@ -1066,10 +1116,11 @@ int Codec::decode(const uint8_t *const *jpegs, const size_t *jsizes, int n, int 
     }
   }
   if ((rc = run_decode(pixel_format, false, err))) return rc;
-  if ((rc = check_decode(err))) return rc;
+  if ((rc = queue_decode_check(err))) return rc;
   CK(h_out_.ensure(dpix_bytes_));
   CK(hipMemcpyAsync(h_out_.p, d_pix_.p, dpix_bytes_, hipMemcpyDeviceToHost, s_));
   CK(hipStreamSynchronize(s_));
+  if ((rc = check_decode(err))) return rc;
   pool_.run(n, [&](int f) {
     std::memcpy(outs[f], h_out_.as<uint8_t>() + dfr_[(size_t)f].out_off,
                 (size_t)dfr_[(size_t)f].g.w * dfr_[(size_t)f].g.h * 3);
@@ -1077,11 +1128,19 @@ int Codec::decode(const uint8_t *const *jpegs, const size_t *jsizes, int n, int 
   return kOk;
 }
 
-int Codec::invert(const uint8_t *const *jpegs, const size_t *jsizes, int n, int quality, int subsamp, int flags,
-                  uint8_t *const *outs, const size_t *caps, size_t *sizes, std::string *err) {
+// The fused default-mode filter, split so one host thread can keep two batches in flight:
+// submit_invert (parse, stage, queue every upload, kernel and download; returns without
+// waiting for the GPU), wait_invert (the done event, the decode checks, the packed layout),
+// fetch_invert (copy-out).  invert() is the three in a row.
+int Codec::submit_invert(const uint8_t *const *jpegs, const size_t *jsizes, int n, int quality, int subsamp,
+                         int flags, std::string *err) {
   int rc = init(err);
   if (rc) return rc;
-  if (n <= 0) return kOk;
+  waited_ = false;
+  if (n <= 0) {
+    *err = "empty batch";
+    return kInvalid;
+  }
   static const bool trace = std::getenv("VF_JPEG_TRACE") != nullptr;
   using clk = std::chrono::steady_clock;
   const auto t0 = clk::now();
@@ -1089,10 +1148,12 @@ int Codec::invert(const uint8_t *const *jpegs, const size_t *jsizes, int n, int 
   const auto t1 = clk::now();
   std::vector<int> ws((size_t)n), hs((size_t)n);
   std::vector<uint64_t> offs((size_t)n);
+  uint64_t guess = 0;
   for (int f = 0; f < n; ++f) {
     ws[(size_t)f] = dfr_[(size_t)f].g.w;
     hs[(size_t)f] = dfr_[(size_t)f].g.h;
     offs[(size_t)f] = dfr_[(size_t)f].out_off;
+    guess += align_up(jsizes[f] + jsizes[f] / 4 + 8192, 64);  // an inverted frame codes to about its input's size
   }
   const bool fast = (flags & kFlagFastDct) != 0;
   if ((rc = prepare_encode(ws.data(), hs.data(), offs.data(), n, quality, subsamp, fast, err))) return rc;
@@ -1111,18 +1172,77 @@ int Codec::invert(const uint8_t *const *jpegs, const size_t *jsizes, int n, int 
       gate_->last = ev_[9];
     }
   }
-  const auto t3 = clk::now();
-  if ((rc = check_decode(err))) return rc;
-  const auto t4 = clk::now();
-  rc = fetch_jpegs(outs, caps, sizes, err);
+  if ((rc = queue_decode_check(err))) return rc;
+  if ((rc = queue_fetch(guess, err))) return rc;
   if (trace) {
-    const auto t5 = clk::now();
     auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
     static const clk::time_point origin = t0;
-    std::fprintf(stderr,
-                 "[vf_jpeg] invert codec %p n=%d at %.3f: prep_dec %.3f prep_enc %.3f queue %.3f wait %.3f fetch %.3f ms\n",
-                 (void *)this, n, ms(origin, t0), ms(t0, t1), ms(t1, t2), ms(t2, t3), ms(t3, t4), ms(t4, t5));
+    std::fprintf(stderr, "[vf_jpeg] submit codec %p n=%d at %.3f: prep_dec %.3f prep_enc %.3f queue %.3f ms\n",
+                 (void *)this, n, ms(origin, t0), ms(t0, t1), ms(t1, t2), ms(t2, clk::now()));
   }
+  return kOk;
+}
+
+void Codec::quiesce() {
+  if (!s_) return;
+  (void)hipSetDevice(device_);
+  (void)hipStreamSynchronize(s_);
+  (void)hipGetLastError();
+}
+
+bool Codec::done_invert() {
+  const hipError_t q = hipEventQuery(done_);
+  if (q == hipSuccess) return true;
+  (void)hipGetLastError();
+  return q != hipErrorNotReady;  // an error counts as done: wait_invert reports it
+}
+
+int Codec::wait_invert(size_t *total, std::string *err) {
+  using clk = std::chrono::steady_clock;
+  const auto t0 = clk::now();
+  CK(hipEventSynchronize(done_));
+  int rc = check_decode(err);
+  if (rc) return rc;
+  if ((rc = finish_fetch(err))) return rc;
+  waited_ = true;
+  *total = (size_t)out_total_;
+  if (std::getenv("VF_JPEG_TRACE"))
+    std::fprintf(stderr, "[vf_jpeg] wait codec %p: %.3f ms, %llu B fetched (%s)\n", (void *)this,
+                 std::chrono::duration<double, std::milli>(clk::now() - t0).count(),
+                 (unsigned long long)out_total_, out_total_ > guess_ ? "second copy" : "one copy");
+  return kOk;
+}
+
+int Codec::fetch_invert(uint8_t *out, size_t cap, size_t *sizes, size_t *offs, std::string *err) {
+  const int n = en_;
+  if (out && cap < out_total_) {
+    *err = "output buffer of " + std::to_string(cap) + " bytes is smaller than the " +
+           std::to_string(out_total_) + " packed bytes";
+    return kInvalid;
+  }
+  for (int f = 0; f < n; ++f) {
+    if (sizes) sizes[f] = (size_t)out_sizes_[(size_t)f];
+    if (offs) offs[f] = (size_t)out_offs_[(size_t)f];
+  }
+  if (out && out_total_) {  // one packed copy, split over the pool
+    constexpr int kParts = 8;
+    const uint64_t per = align_up((out_total_ + kParts - 1) / kParts, 4096);
+    pool_.run(kParts, [&](int i) {
+      const uint64_t b = std::min<uint64_t>(out_total_, per * (uint64_t)i);
+      const uint64_t e = std::min<uint64_t>(out_total_, b + per);
+      if (e > b) std::memcpy(out + b, h_out_.as<uint8_t>() + b, e - b);
+    });
+  }
+  return kOk;
+}
+
+int Codec::invert(const uint8_t *const *jpegs, const size_t *jsizes, int n, int quality, int subsamp, int flags,
+                  uint8_t *const *outs, const size_t *caps, size_t *sizes, std::string *err) {
+  if (n <= 0) return init(err);
+  int rc = submit_invert(jpegs, jsizes, n, quality, subsamp, flags, err);
+  size_t total = 0;
+  if (!rc) rc = wait_invert(&total, err);
+  if (!rc) rc = copy_out(outs, caps, sizes, err);
   return rc;
 }
 
@@ -1162,6 +1282,8 @@ int Codec::bench_invert(const uint8_t *const *jpegs, const size_t *jsizes, int n
       if (hipEventElapsedTime(&t, ev_[pairs[i][0]], ev_[pairs[i][1]]) == hipSuccess) acc[i] += t;
     }
   }
+  if ((rc = queue_decode_check(err))) return rc;
+  CK(hipStreamSynchronize(s_));
   if ((rc = check_decode(err))) return rc;
   *ms = (float)(total_ms / iters);
   if (stage_ms) {

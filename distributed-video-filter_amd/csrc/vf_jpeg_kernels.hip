@@ -1630,7 +1630,9 @@ __global__ __launch_bounds__(256) void k_fdct(const EncFrame *fr, const EncTable
     const int v = vz[j];
     const uint32_t av = (uint32_t)(v < 0 ? -v : v);
     const uint32_t nb = 32 - __clz(av);
-    const uint32_t e = s_ac[t][((run & 15) << 4) + (nb & 15)];
+    // zero coefficients all read entry 0 (one broadcast address): with their own (run, 0)
+    // entries they land on 2 banks, up to 8 distinct addresses each
+    const uint32_t e = s_ac[t][nz ? ((run & 15) << 4) + (nb & 15) : 0u];
     code[j] = ((e >> 8) << nb) | ((uint32_t)(v < 0 ? v - 1 : v) & ((1u << nb) - 1));
     clen[j] = nz ? (e & 0xFF) + nb : 0u;
     nzr[j] = nz ? (uint32_t)(run >> 4) : 0u;

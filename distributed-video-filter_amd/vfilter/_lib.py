@@ -73,6 +73,11 @@ SIGNATURES = {
     "vf_jpeg_decode": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp, _vp]),
     "vf_jpeg_invert": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp,
                                       _vp, _vp]),
+    "vf_jpeg_invert_submit": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                             ctypes.POINTER(ctypes.c_uint64)]),
+    "vf_jpeg_invert_query": (ctypes.c_int, [_vp, ctypes.c_uint64, _c_int_p]),
+    "vf_jpeg_invert_wait": (ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.POINTER(_sz)]),
+    "vf_jpeg_invert_fetch": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, _sz, _vp, _vp]),
     "vf_jpeg_bench_invert": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                             ctypes.c_int, _c_float_p, _c_float_p]),
 }
@@ -374,23 +379,47 @@ class Context:
 
     def jpeg_invert(self, jpegs: Sequence, quality: int, subsamp: int, flags: int = 0) -> list:
         """decode -> bitwise_not -> encode for every JPEG, fused on the GPU; returns bytes."""
+        if len(jpegs) == 0:
+            return []
+        return [v.tobytes() for v in self.jpeg_invert_result(self.jpeg_invert_submit(jpegs, quality, subsamp, flags))]
+
+    # -- the same, asynchronously: submit now, collect later (vf_jpeg_invert_submit & co.) ---------
+    def jpeg_invert_submit(self, jpegs: Sequence, quality: int, subsamp: int, flags: int = 0) -> int:
+        """Stage the batch and queue its GPU work; returns a ticket at once (the inputs may be
+        released as soon as this returns)."""
         n = len(jpegs)
         if n == 0:
-            return []
+            raise ValueError("jpeg_invert_submit: empty batch")
         srcs, ja = self._ptrs(jpegs)
-        caps = []
-        for s in srcs:
-            w, h, _, _ = jpeg_header(s)
-            caps.append(int(self._lib.vf_jpeg_buffer_size(w, h, subsamp)))
-        if not all(caps):
-            raise ValueError("jpeg_invert: unsupported size or subsampling")
-        outs = self._out_arena(caps)
-        _, oa = self._ptrs(outs)
         js = (ctypes.c_size_t * n)(*[s.nbytes for s in srcs])
-        ca = (ctypes.c_size_t * n)(*caps)
+        t = ctypes.c_uint64(0)
+        self._check(self._lib.vf_jpeg_invert_submit(self._ctx, ja, js, n, quality, subsamp, flags, ctypes.byref(t)))
+        self.__dict__.setdefault("_jpeg_n", {})[t.value] = n
+        return t.value
+
+    def jpeg_invert_ready(self, ticket: int) -> bool:
+        done = ctypes.c_int(0)
+        self._check(self._lib.vf_jpeg_invert_query(self._ctx, ticket, ctypes.byref(done)))
+        return bool(done.value)
+
+    def jpeg_invert_result(self, ticket: int) -> list:
+        """Wait for a submitted batch; returns one uint8 array view per frame, all views into
+        one fresh buffer (bytes-like: they can go on the wire as they are)."""
+        n = self.__dict__.get("_jpeg_n", {}).pop(ticket, None)
+        if n is None:
+            raise VFilterError(f"unknown JPEG ticket {ticket}", VF_E_INVALID)
+        total = ctypes.c_size_t(0)
+        self._check(self._lib.vf_jpeg_invert_wait(self._ctx, ticket, ctypes.byref(total)))
+        buf = np.empty(max(1, total.value), np.uint8)
         sz = (ctypes.c_size_t * n)()
-        self._check(self._lib.vf_jpeg_invert(self._ctx, ja, js, n, quality, subsamp, flags, oa, ca, sz))
-        return [outs[i][:sz[i]].tobytes() for i in range(n)]
+        off = (ctypes.c_size_t * n)()
+        self._check(self._lib.vf_jpeg_invert_fetch(self._ctx, ticket, buf.ctypes.data, buf.nbytes, sz, off))
+        return [buf[off[i]:off[i] + sz[i]] for i in range(n)]
+
+    def jpeg_invert_release(self, ticket: int) -> None:
+        """Drop a submitted batch without reading it."""
+        if self.__dict__.get("_jpeg_n", {}).pop(ticket, None) is not None:
+            self._check(self._lib.vf_jpeg_invert_fetch(self._ctx, ticket, None, 0, None, None))
 
     def jpeg_bench_invert(self, jpegs: Sequence, quality: int, subsamp: int, flags: int = 0, iters: int = 10):
         """(mean ms per batch, {stage: ms}) for the GPU part of jpeg_invert on resident inputs."""

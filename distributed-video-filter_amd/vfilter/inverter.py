@@ -15,15 +15,14 @@ is accepted here; the v1 wire format carries the shape when a producer provides 
 JPEG (the reference default, ``use_jpeg=True``, inverter.py:10): ``vfilter.jpeg.TurboJPEG``
 (PyTurboJPEG's API on the gfx950 baseline-JPEG codec, bit-exact with libjpeg-turbo) replaces
 ``turbojpeg.TurboJPEG`` (inverter.py:7,13).  A batch runs decode -> invert -> encode as one
-fused GPU pass; ``submit_batch`` hands it to one of two host threads, so one batch's host
-work (parse, staging, copy-out) overlaps the previous batch's GPU work (the library leases
-each call its own codec, stream and buffers).
+fused GPU pass; ``submit_batch`` stages and queues it (vf_jpeg_invert_submit) and returns, so
+the worker loop receives and stages batch k+1 while batch k is on the GPU — one host thread,
+two codecs (each in-flight batch holds its own codec, stream and buffers).
 """
 from __future__ import annotations
 
 import argparse
 import signal
-import threading
 import time
 from typing import List, Optional, Sequence
 
@@ -48,7 +47,6 @@ class InverterWorker(Worker):
         # inverter.py:13 — TurboJPEG() with PyTurboJPEG's defaults, on this worker's GPU
         self.jpeg = TurboJPEG(ctx=self.ctx, tj_version=tj_version) if use_jpeg else None
         self._registered: List[int] = []
-        self._jpool = None  # executor for asynchronous JPEG batches (submit_batch)
         if install_signal_handlers:                                  # inverter.py:16-18
             signal.signal(signal.SIGINT, self._signal_handler)
             signal.signal(signal.SIGTERM, self._signal_handler)
@@ -115,7 +113,10 @@ class InverterWorker(Worker):
         Ring frames (page-locked) are DMA'd in place; socket payloads are staged.  JPEG
         batches go to a 2-thread executor (fused decode -> invert -> encode per batch)."""
         if self.jpeg and self.delay <= 0:
-            return ("jpeg", self._jpeg_pool().submit(self.process_batch, list(frames), metas, outs), len(frames))
+            try:  # staged and queued now; the loop receives the next batch while this one runs
+                return ("jpeg", self.jpeg.invert_batch_submit(list(frames)), list(frames))
+            except Exception:  # a frame the host parser refuses: frame by frame (worker.py:74-76)
+                return ("done", super().process_batch(frames, metas, outs), [])
         if self.jpeg or self.delay > 0:
             return super().submit_batch(frames, metas, outs)
         srcs, dsts = [], []
@@ -129,21 +130,15 @@ class InverterWorker(Worker):
             return ("done", [e] * len(frames), [])
         return ("gpu", ticket, srcs, dsts)  # srcs kept alive until the ticket completes
 
-    def _jpeg_pool(self):
-        if self._jpool is None:
-            from concurrent.futures import ThreadPoolExecutor
-            self._jpool = ThreadPoolExecutor(max_workers=2, thread_name_prefix="vf-jpeg")
-        return self._jpool
-
     def poll_batch(self, handle, block: bool):
         if handle[0] == "jpeg":
-            fut = handle[1]
-            if not block and not fut.done():
+            _, ticket, frames = handle
+            if not block and not self.jpeg.invert_batch_ready(ticket):
                 return None
             try:
-                return fut.result(), []
-            except Exception as e:
-                return [e] * handle[2], []
+                return self.jpeg.invert_batch_result(ticket), []
+            except Exception:  # e.g. a truncated stream the GPU found: frame by frame
+                return Worker.process_batch(self, frames, [None] * len(frames), [None] * len(frames)), []
         if handle[0] != "gpu":
             return super().poll_batch(handle, block)
         _, ticket, _srcs, dsts = handle
@@ -177,9 +172,6 @@ class InverterWorker(Worker):
             except Exception:
                 pass
         self._registered.clear()
-        if self._jpool is not None:
-            self._jpool.shutdown(wait=True)
-            self._jpool = None
         super().close()
         self.ctx.close()
 

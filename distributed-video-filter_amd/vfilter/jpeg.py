@@ -102,3 +102,16 @@ class TurboJPEG:
         """One fused GPU pass over the batch (safe to call from several threads at once: each
         call leases its own codec)."""
         return self.ctx.jpeg_invert(list(jpeg_bufs), quality, jpeg_subsample, self._enc_flags(flags, quality))
+
+    def invert_batch_submit(self, jpeg_bufs: Sequence, quality: int = 85, jpeg_subsample: int = TJSAMP_422,
+                            flags: int = 0) -> int:
+        """invert_batch, asynchronously: stage and queue the batch, return a ticket at once.
+        One host thread can keep several batches in flight (each holds its own codec)."""
+        return self.ctx.jpeg_invert_submit(list(jpeg_bufs), quality, jpeg_subsample, self._enc_flags(flags, quality))
+
+    def invert_batch_ready(self, ticket: int) -> bool:
+        return self.ctx.jpeg_invert_ready(ticket)
+
+    def invert_batch_result(self, ticket: int) -> List[np.ndarray]:
+        """The inverted JPEGs of a submitted batch (bytes-like uint8 views), in batch order."""
+        return self.ctx.jpeg_invert_result(ticket)

@@ -237,6 +237,27 @@ int vf_jpeg_invert(vf_ctx *ctx, const uint8_t *const *jpegs, const size_t *jpeg_
                    int quality, int subsamp, int flags, uint8_t *const *outs, const size_t *caps,
                    size_t *sizes);
 
+/* vf_jpeg_invert in three steps, so one host thread keeps batches in flight (the worker loop
+ * of worker.py:35-76 receiving batch k+1 while batch k is on the GPU) instead of blocking per
+ * batch:
+ *   vf_jpeg_invert_submit  parses and stages the batch and queues all of its GPU work; returns
+ *                          a ticket without waiting for the GPU.  The inputs are copied: the
+ *                          caller may reuse them at once.  Each in-flight batch holds one of the
+ *                          context's codecs (at most 8 in flight; never blocks);
+ *   vf_jpeg_invert_query   *done = 1 once the batch's results have landed in host memory;
+ *   vf_jpeg_invert_wait    blocks until then; *total = bytes of the packed outputs (frames
+ *                          back to back, 64-B aligned).  A failed batch ends here (ticket gone);
+ *   vf_jpeg_invert_fetch   copies the packed outputs to `out` (cap >= total; frame i is
+ *                          sizes[i] bytes at offsets[i]) and ends the batch.  out == NULL ends
+ *                          it without copying.  VF_E_INVALID with cap too small keeps it.
+ * Same results as vf_jpeg_invert, bit for bit. */
+int vf_jpeg_invert_submit(vf_ctx *ctx, const uint8_t *const *jpegs, const size_t *jpeg_sizes, int n,
+                          int quality, int subsamp, int flags, uint64_t *ticket);
+int vf_jpeg_invert_query(vf_ctx *ctx, uint64_t ticket, int *done);
+int vf_jpeg_invert_wait(vf_ctx *ctx, uint64_t ticket, size_t *total);
+int vf_jpeg_invert_fetch(vf_ctx *ctx, uint64_t ticket, uint8_t *out, size_t cap, size_t *sizes,
+                         size_t *offsets);
+
 /* Benchmark: the GPU part of vf_jpeg_invert (inputs already in HBM) run `iters` times; *ms =
  * mean wall ms per iteration; stage_ms (may be NULL, 8 floats) = mean ms of unstuff, Huffman
  * sync, Huffman write, DC+IDCT, colour+invert, FDCT+Huffman encode, byte stuffing, and the

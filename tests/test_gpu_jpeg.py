@@ -152,7 +152,7 @@ def test_bad_huffman_tables_raise(tj):
 
 
 def test_concurrent_calls_lease_separate_codecs(tj):
-    """Two host threads call invert_batch at once (what the JPEG worker's 2-thread submit
+    """Three host threads call invert_batch at once (a caller sharing one context between threads
     does): each call leases its own codec, stream and buffers, so both stay bit-exact."""
     import threading
     batches = [[J.encode(_img("scene", 10 * t + s, h, w)) for s in range(3)]
@@ -195,3 +195,40 @@ def test_sync_modes_on_hard_content(tj, monkeypatch, mode, subsamp, quality):
     got = tj.invert_batch(jpgs)
     for g, j in zip(got, jpgs):
         assert g == J.invert_jpeg(j)
+
+
+def test_async_submit_keeps_batches_in_flight(tj, vf_ctx):
+    """vf_jpeg_invert_submit / _query / _wait / _fetch (the worker's form): batches submitted
+    back to back from one thread come back bit-exact, in any collection order; a stream the
+    host parser refuses fails at submit, a truncated one at wait (and frees its codec); a
+    released ticket is gone."""
+    batches = [[J.encode(_img("scene", 40 + 3 * b + s, h, w)) for s in range(3)]
+               for b, (h, w) in enumerate([(480, 640), (1080, 1920), (64, 48)])]
+    want = [[J.invert_jpeg(j) for j in b] for b in batches]
+    tickets = [tj.invert_batch_submit(b) for b in batches]
+    for k in (2, 0, 1):
+        got = tj.invert_batch_result(tickets[k])
+        assert [bytes(g) for g in got] == want[k], k
+    t = tj.invert_batch_submit(batches[0])
+    import time
+    t0 = time.time()
+    while not tj.invert_batch_ready(t):
+        assert time.time() - t0 < 30
+    assert [bytes(g) for g in tj.invert_batch_result(t)] == want[0]
+    with pytest.raises(VFilterError):
+        tj.invert_batch_submit([b"\xff\xd8garbage"])
+    good = batches[2][0]
+    t = tj.invert_batch_submit([good, good[: len(good) // 2] + b"\xff\xd9"])
+    with pytest.raises(VFilterError):
+        tj.invert_batch_result(t)
+    t = tj.invert_batch_submit([good])
+    vf_ctx.jpeg_invert_release(t)
+    with pytest.raises(VFilterError):
+        tj.invert_batch_result(t)
+    # at most 8 batches in flight per context; the 9th is refused, not blocked
+    ts = [tj.invert_batch_submit([good]) for _ in range(8 - 0)]
+    with pytest.raises(VFilterError):
+        tj.invert_batch_submit([good])
+    for t in ts:
+        assert bytes(tj.invert_batch_result(t)[0]) == want[2][0]
+    assert tj.invert(good) == want[2][0]

@@ -118,6 +118,29 @@ def test_config4_mixed_resolution_pull_tcp_payloads():
 
 
 @pytest.mark.timeout(120)
+def test_inverter_worker_call_matches_captured_reference(golden_dir):
+    """The product InverterWorker.__call__ (raw) against the reference's own __call__ outputs
+    captured in tests/golden/ref_inverter_call.json (inverter.py:34 -> :41 -> :46); where the
+    reference raises ValueError (sizes other than 480x480) the product inverts."""
+    import hashlib
+    import json
+    from vfilter.inverter import InverterWorker
+    d = json.load(open(os.path.join(golden_dir, "ref_inverter_call.json")))
+    w = InverterWorker("127.0.0.1", 1, 1, 0.0, use_jpeg=False, install_signal_handlers=False, transport="tcp")
+    try:
+        for c in d["cases"]:
+            x = oracle.synthetic_frame(c["seed"], *c["shape"][:2]).tobytes()
+            assert hashlib.sha256(x).hexdigest() == c["input_sha256"]
+            y = bytes(w(x))
+            assert len(y) == c["output_len"] and hashlib.sha256(y).hexdigest() == c["output_sha256"]
+        for e in d["other_sizes"]:
+            x = oracle.synthetic_frame(1, *e["shape"][:2]).tobytes()
+            assert bytes(w(x)) == oracle.invert_bytes(x)
+    finally:
+        w.close()
+
+
+@pytest.mark.timeout(120)
 def test_inverter_worker_call_matches_reference_raw_path():
     """InverterWorker.__call__ on a 480x480 raw frame == the reference's raw path output
     (inverter.py:34 -> :41 -> :46), and any other size works too (the reference drops it)."""

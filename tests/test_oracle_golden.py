@@ -127,3 +127,23 @@ def test_dispatch_slot_matches_reference(golden_dir):
     add(5)
     assert ready() == steps["ready-after-frames-4-5"]
     assert ready() == steps["ready-again-no-new-frame-2"]
+
+
+def test_oracle_raw_call_matches_reference_inverter(golden_dir):
+    """ref_inverter_call.json: the reference's own InverterWorker.__call__ (use_jpeg=False,
+    inverter.py:29-46) on seeded 480x480 frames, captured by capture_inverter_call.py (cv2 is
+    absent: its bitwise_not was numpy's, so this pins the raw framing, see the fixture)."""
+    d = _load(golden_dir, "ref_inverter_call.json")
+    assert len(d["cases"]) >= 4 and "cv2.bitwise_not" in d["stand_ins"]
+    for c in d["cases"]:
+        h, w, _ = c["shape"]
+        x = oracle.synthetic_frame(c["seed"], h, w).tobytes()
+        assert hashlib.sha256(x).hexdigest() == c["input_sha256"], "rng stream drifted"
+        y = oracle.reference_raw_call(x)
+        assert isinstance(y, bytes) and len(y) == c["output_len"]
+        assert hashlib.sha256(y).hexdigest() == c["output_sha256"]
+        assert y[:64].hex() == c["output_prefix_hex"]
+    for e in d["other_sizes"]:
+        with pytest.raises(ValueError) as ei:
+            oracle.reference_raw_call(np.zeros(e["shape"], np.uint8).tobytes())
+        assert e["error_type"] == "ValueError" and str(ei.value) == e["error"]

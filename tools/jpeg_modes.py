@@ -5,6 +5,8 @@ one size per run, each in a fresh process so codec settings (read at codec creat
   2threads     two host threads, each call leasing its own codec (kernels ordered by the
                context's compute gate)
   2threads_nogate   the same with VF_JPEG_GATE=0 (kernels of the two codecs may overlap)
+  async        ONE host thread keeping two batches in flight (invert_batch_submit / _result,
+               vf_jpeg_invert_submit & co.): the InverterWorker's form
 Prints one JSON line per mode.  VF_JPEG_TRACE=1 adds the library's per-call phase times.
   python tools/jpeg_modes.py 1080p [mode]"""
 import json
@@ -19,7 +21,7 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "distributed-video-filter_amd")]
 SIZES = {"480p": (480, 640), "1080p": (1080, 1920), "4k": (2160, 3840)}
 
 
-def run(size, mode, batch=32, reps=12):
+def run(size, mode, batch=32, reps=24):
     from vfilter import Context
     from vfilter.jpeg import TurboJPEG
     from vfilter.synthetic import synthetic_scene
@@ -28,7 +30,20 @@ def run(size, mode, batch=32, reps=12):
     tj = TurboJPEG(ctx=ctx)
     jpgs = tj.encode_batch([synthetic_scene(s, h, w) for s in range(8)])
     jpgs = [jpgs[i % 8] for i in range(batch)]
-    if mode == "1thread":
+    if mode == "async":
+        for _ in range(3):  # warm both codecs (the first use of a codec allocates its buffers)
+            a, b = tj.invert_batch_submit(jpgs), tj.invert_batch_submit(jpgs)
+            tj.invert_batch_result(a)
+            tj.invert_batch_result(b)
+        t0 = time.perf_counter()
+        q = [tj.invert_batch_submit(jpgs)]
+        for _ in range(reps - 1):
+            q.append(tj.invert_batch_submit(jpgs))
+            out = tj.invert_batch_result(q.pop(0))
+        out = tj.invert_batch_result(q.pop(0))
+        dt = time.perf_counter() - t0
+        assert [bytes(o) for o in out] == tj.invert_batch(jpgs)
+    elif mode == "1thread":
         for _ in range(3):
             tj.invert_batch(jpgs)
         t0 = time.perf_counter()
@@ -53,7 +68,7 @@ if __name__ == "__main__":
     if len(sys.argv) > 2:
         run(size, sys.argv[2])
     else:
-        for mode in ("1thread", "2threads", "2threads_nogate"):
+        for mode in ("1thread", "2threads", "async"):
             env = dict(os.environ)
             if mode == "2threads_nogate":
                 env["VF_JPEG_GATE"] = "0"
