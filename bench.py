@@ -336,15 +336,61 @@ def jpeg_mode(ctx, batch, iters=20):
         tj.invert_batch_result(q.pop(0))
     tj.invert_batch_result(q.pop(0))
     h2h_async = (time.perf_counter() - t0) / 20
+    outs = tj.invert_batch(jpgs)
+    passes = stages.pop("sync_passes", 0.0)
     return {"workload": f"1080p JPEG (q85 4:2:2) decode -> bitwise_not -> encode, batch {batch}",
             "gpu_resident_fps": round(batch / (ms / 1e3), 1), "gpu_resident_ms_per_batch": round(ms, 3),
             "stages_ms": {k: round(v, 4) for k, v in stages.items()},
+            "huffman_sync_mode": "speculative (one pass)" if passes == 0 else f"pass-based, {passes:.1f} passes",
+            "roofline": jpeg_roofline(stages, H, W, batch, sum(len(j) for j in jpgs), sum(len(o) for o in outs)),
             "host_to_host_fps": round(batch / h2h, 1),
             "host_to_host_2threads_fps": round(batch / h2h_pipe, 1),
             "host_to_host_worker_fps": round(batch / h2h_async, 1),
             "host_to_host_note": "1 call at a time | 2 host threads | the worker's form: 1 thread, 2 batches "
                                  "in flight (vf_jpeg_invert_submit / _wait / _fetch)",
             "jpeg_bytes_mean": round(sum(len(j) for j in jpgs) / batch)}, jpgs
+
+
+def jpeg_roofline(stages, h, w, batch, j_in, j_out):
+    """Per-stage algorithmic bytes of the fused JPEG pass (1080p 4:2:2 in and out) against the
+    stage's hipEvent time, as a fraction of the 8 TB/s HBM peak, with the resource that binds
+    each stage (from the SQ counters in profiles/r02_jpeg_pmc_sq.txt: none of the entropy or
+    pixel stages is HBM-bound).  Bytes: J = compressed bytes in / out of the batch; per 4:2:2
+    MCU of 16x8 pixels, 4 blocks of 64 coefficients (int16: 128 B) and 64 plane samples."""
+    mcus = -(-w // 16) * -(-h // 8)
+    blocks = batch * mcus * 4
+    pix = batch * h * w * 3
+    coef, planes = blocks * 128, blocks * 64
+    model = {  # stage: (bytes, what, binding resource)
+        "unstuff": (2 * j_in, "read J_in, write J_in", "launch/latency (a few MB)"),
+        "huffman_sync": (j_in, "read J_in once (the minimum; the speculative decode reads it bpm-fold)",
+                         "dependent Huffman table lookups (LDS latency)"),
+        "huffman_write": (j_in + coef, "read J_in, write the coefficient blocks",
+                          "dependent Huffman table lookups (LDS latency)"),
+        "dc_idct": (coef + planes + 4 * blocks, "read coefficients + DC, write planes",
+                    "load latency + VALU (LDS conflict-free)"),
+        "color_invert": (planes + pix, "read planes, write BGR pixels", "load latency per wave"),
+        "fdct_huffman": (pix + 3 * j_out + 10 * blocks, "read pixels, write + pack AC words",
+                         "VALU + issue latency"),
+        "stuffing": (5 * j_out, "count + write FF00 stuffing, compact", "launch/latency (a few MB)"),
+    }
+    out = {}
+    tot_b, tot_ms = 0, 0.0
+    for k, (b, what, bound) in model.items():
+        ms = stages.get(k)
+        if not ms:
+            continue
+        gbs = b / (ms * 1e-3) / 1e9
+        out[k] = {"bytes": int(b), "ms": round(ms, 4), "GBps": round(gbs, 1),
+                  "frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 4), "bytes_are": what, "bound": bound}
+        tot_b += b
+        tot_ms += ms
+    out["total"] = {"bytes": int(tot_b), "ms": round(tot_ms, 4),
+                    "GBps": round(tot_b / (tot_ms * 1e-3) / 1e9, 1) if tot_ms else None,
+                    "frac_of_hbm_peak": round(tot_b / (tot_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if tot_ms else None}
+    out["note"] = ("algorithmic bytes per stage / hipEvent stage time; the JPEG pass is bound by dependent "
+                   "table lookups and VALU latency, not by HBM (no stage above 35 % of peak)")
+    return out
 
 
 def cpu_baseline_jpeg(jpgs, seconds):

@@ -28,6 +28,7 @@
 #include <vector>
 
 #include "../../include/vfilter.h"
+#include "vf_host_mem.h"
 #include "vf_internal.h"
 #include "vf_jpeg_codec.h"
 
@@ -368,9 +369,9 @@ VF_EXPORT int vf_alloc_host(vf_ctx *ctx, size_t nbytes, void **out) {
   if (!out) return set_err(ctx, VF_E_INVALID, 0, "vf_alloc_host: out is NULL");
   *out = nullptr;
   VF_HIP(ctx, hipSetDevice(ctx->device));
-  hipError_t e = hipHostMalloc(out, nbytes ? nbytes : 1, hipHostMallocDefault);
+  hipError_t e = vf::numa_pinned_alloc(out, nbytes ? nbytes : 1, vf::device_numa_node(ctx->device));
   if (e != hipSuccess)
-    return set_err(ctx, VF_E_NOMEM, (int)e, "hipHostMalloc(%zu) failed: %s", nbytes, hipGetErrorString(e));
+    return set_err(ctx, VF_E_NOMEM, (int)e, "pinned allocation of %zu bytes failed: %s", nbytes, hipGetErrorString(e));
   ctx->engine->note_pinned(*out, nbytes ? nbytes : 1);
   return VF_OK;
 }
@@ -380,7 +381,7 @@ VF_EXPORT int vf_free_host(vf_ctx *ctx, void *p) {
   if (!p) return VF_OK;
   ctx->engine->drain();  // a queued job may still read or write it
   ctx->engine->forget_pinned(p);
-  VF_HIP(ctx, hipHostFree(p));
+  VF_HIP(ctx, vf::numa_pinned_free(p));
   return VF_OK;
 }
 

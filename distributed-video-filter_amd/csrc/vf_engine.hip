@@ -24,6 +24,7 @@
 #include <cstdlib>
 #include <cstring>
 
+#include "vf_host_mem.h"
 #include "vf_internal.h"
 
 namespace vf {
@@ -121,8 +122,8 @@ Engine::~Engine() {
   for (auto &s : slots_) {
     for (hipEvent_t e : {s.h0, s.k0, s.k1, s.done})
       if (e) (void)hipEventDestroy(e);
-    if (s.pin_in) (void)hipHostFree(s.pin_in);
-    if (s.pin_out) (void)hipHostFree(s.pin_out);
+    (void)numa_pinned_free(s.pin_in);
+    (void)numa_pinned_free(s.pin_out);
     if (s.d_in) (void)hipFree(s.d_in);
     if (s.d_out) (void)hipFree(s.d_out);
   }
@@ -151,8 +152,9 @@ hipError_t Engine::init(int device, int nslots, size_t slot_bytes, const LaunchC
       *err = std::string("event creation failed: ") + hipGetErrorString(e);
       return e;
     }
-    if ((e = hipHostMalloc((void **)&s.pin_in, slot_bytes, hipHostMallocDefault)) != hipSuccess ||
-        (e = hipHostMalloc((void **)&s.pin_out, slot_bytes, hipHostMallocDefault)) != hipSuccess ||
+    const int node = device_numa_node(device);  // staging on the GPU's own socket
+    if ((e = numa_pinned_alloc((void **)&s.pin_in, slot_bytes, node)) != hipSuccess ||
+        (e = numa_pinned_alloc((void **)&s.pin_out, slot_bytes, node)) != hipSuccess ||
         (e = hipMalloc((void **)&s.d_in, slot_bytes)) != hipSuccess ||
         (e = hipMalloc((void **)&s.d_out, slot_bytes)) != hipSuccess) {
       char buf[160];
@@ -258,6 +260,11 @@ void Engine::drain() {
 // ---- engine thread -----------------------------------------------------------------------
 
 void Engine::fail_all(hipError_t e, const char *what) {
+  // copies already queued for direct (caller-pinned) jobs may still be moving: let them land
+  // before the callers hear of the failure and free or reuse their buffers
+  (void)hipStreamSynchronize(s_in_);
+  (void)hipStreamSynchronize(s_out_);
+  (void)hipGetLastError();
   char buf[256];
   std::snprintf(buf, sizeof buf, "%s failed: %s (%s)", what, hipGetErrorString(e), hipGetErrorName(e));
   std::lock_guard<std::mutex> lk(mu_);

@@ -18,6 +18,7 @@
 #include <string>
 #include <vector>
 
+#include "vf_host_mem.h"
 #include "vf_jpeg.h"
 #include "vf_jpeg_codec.h"
 
@@ -476,18 +477,18 @@ DevBuf::~DevBuf() {
 
 hipError_t HostBuf::ensure(size_t n) {
   if (n <= cap) return hipSuccess;
-  if (p) (void)hipHostFree(p);
+  (void)numa_pinned_free(p);
   p = nullptr;
   cap = 0;
   n = align_up(std::max<size_t>(n, 256), 1 << 20);
-  hipError_t e = hipHostMalloc(&p, n, hipHostMallocDefault);
+  int dev = 0;
+  (void)hipGetDevice(&dev);  // the codec's device (Codec::init set it on this thread)
+  hipError_t e = numa_pinned_alloc(&p, n, device_numa_node(dev));
   if (e == hipSuccess) cap = n;
   return e;
 }
 
-HostBuf::~HostBuf() {
-  if (p) (void)hipHostFree(p);
-}
+HostBuf::~HostBuf() { (void)numa_pinned_free(p); }
 
 // ---- codec -------------------------------------------------------------------------------------
 

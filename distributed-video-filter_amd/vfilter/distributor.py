@@ -57,7 +57,7 @@ from . import transport as tp
 from . import wire
 from .reorder import DisplayBuffer, OrderedBuffer
 from .sharding import chunk_owner
-from .shm import FrameRing
+from .shm import FrameRing, copy_into
 
 
 class _Peer:
@@ -419,9 +419,7 @@ class Distributor:
             slot = self.reserve_frame(nbytes, block)
             if slot is None:
                 return -1
-            src = frame.reshape(-1).view(np.uint8) if isinstance(frame, np.ndarray) else \
-                np.frombuffer(frame, dtype=np.uint8)
-            self.in_view(slot, nbytes)[:] = src
+            copy_into(self.in_view(slot, nbytes), frame)
             return self.commit_frame(slot, nbytes, shape, timestamp, block)
         return self._enqueue(frame, nbytes, shape, None, timestamp, block)
 
