@@ -19,10 +19,12 @@ Prints ONE JSON line on rank 0 (contract in the task statement), including
                 process_scaling_fps: 1, 2, 4, 8 and 16 processes; sizes: 1 core at 480p and 4K
   sizes         kernel-only frames/s and HBM fraction at 480p / 1080p / 4K on this run's GPUs
                 (north star: every size at 1/2/4/8 GPUs), same timing rules as the headline
+  configs4_sweep  BASELINE configs[4]: 1080p batches of 256 ... 4096 frames resident per rank
   end_to_end    host->host rate through vf_invert_batch_host (pageable and pinned): PCIe-bound,
                 reported beside value, never as value.
   jpeg_mode     the reference's default use_jpeg=True path (decode -> invert -> encode) on 1080p
-                JPEGs: GPU-resident and host->host frames/s, with libjpeg-turbo on 1 core beside it.
+                JPEGs: GPU-resident and host->host frames/s (in a child process without torch, as
+                a worker process runs it), per-stage roofline, libjpeg-turbo on 1 core beside it.
   distributor   configs[2] (4K, batch 16, frame-index shards, in-order reassembly) and configs[3]
                 (mixed 480p/1080p/4K stream, ordering overhead) through the distributor with one
                 worker process per GPU of this run: host->host frames/s, never the headline.
@@ -68,10 +70,12 @@ def parse():
     ap.add_argument("--no-distributor", action="store_true",
                     help="skip the configs[2]/[3] distributor leg (worker process per GPU)")
     ap.add_argument("--no-sizes", action="store_true", help="skip the 480p / 1080p / 4K kernel leg")
+    ap.add_argument("--no-sweep", action="store_true", help="skip the configs[4] 256..4096-frame resident sweep")
     ap.add_argument("--cpu-procs", type=int, default=16,
                     help="processes of the multi-process CPU baseline (capped by the CPU affinity; 0 = skip)")
     ap.add_argument("--probe", action="store_true", help=argparse.SUPPRESS)  # child under rocprofv3
     ap.add_argument("--cpu-worker", type=float, default=0.0, help=argparse.SUPPRESS)  # cpu_baseline_multi child
+    ap.add_argument("--jpeg-child", type=int, default=-1, help=argparse.SUPPRESS)  # jpeg leg on device N
     return ap.parse_args()
 
 
@@ -254,6 +258,43 @@ def resolution_leg(ctx, np, rank, world, steps, barrier_sync, reduce_max):
                      "fps": round(world * steps * batch / elapsed, 1),
                      "kernel_GBps_per_gpu": round(gbs, 1), "frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 4)}
     out["note"] = "kernel-only, HBM-resident, whole job over all ranks; GB/s = slowest rank's mean launch"
+    return out
+
+
+def sweep_leg(ctx, np, host_batch, batch, rank, world, barrier_sync, reduce_max,
+              batches=(256, 512, 1024, 2048, 4096), warm_ms=300.0, timed_ms=200.0):
+    """BASELINE.json configs[4]: 1080p invert with 256 ... 4096 frames resident in HBM per
+    rank (1.6-25.5 GB in, the same out), one launch over the whole batch per step.  Each
+    point is warmed for >= warm_ms of kernel time, then >= timed_ms is timed under the
+    headline's rules (barrier + sync on both sides, max over ranks)."""
+    fb = FRAME_BYTES
+    out = {}
+    for nb in batches:
+        bb = nb * fb
+        src, dst = ctx.alloc_device(bb), ctx.alloc_device(bb)
+        for off in range(0, nb, batch):  # the rank's synthetic batch, repeated
+            k = min(batch, nb - off)
+            ctx.upload(src + off * fb, host_batch, k * fb)
+        ctx.sync()
+        done = 0.0
+        while done < warm_ms:
+            ms, _ = ctx.bench_device_ring([src], [dst], bb, 2)
+            done += ms
+        steps = max(3, int(timed_ms / (ms / 2)) + 1)
+        barrier_sync()
+        t0 = time.perf_counter()
+        region, _ = ctx.bench_device_ring([src], [dst], bb, steps)
+        ctx.sync()
+        barrier_sync()
+        elapsed = reduce_max(time.perf_counter() - t0)
+        mean_ms = reduce_max(region / steps)
+        ctx.free_device(src)
+        ctx.free_device(dst)
+        gbs = 2.0 * bb / (mean_ms * 1e-3) / 1e9
+        out[str(nb)] = {"bytes_in_per_rank": bb, "steps": steps, "fps": round(world * nb * steps / elapsed, 1),
+                        "ms_per_launch": round(mean_ms, 4), "kernel_GBps_per_gpu": round(gbs, 1),
+                        "frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 4)}
+    out["note"] = "configs[4]: kernel-only, HBM-resident, whole job over all ranks; GB/s = slowest rank's mean launch"
     return out
 
 
@@ -478,10 +519,37 @@ def distributor_leg(nworkers, ngpu, host_gbps=None, pcie_gbps=None, frames_scale
     return out
 
 
+def jpeg_child(args):
+    """The JPEG leg in a fresh interpreter without torch, as a worker process runs it
+    (`python -m vfilter.inverter` imports no torch); prints one JSON object."""
+    from vfilter import Context
+    ctx = Context(args.jpeg_child)
+    jpeg, jpgs = jpeg_mode(ctx, args.batch)
+    ctx.close()
+    if args.cpu_seconds > 0:
+        jpeg["cpu_reference"] = cpu_baseline_jpeg(jpgs, min(5.0, args.cpu_seconds))
+    print(json.dumps(jpeg), flush=True)
+
+
+def run_jpeg_child(device, batch, cpu_seconds, timeout_s=300):
+    cmd = [sys.executable, os.path.abspath(__file__), "--jpeg-child", str(device), "--batch", str(batch),
+           "--cpu-seconds", str(cpu_seconds)]
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout_s)
+    except subprocess.TimeoutExpired:
+        return {"error": f"timed out after {timeout_s} s"}
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if r.returncode != 0 or not lines:
+        return {"error": f"rc={r.returncode}: {r.stderr[-300:]}"}
+    return json.loads(lines[-1])
+
+
 def main():
     args = parse()
     if args.probe:
         return probe(args)
+    if args.jpeg_child >= 0:
+        return jpeg_child(args)
     if args.cpu_worker:
         return cpu_worker(args.cpu_worker)
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -562,15 +630,19 @@ def main():
         sizes = resolution_leg(ctx, np, rank, world, 100, barrier_sync, reduce_max)
         if rank == 0:
             log(f"sizes: {sizes}")
+    sweep = None
+    if not args.no_sweep:
+        sweep = sweep_leg(ctx, np, host_batch, args.batch, rank, world, barrier_sync, reduce_max)
+        if rank == 0:
+            log(f"configs[4] sweep: {sweep}")
     e2e = None
     cpu = None
     if rank == 0 and not args.no_e2e:
         e2e = end_to_end(ctx, host_batch, args.batch, np)
         log(f"end-to-end: {e2e}")
     jpeg = None
-    jpgs = None
     if rank == 0 and not args.no_jpeg:
-        jpeg, jpgs = jpeg_mode(ctx, args.batch)
+        jpeg = run_jpeg_child(device, args.batch, args.cpu_seconds)
         log(f"jpeg mode: {jpeg}")
     if rank == 0 and args.cpu_seconds > 0:
         # after every timed region (the other ranks wait at the distributor leg's barrier); at
@@ -591,9 +663,6 @@ def main():
         if full:
             cpu["sizes"] = cpu_baseline_sizes(min(3.0, args.cpu_seconds), np)
         log(f"cpu baseline: {cpu}")
-        if jpeg is not None:
-            jpeg["cpu_reference"] = cpu_baseline_jpeg(jpgs, min(5.0, args.cpu_seconds))
-            log(f"jpeg cpu reference: {jpeg['cpu_reference']}")
 
     ctx.close()
 
@@ -606,7 +675,7 @@ def main():
             fanout = distributor_leg(world, max(1, min(world, torch.cuda.device_count())), host_gbps, pcie_gbps)
             log(f"distributor leg: {fanout}")
         if world > 1:
-            dist.barrier()  # the other ranks idle (their GPUs serve the leg's workers)
+            dist.barrier(group=cpu_group)  # host-only: the other ranks idle while rank 0 runs its legs
 
     if rank == 0:
         frames = world * args.steps * args.batch
@@ -640,6 +709,7 @@ def main():
                          "traffic_detail": traffic_detail},
             "cpu_baseline": cpu,
             "sizes": sizes,
+            "configs4_sweep": sweep,
             "end_to_end": e2e,
             "jpeg_mode": jpeg,
             "distributor": fanout,

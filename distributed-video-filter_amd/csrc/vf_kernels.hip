@@ -17,6 +17,8 @@
 // XCD-aware block remapping (guide T1) buys nothing here: no two workgroups touch the
 // same line, so there is no L2 reuse to localise.
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 #include <stdint.h>
 
 #include "vf_internal.h"
@@ -24,56 +26,156 @@
 
 namespace vf {
 
-// src and dst misaligned relative to each other (their addresses differ mod 16): no common
-// 16-B grid exists, so fall back to coalesced bytewise access (64 B per wave-instruction).
-// Only reachable from vf_invert_device with caller pointers at unrelated offsets; the host
-// entry points always stage into 16-B-aligned slot buffers.
-__global__ __launch_bounds__(kBlock) void invert_bytes_kernel(const uint8_t *__restrict__ src,
-                                                              uint8_t *__restrict__ dst,
-                                                              uint64_t n) {
-  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
-  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride)
-    dst[i] = (uint8_t)~src[i];
+// ---- src and dst at different offsets mod 16 ------------------------------------------------
+// (caller views at unrelated offsets, or frames packed at odd offsets).  No common 16-B grid
+// exists, so the kernel keeps the STORES aligned: dst's head bytes go bytewise, and output
+// vector i of the body is the 16 source bytes at delta = 4Q + r bytes into the aligned source
+// vectors A_i, A_i+1.  Each lane loads both (two fully coalesced wave-instructions; the second
+// overlaps the first by all but one 16-B vector per wave, so HBM sees each byte once) and
+// funnel-shifts with v_alignbyte_b32.  Q is a template parameter (uniform register picks), r a
+// run-time byte shift.  Reading A_0 and A_n16 touches up to 15 bytes outside the source range,
+// always inside the 16-B vectors (hence pages) that hold its first and last bytes.
+template <int Q>
+__device__ __forceinline__ u32x4 shift16(u32x4 a, u32x4 b, uint32_t r) {
+  const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  u32x4 o;
+  o.x = __builtin_amdgcn_alignbyte(w[Q + 1], w[Q + 0], r);
+  o.y = __builtin_amdgcn_alignbyte(w[Q + 2], w[Q + 1], r);
+  o.z = __builtin_amdgcn_alignbyte(w[Q + 3], w[Q + 2], r);
+  o.w = __builtin_amdgcn_alignbyte(w[Q + 4], w[Q + 3], r);
+  return o;
 }
 
-// Descriptor-table form: blockIdx.y = frame, blockIdx.x strides within the frame.
+// body vectors [b0, n16) of one range, U per lane per tile, grid-strided by `stride` vectors
+template <int Q, int U>
+__device__ __forceinline__ void shift_body(const u32x4 *__restrict__ sa, u32x4 *__restrict__ d, uint64_t n16,
+                                           uint32_t r, uint64_t b0, uint64_t stride) {
+  constexpr uint64_t TILE = (uint64_t)kBlock * U;
+  const uint32_t t = threadIdx.x;
+  uint64_t t0 = b0;
+  for (; t0 + TILE <= n16; t0 += stride) {
+    u32x4 a[U], b[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      a[j] = ld16<true>(sa + t0 + j * kBlock + t);
+      b[j] = ld16<false>(sa + t0 + j * kBlock + t + 1);
+    }
+#pragma unroll
+    for (int j = 0; j < U; ++j) st16<true>(d + t0 + j * kBlock + t, ~shift16<Q>(a[j], b[j], r));
+  }
+  if (t0 < n16) {
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      const uint64_t i = t0 + (uint64_t)j * kBlock + t;
+      if (i < n16) st16<true>(d + i, ~shift16<Q>(ld16<true>(sa + i), ld16<false>(sa + i + 1), r));
+    }
+  }
+}
+
+template <int Q>
+__global__ __launch_bounds__(kBlock) void invert_shift_kernel(
+    const u32x4 *__restrict__ sa, u32x4 *__restrict__ d, uint64_t n16, uint32_t r,
+    const uint8_t *__restrict__ hsrc, uint8_t *__restrict__ hdst, uint32_t head,
+    const uint8_t *__restrict__ tsrc, uint8_t *__restrict__ tdst, uint32_t tail) {
+  shift_body<Q, 4>(sa, d, n16, r, (uint64_t)blockIdx.x * kBlock * 4, (uint64_t)gridDim.x * kBlock * 4);
+  if (blockIdx.x == 0) {
+    const uint32_t t = threadIdx.x;
+    if (t < head) hdst[t] = (uint8_t)~hsrc[t];
+    if (t < tail) tdst[t] = (uint8_t)~tsrc[t];
+  }
+}
+
+// aligned body vectors [b0, n16), U per lane per tile (the stream kernel's loop, per frame)
+template <int U>
+__device__ __forceinline__ void stream_body(const u32x4 *__restrict__ s, u32x4 *__restrict__ d, uint64_t n16,
+                                            uint64_t b0, uint64_t stride) {
+  constexpr uint64_t TILE = (uint64_t)kBlock * U;
+  const uint32_t t = threadIdx.x;
+  uint64_t t0 = b0;
+  for (; t0 + TILE <= n16; t0 += stride) {
+    u32x4 v[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) v[j] = ld16<true>(s + t0 + j * kBlock + t);
+#pragma unroll
+    for (int j = 0; j < U; ++j) st16<true>(d + t0 + j * kBlock + t, ~v[j]);
+  }
+  if (t0 < n16) {
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      const uint64_t i = t0 + (uint64_t)j * kBlock + t;
+      if (i < n16) st16<true>(d + i, ~ld16<true>(s + i));
+    }
+  }
+}
+
+// Descriptor-table form: blockIdx.y = frame, blockIdx.x strides within the frame, U = 4 vectors
+// per lane per tile; each frame takes the aligned or the shifting path by its own offsets.
 __global__ __launch_bounds__(kBlock) void invert_frames_kernel(const uint8_t *const *srcs,
                                                                uint8_t *const *dsts,
                                                                const size_t *nbytes) {
+  constexpr int U = 4;
   const uint32_t f = blockIdx.y;
   const uint8_t *s = srcs[f];
   uint8_t *d = dsts[f];
   const uint64_t n = nbytes[f];
   const uint32_t t = threadIdx.x;
-  const uint64_t stride16 = (uint64_t)gridDim.x * kBlock;
-  if ((((uintptr_t)s | (uintptr_t)d) & 15) == 0) {
-    const uint64_t n16 = n >> 4;
-    const u32x4 *s4 = reinterpret_cast<const u32x4 *>(s);
-    u32x4 *d4 = reinterpret_cast<u32x4 *>(d);
-    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + t; i < n16; i += stride16)
-      st16<true>(d4 + i, ~ld16<true>(s4 + i));
-    const uint64_t tail0 = n16 << 4;
-    if (blockIdx.x == 0 && tail0 + t < n) d[tail0 + t] = (uint8_t)~s[tail0 + t];
-  } else {
-    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + t; i < n; i += stride16)
-      d[i] = (uint8_t)~s[i];
+  const uint32_t h = (uint32_t)min((uint64_t)((16 - ((uintptr_t)d & 15)) & 15), n);  // dst head bytes
+  const uint64_t n16 = (n - h) >> 4;
+  const uint64_t body = n16 << 4;
+  if (blockIdx.x == 0) {
+    if (t < h) d[t] = (uint8_t)~s[t];
+    const uint64_t tail0 = h + body;
+    if (tail0 + t < n) d[tail0 + t] = (uint8_t)~s[tail0 + t];
+  }
+  if (!n16) return;
+  const uint64_t b0 = (uint64_t)blockIdx.x * kBlock * U, stride = (uint64_t)gridDim.x * kBlock * U;
+  u32x4 *d4 = reinterpret_cast<u32x4 *>(d + h);
+  const uintptr_t sb = (uintptr_t)(s + h);
+  const uint32_t delta = (uint32_t)(sb & 15);
+  const u32x4 *sa = reinterpret_cast<const u32x4 *>(sb - delta);
+  switch (delta >> 2) {  // uniform per workgroup
+    case 0:
+      if (delta == 0) stream_body<U>(sa, d4, n16, b0, stride);
+      else shift_body<0, U>(sa, d4, n16, delta & 3, b0, stride);
+      break;
+    case 1: shift_body<1, U>(sa, d4, n16, delta & 3, b0, stride); break;
+    case 2: shift_body<2, U>(sa, d4, n16, delta & 3, b0, stride); break;
+    default: shift_body<3, U>(sa, d4, n16, delta & 3, b0, stride); break;
   }
 }
 
 // ---- launchers ----------------------------------------------------------------------
+
+// src and dst at different offsets mod 16: dst's head bytewise, then the shifting body.
+static hipError_t launch_shift(const uint8_t *s, uint8_t *d, size_t nbytes, int max_blocks, hipStream_t stream) {
+  const uint32_t h = (uint32_t)std::min<size_t>((16 - ((uintptr_t)d & 15)) & 15, nbytes);
+  const uint64_t n16 = (nbytes - h) >> 4;
+  const uint32_t tail = (uint32_t)((nbytes - h) & 15);
+  const uintptr_t sb = (uintptr_t)(s + h);
+  const uint32_t delta = (uint32_t)(sb & 15);  // != 0: the offsets differ mod 16
+  const u32x4 *sa = reinterpret_cast<const u32x4 *>(sb - delta);
+  u32x4 *d4 = reinterpret_cast<u32x4 *>(d + h);
+  constexpr uint64_t TILE = (uint64_t)kBlock * 4;
+  uint64_t blocks = n16 ? (n16 + TILE - 1) / TILE : 1;
+  if (blocks > (uint64_t)max_blocks) blocks = (uint64_t)max_blocks;
+  const uint8_t *ts = s + h + (n16 << 4);
+  uint8_t *td = d + h + (n16 << 4);
+  const dim3 g((unsigned)blocks), b(kBlock);
+  switch (delta >> 2) {
+    case 0: hipLaunchKernelGGL(invert_shift_kernel<0>, g, b, 0, stream, sa, d4, n16, delta & 3, s, d, h, ts, td, tail); break;
+    case 1: hipLaunchKernelGGL(invert_shift_kernel<1>, g, b, 0, stream, sa, d4, n16, delta & 3, s, d, h, ts, td, tail); break;
+    case 2: hipLaunchKernelGGL(invert_shift_kernel<2>, g, b, 0, stream, sa, d4, n16, delta & 3, s, d, h, ts, td, tail); break;
+    default: hipLaunchKernelGGL(invert_shift_kernel<3>, g, b, 0, stream, sa, d4, n16, delta & 3, s, d, h, ts, td, tail); break;
+  }
+  return hipGetLastError();
+}
 
 hipError_t launch_invert(const void *dsrc, void *ddst, size_t nbytes, const LaunchCfg &cfg,
                          hipStream_t stream) {
   if (nbytes == 0) return hipSuccess;
   const uint8_t *s = static_cast<const uint8_t *>(dsrc);
   uint8_t *d = static_cast<uint8_t *>(ddst);
-  if ((((uintptr_t)s ^ (uintptr_t)d) & 15) != 0) {
-    uint64_t blocks = (nbytes + kBlock - 1) / kBlock;
-    if (blocks > (uint64_t)cfg.max_blocks) blocks = (uint64_t)cfg.max_blocks;
-    hipLaunchKernelGGL(invert_bytes_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, s,
-                       d, (uint64_t)nbytes);
-    return hipGetLastError();
-  }
+  if ((((uintptr_t)s ^ (uintptr_t)d) & 15) != 0) return launch_shift(s, d, nbytes, cfg.max_blocks, stream);
   return launch_stream<4, true, true>(s, d, nbytes, cfg.max_blocks, stream);
 }
 
@@ -81,8 +183,8 @@ hipError_t launch_invert_frames(const void *const *dsrcs, void *const *ddsts,
                                 const size_t *nbytes, int n, size_t total_bytes,
                                 const LaunchCfg &cfg, hipStream_t stream) {
   if (n <= 0) return hipSuccess;
-  // Spread one frame over enough blocks that the whole launch fills the chip.
-  const uint64_t per_frame = (total_bytes / (uint64_t)n + 16ull * kBlock - 1) / (16ull * kBlock);
+  // Spread one frame over enough blocks (one 16-KiB tile each) that the launch fills the chip.
+  const uint64_t per_frame = (total_bytes / (uint64_t)n + 64ull * kBlock - 1) / (64ull * kBlock);
   uint64_t gx = per_frame ? per_frame : 1;
   const uint64_t cap = (uint64_t)cfg.max_blocks / (uint64_t)n + 1;
   if (gx > cap) gx = cap;

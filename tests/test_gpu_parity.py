@@ -117,6 +117,65 @@ def test_device_entry_alignment(vf_ctx, soff, doff):
         vf_ctx.free_device(dd)
 
 
+def test_device_all_relative_offsets(vf_ctx):
+    """Every (src mod 16, dst mod 16) pair: equal offsets take the streaming kernel, unequal
+    ones the shifting kernel (aligned stores, v_alignbyte funnel shifts).  Sizes below, at and
+    across one 16-KiB tile; no byte outside [dst, dst + n) is touched."""
+    x = np.random.default_rng(5).integers(0, 256, 70_000, dtype=np.uint8)
+    ds = vf_ctx.alloc_device(x.nbytes + 64)
+    dd = vf_ctx.alloc_device(x.nbytes + 64)
+    try:
+        vf_ctx.upload(ds, np.zeros(x.nbytes + 64, np.uint8), x.nbytes + 64)
+        for soff in range(16):
+            vf_ctx.upload(ds + soff, x, x.nbytes)
+            for doff in range(16):
+                for n in (1, 15, 17, 4095, 16 * 1024 + 5, 70_000 - 16):
+                    vf_ctx.memset_device(dd, 0x5A, x.nbytes + 64)
+                    vf_ctx.invert_device(ds + soff, dd + doff, n)
+                    y = np.empty(x.nbytes + 64, np.uint8)
+                    vf_ctx.download(y, dd, y.nbytes)
+                    vf_ctx.sync()
+                    assert np.array_equal(y[doff:doff + n], oracle.invert(x[:n])), (soff, doff, n)
+                    assert (y[:doff] == 0x5A).all() and (y[doff + n:] == 0x5A).all(), (soff, doff, n)
+    finally:
+        vf_ctx.free_device(ds)
+        vf_ctx.free_device(dd)
+
+
+def test_device_frames_every_offset(vf_ctx):
+    """The descriptor kernel with 32 frames at every src/dst offset mod 16 (aligned and
+    shifted paths in one launch), sizes from 1 B to a 1080p frame."""
+    rng = np.random.default_rng(9)
+    sizes = [int(v) for v in rng.integers(1, 200_000, 31)] + [1920 * 1080 * 3]
+    frames = [rng.integers(0, 256, n, dtype=np.uint8) for n in sizes]
+    srcs = [vf_ctx.alloc_device(n + 32) for n in sizes]
+    dsts = [vf_ctx.alloc_device(n + 32) for n in sizes]
+    soffs = [i % 16 for i in range(32)]
+    doffs = [(7 * i + 3) % 16 for i in range(32)]
+    tables = [vf_ctx.alloc_device(8 * 32) for _ in range(3)]
+    try:
+        for f, s, o in zip(frames, srcs, soffs):
+            vf_ctx.upload(s + o, f, f.nbytes)
+        for d, n in zip(dsts, sizes):
+            vf_ctx.memset_device(d, 0x5A, n + 32)
+        sp = np.array([s + o for s, o in zip(srcs, soffs)], np.uint64)
+        dp = np.array([d + o for d, o in zip(dsts, doffs)], np.uint64)
+        nb = np.array(sizes, np.uint64)
+        for t, a in zip(tables, (sp, dp, nb)):
+            vf_ctx.upload(t, a, a.nbytes)
+        vf_ctx.invert_device_frames(tables[0], tables[1], tables[2], 32, sum(sizes))
+        vf_ctx.sync()
+        for f, d, o, n in zip(frames, dsts, doffs, sizes):
+            y = np.empty(n + 32, np.uint8)
+            vf_ctx.download(y, d, n + 32)
+            vf_ctx.sync()
+            assert np.array_equal(y[o:o + n], np.bitwise_not(f)), (o, n)
+            assert (y[:o] == 0x5A).all() and (y[o + n:] == 0x5A).all()
+    finally:
+        for p in srcs + dsts + tables:
+            vf_ctx.free_device(p)
+
+
 @pytest.mark.parametrize("soff,n", [(3, (600 << 20) + 77), (0, (512 << 20) + 16), (7, 1_300_000_009)])
 def test_device_split_launch_ragged(vf_ctx, soff, n):
     """Bodies above 512 MiB are cut into <= 256 MiB sub-launches (vf_kernels.hip

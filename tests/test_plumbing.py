@@ -284,7 +284,7 @@ def test_failed_frames_are_reported_and_skipped():
         d.cleanup()
 
 
-def test_perfetto_trace_reference_schema_plus_gpu_spans(tmp_path):
+def test_perfetto_trace_reference_schema_plus_gpu_spans(tmp_path, capsys):
     """export_perfetto_trace writes the reference's Chrome-trace schema
     (distributor.py:100-146): 'i' capture instants, 'X' worker spans keyed by worker pid; plus
     GPU spans on named tracks of the worker's pid."""
@@ -312,6 +312,15 @@ def test_perfetto_trace_reference_schema_plus_gpu_spans(tmp_path):
         assert [g["tid"] for g in gpu] == [1, 2, 3] and all(g["pid"] == 4242 for g in gpu)
         meta = [e for e in ev if e["ph"] == "M"]
         assert {m["args"]["name"] for m in meta} == {"GPU H2D", "GPU kernel", "GPU D2H"}
+        # the reference's summary after an export (distributor.py:151-171), plus the GPU stages
+        d.add_frame_for_distribution(b"def", t0 + 0.6)
+        d.export_perfetto_trace()
+        out = capsys.readouterr().out
+        assert "Average frame capture interval: 100.00ms" in out and "Frame capture rate: 10.0 FPS" in out
+        assert "Average processing duration: 250.00ms" in out and "Processing rate: 4.0 FPS" in out
+        assert "Total frames processed: 1" in out and "GPU kernel: 1 spans" in out
+        sm = d.trace_summary()
+        assert abs(sm["gpu"]["H2D"]["GBps"] - 3 / 0.1 / 1e9) < 1e-12
     finally:
         d.cleanup()
 
