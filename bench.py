@@ -630,16 +630,16 @@ def main():
         sizes = resolution_leg(ctx, np, rank, world, 100, barrier_sync, reduce_max)
         if rank == 0:
             log(f"sizes: {sizes}")
+    e2e = None
+    cpu = None
+    if rank == 0 and not args.no_e2e:  # before the sweep's 51 GB of allocations come and go
+        e2e = end_to_end(ctx, host_batch, args.batch, np)
+        log(f"end-to-end: {e2e}")
     sweep = None
     if not args.no_sweep:
         sweep = sweep_leg(ctx, np, host_batch, args.batch, rank, world, barrier_sync, reduce_max)
         if rank == 0:
             log(f"configs[4] sweep: {sweep}")
-    e2e = None
-    cpu = None
-    if rank == 0 and not args.no_e2e:
-        e2e = end_to_end(ctx, host_batch, args.batch, np)
-        log(f"end-to-end: {e2e}")
     jpeg = None
     if rank == 0 and not args.no_jpeg:
         jpeg = run_jpeg_child(device, args.batch, args.cpu_seconds)
