@@ -63,7 +63,7 @@ from .shm import FrameRing, copy_into
 class _Peer:
     __slots__ = ("pid", "version", "wid", "requests", "frames_sent", "results", "errors", "home_shard", "shm",
                  "numa", "slice", "queue", "inflight", "quarantine", "batches", "alive", "gone", "evictions",
-                 "order")
+                 "order", "last_seen", "waiting_since")
 
     def __init__(self, pid: bytes, req: wire.Request, order: int):
         self.pid = pid
@@ -85,6 +85,8 @@ class _Peer:
         self.alive = True
         self.gone = False                     # connection closed: no result can come any more
         self.evictions = 0
+        self.last_seen = time.monotonic()     # last request or result
+        self.waiting_since: Optional[float] = None  # frames wait for it, it has not asked
 
 
 class _Slice:
@@ -634,6 +636,7 @@ class Distributor:
                     return
             elif not p.alive and not p.gone:
                 self._revive(p)
+            p.last_seen = time.monotonic()
             if req.version == 0 and self.policy == "latest":
                 self._serve_latest_v0(p)                      # distributor.py:229-241
                 return
@@ -847,13 +850,27 @@ class Distributor:
 
     # ---- worker loss -----------------------------------------------------------------------
     def _check_deadlines(self) -> None:
+        """Evict a worker whose oldest batch is past ``batch_timeout``, and one that has frames
+        waiting for it but has neither asked for them nor had anything in flight for as long
+        (it stopped asking without closing its connection; ZeroMQ reports no disconnects)."""
         if self.batch_timeout <= 0:
             return
         now = time.monotonic()
         with self._cv:
             for p in list(self._peers.values()):
-                if p.alive and p.batches and now - p.batches[0][0] > self.batch_timeout:
+                if not p.alive:
+                    continue
+                if p.batches and now - p.batches[0][0] > self.batch_timeout:
                     self._evict(p, f"no result within {self.batch_timeout:g} s")
+                    continue
+                idle = (self.policy != "latest" and not p.batches and not p.requests
+                        and any(self._lanes_of(p)))
+                if not idle:
+                    p.waiting_since = None
+                elif p.waiting_since is None:
+                    p.waiting_since = now
+                elif now - p.waiting_since > self.batch_timeout:
+                    self._evict(p, f"frames waiting, no request for {self.batch_timeout:g} s")
 
     def _evict(self, p: _Peer, reason: str, gone: bool = False) -> None:
         """Take ``p`` out of service: re-queue (or lose, after ``max_attempts``) what it holds."""
@@ -936,6 +953,8 @@ class Distributor:
                               int(sp.get("bytes", 0)))
         with self._cv:
             sender = self._by_wid.get(res.wid) if res.wid else None
+            if sender is not None:
+                sender.last_seen = time.monotonic()
         for m, payload in zip(res.metas, res.payloads):
             self.log_frame_complete_timing(m.index, m.start, m.end, "frame_inverted_received", pid_val)
             with self._cv:
@@ -965,11 +984,13 @@ class Distributor:
                 if m.slot is not None and slot is None:
                     continue  # a ring result with no dispatch record: nothing to read it from
                 keep = self.zero_copy and m.slot is not None
-                if m.slot is not None:
-                    view = self.out_view(slot, m.nbytes)
-                    data = view if keep else bytes(view)
-                else:
-                    data = payload
+            # this copy (and its slot) is ours alone now: read the result outside the lock
+            if m.slot is not None:
+                view = self.out_view(slot, m.nbytes)
+                data = view if keep else bytes(view)
+            else:
+                data = payload
+            with self._cv:
                 if keep:
                     self._held[m.index] = slot
                 else:

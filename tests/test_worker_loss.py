@@ -289,3 +289,50 @@ def test_per_worker_slices_numa_bound():
         for s in socks:
             s.close()
         d.cleanup()
+
+
+@pytest.mark.timeout(60)
+def test_worker_that_stops_asking_is_evicted():
+    """A worker that keeps its connection but stops asking (no disconnect notice: ZeroMQ
+    gives none) while frames wait for it loses its shard after the timeout."""
+    d = Distributor(0, 0, policy="shard", reassembly="ordered", shard_workers=2, shard_chunk=1, queue_size=64,
+                    transport="tcp", host="127.0.0.1", verbose=False, batch_timeout=0.3)
+    d.running = True
+    a, b = _ManualWorker(d, "A"), _ManualWorker(d, "B")
+    coll = threading.Thread(target=d.check_inverter_output, daemon=True)
+    coll.start()
+    try:
+        a.request(credit=1)
+        _step_until(d, lambda: d.num_workers() == 1)
+        b.request(credit=1)
+        _step_until(d, lambda: d.num_workers() == 2)
+        d.add_frame_for_distribution(b"\\x00")          # index 0 -> shard 0 -> A
+        d.dispatch_step(0)
+        da = a.recv()
+        a.answer(da)                                     # A's credit is used; it never asks again
+        for i in range(1, 5):
+            d.add_frame_for_distribution(bytes([i]))     # shard 0 (even) waits for A
+        d.dispatch_step(0)
+        db = b.recv()
+        b.answer(db)
+        t0 = time.monotonic()
+        while d.ordering_stats()["evictions"] == 0:
+            d.dispatch_step(1)
+            assert time.monotonic() - t0 < 5
+        got = [m.index for m in da.metas + db.metas]
+        while len(got) < 5:
+            b.request(credit=4)
+            _step_until(d, lambda: b.dealer.poll(0))
+            dd = b.recv()
+            b.answer(dd)
+            got += [m.index for m in dd.metas]
+        assert sorted(got) == list(range(5))
+        for i in range(5):
+            item = d.get_next_frame(timeout=5)
+            assert item is not None and item[0] == i
+    finally:
+        d.running = False
+        coll.join(2)
+        a.close()
+        b.close()
+        d.cleanup()
