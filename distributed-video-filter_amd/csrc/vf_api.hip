@@ -389,7 +389,7 @@ VF_EXPORT int vf_host_register(vf_ctx *ctx, void *p, size_t nbytes) {
   VF_CHECK_CTX(ctx);
   if (!p || !nbytes) return set_err(ctx, VF_E_INVALID, 0, "vf_host_register: empty range");
   VF_HIP(ctx, hipSetDevice(ctx->device));
-  VF_HIP(ctx, hipHostRegister(p, nbytes, hipHostRegisterDefault));
+  VF_HIP(ctx, hipHostRegister(p, nbytes, hipHostRegisterMapped));
   ctx->engine->note_pinned(p, nbytes);
   return VF_OK;
 }

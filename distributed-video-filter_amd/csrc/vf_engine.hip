@@ -119,6 +119,7 @@ Engine::~Engine() {
   (void)hipSetDevice(device_);
   if (s_in_) (void)hipStreamSynchronize(s_in_);
   if (s_out_) (void)hipStreamSynchronize(s_out_);
+  if (s_map_) (void)hipStreamSynchronize(s_map_);
   for (auto &s : slots_) {
     for (hipEvent_t e : {s.h0, s.k0, s.k1, s.done})
       if (e) (void)hipEventDestroy(e);
@@ -130,6 +131,7 @@ Engine::~Engine() {
   for (hipEvent_t e : free_events_) (void)hipEventDestroy(e);
   if (s_in_) (void)hipStreamDestroy(s_in_);
   if (s_out_) (void)hipStreamDestroy(s_out_);
+  if (s_map_) (void)hipStreamDestroy(s_map_);
 }
 
 hipError_t Engine::init(int device, int nslots, size_t slot_bytes, const LaunchCfg &cfg,
@@ -141,6 +143,8 @@ hipError_t Engine::init(int device, int nslots, size_t slot_bytes, const LaunchC
   hipError_t e = hipSetDevice(device);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&s_in_, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&s_out_, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&s_map_, hipStreamNonBlocking);
+  zero_copy_ = env_or("VF_ZEROCOPY", 1) != 0;
   if (e != hipSuccess) {
     *err = std::string("stream creation failed: ") + hipGetErrorString(e);
     return e;
@@ -171,14 +175,21 @@ hipError_t Engine::init(int device, int nslots, size_t slot_bytes, const LaunchC
 // ---- page-locked range registry (so `direct` needs no runtime query per frame) ----------------
 
 void Engine::note_pinned(const void *p, size_t n) {
+  // the device address of the range (page-locked memory is mapped into the GPU's address
+  // space; the runtime says where), or 0 if the runtime does not know the range as mapped
+  void *dev = nullptr;
+  if (hipHostGetDevicePointer(&dev, const_cast<void *>(p), 0) != hipSuccess) {
+    (void)hipGetLastError();
+    dev = nullptr;
+  }
   std::lock_guard<std::mutex> lk(pin_mu_);
-  pinned_.emplace_back((uintptr_t)p, n);
+  pinned_.push_back(PinRange{(uintptr_t)p, n, (uintptr_t)dev});
 }
 
 void Engine::forget_pinned(const void *p) {
   std::lock_guard<std::mutex> lk(pin_mu_);
   pinned_.erase(std::remove_if(pinned_.begin(), pinned_.end(),
-                               [p](const std::pair<uintptr_t, size_t> &r) { return r.first == (uintptr_t)p; }),
+                               [p](const PinRange &r) { return r.host == (uintptr_t)p; }),
                 pinned_.end());
 }
 
@@ -187,7 +198,7 @@ bool Engine::is_pinned(const void *p, size_t len) {
     std::lock_guard<std::mutex> lk(pin_mu_);
     const uintptr_t a = (uintptr_t)p;
     for (const auto &r : pinned_)
-      if (a >= r.first && a + len <= r.first + r.second) return true;
+      if (a >= r.host && a + len <= r.host + r.len) return true;
   }
   hipPointerAttribute_t attr;
   std::memset(&attr, 0, sizeof attr);
@@ -198,14 +209,30 @@ bool Engine::is_pinned(const void *p, size_t len) {
   return attr.type == hipMemoryTypeHost;
 }
 
+uint8_t *Engine::mapped(const void *p, size_t len) {
+  std::lock_guard<std::mutex> lk(pin_mu_);
+  const uintptr_t a = (uintptr_t)p;
+  for (const auto &r : pinned_)
+    if (r.dev && a >= r.host && a + len <= r.host + r.len) return reinterpret_cast<uint8_t *>(r.dev + (a - r.host));
+  return nullptr;
+}
+
 // ---- engine: caller side ---------------------------------------------------------------------
 
 uint64_t Engine::submit(std::vector<Seg> &&segs) {
   auto job = std::make_unique<Job>();
+  job->mapped = zero_copy_;
   for (const Seg &s : segs) {
     job->total += s.len;
-    if (job->direct && s.len && !(is_pinned(s.src, s.len) && is_pinned(s.dst, s.len))) job->direct = false;
+    if (!s.len) continue;
+    if (job->mapped) {
+      uint8_t *ds = mapped(s.src, s.len), *dd = mapped(s.dst, s.len);
+      if (ds && dd) job->dsegs.push_back(Seg{ds, dd, s.len});
+      else job->mapped = false;
+    }
+    if (job->direct && !(is_pinned(s.src, s.len) && is_pinned(s.dst, s.len))) job->direct = false;
   }
+  if (!job->mapped) job->dsegs.clear();
   // Chunk size: the slot size for big jobs; small jobs still get >= 2 chunks per slot so the
   // ring fills (480p x 32 = 29 MB in 16 MiB chunks is only 2 chunks).
   const size_t kMinChunk = (size_t)1 << 20;
@@ -264,6 +291,7 @@ void Engine::fail_all(hipError_t e, const char *what) {
   // before the callers hear of the failure and free or reuse their buffers
   (void)hipStreamSynchronize(s_in_);
   (void)hipStreamSynchronize(s_out_);
+  (void)hipStreamSynchronize(s_map_);
   (void)hipGetLastError();
   char buf[256];
   std::snprintf(buf, sizeof buf, "%s failed: %s (%s)", what, hipGetErrorString(e), hipGetErrorName(e));
@@ -283,6 +311,7 @@ void Engine::fail_all(hipError_t e, const char *what) {
   }
   pending_.clear();
   live_.clear();
+  mapped_live_.clear();
   done_cv_.notify_all();
 }
 
@@ -300,13 +329,14 @@ size_t Engine::chunk_size(const Job &job) const {
 
 bool Engine::step_fill() {
   Slot &s = slots_[fill_];
-  if (s.state != Slot::kFree) return false;
   Job *job = nullptr;
   {
     std::lock_guard<std::mutex> lk(mu_);
     if (pending_.empty()) return false;
     job = pending_.front().get();
   }
+  if (job->mapped) return launch_mapped(job);
+  if (s.state != Slot::kFree) return false;
   hipError_t e = hipSuccess;
   if (!job->started) {
     job->start = take_event();
@@ -433,6 +463,73 @@ bool Engine::step_retire() {
   return true;
 }
 
+// A zero-copy job: its ranges in launches of up to kMappedMax on the mapped stream, between a
+// start and an end event; no slot, no staging.
+bool Engine::launch_mapped(Job *job) {
+  job->start = take_event();
+  job->end = take_event();
+  if (!job->start || !job->end) {
+    fail_all(hipErrorOutOfMemory, "hipEventCreate");
+    return true;
+  }
+  hipError_t e = hipEventRecord(job->start, s_map_);
+  MappedBatch b;
+  for (size_t i = 0; i < job->dsegs.size() && e == hipSuccess; i += kMappedMax) {
+    const int n = (int)std::min<size_t>(kMappedMax, job->dsegs.size() - i);
+    size_t bytes = 0;
+    for (int k = 0; k < n; ++k) {
+      const Seg &g = job->dsegs[i + k];
+      b.src[k] = g.src;
+      b.dst[k] = g.dst;
+      b.n[k] = g.len;
+      bytes += g.len;
+    }
+    e = launch_invert_mapped(b, n, bytes, s_map_);
+  }
+  if (e == hipSuccess) e = hipEventRecord(job->end, s_map_);
+  if (e != hipSuccess) {
+    fail_all(e, "zero-copy launch");
+    return true;
+  }
+  job->started = job->all_submitted = true;
+  std::lock_guard<std::mutex> lk(mu_);
+  mapped_live_.push_back(job);
+  live_.push_back(std::move(pending_.front()));
+  pending_.pop_front();
+  return true;
+}
+
+bool Engine::step_mapped_retire() {
+  if (mapped_live_.empty()) return false;
+  Job *job = mapped_live_.front();
+  hipError_t err = hipSuccess;
+  if (!fired(job->end, &err)) {
+    if (err != hipSuccess) fail_all(err, "hipEventQuery");
+    return err != hipSuccess;
+  }
+  float ms = -1.f;
+  if (hipEventElapsedTime(&ms, job->start, job->end) != hipSuccess) ms = -1.f;
+  JobResult r;
+  r.kernel_ms = ms;
+  r.gpu_ms = ms;
+  r.zero_copy = true;
+  r.timeline.push_back(ChunkTime{job->total, 0.f, 0.f, ms, ms});  // one launch does all of it
+  give_event(job->start);
+  give_event(job->end);
+  std::lock_guard<std::mutex> lk(mu_);
+  mapped_live_.pop_front();
+  results_[job->id] = std::move(r);
+  while (results_.size() > kMaxResults) results_.erase(results_.begin());
+  unfinished_.erase(job->id);
+  for (auto it = live_.begin(); it != live_.end(); ++it)
+    if (it->get() == job) {
+      live_.erase(it);
+      break;
+    }
+  done_cv_.notify_all();
+  return true;
+}
+
 hipEvent_t Engine::take_event() {
   if (!free_events_.empty()) {
     hipEvent_t e = free_events_.back();
@@ -458,12 +555,13 @@ void Engine::run() {
   for (;;) {
     {
       std::unique_lock<std::mutex> lk(mu_);
-      cv_.wait(lk, [&] { return stop_ || !pending_.empty() || busy_slots() > 0; });
-      if (stop_ && pending_.empty() && busy_slots() == 0) return;
+      cv_.wait(lk, [&] { return stop_ || !pending_.empty() || busy_slots() > 0 || !mapped_live_.empty(); });
+      if (stop_ && pending_.empty() && busy_slots() == 0 && mapped_live_.empty()) return;
     }
     bool progress = false;
     // retire first (frees a slot), then start the D2H of finished kernels, then refill
     while (step_retire()) progress = true;
+    while (step_mapped_retire()) progress = true;
     while (step_d2h()) progress = true;
     while (step_fill()) progress = true;
     if (!progress) std::this_thread::yield();

@@ -74,7 +74,7 @@ inline hipError_t numa_pinned_alloc(void **out, size_t n, int node) {
       const long rc = syscall(SYS_mbind, p, len, 1 /* MPOL_PREFERRED */, mask, 16ul * 64 + 1, 0u);
       if (rc == 0) {
         std::memset(p, 0, len);  // fault the pages in on the node before locking them
-        if (hipHostRegister(p, len, hipHostRegisterDefault) == hipSuccess) {
+        if (hipHostRegister(p, len, hipHostRegisterMapped) == hipSuccess) {
           std::lock_guard<std::mutex> lk(PinnedRegistry::get().mu);
           PinnedRegistry::get().mapped[p] = len;
           *out = p;

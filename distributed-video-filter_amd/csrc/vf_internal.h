@@ -30,6 +30,16 @@ hipError_t launch_invert_frames(const void *const *dsrcs, void *const *ddsts,
                                 const size_t *nbytes, int n, size_t total_bytes,
                                 const LaunchCfg &cfg, hipStream_t stream);
 
+// Up to kMappedMax page-locked host ranges, by their device addresses, inverted in place over
+// PCIe by one launch (vf_kernels.hip invert_mapped_kernel; passed by value as kernel arguments).
+constexpr int kMappedMax = 64;
+struct MappedBatch {
+  const uint8_t *src[kMappedMax];
+  uint8_t *dst[kMappedMax];
+  uint64_t n[kMappedMax];
+};
+hipError_t launch_invert_mapped(const MappedBatch &b, int n, size_t total_bytes, hipStream_t stream);
+
 // ---- host -> host pipeline (vf_engine.hip) --------------------------------------------------
 
 // memcpy of large staging chunks split over a few persistent threads: one core moves
@@ -76,6 +86,7 @@ struct JobResult {
   std::string msg;
   float kernel_ms = 0.f;  // sum of the job's kernel durations
   float gpu_ms = -1.f;    // job start -> last D2H done
+  bool zero_copy = false; // inverted in place over PCIe (no slot ring)
   std::vector<ChunkTime> timeline;
 };
 
@@ -93,6 +104,9 @@ class Engine {
   void note_pinned(const void *p, size_t n);
   void forget_pinned(const void *p);
   bool is_pinned(const void *p, size_t len);
+  // device address of [p, p + len) when it lies inside one range noted above and that range is
+  // mapped into the device's address space; else nullptr
+  uint8_t *mapped(const void *p, size_t len);
 
  private:
   struct Piece {
@@ -105,6 +119,9 @@ class Engine {
     uint64_t id = 0;
     std::vector<Seg> segs;
     bool direct = true;  // every byte page-locked: DMA straight from/to the caller
+    bool mapped = false;  // every byte in a noted, device-mapped range: inverted in place over PCIe
+    std::vector<Seg> dsegs;  // mapped: the segments by their device addresses
+    hipEvent_t end = nullptr;  // mapped: after the job's last launch
     size_t total = 0, chunk = 0;
     size_t queued = 0;            // bytes put into slots so far
     size_t seg = 0, seg_off = 0;  // fill cursor
@@ -130,6 +147,8 @@ class Engine {
   bool step_fill();
   bool step_d2h();
   bool step_retire();
+  bool launch_mapped(Job *job);
+  bool step_mapped_retire();
   void fail_all(hipError_t e, const char *what);
   int busy_slots() const;
   hipEvent_t take_event();
@@ -139,6 +158,9 @@ class Engine {
   LaunchCfg cfg_;
   size_t slot_bytes_ = 0;
   hipStream_t s_in_ = nullptr, s_out_ = nullptr;
+  hipStream_t s_map_ = nullptr;  // zero-copy launches (beside the slot ring's two streams)
+  bool zero_copy_ = true;        // VF_ZEROCOPY=0: caller-pinned jobs take the slot ring
+  std::deque<Job *> mapped_live_;  // launched zero-copy jobs, in launch order
   std::vector<Slot> slots_;
   size_t fill_ = 0, d2h_ = 0, retire_ = 0;
   std::unique_ptr<CopyPool> pool_;
@@ -154,8 +176,13 @@ class Engine {
   std::set<uint64_t> unfinished_;
   std::map<uint64_t, JobResult> results_;     // finished, not yet collected by wait()
 
+  struct PinRange {
+    uintptr_t host;
+    size_t len;
+    uintptr_t dev;  // 0: not mapped into the device's address space
+  };
   std::mutex pin_mu_;
-  std::vector<std::pair<uintptr_t, size_t>> pinned_;
+  std::vector<PinRange> pinned_;
   std::thread thread_;
 };
 

@@ -108,16 +108,10 @@ __device__ __forceinline__ void stream_body(const u32x4 *__restrict__ s, u32x4 *
   }
 }
 
-// Descriptor-table form: blockIdx.y = frame, blockIdx.x strides within the frame, U = 4 vectors
-// per lane per tile; each frame takes the aligned or the shifting path by its own offsets.
-__global__ __launch_bounds__(kBlock) void invert_frames_kernel(const uint8_t *const *srcs,
-                                                               uint8_t *const *dsts,
-                                                               const size_t *nbytes) {
-  constexpr int U = 4;
-  const uint32_t f = blockIdx.y;
-  const uint8_t *s = srcs[f];
-  uint8_t *d = dsts[f];
-  const uint64_t n = nbytes[f];
+// One range [s, s + n) of a multi-range launch: blockIdx.x strides within it, U vectors per lane
+// per tile; the aligned or the shifting path by the range's own offsets.
+template <int U>
+__device__ __forceinline__ void invert_range(const uint8_t *s, uint8_t *d, uint64_t n) {
   const uint32_t t = threadIdx.x;
   const uint32_t h = (uint32_t)min((uint64_t)((16 - ((uintptr_t)d & 15)) & 15), n);  // dst head bytes
   const uint64_t n16 = (n - h) >> 4;
@@ -142,6 +136,27 @@ __global__ __launch_bounds__(kBlock) void invert_frames_kernel(const uint8_t *co
     case 2: shift_body<2, U>(sa, d4, n16, delta & 3, b0, stride); break;
     default: shift_body<3, U>(sa, d4, n16, delta & 3, b0, stride); break;
   }
+}
+
+// Descriptor-table form (device memory): blockIdx.y = frame, U = 4.
+__global__ __launch_bounds__(kBlock) void invert_frames_kernel(const uint8_t *const *srcs,
+                                                               uint8_t *const *dsts,
+                                                               const size_t *nbytes) {
+  const uint32_t f = blockIdx.y;
+  invert_range<4>(srcs[f], dsts[f], nbytes[f]);
+}
+
+// Page-locked host ranges in place (zero-copy): the kernel reads the caller's source over PCIe
+// and writes the caller's destination over PCIe, so each byte crosses the link once each way
+// with no HBM staging, no chunk ring and no host step between the two directions.  Measured
+// (tools/zerocopy_probe.hip, profiles/r02_zerocopy_probe.jsonl): one launch over 1080p x 32
+// moves 48.4-48.5 GB/s each way, equal to two SDMA copies running at once (48.5), with
+// 96-128 workgroups and one 16-B vector per lane in flight (more waves only queue behind the
+// link: 44-45 GB/s at 384).  The descriptors travel in the kernel arguments (<= kMappedMax
+// ranges per launch), so nothing is uploaded first.
+__global__ __launch_bounds__(kBlock) void invert_mapped_kernel(MappedBatch b) {
+  const uint32_t f = blockIdx.y;
+  invert_range<1>(b.src[f], b.dst[f], b.n[f]);
 }
 
 // ---- launchers ----------------------------------------------------------------------
@@ -191,6 +206,19 @@ hipError_t launch_invert_frames(const void *const *dsrcs, void *const *ddsts,
   hipLaunchKernelGGL(invert_frames_kernel, dim3((unsigned)gx, (unsigned)n), dim3(kBlock), 0,
                      stream, reinterpret_cast<const uint8_t *const *>(dsrcs),
                      reinterpret_cast<uint8_t *const *>(ddsts), nbytes);
+  return hipGetLastError();
+}
+
+hipError_t launch_invert_mapped(const MappedBatch &b, int n, size_t total_bytes, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  if (n > kMappedMax) return hipErrorInvalidValue;
+  // Workgroups over the whole launch: 128 keep the link busy for large ranges; below 16 MiB the
+  // fixed start-up latency dominates and 256 finish sooner (zerocopy_probe: 6.2 MB at 256 WG
+  // 33-34 GB/s, at 128 31-32).
+  const uint64_t target = total_bytes < (16ull << 20) ? 256 : 128;
+  uint64_t gx = target / (uint64_t)n;
+  if (gx == 0) gx = 1;
+  hipLaunchKernelGGL(invert_mapped_kernel, dim3((unsigned)gx, (unsigned)n), dim3(kBlock), 0, stream, b);
   return hipGetLastError();
 }
 

@@ -342,9 +342,9 @@ def test_async_frames_on_pinned_memory(vf_ctx):
         ys = [np.empty_like(x) for x in xs]
         t_pin = vf_ctx.invert_frames_async([ps[0]], [pd[0]], [sizes[0]])
         t_pg = vf_ctx.invert_frames_async(xs, ys, [x.nbytes for x in xs])
-        vf_ctx.wait(t_pg)
-        assert vf_ctx.query(t_pin)  # jobs complete in submission order
+        vf_ctx.wait(t_pg)  # the pinned job runs zero-copy beside the ring: any completion order
         vf_ctx.wait(t_pin)
+        assert np.array_equal(hd[0], oracle.invert(hs[0]))
         for x, y_ in zip(xs, ys):
             assert np.array_equal(y_, oracle.invert(x))
         with pytest.raises(vfilter.VFilterError, match="unknown ticket"):
@@ -354,3 +354,100 @@ def test_async_frames_on_pinned_memory(vf_ctx):
     finally:
         for p in ps + pd:
             vf_ctx.free_host(p)
+
+
+def _zero_copy(tl):
+    """A zero-copy call reports one record whose H2D start = kernel start = 0 and kernel end =
+    D2H end (one launch read the source and wrote the destination over PCIe)."""
+    return len(tl) == 1 and tl[0][1] == 0.0 and tl[0][2] == 0.0 and tl[0][3] == tl[0][4]
+
+
+def test_zero_copy_ranges_every_offset_and_split(vf_ctx):
+    """Page-locked ranges from vf_alloc_host are inverted in place over PCIe (one launch per 64
+    ranges, descriptors in the kernel arguments): every relative src/dst offset mod 16 with
+    ragged lengths, 0-length ranges, 150 ranges (3 launches), and interior pointers of a
+    registered numpy buffer -- bit-exact, and the timeline says the zero-copy path ran."""
+    cap = 8 << 20
+    ps, pd = vf_ctx.alloc_host(cap), vf_ctx.alloc_host(cap)
+    try:
+        hs = np.ctypeslib.as_array((ctypes.c_uint8 * cap).from_address(ps))
+        hd = np.ctypeslib.as_array((ctypes.c_uint8 * cap).from_address(pd))
+        hs[:] = np.random.default_rng(11).integers(0, 256, cap, dtype=np.uint8)
+        rng = np.random.default_rng(12)
+        # one range per (src offset, dst offset) pair, each in its own 32 KiB cell
+        srcs, dsts, sizes = [], [], []
+        for so in range(16):
+            for do in range(16):
+                cell = (so * 16 + do) * 32768
+                srcs.append(ps + cell + so)
+                dsts.append(pd + cell + do)
+                sizes.append(int(rng.integers(1, 32768 - 16)))
+        for lo in range(0, len(srcs), 150):  # 150 ranges per call: launches of 64, 64, 22
+            hd[:] = 0
+            sel = slice(lo, lo + 150)
+            vf_ctx.invert_frames_host(srcs[sel], dsts[sel], sizes[sel])
+            assert _zero_copy(vf_ctx.last_timeline())
+            for s_, d_, n in zip(srcs[sel], dsts[sel], sizes[sel]):
+                so, do = s_ - ps, d_ - pd
+                assert np.array_equal(hd[do:do + n], ~hs[so:so + n]), (so % 16, do % 16, n)
+                assert hd[do + n] == 0  # nothing past the range
+        # 0-length ranges mixed in, and one large range (1080p x 1, 7 MiB)
+        hd[:] = 0
+        vf_ctx.invert_frames_host([ps, ps + 100, ps + 4096], [pd, pd + 100, pd + 4096],
+                                  [0, 3, FB_1080])
+        assert np.array_equal(hd[100:103], ~hs[100:103]) and hd[99] == 0 and hd[103] == 0
+        assert np.array_equal(hd[4096:4096 + FB_1080], ~hs[4096:4096 + FB_1080])
+        # async, several jobs in flight on the zero-copy stream
+        ts = [vf_ctx.invert_frames_async([ps + k * (1 << 20)], [pd + k * (1 << 20)], [1 << 20])
+              for k in range(8)]
+        for t in ts:
+            vf_ctx.wait(t)
+        assert np.array_equal(hd, ~hs)
+    finally:
+        vf_ctx.free_host(ps)
+        vf_ctx.free_host(pd)
+    # interior pointers of a registered numpy buffer (a shared-memory frame ring's case)
+    buf = np.random.default_rng(13).integers(0, 256, 3 << 20, dtype=np.uint8)
+    out = np.zeros_like(buf)
+    a, b = vf_ctx.host_register(buf), vf_ctx.host_register(out)
+    try:
+        vf_ctx.invert_frames_host([buf[5:], buf[1 << 20:]], [out[9:], out[(1 << 20) + 3:]],
+                                  [(1 << 20) - 100, (2 << 20) - 7])
+        assert _zero_copy(vf_ctx.last_timeline())
+        assert np.array_equal(out[9:9 + (1 << 20) - 100], ~buf[5:5 + (1 << 20) - 100])
+        n2 = (2 << 20) - 7
+        assert np.array_equal(out[(1 << 20) + 3:(1 << 20) + 3 + n2], ~buf[1 << 20:(1 << 20) + n2])
+    finally:
+        vf_ctx.host_unregister(a)
+        vf_ctx.host_unregister(b)
+
+
+def test_zero_copy_falls_back_and_can_be_disabled(vf_ctx, monkeypatch):
+    """A job with any byte outside the noted page-locked ranges takes the slot ring (staged),
+    and VF_ZEROCOPY=0 at context creation sends page-locked jobs to the ring's direct DMA:
+    both bit-exact, with the ring's per-chunk timeline."""
+    n = 3 * (16 << 20) + 77
+    p = vf_ctx.alloc_host(n)
+    try:
+        h = np.ctypeslib.as_array((ctypes.c_uint8 * n).from_address(p))
+        h[:] = np.random.default_rng(14).integers(0, 256, n, dtype=np.uint8)
+        y = np.empty(n, np.uint8)  # pageable destination
+        vf_ctx.invert_host(p, y, n)
+        assert not _zero_copy(vf_ctx.last_timeline())
+        assert np.array_equal(y, ~h)
+    finally:
+        vf_ctx.free_host(p)
+    monkeypatch.setenv("VF_ZEROCOPY", "0")
+    with vfilter.Context(0, max_frame_bytes=FB_1080, max_batch=4) as ctx:
+        ps, pd = ctx.alloc_host(n), ctx.alloc_host(n)
+        try:
+            hs = np.ctypeslib.as_array((ctypes.c_uint8 * n).from_address(ps))
+            hd = np.ctypeslib.as_array((ctypes.c_uint8 * n).from_address(pd))
+            hs[:] = np.random.default_rng(15).integers(0, 256, n, dtype=np.uint8)
+            ctx.invert_host(ps, pd, n)
+            tl = ctx.last_timeline()
+            assert len(tl) >= 3 and sum(t[0] for t in tl) == n
+            assert np.array_equal(hd, ~hs)
+        finally:
+            ctx.free_host(ps)
+            ctx.free_host(pd)
