@@ -300,9 +300,9 @@ def sweep_leg(ctx, np, host_batch, batch, rank, world, barrier_sync, reduce_max,
 
 def end_to_end(ctx, host_batch, batch, np, reps=16):
     """Host->host frames/s (PCIe-inclusive): one synchronous vf_invert_batch_host call per
-    batch from pageable numpy memory and from pinned memory, and the worker's pipelined form
-    (vf_invert_frames_async, two batches in flight, pinned) that keeps the engine busy across
-    batches."""
+    batch from pageable numpy memory (staged through the slot ring) and from pinned memory
+    (vf_alloc_host: inverted in place over PCIe by one launch, the zero-copy path), and the
+    worker's pipelined form (vf_invert_frames_async, two batches in flight, pinned)."""
     import ctypes
     nb = host_batch.nbytes
     out = np.empty_like(host_batch)
@@ -336,6 +336,7 @@ def end_to_end(ctx, host_batch, batch, np, reps=16):
         for p in ps + pd:
             ctx.free_host(p)
     res["pcie_ceiling_fps"] = round(63e9 / FRAME_BYTES, 0)  # Gen5 x16 spec, one direction
+    res["pinned_path"] = "zero-copy" if os.environ.get("VF_ZEROCOPY", "1") != "0" else "slot ring (direct DMA)"
     res["note"] = "host->host incl. PCIe both directions; never the headline value"
     return res
 

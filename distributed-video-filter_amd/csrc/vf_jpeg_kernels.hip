@@ -1532,16 +1532,14 @@ __global__ __launch_bounds__(256) void k_fdct(const EncFrame *fr, const EncTable
   __shared__ int32_t ws[32][8][9];
   __shared__ int16_t qo[32][64];
   __shared__ uint32_t acw[32][kAcWords];
-  __shared__ uint16_t s_recip[2][64], s_corr[2][64];
-  __shared__ int16_t s_shift[2][64];
+  // quantiser entry of natural position n: {recip | corr << 16, shift | zigzag(n) << 16}, so
+  // pass 2's lane reads one 8-B entry per coefficient (8 lanes: 64 contiguous bytes)
+  __shared__ uint2 s_q[2][64];
   __shared__ uint32_t s_ac[2][256];
-  __shared__ uint8_t s_zig[64];
-  if (threadIdx.x < 64) s_zig[threadIdx.x] = kZig[threadIdx.x];
   if (threadIdx.x < 128) {
     const int t = threadIdx.x >> 6, i = threadIdx.x & 63;
-    s_recip[t][i] = tab->recip[t][i];
-    s_corr[t][i] = tab->corr[t][i];
-    s_shift[t][i] = tab->shift[t][i];
+    s_q[t][i] = make_uint2((uint32_t)tab->recip[t][i] | ((uint32_t)tab->corr[t][i] << 16),
+                           (uint32_t)(uint16_t)tab->shift[t][i] | ((uint32_t)kZig[i] << 16));
   }
   for (int i = threadIdx.x; i < 512; i += 256) s_ac[i >> 8][i & 255] = tab->ac[i >> 8][i & 255];
   for (int i = threadIdx.x; i < 32 * (int)kAcWords; i += 256) (&acw[0][0])[i] = 0;
@@ -1594,8 +1592,8 @@ __global__ __launch_bounds__(256) void k_fdct(const EncFrame *fr, const EncTable
     else fdct_islow_line(v, 1);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const int n = i * 8 + r;
-      qo[slot][qo_at(slot, s_zig[n])] = quantize(v[i], s_recip[t][n], s_corr[t][n], s_shift[t][n]);
+      const uint2 q = s_q[t][i * 8 + r];
+      qo[slot][qo_at(slot, q.y >> 16)] = quantize(v[i], q.x & 0xFFFF, q.x >> 16, (int32_t)(int16_t)(q.y & 0xFFFF));
     }
   }
   __syncthreads();

@@ -22,7 +22,7 @@ for name, (h, w, b) in {"1080p": (1080, 1920, 32), "4k": (2160, 3840, 16)}.items
     host = np.random.default_rng(0).integers(0, 256, b * h * w * 3, dtype=np.uint8)
     r = bench.end_to_end(ctx, host, b, np)
     r.update({"size": name, "batch": b, "VF_NUMA": os.environ.get("VF_NUMA", "1"),
-              "VF_ZEROCOPY": os.environ.get("VF_ZEROCOPY", "1"),
+              "VF_ZEROCOPY": os.environ.get("VF_ZEROCOPY", "1"), "VF_SCATTER": os.environ.get("VF_SCATTER", "1"),
               "gpu_numa_node": gpu_numa_node(dev), "numa_nodes": node_count(),
               "cpu": os.sched_getaffinity(0).__len__()})
     r.pop("note", None)
