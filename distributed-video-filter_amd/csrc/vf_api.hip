@@ -531,7 +531,7 @@ class CodecLease {
       c_ = ctx->jpeg_free.back();
       ctx->jpeg_free.pop_back();
     } else {
-      static const bool gated = env_size("VF_JPEG_GATE", 1) != 0;
+      static const bool gated = env_size("VF_JPEG_GATE", 0) != 0;
       c_ = new (std::nothrow) vf::jpeg::Codec(ctx->device, gated ? &ctx->jpeg_gate : nullptr);
       if (c_) ctx->jpeg_all.push_back(c_);
     }
@@ -565,7 +565,7 @@ vf::jpeg::Codec *lease_nowait(vf_ctx *ctx) {
     return c;
   }
   if (ctx->jpeg_all.size() >= kMaxJpegJobs) return nullptr;
-  static const bool gated = env_size("VF_JPEG_GATE", 1) != 0;
+  static const bool gated = env_size("VF_JPEG_GATE", 0) != 0;
   vf::jpeg::Codec *c = new (std::nothrow) vf::jpeg::Codec(ctx->device, gated ? &ctx->jpeg_gate : nullptr);
   if (c) ctx->jpeg_all.push_back(c);
   return c;

@@ -141,14 +141,11 @@ hipError_t Engine::init(int device, int nslots, size_t slot_bytes, const LaunchC
   slot_bytes_ = slot_bytes;
   pool_.reset(new CopyPool((int)env_or("VF_HOST_THREADS", 8)));
   hipError_t e = hipSetDevice(device);
-  if (e == hipSuccess) e = hipStreamCreateWithFlags(&s_in_, hipStreamNonBlocking);
-  if (e == hipSuccess) e = hipStreamCreateWithFlags(&s_out_, hipStreamNonBlocking);
-  if (e == hipSuccess) e = hipStreamCreateWithFlags(&s_map_, hipStreamNonBlocking);
-  zero_copy_ = env_or("VF_ZEROCOPY", 1) != 0;
   if (e != hipSuccess) {
-    *err = std::string("stream creation failed: ") + hipGetErrorString(e);
+    *err = std::string("hipSetDevice failed: ") + hipGetErrorString(e);
     return e;
   }
+  zero_copy_ = env_or("VF_ZEROCOPY", 1) != 0;
   slots_.resize((size_t)nslots);
   for (auto &s : slots_) {
     if ((e = hipEventCreate(&s.h0)) != hipSuccess || (e = hipEventCreate(&s.k0)) != hipSuccess ||
@@ -170,6 +167,21 @@ hipError_t Engine::init(int device, int nslots, size_t slot_bytes, const LaunchC
   }
   thread_ = std::thread([this] { run(); });
   return hipSuccess;
+}
+
+// The engine's three streams are created with its first job, not with the context: HIP maps
+// streams onto a few hardware queues per process (GPU_MAX_HW_QUEUES, 4 by default), and a
+// process that only runs JPEG batches would otherwise lose three of them to idle streams and
+// put its two codecs' streams on one queue, where each batch's copies and event waits stall
+// the other's kernels (1080p worker form 15.0-15.3 k fps on 4 queues, 19.9 k on 8:
+// profiles/r02_jpeg_hwq.jsonl).
+hipError_t Engine::ensure_streams() {
+  if (s_map_) return hipSuccess;
+  hipError_t e = hipSuccess;
+  if (!s_in_) e = hipStreamCreateWithFlags(&s_in_, hipStreamNonBlocking);
+  if (e == hipSuccess && !s_out_) e = hipStreamCreateWithFlags(&s_out_, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&s_map_, hipStreamNonBlocking);
+  return e;
 }
 
 // ---- page-locked range registry (so `direct` needs no runtime query per frame) ----------------
@@ -289,9 +301,8 @@ void Engine::drain() {
 void Engine::fail_all(hipError_t e, const char *what) {
   // copies already queued for direct (caller-pinned) jobs may still be moving: let them land
   // before the callers hear of the failure and free or reuse their buffers
-  (void)hipStreamSynchronize(s_in_);
-  (void)hipStreamSynchronize(s_out_);
-  (void)hipStreamSynchronize(s_map_);
+  for (hipStream_t st : {s_in_, s_out_, s_map_})
+    if (st) (void)hipStreamSynchronize(st);
   (void)hipGetLastError();
   char buf[256];
   std::snprintf(buf, sizeof buf, "%s failed: %s (%s)", what, hipGetErrorString(e), hipGetErrorName(e));
@@ -557,6 +568,13 @@ void Engine::run() {
       std::unique_lock<std::mutex> lk(mu_);
       cv_.wait(lk, [&] { return stop_ || !pending_.empty() || busy_slots() > 0 || !mapped_live_.empty(); });
       if (stop_ && pending_.empty() && busy_slots() == 0 && mapped_live_.empty()) return;
+    }
+    if (!s_map_) {
+      const hipError_t e = ensure_streams();
+      if (e != hipSuccess) {
+        fail_all(e, "stream creation");
+        continue;
+      }
     }
     bool progress = false;
     // retire first (frees a slot), then start the D2H of finished kernels, then refill

@@ -143,6 +143,7 @@ class Engine {
   static constexpr size_t kMaxResults = 1024;
 
   void run();
+  hipError_t ensure_streams();
   size_t chunk_size(const Job &job) const;
   bool step_fill();
   bool step_d2h();

@@ -75,11 +75,14 @@ class TaskPool {
   const std::function<void(int)> *fn_ = nullptr;
 };
 
-// Orders the GPU compute of the codecs of one context: a codec holds `mu` while it queues its
-// kernels, its stream first waits for `last` (the previous holder's kernels-done event) and
-// then publishes its own.  Kernels of two batches therefore never share the GPU (measured:
-// two 4K batches run concurrently took 12 ms each instead of 6), while one batch's host work
-// and copies still overlap the other's kernels.
+// Orders the GPU compute of the codecs of one context (VF_JPEG_GATE=1; off by default): a
+// codec holds `mu` while it queues its kernels, its stream first waits for `last` (the
+// previous holder's kernels-done event) and then publishes its own, so kernels of two batches
+// never share the GPU.  Round 1 measured two concurrent 4K batches at 12 ms each instead of 6,
+// but the codecs' streams then shared one hardware queue with the engine's idle streams; with
+// the engine's streams created on first use, two batches in flight run faster ungated
+// (worker form, 1080p 22.6 k vs 20.0 k fps, 480p 64.2 k vs 50.9 k, 4K 6.88 k vs 6.36 k:
+// profiles/r02_jpeg_hwq2.jsonl).
 struct ComputeGate {
   std::mutex mu;
   hipEvent_t last = nullptr;
