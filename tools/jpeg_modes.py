@@ -7,6 +7,7 @@ one size per run, each in a fresh process so codec settings (read at codec creat
   2threads_nogate   the same with VF_JPEG_GATE=0 (kernels of the two codecs may overlap)
   async        ONE host thread keeping two batches in flight (invert_batch_submit / _result,
                vf_jpeg_invert_submit & co.): the InverterWorker's form
+  async3       the same with three batches in flight
 Prints one JSON line per mode.  VF_JPEG_TRACE=1 adds the library's per-call phase times.
   python tools/jpeg_modes.py 1080p [mode]"""
 import json
@@ -30,17 +31,20 @@ def run(size, mode, batch=32, reps=24):
     tj = TurboJPEG(ctx=ctx)
     jpgs = tj.encode_batch([synthetic_scene(s, h, w) for s in range(8)])
     jpgs = [jpgs[i % 8] for i in range(batch)]
-    if mode == "async":
-        for _ in range(3):  # warm both codecs (the first use of a codec allocates its buffers)
-            a, b = tj.invert_batch_submit(jpgs), tj.invert_batch_submit(jpgs)
-            tj.invert_batch_result(a)
-            tj.invert_batch_result(b)
+    if mode.startswith("async"):
+        depth = int(mode[5:] or 2)  # batches in flight ("async" = 2, "async3" = 3)
+        for _ in range(3):  # warm the codecs (the first use of a codec allocates its buffers)
+            ts = [tj.invert_batch_submit(jpgs) for _ in range(depth)]
+            for t in ts:
+                tj.invert_batch_result(t)
         t0 = time.perf_counter()
-        q = [tj.invert_batch_submit(jpgs)]
-        for _ in range(reps - 1):
+        q = [tj.invert_batch_submit(jpgs) for _ in range(depth - 1)]
+        for _ in range(reps - depth + 1):
             q.append(tj.invert_batch_submit(jpgs))
             out = tj.invert_batch_result(q.pop(0))
-        out = tj.invert_batch_result(q.pop(0))
+        for t in q[:-1]:
+            tj.invert_batch_result(t)
+        out = tj.invert_batch_result(q[-1])
         dt = time.perf_counter() - t0
         assert [bytes(o) for o in out] == tj.invert_batch(jpgs)
     elif mode == "1thread":
