@@ -298,7 +298,7 @@ def sweep_leg(ctx, np, host_batch, batch, rank, world, barrier_sync, reduce_max,
     return out
 
 
-def end_to_end(ctx, host_batch, batch, np, reps=16):
+def end_to_end(ctx, host_batch, batch, np, reps=16, labels=("pageable", "pinned", "pinned_pipelined")):
     """Host->host frames/s (PCIe-inclusive): one synchronous vf_invert_batch_host call per
     batch from pageable numpy memory (staged through the slot ring) and from pinned memory
     (vf_alloc_host: inverted in place over PCIe by one launch, the zero-copy path), and the
@@ -312,7 +312,7 @@ def end_to_end(ctx, host_batch, batch, np, reps=16):
     try:
         for p in ps:
             np.ctypeslib.as_array((ctypes.c_uint8 * nb).from_address(p))[:] = host_batch
-        for label in ("pageable", "pinned", "pinned_pipelined"):
+        for label in labels:
             src, dst = (host_batch, out) if label == "pageable" else (ps[0], pd[0])
             ctx.invert_batch_host(src, dst, FRAME_BYTES, batch)  # warm (first DMA touch)
             if label == "pinned_pipelined":
@@ -339,6 +339,28 @@ def end_to_end(ctx, host_batch, batch, np, reps=16):
     res["pinned_path"] = "zero-copy" if os.environ.get("VF_ZEROCOPY", "1") != "0" else "slot ring (direct DMA)"
     res["note"] = "host->host incl. PCIe both directions; never the headline value"
     return res
+
+
+def end_to_end_ring(device, host_batch, batch, np, reps=16):
+    """The same pinned calls through the slot ring (the north star's double-buffered
+    hipMemcpyAsync H2D || kernel || D2H on separate streams), on a context made with
+    VF_ZEROCOPY=0, reported next to the zero-copy default."""
+    from vfilter import Context
+    old = os.environ.get("VF_ZEROCOPY")
+    os.environ["VF_ZEROCOPY"] = "0"  # read by vf_create
+    try:
+        ctx = Context(device, max_frame_bytes=FRAME_BYTES, max_batch=batch)
+    finally:
+        if old is None:
+            os.environ.pop("VF_ZEROCOPY")
+        else:
+            os.environ["VF_ZEROCOPY"] = old
+    try:
+        r = end_to_end(ctx, host_batch, batch, np, reps, labels=("pinned", "pinned_pipelined"))
+    finally:
+        ctx.close()
+    return {k: r[k] for k in ("pinned_fps", "pinned_GBps_each_way", "pinned_pipelined_fps",
+                              "pinned_pipelined_GBps_each_way")}
 
 
 def jpeg_mode(ctx, batch, iters=20):
@@ -637,6 +659,7 @@ def main():
     cpu = None
     if rank == 0 and not args.no_e2e:  # before the sweep's 51 GB of allocations come and go
         e2e = end_to_end(ctx, host_batch, args.batch, np)
+        e2e["slot_ring"] = end_to_end_ring(device, host_batch, args.batch, np)
         log(f"end-to-end: {e2e}")
     sweep = None
     if not args.no_sweep:
