@@ -143,7 +143,11 @@ class Distributor:
         self._ordered = OrderedBuffer(0)
         self._released: Deque[tuple] = collections.deque()
         self._lock = threading.RLock()
+        # two conditions on the one lock: producers wait on _cv (a free slot, room in the
+        # queue), the in-order consumer on _cv_out (a released result), so a freed slot does
+        # not wake the consumer and a released result does not wake the producers
         self._cv = threading.Condition(self._lock)
+        self._cv_out = threading.Condition(self._lock)
         # transport (distributor.py:26-35)
         self.transport = tp.resolve(transport)
         self._zctx = tp.make_context(self.transport)
@@ -223,6 +227,7 @@ class Distributor:
         self.running = False
         with self._cv:
             self._cv.notify_all()
+            self._cv_out.notify_all()
 
     def cleanup(self):
         self.stop()
@@ -505,8 +510,7 @@ class Distributor:
             if self.policy == "latest":
                 self._ingest_latest(item)
             else:
-                self._lane_for(item).append(item)
-                self._cv.notify_all()
+                self._lane_for(item).append(item)  # the dispatch thread polls; nobody waits on this
             self.log_frame_timing(idx, timestamp, "frame_captured")
         return idx
 
@@ -555,8 +559,7 @@ class Distributor:
         self._copy_done(item["frame_index"])
         if self.reassembly == "ordered":
             self._ordered.mark_lost(item["frame_index"])
-            self._released.extend(self._ordered.pop_ready())
-            self._cv.notify_all()
+            self._release_ready()
         return slot if keep_slot else None
 
     def _evict_oldest_queued_slot(self) -> Optional[int]:
@@ -584,8 +587,15 @@ class Distributor:
         self._settle(idx)
         if self.reassembly == "ordered":
             self._ordered.mark_lost(idx)
-            self._released.extend(self._ordered.pop_ready())
+            self._release_ready()
         self._cv.notify_all()
+
+    def _release_ready(self) -> None:
+        """Move results that are next in index order to the consumer's queue (lock held)."""
+        ready = self._ordered.pop_ready()
+        if ready:
+            self._released.extend(ready)
+            self._cv_out.notify_all()
 
     # ---- dispatch (distributor.py:205-251) ------------------------------------------------
     def handle_distribute_requests(self):
@@ -947,17 +957,20 @@ class Distributor:
         return None, None
 
     def _on_result(self, res: wire.Result):
+        """One result message (a batch): bookkeeping for all its frames under one lock hold,
+        the result bytes read outside it (each copy and its slot are this thread's alone once
+        taken out of the in-flight set), then one hold to hand them to the reassembly."""
         pid_val = int(res.pid) if res.pid.isdigit() else res.pid
         for sp in res.spans:
             self.log_gpu_span(sp.get("name", "?"), float(sp["begin"]), float(sp["end"]), pid_val,
                               int(sp.get("bytes", 0)))
+        reads = []
         with self._cv:
             sender = self._by_wid.get(res.wid) if res.wid else None
             if sender is not None:
                 sender.last_seen = time.monotonic()
-        for m, payload in zip(res.metas, res.payloads):
-            self.log_frame_complete_timing(m.index, m.start, m.end, "frame_inverted_received", pid_val)
-            with self._cv:
+            for m, payload in zip(res.metas, res.payloads):
+                self.log_frame_complete_timing(m.index, m.start, m.end, "frame_inverted_received", pid_val)
                 q, it = self._find_copy(sender, m.index)
                 slot = it.get("slot") if it is not None else None
                 if q is not None:
@@ -978,19 +991,22 @@ class Distributor:
                     self._free_slot(slot)
                     if self.reassembly == "ordered":
                         self._ordered.mark_lost(m.index)
-                        self._released.extend(self._ordered.pop_ready())
-                        self._cv.notify_all()
+                        self._release_ready()
                     continue
                 if m.slot is not None and slot is None:
                     continue  # a ring result with no dispatch record: nothing to read it from
-                keep = self.zero_copy and m.slot is not None
-            # this copy (and its slot) is ours alone now: read the result outside the lock
+                reads.append((m, payload, slot, self.zero_copy and m.slot is not None))
+        if not reads:
+            return
+        out = []
+        for m, payload, slot, keep in reads:
             if m.slot is not None:
                 view = self.out_view(slot, m.nbytes)
-                data = view if keep else bytes(view)
+                out.append((m, view if keep else bytes(view), slot, keep))
             else:
-                data = payload
-            with self._cv:
+                out.append((m, payload, slot, keep))
+        with self._cv:
+            for m, data, slot, keep in out:
                 if keep:
                     self._held[m.index] = slot
                 else:
@@ -1002,8 +1018,8 @@ class Distributor:
                     self._ordered.push(m.index, data, {"process_id": res.pid, "start_time": m.start,
                                                        "end_time": m.end, "shape": m.shape,
                                                        "slot": slot if keep else None})
-                    self._released.extend(self._ordered.pop_ready())
-                self._cv.notify_all()
+            if self.reassembly != "display":
+                self._release_ready()
 
     # ---- reassembly API (distributor.py:291-354) ---------------------------------------
     def cleanup_old_frames(self):
@@ -1037,7 +1053,7 @@ class Distributor:
                     return None
                 if not self.running and not self._released:
                     return None
-                self._cv.wait(rem if rem is not None else 0.1)
+                self._cv_out.wait(rem if rem is not None else 0.1)
             return self._released.popleft()
 
     def release_frame(self, index: int) -> None:

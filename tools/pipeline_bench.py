@@ -12,6 +12,13 @@ in-order release), reorder wait and buffer depth.
 
   python tools/pipeline_bench.py --workers 2 --size 4k --batch 16 --frames 512
   python tools/pipeline_bench.py --workers 2 --size mixed --policy pull
+  python tools/pipeline_bench.py --workers 1 --size 1080p --jpeg --batch 32   # the reference default mode
+
+``--jpeg``: frames are JPEGs (the app's encode, webcam_app.py:110, here the product's GPU
+encoder on camera-like scenes) and the workers run in the reference's default JPEG mode
+(decode -> bitwise_not -> encode, inverter.py:32-44); results are JPEGs of their own sizes,
+each compared byte for byte with the product's own invert of the same input (the GPU codec's
+parity with libjpeg-turbo is tests/test_gpu_jpeg.py's job).
 
 Producer modes: ``copy`` (default) — each frame is copied into its slot from a pre-generated
 frame (what a producer that cannot decode straight into the ring pays); ``resident`` — ring
@@ -51,13 +58,26 @@ def main():
     ap.add_argument("--ring-slots", type=int, default=0,
                     help="slots per worker slice (0 = 3 batches, capped by /dev/shm)")
     ap.add_argument("--verify-every", type=int, default=8)
-    ap.add_argument("--inflight", type=int, default=2, help="batches in progress per worker")
+    ap.add_argument("--inflight", type=int, default=0,
+                    help="batches in progress per worker (0: the worker's default, 2 raw / 3 JPEG)")
+    ap.add_argument("--jpeg", action="store_true", help="JPEG frames, workers in JPEG mode")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
 
     shapes = [SIZES["480p"], SIZES["1080p"], SIZES["4k"]] if args.size == "mixed" else [SIZES[args.size]]
     fbytes = [h * w * 3 for h, w in shapes]
-    slot_bytes = max(fbytes)
+    jpgs = want = None
+    if args.jpeg:  # 8 distinct JPEGs per shape and their inverted JPEGs, from the product
+        from vfilter import Context
+        from vfilter.jpeg import TurboJPEG
+        from vfilter.synthetic import synthetic_scene
+        with Context(int(os.environ.get("VF_DEVICE", "0"))) as cctx:
+            tj = TurboJPEG(ctx=cctx)
+            jpgs = [bytes(j) for h, w in shapes for j in tj.encode_batch([synthetic_scene(s, h, w) for s in range(8)])]
+            want = [bytes(o) for o in tj.invert_batch(jpgs)]
+        fbytes = [len(j) for j in jpgs]
+        shapes = [None] * len(jpgs)
+    slot_bytes = max(fbytes) * 2 if args.jpeg else max(fbytes)  # room for a result larger than its input
     slots = args.ring_slots or 3 * args.batch
     free = shm_free_bytes()
     if free is not None:
@@ -75,11 +95,14 @@ def main():
     procs = []
     for i in range(args.workers):
         e = dict(env, VF_DEVICE=str(i % ngpu))
-        procs.append(subprocess.Popen([sys.executable, "-m", "vfilter.inverter", "--raw", "--host", "127.0.0.1",
-                                       "--distribute-port", str(d.distribute_port), "--collect-port",
-                                       str(d.collect_port), "--batch", str(args.batch), "--transport", "tcp",
-                                       "--inflight", str(args.inflight)],
-                                      env=e, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE))
+        cmd = [sys.executable, "-m", "vfilter.inverter", "--host", "127.0.0.1",
+               "--distribute-port", str(d.distribute_port), "--collect-port",
+               str(d.collect_port), "--batch", str(args.batch), "--transport", "tcp"]
+        if not args.jpeg:
+            cmd.append("--raw")
+        if args.inflight:
+            cmd += ["--inflight", str(args.inflight)]
+        procs.append(subprocess.Popen(cmd, env=e, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE))
     result = {}
     try:
         t0 = time.time()
@@ -94,7 +117,8 @@ def main():
         if args.producer == "resident":
             for s in range(d.total_slots()):
                 d.in_view(s, slot_bytes)[:] = rng.integers(0, 256, slot_bytes, dtype=np.uint8)
-        pregen = [rng.integers(0, 256, fb, dtype=np.uint8) for fb in fbytes]
+        pregen = ([np.frombuffer(j, np.uint8) for j in jpgs] if args.jpeg else
+                  [rng.integers(0, 256, fb, dtype=np.uint8) for fb in fbytes])
         # warmup: every worker maps and page-locks its slice on its first batch (hipHostRegister,
         # ~0.15 s per GB) -- a one-off start-up cost kept out of the timing
         warm = 2 * args.batch * args.workers * len(shapes)
@@ -114,7 +138,7 @@ def main():
                 if args.producer == "copy":
                     copy_into(d.frame_view(slot, nb), pregen[k])
                 commit_t[i] = time.perf_counter()
-                d.commit_frame(slot, nb, shape=[shapes[k][0], shapes[k][1], 3])
+                d.commit_frame(slot, nb, shape=None if args.jpeg else [shapes[k][0], shapes[k][1], 3])
 
         th = threading.Thread(target=produce, daemon=True)
         th.start()
@@ -141,10 +165,15 @@ def main():
             idx, view, info = item
             if idx != i:
                 errors.append(f"order: got {idx} expected {i}")
-            src = d.in_view(info["slot"], view.nbytes)
             if i >= warm:
-                total_bytes += view.nbytes
+                total_bytes += fbytes[i % len(fbytes)] if args.jpeg else view.nbytes
             release_t[i] = time.perf_counter()
+            if args.jpeg:  # every result in full: a compressed frame is small
+                if bytes(view) != want[i % len(want)]:
+                    errors.append(f"frame {i} differs")
+                d.release_frame(idx)
+                continue
+            src = d.in_view(info["slot"], view.nbytes)
             if i % args.verify_every == 0:
                 pending.append(vpool.submit(full_check, i, idx, view, src))
             else:
@@ -162,8 +191,9 @@ def main():
         st = d.ordering_stats()
         st["max_depth"] = max(st["max_depth"], d_stats0["max_depth"])
         slices = [w["slice"] for w in st["workers"].values() if w["slice"]]
-        result = {"kind": "pipeline", "size": args.size, "workers": args.workers, "gpus": min(ngpu, args.workers),
-                  "inflight_per_worker": args.inflight,
+        result = {"kind": "pipeline_jpeg" if args.jpeg else "pipeline", "size": args.size,
+                  "workers": args.workers, "gpus": min(ngpu, args.workers),
+                  "inflight_per_worker": args.inflight or (3 if args.jpeg else 2),
                   "policy": args.policy, "producer": args.producer, "batch": args.batch, "frames": n,
                   "ring_slots_per_worker": slots, "verify_full_every": args.verify_every,
                   "slice_bytes_per_worker": slices[0]["bytes"] if slices else None,
@@ -173,6 +203,9 @@ def main():
                   "reorder_wait_mean_ms": round(st["reorder_wait_mean_ms"], 3),
                   "reorder_wait_max_ms": round(st["reorder_wait_max_ms"], 3), "max_buffer_depth": st["max_depth"],
                   "out_of_order_arrivals": st["out_of_order"], "errors": errors[:5], "n_errors": len(errors)}
+        if args.jpeg:
+            result["jpeg_bytes_in_mean"] = round(float(np.mean(fbytes)))
+            result["GBps_note"] = "compressed bytes in"
         print(json.dumps(result), flush=True)
         if args.out:
             with open(args.out, "a") as f:
