@@ -462,6 +462,12 @@ class Distributor:
                     return None
                 self._cv.wait(0.05)
 
+    def reserved_index(self, slot: int) -> Optional[int]:
+        """The frame index a reservation already carries (per-worker slices fix it at
+        ``reserve_frame``), else None (it is taken at ``commit_frame``)."""
+        with self._lock:
+            return self._reserved.get(slot)
+
     def commit_frame(self, slot: int, nbytes: int, shape=None, timestamp=None, block: bool = True) -> int:
         """Queue the frame written into ``slot``; returns its index (as add_frame_for_distribution)."""
         return self._enqueue(None, nbytes, shape, slot, time.time() if timestamp is None else timestamp, block)

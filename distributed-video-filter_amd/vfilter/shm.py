@@ -105,10 +105,12 @@ _copy_pool = None
 _COPY_SPLIT = 4 << 20  # frames from 4 MiB on are copied by several threads
 
 
-def copy_into(dst: np.ndarray, src) -> None:
+def copy_into(dst: np.ndarray, src, threads: int = 4) -> None:
     """dst[:] = src for a frame going into a ring slot.  One core copies ~10-25 GB/s, well
-    under one GPU's PCIe Gen5 x16 rate; large frames are split over a few threads with
-    ``ctypes.memmove`` (which releases the GIL), so the producer does not cap a 4K stream."""
+    under one GPU's PCIe Gen5 x16 rate; large frames are split over ``threads`` threads with
+    ``ctypes.memmove`` (which releases the GIL), so the producer does not cap a 4K stream.
+    ``threads=1``: one memmove on the calling thread, still without the GIL (for producers
+    that already copy from several threads at once)."""
     s = src if isinstance(src, np.ndarray) else np.frombuffer(src, dtype=np.uint8)
     s = s.reshape(-1).view(np.uint8)
     n = s.nbytes
@@ -118,13 +120,16 @@ def copy_into(dst: np.ndarray, src) -> None:
         dst[:] = s
         return
     import ctypes
+    d0, s0 = dst.ctypes.data, s.ctypes.data
+    if threads <= 1:
+        ctypes.memmove(d0, s0, n)
+        return
     global _copy_pool
     if _copy_pool is None:
         from concurrent.futures import ThreadPoolExecutor
         _copy_pool = ThreadPoolExecutor(max_workers=4, thread_name_prefix="vf-copy")
     parts = 4
     per = ((n + parts - 1) // parts + 4095) & ~4095
-    d0, s0 = dst.ctypes.data, s.ctypes.data
 
     def part(i):
         b = i * per

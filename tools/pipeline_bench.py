@@ -61,6 +61,9 @@ def main():
     ap.add_argument("--inflight", type=int, default=0,
                     help="batches in progress per worker (0: the worker's default, 2 raw / 3 JPEG)")
     ap.add_argument("--jpeg", action="store_true", help="JPEG frames, workers in JPEG mode")
+    ap.add_argument("--producers", type=int, default=0,
+                    help="producer threads (0: one per worker, at most 8); each reserves, fills and "
+                         "commits its own frames, so copies into the slices run in parallel")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
 
@@ -128,24 +131,39 @@ def main():
         errors = []
         started = threading.Event()
 
+        nprod = args.producers or min(8, args.workers)
+        # the frame a reservation gets decides what goes in it: index i carries content i % len(shapes)
+        # (the distributor fixes the index at reservation, in call order across producers)
+        count_lock = threading.Lock()
+        counter = [0]
+
         def produce():
-            for i in range(warm + n):
-                if i == warm:
+            while True:
+                with count_lock:
+                    i = counter[0]
+                    if i >= warm + n:
+                        return
+                    counter[0] += 1
+                if i >= warm:
                     started.wait()
-                k = i % len(shapes)
+                slot = d.reserve_frame(max_nb)
+                idx = d.reserved_index(slot)
+                idx = i if idx is None else idx
+                k = idx % len(shapes)
                 nb = fbytes[k]
-                slot = d.reserve_frame(nb)
                 if args.producer == "copy":
-                    copy_into(d.frame_view(slot, nb), pregen[k])
-                commit_t[i] = time.perf_counter()
+                    copy_into(d.frame_view(slot, nb), pregen[k], threads=1 if nprod > 1 else 4)
+                commit_t[idx] = time.perf_counter()
                 d.commit_frame(slot, nb, shape=None if args.jpeg else [shapes[k][0], shapes[k][1], 3])
 
-        th = threading.Thread(target=produce, daemon=True)
-        th.start()
-        # full checks (np.bitwise_not of a whole 4K frame: ~5 ms of one core) run on a small
-        # pool beside the consumer, which releases a slot once its check is done
+        max_nb = max(fbytes)
+        ths = [threading.Thread(target=produce, daemon=True) for _ in range(nprod)]
+        for th in ths:
+            th.start()
+        # full checks (np.bitwise_not of a whole 4K frame: ~5 ms of one core) run on a pool
+        # beside the consumer, which releases a slot once its check is done
         from concurrent.futures import ThreadPoolExecutor
-        vpool = ThreadPoolExecutor(max_workers=4, thread_name_prefix="verify")
+        vpool = ThreadPoolExecutor(max_workers=max(4, min(16, 2 * args.workers)), thread_name_prefix="verify")
         pending = []
 
         def full_check(i, idx, view, src):
@@ -185,13 +203,14 @@ def main():
         for f in pending:
             f.result()
         vpool.shutdown()
-        th.join()
+        for th in ths:
+            th.join()
         el = t_end - t_start
         lat = (release_t[warm:] - commit_t[warm:]) * 1e3
         st = d.ordering_stats()
         st["max_depth"] = max(st["max_depth"], d_stats0["max_depth"])
         slices = [w["slice"] for w in st["workers"].values() if w["slice"]]
-        result = {"kind": "pipeline_jpeg" if args.jpeg else "pipeline", "size": args.size,
+        result = {"kind": "pipeline_jpeg" if args.jpeg else "pipeline", "size": args.size, "producers": nprod,
                   "workers": args.workers, "gpus": min(ngpu, args.workers),
                   "inflight_per_worker": args.inflight or (3 if args.jpeg else 2),
                   "policy": args.policy, "producer": args.producer, "batch": args.batch, "frames": n,
