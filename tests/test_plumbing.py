@@ -353,3 +353,50 @@ def test_zero_copy_reserve_commit_and_release():
     finally:
         stop_workers(stop, procs)
         d.cleanup()
+
+
+@pytest.mark.timeout(120)
+def test_concurrent_producers_fill_the_frame_their_reservation_fixed():
+    """Several producer threads reserve, fill and commit at once (tools/pipeline_bench.py's
+    producer): with per-worker slices the index is fixed at reservation
+    (``reserved_index``), so each thread writes the content of that index; the in-order
+    consumer sees every index once, with its own content, and every slot comes back."""
+    d = _dist(policy="pull", reassembly="ordered", queue_size=12, ring_slots=6, ring_slot_bytes=48 * 40 * 3,
+              zero_copy=True)
+    stop, procs = spawn_workers(2, d.distribute_port, d.collect_port, protocol="v1", batch=3)
+    try:
+        while d.num_workers() < 2:
+            time.sleep(0.05)
+        kinds = _frames(5, [(48, 40), (16, 8), (33, 7)])
+        n = 90
+        counter = iter(range(n))
+        lock = threading.Lock()
+
+        def produce():
+            while True:
+                with lock:
+                    if next(counter, None) is None:
+                        return
+                slot = d.reserve_frame(max(f.nbytes for f in kinds))
+                idx = d.reserved_index(slot)
+                assert idx is not None
+                f = kinds[idx % len(kinds)]
+                d.frame_view(slot, f.nbytes)[:] = f.reshape(-1)
+                d.commit_frame(slot, f.nbytes, shape=list(f.shape))
+
+        ths = [threading.Thread(target=produce) for _ in range(3)]
+        for th in ths:
+            th.start()
+        for i in range(n):
+            item = d.get_next_frame(timeout=30)
+            assert item is not None, d.ordering_stats()
+            idx, view, _ = item
+            assert idx == i
+            assert view.tobytes() == oracle.invert_bytes(kinds[i % len(kinds)].tobytes()), i
+            d.release_frame(idx)
+        for th in ths:
+            th.join()
+        assert d.free_slots() == d.total_slots()
+    finally:
+        stop_workers(stop, procs)
+        d.cleanup()
