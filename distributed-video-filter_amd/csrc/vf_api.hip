@@ -151,6 +151,13 @@ int run_sync(vf_ctx *ctx, std::vector<vf::Seg> &&segs) {
     ctx->timeline.clear();
     return VF_OK;
   }
+  vf::JobResult r;
+  if (ctx->engine->run_now(segs, &r)) {  // page-locked, device-mapped: launched from this thread
+    ctx->last_kernel_ms = r.kernel_ms;
+    ctx->timeline = std::move(r.timeline);
+    if (r.status != VF_OK) return set_err(ctx, r.status, (int)r.hip, "%s", r.msg.c_str());
+    return VF_OK;
+  }
   return finish(ctx, ctx->engine->submit(std::move(segs)), nullptr);
 }
 

@@ -176,11 +176,14 @@ hipError_t Engine::init(int device, int nslots, size_t slot_bytes, const LaunchC
 // the other's kernels (1080p worker form 15.0-15.3 k fps on 4 queues, 19.9 k on 8:
 // profiles/r02_jpeg_hwq.jsonl).
 hipError_t Engine::ensure_streams() {
-  if (s_map_) return hipSuccess;
-  hipError_t e = hipSuccess;
-  if (!s_in_) e = hipStreamCreateWithFlags(&s_in_, hipStreamNonBlocking);
+  if (streams_ready_.load(std::memory_order_acquire)) return hipSuccess;
+  std::lock_guard<std::mutex> lk(stream_mu_);
+  if (streams_ready_.load(std::memory_order_relaxed)) return hipSuccess;
+  hipError_t e = hipSetDevice(device_);
+  if (e == hipSuccess && !s_in_) e = hipStreamCreateWithFlags(&s_in_, hipStreamNonBlocking);
   if (e == hipSuccess && !s_out_) e = hipStreamCreateWithFlags(&s_out_, hipStreamNonBlocking);
-  if (e == hipSuccess) e = hipStreamCreateWithFlags(&s_map_, hipStreamNonBlocking);
+  if (e == hipSuccess && !s_map_) e = hipStreamCreateWithFlags(&s_map_, hipStreamNonBlocking);
+  if (e == hipSuccess) streams_ready_.store(true, std::memory_order_release);
   return e;
 }
 
@@ -268,6 +271,65 @@ uint64_t Engine::submit(std::vector<Seg> &&segs) {
   pending_.push_back(std::move(job));
   cv_.notify_all();
   return id;
+}
+
+bool Engine::run_now(const std::vector<Seg> &segs, JobResult *out) {
+  if (!zero_copy_) return false;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (broken_) return false;  // the engine path reports it
+  }
+  std::vector<Seg> dsegs;
+  size_t total = 0;
+  for (const Seg &s : segs) {
+    if (!s.len) continue;
+    uint8_t *ds = mapped(s.src, s.len), *dd = mapped(s.dst, s.len);
+    if (!ds || !dd) return false;
+    dsegs.push_back(Seg{ds, dd, s.len});
+    total += s.len;
+  }
+  if (dsegs.empty() || hipSetDevice(device_) != hipSuccess || ensure_streams() != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  hipEvent_t a = take_event(), b = take_event();
+  if (!a || !b) {
+    give_event(a);
+    give_event(b);
+    return false;
+  }
+  hipError_t e = hipEventRecord(a, s_map_);
+  MappedBatch mb;
+  for (size_t i = 0; i < dsegs.size() && e == hipSuccess; i += kMappedMax) {
+    const int n = (int)std::min<size_t>(kMappedMax, dsegs.size() - i);
+    size_t bytes = 0;
+    for (int k = 0; k < n; ++k) {
+      mb.src[k] = dsegs[i + k].src;
+      mb.dst[k] = dsegs[i + k].dst;
+      mb.n[k] = dsegs[i + k].len;
+      bytes += dsegs[i + k].len;
+    }
+    e = launch_invert_mapped(mb, n, bytes, s_map_);
+  }
+  if (e == hipSuccess) e = hipEventRecord(b, s_map_);
+  if (e == hipSuccess) e = hipEventSynchronize(b);
+  *out = JobResult();
+  if (e != hipSuccess) {
+    (void)hipStreamSynchronize(s_map_);  // nothing may land in the caller's buffers later
+    (void)hipGetLastError();
+    out->status = kStatusHip;
+    out->hip = e;
+    out->msg = std::string("zero-copy launch failed: ") + hipGetErrorString(e);
+  } else {
+    float ms = -1.f;
+    if (hipEventElapsedTime(&ms, a, b) != hipSuccess) ms = -1.f;
+    out->kernel_ms = out->gpu_ms = ms;
+    out->zero_copy = true;
+    out->timeline.push_back(ChunkTime{total, 0.f, 0.f, ms, ms});
+  }
+  give_event(a);
+  give_event(b);
+  return true;
 }
 
 bool Engine::wait(uint64_t id, JobResult *out) {
@@ -569,7 +631,7 @@ void Engine::run() {
       cv_.wait(lk, [&] { return stop_ || !pending_.empty() || busy_slots() > 0 || !mapped_live_.empty(); });
       if (stop_ && pending_.empty() && busy_slots() == 0 && mapped_live_.empty()) return;
     }
-    if (!s_map_) {
+    if (!streams_ready_.load(std::memory_order_acquire)) {
       const hipError_t e = ensure_streams();
       if (e != hipSuccess) {
         fail_all(e, "stream creation");

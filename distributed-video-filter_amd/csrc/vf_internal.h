@@ -4,6 +4,7 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <atomic>
 #include <condition_variable>
 #include <deque>
 #include <map>
@@ -97,6 +98,9 @@ class Engine {
   hipError_t init(int device, int nslots, size_t slot_bytes, const LaunchCfg &cfg, std::string *err);
 
   uint64_t submit(std::vector<Seg> &&segs);  // returns the job id (> 0); never blocks on the GPU
+  // Synchronous zero-copy on the calling thread (no hand-off to the engine thread and back):
+  // false, with nothing done, unless every byte lies in noted device-mapped ranges.
+  bool run_now(const std::vector<Seg> &segs, JobResult *out);
   bool wait(uint64_t id, JobResult *out);    // false: unknown id
   bool query(uint64_t id, bool *done);       // false: unknown id
   void drain();                              // wait for every submitted job
@@ -160,6 +164,8 @@ class Engine {
   size_t slot_bytes_ = 0;
   hipStream_t s_in_ = nullptr, s_out_ = nullptr;
   hipStream_t s_map_ = nullptr;  // zero-copy launches (beside the slot ring's two streams)
+  std::mutex stream_mu_;         // creation of the three streams (engine thread or run_now)
+  std::atomic<bool> streams_ready_{false};
   bool zero_copy_ = true;        // VF_ZEROCOPY=0: caller-pinned jobs take the slot ring
   std::deque<Job *> mapped_live_;  // launched zero-copy jobs, in launch order
   std::vector<Slot> slots_;
