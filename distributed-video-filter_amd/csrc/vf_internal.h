@@ -38,6 +38,7 @@ struct MappedBatch {
   const uint8_t *src[kMappedMax];
   uint8_t *dst[kMappedMax];
   uint64_t n[kMappedMax];
+  uint32_t tile0[kMappedMax + 1];  // first 4-KiB tile of each range (set by the launcher)
 };
 hipError_t launch_invert_mapped(const MappedBatch &b, int n, size_t total_bytes, hipStream_t stream);
 

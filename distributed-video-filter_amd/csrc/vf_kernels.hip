@@ -153,10 +153,43 @@ __global__ __launch_bounds__(kBlock) void invert_frames_kernel(const uint8_t *co
 // moves 48.4-48.5 GB/s each way, equal to two SDMA copies running at once (48.5), with
 // 96-128 workgroups and one 16-B vector per lane in flight (more waves only queue behind the
 // link: 44-45 GB/s at 384).  The descriptors travel in the kernel arguments (<= kMappedMax
-// ranges per launch), so nothing is uploaded first.
-__global__ __launch_bounds__(kBlock) void invert_mapped_kernel(MappedBatch b) {
-  const uint32_t f = blockIdx.y;
-  invert_range<1>(b.src[f], b.dst[f], b.n[f]);
+// ranges per launch), so nothing is uploaded first.  Work is split in 4-KiB tiles (256 lanes
+// x 16 B) numbered across all ranges, and the grid strides over the tile numbers: ranges of
+// different sizes (a 480p / 1080p / 4K batch) get workgroups in proportion to their bytes,
+// so the link stays busy until the last byte instead of waiting on the 4K frames' share.
+__global__ __launch_bounds__(kBlock) void invert_mapped_kernel(MappedBatch b, uint32_t nranges) {
+  const uint32_t total = b.tile0[nranges];
+  const uint32_t t = threadIdx.x;
+  uint32_t k = 0;
+  for (uint32_t tile = blockIdx.x; tile < total; tile += gridDim.x) {
+    while (tile >= b.tile0[k + 1]) ++k;  // uniform: the grid's tiles only move forward
+    const uint8_t *s = b.src[k];
+    uint8_t *d = b.dst[k];
+    const uint64_t n = b.n[k];
+    const uint32_t h = (uint32_t)min((uint64_t)((16 - ((uintptr_t)d & 15)) & 15), n);  // dst head bytes
+    const uint64_t n16 = (n - h) >> 4;
+    const uint32_t lt = tile - b.tile0[k];
+    if (lt == 0) {  // the range's first tile also does its head and tail bytes
+      if (t < h) d[t] = (uint8_t)~s[t];
+      const uint64_t tail0 = h + (n16 << 4);
+      if (tail0 + t < n) d[tail0 + t] = (uint8_t)~s[tail0 + t];
+    }
+    const uint64_t i = (uint64_t)lt * kBlock + t;
+    if (i >= n16) continue;
+    u32x4 *d4 = reinterpret_cast<u32x4 *>(d + h);
+    const uintptr_t sb = (uintptr_t)(s + h);
+    const uint32_t delta = (uint32_t)(sb & 15), r = delta & 3;
+    const u32x4 *sa = reinterpret_cast<const u32x4 *>(sb - delta);
+    switch (delta >> 2) {  // uniform per range
+      case 0:
+        if (delta == 0) st16<true>(d4 + i, ~ld16<true>(sa + i));
+        else st16<true>(d4 + i, ~shift16<0>(ld16<true>(sa + i), ld16<false>(sa + i + 1), r));
+        break;
+      case 1: st16<true>(d4 + i, ~shift16<1>(ld16<true>(sa + i), ld16<false>(sa + i + 1), r)); break;
+      case 2: st16<true>(d4 + i, ~shift16<2>(ld16<true>(sa + i), ld16<false>(sa + i + 1), r)); break;
+      default: st16<true>(d4 + i, ~shift16<3>(ld16<true>(sa + i), ld16<false>(sa + i + 1), r)); break;
+    }
+  }
 }
 
 // ---- launchers ----------------------------------------------------------------------
@@ -212,13 +245,22 @@ hipError_t launch_invert_frames(const void *const *dsrcs, void *const *ddsts,
 hipError_t launch_invert_mapped(const MappedBatch &b, int n, size_t total_bytes, hipStream_t stream) {
   if (n <= 0) return hipSuccess;
   if (n > kMappedMax) return hipErrorInvalidValue;
-  // Workgroups over the whole launch: 128 keep the link busy for large ranges; below 16 MiB the
-  // fixed start-up latency dominates and 256 finish sooner (zerocopy_probe: 6.2 MB at 256 WG
-  // 33-34 GB/s, at 128 31-32).
-  const uint64_t target = total_bytes < (16ull << 20) ? 256 : 128;
-  uint64_t gx = target / (uint64_t)n;
-  if (gx == 0) gx = 1;
-  hipLaunchKernelGGL(invert_mapped_kernel, dim3((unsigned)gx, (unsigned)n), dim3(kBlock), 0, stream, b);
+  MappedBatch a = b;
+  uint64_t tiles = 0;
+  for (int k = 0; k < n; ++k) {
+    const uint64_t h = std::min<uint64_t>((16 - ((uintptr_t)a.dst[k] & 15)) & 15, a.n[k]);
+    const uint64_t n16 = (a.n[k] - h) >> 4;
+    a.tile0[k] = (uint32_t)tiles;
+    tiles += n16 ? (n16 + kBlock - 1) / kBlock : 1;  // at least one tile: head and tail bytes
+    if (tiles > 0xFFFFFFFFull) return hipErrorInvalidValue;  // > 16 TB in one launch
+  }
+  a.tile0[n] = (uint32_t)tiles;
+  // Workgroups: 128 keep the link busy for large launches; below 16 MiB the fixed start-up
+  // latency dominates and 256 finish sooner (zerocopy_probe: 6.2 MB at 256 WG 33-34 GB/s,
+  // at 128 31-32).
+  uint64_t grid = total_bytes < (16ull << 20) ? 256 : 128;
+  if (grid > tiles) grid = tiles;
+  hipLaunchKernelGGL(invert_mapped_kernel, dim3((unsigned)grid), dim3(kBlock), 0, stream, a, (uint32_t)n);
   return hipGetLastError();
 }
 

@@ -397,6 +397,14 @@ def test_zero_copy_ranges_every_offset_and_split(vf_ctx):
                                   [0, 3, FB_1080])
         assert np.array_equal(hd[100:103], ~hs[100:103]) and hd[99] == 0 and hd[103] == 0
         assert np.array_equal(hd[4096:4096 + FB_1080], ~hs[4096:4096 + FB_1080])
+        # very different sizes in one launch (a 480p / 1080p / 4K-like mix): the tiles are
+        # numbered across the ranges, so each range is covered whatever its share
+        hd[:] = 0
+        offs = [(7, 3, 17), (100, 5000, 921600 + 5), (2 << 20, (2 << 20) + 9, 3 << 20), (64, (6 << 20) + 64, 31)]
+        vf_ctx.invert_frames_host([ps + a for a, _, _ in offs], [pd + b for _, b, _ in offs], [n for _, _, n in offs])
+        assert _zero_copy(vf_ctx.last_timeline())
+        for a, b, n in offs:
+            assert np.array_equal(hd[b:b + n], ~hs[a:a + n]), (a, b, n)
         # async, several jobs in flight on the zero-copy stream
         ts = [vf_ctx.invert_frames_async([ps + k * (1 << 20)], [pd + k * (1 << 20)], [1 << 20])
               for k in range(8)]
