@@ -488,6 +488,8 @@ def distributor_leg(nworkers, ngpu, host_gbps=None, pcie_gbps=None, frames_scale
       configs[2]_resident  the same with frames committed in place (no producer copy)
       configs[3]           480p / 1080p / 4K interleaved 1:1:1, batch 16, pull policy,
                            producer copy, reporting the ordering overhead
+      jpeg_1080p           the reference's default deployment: 1080p JPEG frames (q85 4:2:2),
+                           workers in JPEG mode (3 batches of 32 in flight), pull policy
     Every 8th frame is verified in full, the others on their first and last 4 KiB.  Beside each
     leg: the ceilings for this many GPUs — PCIe (the pinned pipelined rate measured in
     end_to_end, each way, per GPU) and host DRAM (the host's measured r+w bandwidth from the
@@ -504,10 +506,13 @@ def distributor_leg(nworkers, ngpu, host_gbps=None, pcie_gbps=None, frames_scale
                                      "resident", "--frames", str(int(256 * nworkers * frames_scale))], k4, 2.25),
             "configs[3]": (["--size", "mixed", "--batch", "16", "--policy", "pull", "--producer", "copy",
                             "--frames", str(int(384 * nworkers * frames_scale))],
-                           (640 * 480 + 1920 * 1080 + 3840 * 2160) * 3 // 3, 4.25)}
+                           (640 * 480 + 1920 * 1080 + 3840 * 2160) * 3 // 3, 4.25),
+            # the reference's default deployment: JPEG frames, workers in JPEG mode
+            "jpeg_1080p": (["--jpeg", "--size", "1080p", "--batch", "32", "--policy", "pull",
+                            "--frames", str(int(4096 * nworkers * frames_scale))], 181876, None)}
     out = {}
     for name, (extra, fbytes, host_x) in legs.items():
-        cmd = [sys.executable, tool, "--workers", str(nworkers), "--gpus", str(ngpu), "--inflight", "2"] + extra
+        cmd = [sys.executable, tool, "--workers", str(nworkers), "--gpus", str(ngpu)] + extra
         t0 = time.time()
         p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
                              start_new_session=True)
@@ -523,18 +528,22 @@ def distributor_leg(nworkers, ngpu, host_gbps=None, pcie_gbps=None, frames_scale
             out[name] = {"error": f"rc={p.returncode}: {se[-300:]}"}
             continue
         r = json.loads(lines[-1])
-        keep = ("size", "workers", "gpus", "policy", "producer", "batch", "frames", "fps", "GBps_each_way",
+        keep = ("kind", "size", "workers", "gpus", "policy", "producer", "producers", "batch", "inflight_per_worker",
+                "ring_slots_per_worker", "frames", "fps", "GBps_each_way",
                 "latency_ms_mean", "latency_ms_p99", "reorder_wait_mean_ms", "reorder_wait_max_ms",
                 "max_buffer_depth", "out_of_order_arrivals", "n_errors", "verify_full_every",
                 "slice_bytes_per_worker", "slice_numa", "slice_numa_bound", "evictions", "frames_lost")
         leg = {k: r[k] for k in keep if k in r}
         leg["fps_per_gpu"] = round(r["fps"] / max(1, min(ngpu, nworkers)), 1)
-        ceil = {"frame_bytes_mean": fbytes, "host_bytes_per_frame": f"{host_x} x frame"}
-        if pcie_gbps:
-            ceil["pcie_fps"] = round(min(ngpu, nworkers) * pcie_gbps * 1e9 / fbytes, 1)
-        if host_gbps:
-            ceil["host_dram_fps"] = round(host_gbps * 1e9 / (host_x * fbytes), 1)
-        leg["ceilings"] = ceil
+        if host_x is not None:
+            ceil = {"frame_bytes_mean": fbytes, "host_bytes_per_frame": f"{host_x} x frame"}
+            if pcie_gbps:
+                ceil["pcie_fps"] = round(min(ngpu, nworkers) * pcie_gbps * 1e9 / fbytes, 1)
+            if host_gbps:
+                ceil["host_dram_fps"] = round(host_gbps * 1e9 / (host_x * fbytes), 1)
+            leg["ceilings"] = ceil
+        else:  # JPEG: bound by the GPU codec, compared with its worker-form rate in jpeg_mode
+            leg["jpeg_bytes_in_mean"] = r.get("jpeg_bytes_in_mean")
         leg["wall_s"] = round(time.time() - t0, 1)
         out[name] = leg
     out["note"] = ("host->host through distributor + per-worker shared-memory ring slices + one worker process "
