@@ -67,7 +67,7 @@ from .shm import FrameRing, copy_into
 
 
 class _Peer:
-    __slots__ = ("pid", "version", "wid", "requests", "frames_sent", "results", "errors", "home_shard", "shm",
+    __slots__ = ("pid", "version", "wid", "requests", "frames_sent", "batches_sent", "results", "errors", "home_shard", "shm",
                  "numa", "slice", "queue", "inflight", "quarantine", "batches", "alive", "gone", "evictions",
                  "order", "last_seen", "waiting_since")
 
@@ -80,6 +80,7 @@ class _Peer:
         self.order = order                    # registration order
         self.requests: Deque[int] = collections.deque()  # credits of outstanding requests
         self.frames_sent = 0
+        self.batches_sent = 0
         self.results = 0
         self.errors = 0
         self.home_shard: Optional[int] = None
@@ -852,6 +853,7 @@ class Distributor:
             ok = self.distribute_socket.send(p.pid, wire.encode_dispatch(metas, payloads, ring))
         if ok:
             p.frames_sent += len(items)
+            p.batches_sent += 1
             batch = [time.monotonic(), set()]
             for it in items:
                 it["attempts"] += 1
@@ -1099,7 +1101,8 @@ class Distributor:
                       "result_errors": self.result_errors, "frames_lost": self.frames_lost,
                       "frames_requeued": self.frames_requeued, "duplicates": self.duplicates,
                       "evictions": self.evictions, "departures": self.departures,
-                      "workers": {p.pid.hex(): {"sent": p.frames_sent, "results": p.results, "alive": p.alive,
+                      "workers": {p.pid.hex(): {"sent": p.frames_sent, "batches": p.batches_sent,
+                                                "results": p.results, "alive": p.alive,
                                                 "home_shard": p.home_shard,
                                                 "shards": sorted(k for k, o in self._shard_owner.items()
                                                                  if o == p.pid),

@@ -18,7 +18,14 @@ from vfilter.worker import Worker  # noqa: E402
 
 
 class OracleWorker(Worker):
-    delay = 0.0
+    delay = 0.0        # per frame
+    batch_delay = 0.0  # per batch: a fixed cost per call, like a GPU launch + host staging
+
+    def process_batch(self, frames, metas, outs):
+        if self.batch_delay > 0:
+            import time
+            time.sleep(self.batch_delay)
+        return super().process_batch(frames, metas, outs)
 
     def __call__(self, frame):
         from oracle import oracle
@@ -44,7 +51,7 @@ def _watch(stop_event, worker):
 
 
 def run_worker(dport, cport, stop_event, protocol="v1", batch=4, transport="tcp", kind="oracle",
-               delay=0.0, device=0, use_jpeg=False):
+               delay=0.0, device=0, use_jpeg=False, batch_delay=0.0, inflight=1):
     if kind == "gpu":
         from vfilter.inverter import InverterWorker
         w = InverterWorker("127.0.0.1", dport, cport, delay, use_jpeg=use_jpeg, device=device,
@@ -52,8 +59,9 @@ def run_worker(dport, cport, stop_event, protocol="v1", batch=4, transport="tcp"
                            transport=transport)
     else:
         cls = ResizingWorker if kind == "resizing" else OracleWorker
-        w = cls("127.0.0.1", dport, cport, batch=batch, protocol=protocol, transport=transport)
+        w = cls("127.0.0.1", dport, cport, batch=batch, protocol=protocol, transport=transport, inflight=inflight)
         w.delay = delay
+        w.batch_delay = batch_delay
     threading.Thread(target=_watch, args=(stop_event, w), daemon=True).start()
     try:
         w.start()

@@ -400,3 +400,31 @@ def test_concurrent_producers_fill_the_frame_their_reservation_fixed():
     finally:
         stop_workers(stop, procs)
         d.cleanup()
+
+
+def test_busy_worker_request_waits_to_be_filled():
+    """Batch filling (the dispatch rule): while a worker has a batch in flight, its request for
+    `credit` frames is held until that many are queued or the oldest has waited batch_wait;
+    an idle worker, a v0 worker, a credit of 1 and batch_wait=0 are answered at once."""
+    from vfilter.distributor import _Peer
+    d = Distributor(0, 0, transport="tcp", host="127.0.0.1", verbose=False, policy="pull",
+                    reassembly="ordered", batch_wait=0.5)
+    try:
+        p = _Peer(b"w", wire.Request(version=1, credit=8), 0)
+        now = time.monotonic()
+        d._pending.extend({"frame_index": i, "queued_at": now} for i in range(3))
+        assert not d._fill_pending(p, 8)               # idle worker: serve what there is
+        p.inflight[99] = {"frame_index": 99}
+        assert d._fill_pending(p, 8)                   # busy: wait for 8 ...
+        assert not d._fill_pending(p, 3)               # ... or serve a request that is full
+        assert not d._fill_pending(p, 1)
+        d._pending[0]["queued_at"] = now - 0.6         # ... or once the oldest waited batch_wait
+        assert not d._fill_pending(p, 8)
+        d._pending[0]["queued_at"] = now
+        d.batch_wait = 0.0
+        assert not d._fill_pending(p, 8)
+        d.batch_wait = 0.5
+        p.version = 0
+        assert not d._fill_pending(p, 8)
+    finally:
+        d.cleanup()
