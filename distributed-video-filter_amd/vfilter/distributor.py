@@ -54,7 +54,7 @@ import os
 import queue
 import threading
 import time
-from typing import Deque, Dict, List, Optional
+from typing import Sequence, Deque, Dict, List, Optional
 
 import numpy as np
 
@@ -470,6 +470,18 @@ class Distributor:
                     return None
                 self._cv.wait(0.05)
 
+    def reserve_frames(self, nbytes: int, n: int, block: bool = True) -> List[int]:
+        """Up to ``n`` reservations under one lock hold (at least one when ``block``), each as
+        ``reserve_frame``: a producer of many small frames (JPEG) pays the lock once per group."""
+        out: List[int] = []
+        with self._cv:
+            while len(out) < n:
+                slot = self.reserve_frame(nbytes, block=block and not out)
+                if slot is None:
+                    break
+                out.append(slot)
+        return out
+
     def reserved_index(self, slot: int) -> Optional[int]:
         """The frame index a reservation already carries (per-worker slices fix it at
         ``reserve_frame``), else None (it is taken at ``commit_frame``)."""
@@ -479,6 +491,13 @@ class Distributor:
     def commit_frame(self, slot: int, nbytes: int, shape=None, timestamp=None, block: bool = True) -> int:
         """Queue the frame written into ``slot``; returns its index (as add_frame_for_distribution)."""
         return self._enqueue(None, nbytes, shape, slot, time.time() if timestamp is None else timestamp, block)
+
+    def commit_frames(self, slots: Sequence[int], nbytes: Sequence[int], shapes=None, timestamp=None) -> List[int]:
+        """``commit_frame`` for a group of filled reservations, under one lock hold."""
+        ts = time.time() if timestamp is None else timestamp
+        with self._cv:
+            return [self._enqueue(None, nb, shapes[i] if shapes is not None else None, s_, ts, True)
+                    for i, (s_, nb) in enumerate(zip(slots, nbytes))]
 
     def cancel_frame(self, slot: int) -> None:
         """Give back a reserved slot that will not be committed (its index, if one was fixed at
@@ -1085,10 +1104,28 @@ class Distributor:
                 self._cv_out.wait(rem if rem is not None else 0.1)
             return self._released.popleft()
 
+    def get_next_frames(self, max_n: int, timeout: Optional[float] = None) -> list:
+        """reassembly='ordered': up to ``max_n`` next results in index order (at least one, or
+        an empty list on timeout), taken under one lock hold."""
+        first = self.get_next_frame(timeout)
+        if first is None:
+            return []
+        out = [first]
+        with self._cv:
+            while self._released and len(out) < max_n:
+                out.append(self._released.popleft())
+        return out
+
     def release_frame(self, index: int) -> None:
         """zero_copy: return frame ``index``'s ring slot once its result view is consumed."""
         with self._cv:
             self._free_slot(self._held.pop(index, None))
+
+    def release_frames(self, indices: Sequence[int]) -> None:
+        """``release_frame`` for a group of consumed results, under one lock hold."""
+        with self._cv:
+            for i in indices:
+                self._free_slot(self._held.pop(i, None))
 
     def num_workers(self) -> int:
         with self._lock:

@@ -428,3 +428,50 @@ def test_busy_worker_request_waits_to_be_filled():
         assert not d._fill_pending(p, 8)
     finally:
         d.cleanup()
+
+
+@pytest.mark.timeout(120)
+def test_grouped_reserve_commit_get_release():
+    """The grouped forms (reserve_frames / commit_frames / get_next_frames / release_frames)
+    behave as their one-frame forms called in a row: every index once, in order, with its
+    own content, and every slot back."""
+    d = _dist(policy="pull", reassembly="ordered", queue_size=16, ring_slots=10, ring_slot_bytes=24 * 20 * 3,
+              zero_copy=True)
+    stop, procs = spawn_workers(2, d.distribute_port, d.collect_port, protocol="v1", batch=4)
+    try:
+        while d.num_workers() < 2:
+            time.sleep(0.05)
+        kinds = _frames(4, [(24, 20), (5, 3)])
+        n = 120
+
+        def produce():
+            done = 0
+            while done < n:
+                slots = d.reserve_frames(24 * 20 * 3, min(6, n - done))
+                assert slots
+                nbs, shs = [], []
+                for s_ in slots:
+                    f = kinds[d.reserved_index(s_) % len(kinds)]
+                    d.frame_view(s_, f.nbytes)[:] = f.reshape(-1)
+                    nbs.append(f.nbytes)
+                    shs.append(list(f.shape))
+                d.commit_frames(slots, nbs, shs)
+                done += len(slots)
+
+        th = threading.Thread(target=produce)
+        th.start()
+        i = 0
+        while i < n:
+            items = d.get_next_frames(5, timeout=30)
+            assert items, d.ordering_stats()
+            for idx, view, _ in items:
+                assert idx == i
+                assert view.tobytes() == oracle.invert_bytes(kinds[i % len(kinds)].tobytes()), i
+                i += 1
+            d.release_frames([it[0] for it in items])
+        th.join()
+        assert d.free_slots() == d.total_slots()
+        assert d.get_next_frames(3, timeout=0.2) == []
+    finally:
+        stop_workers(stop, procs)
+        d.cleanup()

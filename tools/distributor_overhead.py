@@ -48,6 +48,8 @@ def main():
     ap.add_argument("--inflight", type=int, default=3)
     ap.add_argument("--policy", default="pull", choices=("pull", "shard"))
     ap.add_argument("--profile", action="store_true")
+    ap.add_argument("--group", type=int, default=1,
+                    help="frames per reserve_frames / commit_frames / get_next_frames / release_frames call")
     args = ap.parse_args()
     import multiprocessing as mp
     mctx = mp.get_context("spawn")
@@ -71,10 +73,13 @@ def main():
         n = args.frames
 
         def produce():
-            for i in range(warm + n):
-                slot = d.reserve_frame(args.bytes)
-                d.frame_view(slot, args.bytes)[:] = src
-                d.commit_frame(slot, args.bytes)
+            i = 0
+            while i < warm + n:
+                slots = d.reserve_frames(args.bytes, min(args.group, warm + n - i))
+                for slot in slots:
+                    d.frame_view(slot, args.bytes)[:] = src
+                d.commit_frames(slots, [args.bytes] * len(slots))
+                i += len(slots)
 
         th = threading.Thread(target=produce, daemon=True, name="producer")
         samples = {}
@@ -105,14 +110,17 @@ def main():
         if args.profile:
             threading.Thread(target=sampler, daemon=True).start()
         th.start()
-        for i in range(warm + n):
-            if i == warm:
+        i = 0
+        t_start = None
+        while i < warm + n:
+            if t_start is None and i >= warm:
                 t_start = time.perf_counter()
                 samples.clear()
-            item = d.get_next_frame(timeout=60)
-            if item is None:
+            items = d.get_next_frames(min(args.group, warm + n - i), timeout=60)
+            if not items:
                 raise RuntimeError(f"frame {i} never arrived: {d.ordering_stats()}")
-            d.release_frame(item[0])
+            d.release_frames([it[0] for it in items])
+            i += len(items)
         el = time.perf_counter() - t_start
         stop_sampling.set()
         th.join()

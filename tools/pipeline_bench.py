@@ -154,24 +154,34 @@ def main():
         count_lock = threading.Lock()
         counter = [0]
 
+        group = max(1, min(16, args.batch // 2))  # reservations and commits per lock hold
+
         def produce():
             while True:
                 with count_lock:
-                    i = counter[0]
-                    if i >= warm + n:
+                    i0 = counter[0]
+                    if i0 >= warm + n:
                         return
-                    counter[0] += 1
-                if i >= warm:
+                    g = min(group, warm + n - i0, warm - i0 if i0 < warm else group)
+                    counter[0] += g
+                if i0 >= warm:
                     started.wait()
-                slot = d.reserve_frame(max_nb)
-                idx = d.reserved_index(slot)
-                idx = i if idx is None else idx
-                k = idx % len(shapes)
-                nb = fbytes[k]
-                if args.producer == "copy":
-                    copy_into(d.frame_view(slot, nb), pregen[k], threads=1 if nprod > 1 else 4)
-                commit_t[idx] = time.perf_counter()
-                d.commit_frame(slot, nb, shape=None if args.jpeg else [shapes[k][0], shapes[k][1], 3])
+                done_ = 0
+                while done_ < g:
+                    slots = d.reserve_frames(max_nb, g - done_)
+                    nbs, shs = [], []
+                    for j, slot in enumerate(slots):
+                        idx = d.reserved_index(slot)
+                        idx = i0 + done_ + j if idx is None else idx
+                        k = idx % len(shapes)
+                        nb = fbytes[k]
+                        if args.producer == "copy":
+                            copy_into(d.frame_view(slot, nb), pregen[k], threads=1 if nprod > 1 else 4)
+                        commit_t[idx] = time.perf_counter()
+                        nbs.append(nb)
+                        shs.append(None if args.jpeg else [shapes[k][0], shapes[k][1], 3])
+                    d.commit_frames(slots, nbs, shs)
+                    done_ += len(slots)
 
         max_nb = max(fbytes)
         ths = [threading.Thread(target=produce, daemon=True) for _ in range(nprod)]
@@ -189,6 +199,9 @@ def main():
             d.release_frame(idx)
 
         total_bytes = 0
+        import collections
+        got = collections.deque()  # results taken in groups (get_next_frames), slots given back in groups
+        to_release = []
         for i in range(warm + n):
             if i == warm:
                 if sampler is not None:
@@ -196,10 +209,14 @@ def main():
                 d_stats0 = d.ordering_stats()
                 t_start = time.perf_counter()
                 started.set()
-            item = d.get_next_frame(timeout=120)
-            if item is None:
-                raise RuntimeError(f"frame {i} never arrived: {d.ordering_stats()}")
-            idx, view, info = item
+            if not got:
+                if to_release:
+                    d.release_frames(to_release)
+                    to_release = []
+                got.extend(d.get_next_frames(64, timeout=120))
+                if not got:
+                    raise RuntimeError(f"frame {i} never arrived: {d.ordering_stats()}")
+            idx, view, info = got.popleft()
             if idx != i:
                 errors.append(f"order: got {idx} expected {i}")
             if i >= warm:
@@ -215,7 +232,7 @@ def main():
                     ok = view[:4096].tobytes() == want[k_][:4096] and view[-4096:].tobytes() == want[k_][-4096:]
                 if not ok:
                     errors.append(f"frame {i} differs")
-                d.release_frame(idx)
+                to_release.append(idx)
                 continue
             src = d.in_view(info["slot"], view.nbytes)
             if i % args.verify_every == 0:
@@ -224,8 +241,10 @@ def main():
                 if not (np.array_equal(view[:4096], np.bitwise_not(src[:4096])) and
                         np.array_equal(view[-4096:], np.bitwise_not(src[-4096:]))):
                     errors.append(f"frame {i} differs")
-                d.release_frame(idx)
+                to_release.append(idx)
         t_end = time.perf_counter()
+        if to_release:
+            d.release_frames(to_release)
         if sampler is not None:
             sampler.stop()
             with open(args.profile + ".distributor", "w") as f:
