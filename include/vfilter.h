@@ -109,10 +109,13 @@ int vf_invert_batch_host(vf_ctx *ctx, const uint8_t *src, uint8_t *dst,
                          size_t frame_bytes, int n);
 
 /* Invert `n` separately allocated frames (srcs[i] -> dsts[i], nbytes[i] bytes each; sizes
- * may differ, e.g. a mixed 480p/1080p/4K batch).  Frames are gathered into the staging
- * slots, filtered with one kernel launch per slot and scattered back, so small frames are
- * not paid for one launch each.  Replaces worker.py:50-57 + inverter.py:29-46 for a batch
- * of raw frames. */
+ * may differ, e.g. a mixed 480p/1080p/4K batch).  Frames in page-locked, device-mapped
+ * memory are inverted by one launch per 64 frames, all at once (zero-copy); others are
+ * gathered into the staging slots, filtered with one launch per slot and scattered back, so
+ * small frames are not paid for one launch each.  Frames are independent: one frame's
+ * destination must not overlap another frame's source or destination (a frame's own src and
+ * dst may be equal).  Replaces worker.py:50-57 + inverter.py:29-46 for a batch of raw
+ * frames. */
 int vf_invert_frames_host(vf_ctx *ctx, const uint8_t *const *srcs, uint8_t *const *dsts,
                           const size_t *nbytes, int n);
 
