@@ -169,6 +169,43 @@ void sync_table(const HuffDec &t, bool dc, HuffSync *s) {
   }
 }
 
+// decode_table + sync_table through a small per-thread cache keyed by the DHT content: the
+// frames of a stream share their tables (one encoder, one set of settings), so a batch builds
+// each distinct table once per parsing thread instead of 6 times per frame (2 x 2^kLook
+// entries each; the table build was most of the host-side parse of a 480p batch).
+bool build_tables(const uint8_t bits[17], const uint8_t *vals, bool dc, HuffDec *t, HuffSync *s) {
+  struct Entry {
+    bool valid = false, dc = false;
+    uint8_t bits[17];
+    uint8_t vals[256];
+    HuffDec t;
+    HuffSync s;
+  };
+  static thread_local Entry cache[4];
+  static thread_local int next = 0;
+  int nvals = 0;
+  for (int l = 1; l <= 16; ++l) nvals += bits[l];
+  if (nvals > 256) return false;
+  for (Entry &e : cache)
+    if (e.valid && e.dc == dc && std::memcmp(e.bits, bits, 17) == 0 && std::memcmp(e.vals, vals, (size_t)nvals) == 0) {
+      std::memcpy(t, &e.t, sizeof *t);
+      std::memcpy(s, &e.s, sizeof *s);
+      return true;
+    }
+  if (!decode_table(bits, vals, dc, t)) return false;
+  sync_table(*t, dc, s);
+  Entry &e = cache[next];
+  next = (next + 1) & 3;
+  e.valid = true;
+  e.dc = dc;
+  std::memcpy(e.bits, bits, 17);
+  std::memset(e.vals, 0, sizeof e.vals);
+  std::memcpy(e.vals, vals, (size_t)nvals);
+  std::memcpy(&e.t, t, sizeof *t);
+  std::memcpy(&e.s, s, sizeof *s);
+  return true;
+}
+
 struct Parsed {
   int w = 0, h = 0, ncomp = 0, restart = 0;
   int id[3] = {}, hs[3] = {}, vs[3] = {}, tq[3] = {}, td[3] = {}, ta[3] = {};
@@ -613,13 +650,11 @@ int Codec::prepare_decode(const uint8_t *const *jpegs, const size_t *sizes, int 
     }
     for (int c = 0; c < P.ncomp; ++c) {
       std::memcpy(F.q[c], P.qt[P.tq[c]], sizeof F.q[c]);
-      if (!decode_table(P.dcbits[P.td[c]], P.dcvals[P.td[c]], true, &F.dc[c]) ||
-          !decode_table(P.acbits[P.ta[c]], P.acvals[P.ta[c]], false, &F.ac[c])) {
+      if (!build_tables(P.dcbits[P.td[c]], P.dcvals[P.td[c]], true, &F.dc[c], &F.sdc[c]) ||
+          !build_tables(P.acbits[P.ta[c]], P.acvals[P.ta[c]], false, &F.ac[c], &F.sac[c])) {
         e = "bad Huffman table";
         return;
       }
-      sync_table(F.dc[c], true, &F.sdc[c]);
-      sync_table(F.ac[c], false, &F.sac[c]);
     }
     const size_t len = P.scan_end - P.scan_off;
     if (len == 0 || len > (1u << 28)) e = "empty or oversized entropy-coded segment";

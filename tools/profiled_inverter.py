@@ -23,4 +23,14 @@ def _dump():
 
 from vfilter.inverter import main  # noqa: E402
 
+if os.environ.get("VF_CPROFILE"):  # deterministic per-function profile of the worker's main thread
+    import cProfile
+    import pstats
+    prof = cProfile.Profile()
+    try:
+        rc = prof.runcall(main, sys.argv[1:])
+    finally:
+        with open(f"{_out}.{os.getpid()}.cprofile", "w") as f:
+            pstats.Stats(prof, stream=f).sort_stats("tottime").print_stats(35)
+    sys.exit(rc)
 sys.exit(main(sys.argv[1:]))
