@@ -737,6 +737,17 @@ VF_EXPORT int vf_jpeg_invert_fetch(vf_ctx *ctx, uint64_t ticket, uint8_t *out, s
   return jpeg_status(ctx, rc, "vf_jpeg_invert_fetch: " + err);
 }
 
+VF_EXPORT int vf_jpeg_invert_scatter(vf_ctx *ctx, uint64_t ticket, uint8_t *const *outs, const size_t *caps,
+                                     size_t *sizes, int *placed) {
+  VF_CHECK_CTX(ctx);
+  vf::jpeg::Codec *c = job_codec(ctx, ticket);
+  if (!c || !outs || !caps || !sizes || !placed)
+    return set_err(ctx, VF_E_INVALID, 0, "vf_jpeg_invert_scatter: unknown ticket %llu or NULL argument",
+                   (unsigned long long)ticket);
+  if (!c->waited()) return set_err(ctx, VF_E_INVALID, 0, "vf_jpeg_invert_scatter: call vf_jpeg_invert_wait first");
+  return jpeg_status(ctx, c->scatter_invert(outs, caps, sizes, placed), "vf_jpeg_invert_scatter");
+}
+
 VF_EXPORT int vf_jpeg_bench_invert(vf_ctx *ctx, const uint8_t *const *jpegs, const size_t *jpeg_sizes, int n,
                                    int quality, int subsamp, int flags, int iters, float *ms, float *stage_ms) {
   VF_CHECK_CTX(ctx);

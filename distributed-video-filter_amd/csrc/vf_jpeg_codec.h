@@ -114,6 +114,9 @@ class Codec {
   bool done_invert();
   int wait_invert(size_t *total, std::string *err);
   int fetch_invert(uint8_t *out, size_t cap, size_t *sizes, size_t *offs, std::string *err);
+  // after wait_invert: frame f's JPEG into outs[f] when it is not NULL and fits caps[f];
+  // sizes[f] = its size either way, *placed = how many were copied; the batch stays fetchable
+  int scatter_invert(uint8_t *const *outs, const size_t *caps, size_t *sizes, int *placed);
   uint64_t fetch_refills() const { return fetch_refills_; }
   bool waited() const { return waited_; }
   // wait for anything still queued on the codec's stream (after a failed call, before the codec

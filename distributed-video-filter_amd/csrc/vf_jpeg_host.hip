@@ -1249,6 +1249,21 @@ int Codec::wait_invert(size_t *total, std::string *err) {
   return kOk;
 }
 
+int Codec::scatter_invert(uint8_t *const *outs, const size_t *caps, size_t *sizes, int *placed) {
+  const int n = en_;
+  int count = 0;
+  for (int f = 0; f < n; ++f) {
+    sizes[f] = (size_t)out_sizes_[(size_t)f];
+    count += outs[f] && out_sizes_[(size_t)f] <= caps[f];
+  }
+  pool_.run(n, [&](int f) {
+    if (outs[f] && out_sizes_[(size_t)f] <= caps[f])
+      std::memcpy(outs[f], h_out_.as<uint8_t>() + out_offs_[(size_t)f], out_sizes_[(size_t)f]);
+  });
+  *placed = count;
+  return kOk;
+}
+
 int Codec::fetch_invert(uint8_t *out, size_t cap, size_t *sizes, size_t *offs, std::string *err) {
   const int n = en_;
   if (out && cap < out_total_) {

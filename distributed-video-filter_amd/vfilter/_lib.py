@@ -78,6 +78,7 @@ SIGNATURES = {
     "vf_jpeg_invert_query": (ctypes.c_int, [_vp, ctypes.c_uint64, _c_int_p]),
     "vf_jpeg_invert_wait": (ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.POINTER(_sz)]),
     "vf_jpeg_invert_fetch": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, _sz, _vp, _vp]),
+    "vf_jpeg_invert_scatter": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, _vp, _vp, ctypes.POINTER(ctypes.c_int)]),
     "vf_jpeg_bench_invert": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                             ctypes.c_int, _c_float_p, _c_float_p]),
 }
@@ -415,6 +416,37 @@ class Context:
         off = (ctypes.c_size_t * n)()
         self._check(self._lib.vf_jpeg_invert_fetch(self._ctx, ticket, buf.ctypes.data, buf.nbytes, sz, off))
         return [buf[off[i]:off[i] + sz[i]] for i in range(n)]
+
+    def jpeg_invert_result_into(self, ticket: int, outs: Sequence) -> list:
+        """Wait for a submitted batch and write frame i's JPEG into ``outs[i]`` (a writable uint8
+        array, e.g. the output half of the frame's ring slot) when it fits; returns per frame a
+        view ``outs[i][:size]``, or, for a frame without room (or ``outs[i]`` None), a view into
+        one fresh buffer holding it (vf_jpeg_invert_scatter, then a packed fetch only if needed)."""
+        n = self.__dict__.get("_jpeg_n", {}).pop(ticket, None)
+        if n is None:
+            raise VFilterError(f"unknown JPEG ticket {ticket}", VF_E_INVALID)
+        if len(outs) != n:
+            self.__dict__["_jpeg_n"][ticket] = n
+            raise ValueError(f"jpeg_invert_result_into: {len(outs)} outputs for a batch of {n}")
+        total = ctypes.c_size_t(0)
+        self._check(self._lib.vf_jpeg_invert_wait(self._ctx, ticket, ctypes.byref(total)))
+        op = (ctypes.c_void_p * n)(*[None if o is None else o.ctypes.data for o in outs])
+        caps = (ctypes.c_size_t * n)(*[0 if o is None else o.nbytes for o in outs])
+        sz = (ctypes.c_size_t * n)()
+        placed = ctypes.c_int(0)
+        try:
+            self._check(self._lib.vf_jpeg_invert_scatter(self._ctx, ticket, op, caps, sz, ctypes.byref(placed)))
+        except Exception:
+            self._lib.vf_jpeg_invert_fetch(self._ctx, ticket, None, 0, None, None)
+            raise
+        res = [outs[i][:sz[i]] if outs[i] is not None and sz[i] <= caps[i] else None for i in range(n)]
+        if placed.value == n:
+            self._check(self._lib.vf_jpeg_invert_fetch(self._ctx, ticket, None, 0, None, None))
+            return res
+        buf = np.empty(max(1, total.value), np.uint8)
+        off = (ctypes.c_size_t * n)()
+        self._check(self._lib.vf_jpeg_invert_fetch(self._ctx, ticket, buf.ctypes.data, buf.nbytes, sz, off))
+        return [r if r is not None else buf[off[i]:off[i] + sz[i]] for i, r in enumerate(res)]
 
     def jpeg_invert_release(self, ticket: int) -> None:
         """Drop a submitted batch without reading it."""

@@ -22,6 +22,7 @@ two codecs (each in-flight batch holds its own codec, stream and buffers).
 from __future__ import annotations
 
 import argparse
+import os
 import signal
 import time
 from typing import List, Optional, Sequence
@@ -50,6 +51,8 @@ class InverterWorker(Worker):
         self.ctx = Context(self.device, max_frame_bytes=max_frame_bytes, max_batch=max(1, self.batch))
         # inverter.py:13 — TurboJPEG() with PyTurboJPEG's defaults, on this worker's GPU
         self.jpeg = TurboJPEG(ctx=self.ctx, tj_version=tj_version) if use_jpeg else None
+        # re-encoded JPEGs written straight into their ring slots (VF_JPEG_SCATTER=0: copied by the loop)
+        self.sized_results = self.jpeg is not None and os.environ.get("VF_JPEG_SCATTER", "1") != "0"
         self._registered: List[int] = []
         if install_signal_handlers:                                  # inverter.py:16-18
             signal.signal(signal.SIGINT, self._signal_handler)
@@ -114,11 +117,12 @@ class InverterWorker(Worker):
     def submit_batch(self, frames: Sequence, metas: Sequence[wire.FrameMeta], outs: Sequence):
         """Queue the batch with vf_invert_frames_async and return to receiving at once: the
         context's engine thread streams consecutive batches through the GPU back to back.
-        Ring frames (page-locked) are DMA'd in place; socket payloads are staged.  JPEG
-        batches go to a 2-thread executor (fused decode -> invert -> encode per batch)."""
+        Ring frames (page-locked) are inverted in place (zero-copy); socket payloads are staged.
+        JPEG batches are queued on a codec of their own (vf_jpeg_invert_submit: fused decode ->
+        invert -> encode) and collected later, ring frames' results straight into their slots."""
         if self.jpeg and self.delay <= 0:
             try:  # staged and queued now; the loop receives the next batch while this one runs
-                return ("jpeg", self.jpeg.invert_batch_submit(list(frames)), list(frames))
+                return ("jpeg", self.jpeg.invert_batch_submit(list(frames)), list(frames), list(outs))
             except Exception:  # a frame the host parser refuses: frame by frame (worker.py:74-76)
                 return ("done", super().process_batch(frames, metas, outs), [])
         if self.jpeg or self.delay > 0:
@@ -136,10 +140,12 @@ class InverterWorker(Worker):
 
     def poll_batch(self, handle, block: bool):
         if handle[0] == "jpeg":
-            _, ticket, frames = handle
+            _, ticket, frames, outs = handle
             if not block and not self.jpeg.invert_batch_ready(ticket):
                 return None
             try:
+                if any(o is not None for o in outs):  # ring frames: straight into their slots
+                    return self.jpeg.invert_batch_result_into(ticket, outs), []
                 return self.jpeg.invert_batch_result(ticket), []
             except Exception:  # e.g. a truncated stream the GPU found: frame by frame
                 return Worker.process_batch(self, frames, [None] * len(frames), [None] * len(frames)), []

@@ -115,3 +115,8 @@ class TurboJPEG:
     def invert_batch_result(self, ticket: int) -> List[np.ndarray]:
         """The inverted JPEGs of a submitted batch (bytes-like uint8 views), in batch order."""
         return self.ctx.jpeg_invert_result(ticket)
+
+    def invert_batch_result_into(self, ticket: int, outs: Sequence) -> List[np.ndarray]:
+        """The same, each JPEG written straight into ``outs[i]`` when it fits there (e.g. the
+        output half of its ring slot); a frame without room comes back in a fresh buffer."""
+        return self.ctx.jpeg_invert_result_into(ticket, outs)

@@ -33,13 +33,18 @@ from .shm import FrameRing
 
 
 def _same_buffer(r, o) -> bool:
-    """True when result ``r`` is the ring output view ``o`` (written in place)."""
+    """True when result ``r`` was written in place at the start of ring output view ``o``
+    (the whole view, or, for a plugin whose results have their own size, a prefix of it)."""
     if o is None or not isinstance(r, np.ndarray):
         return False
-    return r.nbytes == o.nbytes and (r.nbytes == 0 or r.ctypes.data == o.ctypes.data)
+    return r.nbytes <= o.nbytes and (r.nbytes == 0 or r.ctypes.data == o.ctypes.data)
 
 
 class Worker:
+    # True for a plugin whose results have their own size (a re-encoded JPEG): ring frames then
+    # get their slot's whole output half to write into, and the result carries its length
+    sized_results = False
+
     def __init__(self, host: str = "localhost", distribute_port: int = 5555, collect_port: int = 5556, *,
                  transport: str = "auto", protocol: str = "v1", batch: int = 1, depth: int = 0,
                  inflight: int = 1, verbose: bool = False):
@@ -207,7 +212,8 @@ class Worker:
         for m, p in zip(d.metas, d.payloads):
             if m.slot is not None:
                 frames.append(ring.in_view(m.slot, m.nbytes))
-                outs.append(ring.out_view(m.slot, m.nbytes))
+                # a plugin whose results have their own size (JPEG) gets the whole output half
+                outs.append(ring.out_view(m.slot, ring.slot_bytes if self.sized_results else m.nbytes))
             else:
                 frames.append(p)
                 outs.append(None)
@@ -233,7 +239,11 @@ class Worker:
                 print(f"Error in worker: frame {m.index}: {r}")
             elif m.slot is None:
                 payload = r
-            elif not _same_buffer(r, o):
+            elif _same_buffer(r, o):
+                if r.nbytes != m.nbytes:  # written in place, with its own length
+                    om.nbytes = r.nbytes
+                    om.shape = None
+            else:
                 # a result of its own size (JPEG): into the slot's output half when it fits,
                 # else back over the socket; either way the result carries its length
                 rb = np.frombuffer(r, dtype=np.uint8)

@@ -267,6 +267,15 @@ int vf_jpeg_invert_wait(vf_ctx *ctx, uint64_t ticket, size_t *total);
 int vf_jpeg_invert_fetch(vf_ctx *ctx, uint64_t ticket, uint8_t *out, size_t cap, size_t *sizes,
                          size_t *offsets);
 
+/* After vf_jpeg_invert_wait: frame i's inverted JPEG straight into outs[i] when outs[i] is not
+ * NULL and the JPEG fits caps[i] (e.g. the output half of the frame's shared-memory ring slot),
+ * so the caller needs no packed buffer and no second copy.  sizes[i] = frame i's size either
+ * way; *placed = how many frames were copied.  The batch stays open: release it with
+ * vf_jpeg_invert_fetch(ctx, ticket, NULL, 0, NULL, NULL), or fetch the frames that did not
+ * fit with a packed buffer first. */
+int vf_jpeg_invert_scatter(vf_ctx *ctx, uint64_t ticket, uint8_t *const *outs, const size_t *caps,
+                           size_t *sizes, int *placed);
+
 /* Benchmark: the GPU part of vf_jpeg_invert (inputs already in HBM) run `iters` times; *ms =
  * mean wall ms per iteration; stage_ms (may be NULL, 8 floats) = mean ms of unstuff, Huffman
  * sync, Huffman write, DC+IDCT, colour+invert, FDCT+Huffman encode, byte stuffing, and the

@@ -232,3 +232,26 @@ def test_async_submit_keeps_batches_in_flight(tj, vf_ctx):
     for t in ts:
         assert bytes(tj.invert_batch_result(t)[0]) == want[2][0]
     assert tj.invert(good) == want[2][0]
+
+
+def test_async_result_scattered_into_caller_buffers(tj):
+    """vf_jpeg_invert_scatter (the worker's ring path): each inverted JPEG goes straight into
+    its own buffer when it fits; a frame with a buffer too small, or none, comes back from a
+    packed fetch; all bit-exact, and the ticket is released either way."""
+    jpgs = [J.encode(_img("scene", 70 + s, h, w)) for s, (h, w) in enumerate([(480, 640), (64, 48), (1080, 1920),
+                                                                                (17, 13)])]
+    want = [J.invert_jpeg(j) for j in jpgs]
+    outs = [np.zeros(len(want[0]) + 100, np.uint8), np.zeros(len(want[1]) - 1, np.uint8), None,
+            np.zeros(len(want[3]), np.uint8)]
+    t = tj.invert_batch_submit(jpgs)
+    got = tj.invert_batch_result_into(t, outs)
+    for i, (g, w) in enumerate(zip(got, want)):
+        assert bytes(g) == w, i
+    assert got[0].ctypes.data == outs[0].ctypes.data and got[3].ctypes.data == outs[3].ctypes.data
+    assert not outs[1].any()  # too small: untouched
+    with pytest.raises(VFilterError):
+        tj.invert_batch_result(t)  # released
+    # every frame fits: no packed fetch at all
+    outs = [np.zeros(len(w) + 8, np.uint8) for w in want]
+    got = tj.invert_batch_result_into(tj.invert_batch_submit(jpgs), outs)
+    assert [bytes(g) for g in got] == want
