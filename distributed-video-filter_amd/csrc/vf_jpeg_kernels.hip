@@ -891,13 +891,23 @@ __global__ __launch_bounds__(256) void k_finalize(const DecFrame *fr, const uint
   }
 }
 
+// The workgroup's stream words are staged in LDS first (as k_spec does): every refill of a
+// thread's bit buffer is then an LDS read instead of a dependent global load, the chain a
+// subsequence's decode waits on (k_write has only ~3 waves per SIMD to hide it with).
 __global__ __launch_bounds__(256) void k_write(const DecFrame *fr, const uint8_t *us, const uint32_t *us_len,
                                                const uint64_t *exits, const uint32_t *bstart, int16_t *coef,
                                                int32_t *dcseq) {
   __shared__ HuffDec tabs[6];
+  __shared__ uint32_t s_w[kSpecWords];
   const DecFrame &F = fr[blockIdx.y];
   if (blockIdx.x * 256 >= F.nsub_max) return;
-  load_tables(F, tabs);
+  // this workgroup's 256 subsequences of stream words, plus overshoot and lookahead, from the
+  // frame's padded unstuffed region (an entry state lies at or after its subsequence's start)
+  const uint32_t woff = blockIdx.x * 256 * (kSubBits / 32);
+  const uint32_t fwords = (((F.in_len + 64) + 15) & ~15u) / 4;
+  const uint32_t *gw = reinterpret_cast<const uint32_t *>(us + F.us_off);
+  for (uint32_t k = threadIdx.x; k < kSpecWords; k += 256) s_w[k] = woff + k < fwords ? gw[woff + k] : 0u;
+  load_tables(F, tabs);  // its barrier also publishes s_w
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   const uint32_t nbits = us_len[blockIdx.y] * 8u;
   const uint32_t nsub = (nbits + kSubBits - 1) / kSubBits;
@@ -906,7 +916,7 @@ __global__ __launch_bounds__(256) void k_write(const DecFrame *fr, const uint8_t
   const uint64_t st = i == 0 ? 0 : exits[gi - 1];
   const uint32_t end = (i + 1 == nsub) ? nbits : (i + 1) * kSubBits;
   BitReader br;
-  br.init(us + F.us_off, (uint32_t)(st >> 16));
+  br.init_words(s_w, (uint32_t)(st >> 16), woff);
   uint32_t z = (st >> 8) & 0xFF, c = st & 0xFF, blocks = 0;
   decode_span<true>(br, end, z, c, blocks, HuffGeom(F.g), tabs, tabs + 3, bstart[gi], coef + F.blk0 * 64, dcseq,
                     F.dcbase);
