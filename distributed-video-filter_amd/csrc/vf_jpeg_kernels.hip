@@ -992,13 +992,6 @@ __device__ __forceinline__ uint32_t idct_limit(int32_t x) {
   return m < 128 ? (uint32_t)(m + 128) : m < 512 ? 255u : m < 896 ? 0u : (uint32_t)(m - 896);
 }
 
-__device__ __forceinline__ void block_pos(const Geom &g, uint32_t b, uint32_t *k, uint32_t *bx, uint32_t *by) {
-  const uint32_t mcu = b / (uint32_t)g.bpm, c = b % (uint32_t)g.bpm;
-  *k = (uint32_t)g.bcomp[c];
-  *bx = (mcu % (uint32_t)g.mcux) * (uint32_t)g.mh[*k] + (uint32_t)g.bxo[c];
-  *by = (mcu / (uint32_t)g.mcux) * (uint32_t)g.mv[*k] + (uint32_t)g.byo[c];
-}
-
 // Measured (tools/gpu_jpeg_variants.sh, profiles/r01_jpeg_idct_variants.txt; dc + idct ms at
 // 1080p / 4K): 1 block per lane group with separate LDS for the two passes 0.200 / 0.73 (the
 // earlier kernel); aliased 0.202 / 0.74; 2 blocks not aliased 0.21 / 0.76; 2 blocks aliased
@@ -1378,87 +1371,65 @@ __device__ __forceinline__ int16_t quantize(int32_t x, uint32_t recip, uint32_t 
   return (int16_t)p;
 }
 
-// N adjacent pixels of row py from px (edges replicated: jccolor.c on expand_right_edge /
-// expand_bottom_edge input), split into r/g/b; 8-byte vector loads when the span is inside
-// the image and aligned.
-template <int N>
-__device__ __forceinline__ void load_rgb(const uint8_t *img, int w, int h, int px, int py, bool bgr, int *r, int *g,
-                                         int *b) {
-  py = py < h ? py : h - 1;
-  const uint8_t *src = img + ((size_t)py * w + px) * 3;
-  if (px + N <= w && ((uintptr_t)src & 7) == 0) {
-    uint32_t wd[N * 3 / 4];
-#pragma unroll
-    for (int q = 0; q < N * 3 / 8; ++q) {
-      const uint2 v = reinterpret_cast<const uint2 *>(src)[q];
-      wd[2 * q] = v.x;
-      wd[2 * q + 1] = v.y;
-    }
-#pragma unroll
-    for (int j = 0; j < N; ++j) {
-      const int c0 = (int)((wd[(3 * j) / 4] >> (8 * ((3 * j) % 4))) & 0xFF);
-      const int c1 = (int)((wd[(3 * j + 1) / 4] >> (8 * ((3 * j + 1) % 4))) & 0xFF);
-      const int c2 = (int)((wd[(3 * j + 2) / 4] >> (8 * ((3 * j + 2) % 4))) & 0xFF);
-      r[j] = bgr ? c2 : c0;
-      g[j] = c1;
-      b[j] = bgr ? c0 : c2;
-    }
+// jccolor.c rgb_ycc_convert for one component over a pixel's bytes in memory order:
+// (a0 * c0 + a1 * c1 + a2 * c2 + bias) >> 16.  The component and the channel order are
+// wave-uniform in k_fdct, so the coefficients sit in scalar registers and a pixel costs three
+// multiply-adds with no per-pixel select.  No sum is negative (Cb and Cr carry 128 << 16:
+// their smallest sums are 575535 and 65535), so the shift is jccolor.c's.
+struct Ycc {
+  int a0, a1, a2, bias;
+};
+__device__ __forceinline__ Ycc ycc_coefs(int k, bool bgr) {
+  int r, g, b, bias = (128 << 16) + 32767;
+  if (k == 0) {
+    r = 19595, g = 38470, b = 7471, bias = 32768;
+  } else if (k == 1) {
+    r = -11059, g = -21709, b = 32768;
   } else {
-    const uint8_t *row = img + (size_t)py * w * 3;
-#pragma unroll
-    for (int j = 0; j < N; ++j) {
-      const int x = px + j < w ? px + j : w - 1;
-      const uint8_t *q = row + (size_t)x * 3;
-      r[j] = bgr ? q[2] : q[0];
-      g[j] = q[1];
-      b[j] = bgr ? q[0] : q[2];
-    }
+    r = 32768, g = -27439, b = -5329;
   }
+  return bgr ? Ycc{b, g, r, bias} : Ycc{r, g, b, bias};
+}
+__device__ __forceinline__ int ycc_apply(const Ycc &q, int c0, int c1, int c2) {
+  return (q.a0 * c0 + q.a1 * c1 + q.a2 * c2 + q.bias) >> 16;
 }
 
-__device__ __forceinline__ int ycc_comp(int k, int r, int g, int b) {  // jccolor.c rgb_ycc_convert
-  if (k == 0) return (19595 * r + 38470 * g + 7471 * b + 32768) >> 16;
-  if (k == 1) return (-11059 * r - 21709 * g + 32768 * b + (128 << 16) + 32767) >> 16;
-  return (32768 * r - 27439 * g - 5329 * b + (128 << 16) + 32767) >> 16;
-}
-
-// Component k of the 8 * H pixels of row py from px, summed in groups of H into v[0..7]
+// One component of the 8 * H pixels of row py from px, summed in groups of H into v[0..7]
 // (assigned when `first`, else added: a second row of h2v2).  Edges replicated
 // (jccolor.c on expand_right_edge / expand_bottom_edge input).  4 pixels (3 dwords) at a
 // time, so at most 12 channel values are live instead of 3 * 8 * H.
 template <int H>
-__device__ __forceinline__ void line_acc(const uint8_t *img, int w, int h, int px, int py, bool bgr, int k,
+__device__ __forceinline__ void line_acc(const uint8_t *img, int w, int h, int px, int py, const Ycc &q,
                                          int32_t v[8], bool first) {
   py = py < h ? py : h - 1;
   const uint8_t *row = img + (size_t)py * w * 3;
   const uint8_t *src = row + (size_t)px * 3;
   const bool fast = px + 8 * H <= w && ((uintptr_t)src & 3) == 0;
 #pragma unroll
-  for (int q = 0; q < 2 * H; ++q) {
+  for (int qd = 0; qd < 2 * H; ++qd) {
     int c[4];
     if (fast) {
-      const uint32_t *s32 = reinterpret_cast<const uint32_t *>(src) + 3 * q;
-      const uint32_t w0 = s32[0], w1 = s32[1], w2 = s32[2];
-      const uint32_t wd[3] = {w0, w1, w2};
+      const uint32_t *s32 = reinterpret_cast<const uint32_t *>(src) + 3 * qd;
+      const uint32_t wd[3] = {s32[0], s32[1], s32[2]};
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int c0 = (int)((wd[(3 * j) / 4] >> (8 * ((3 * j) % 4))) & 0xFF);
         const int c1 = (int)((wd[(3 * j + 1) / 4] >> (8 * ((3 * j + 1) % 4))) & 0xFF);
         const int c2 = (int)((wd[(3 * j + 2) / 4] >> (8 * ((3 * j + 2) % 4))) & 0xFF);
-        c[j] = bgr ? ycc_comp(k, c2, c1, c0) : ycc_comp(k, c0, c1, c2);
+        c[j] = ycc_apply(q, c0, c1, c2);
       }
     } else {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        int x = px + 4 * q + j;
+        int x = px + 4 * qd + j;
         x = x < w ? x : w - 1;
         const uint8_t *p = row + (size_t)x * 3;
-        c[j] = bgr ? ycc_comp(k, p[2], p[1], p[0]) : ycc_comp(k, p[0], p[1], p[2]);
+        c[j] = ycc_apply(q, p[0], p[1], p[2]);
       }
     }
 #pragma unroll
     for (int j = 0; j < 4 / H; ++j) {
-      const int o = q * (4 / H) + j;
+      const int o = qd * (4 / H) + j;
       int sum = 0;
 #pragma unroll
       for (int e = 0; e < H; ++e) sum += c[j * H + e];
@@ -1521,9 +1492,10 @@ __device__ __forceinline__ uint32_t qo_at(uint32_t slot, uint32_t zz) {
   return (((zz >> 3) ^ ((0x7250u >> (4 * (slot & 3))) & 7)) << 3) | (zz & 7);
 }
 
-// 8 lanes per block.  A workgroup takes M = 32 / bpm whole MCUs and orders its 32 block
-// slots block-in-MCU-major (slot s -> block-in-MCU s / M of MCU s % M), so a wave's 8 blocks
-// are mostly one component and the luma / chroma sampling paths do not diverge in a wave.
+// 8 lanes per block.  A wave codes block-in-MCU c of 8 consecutive MCUs (an MCU group); a
+// workgroup takes 4 (group, c) units in group-major order.  The component, its sampling, its
+// colour coefficients and its tables are therefore wave-uniform: they live in scalar
+// registers, no lane divides, and luma / chroma paths never diverge in a wave.
 // After quantisation the 8 lanes Huffman-code the block's AC coefficients (jchuff.c
 // encode_one_block, AC part): the quantised block sits in LDS in zigzag order, so lane r
 // reads zigzag positions 8r..8r+7 with one 16-B load.  Each lane finds the run before each of
@@ -1532,13 +1504,15 @@ __device__ __forceinline__ uint32_t qo_at(uint32_t slot, uint32_t zz) {
 // its offset from an 8-lane scan of the lanes' bit counts, and writes its bits through a
 // register accumulator into an LDS image of the block's AC stream that is then copied out.
 // Outputs per block: quantised DC, AC bit count, AC bits (MSB-first words).
+constexpr uint32_t kFdctGroup = 8;  // MCUs per wave
 __global__ __launch_bounds__(256) void k_fdct(const EncFrame *fr, const EncTables *tab, const uint8_t *pix,
                                               int16_t *dcq, uint32_t *acbits, uint32_t *acscr, int bgr,
                                               int fastdct) {
   const EncFrame &F = fr[blockIdx.y];
   const Geom &g = F.g;
-  const uint32_t M = 32 / (uint32_t)g.bpm;
-  if (blockIdx.x * M >= (uint32_t)g.nmcu) return;
+  const uint32_t bpm = (uint32_t)g.bpm, nmcu = (uint32_t)g.nmcu;
+  const uint32_t ngroups = (nmcu + kFdctGroup - 1) / kFdctGroup;
+  if (blockIdx.x * 4 >= ngroups * bpm) return;
   __shared__ int32_t ws[32][8][9];
   __shared__ int16_t qo[32][64];
   __shared__ uint32_t acw[32][kAcWords];
@@ -1553,14 +1527,21 @@ __global__ __launch_bounds__(256) void k_fdct(const EncFrame *fr, const EncTable
   }
   for (int i = threadIdx.x; i < 512; i += 256) s_ac[i >> 8][i & 255] = tab->ac[i >> 8][i & 255];
   for (int i = threadIdx.x; i < 32 * (int)kAcWords; i += 256) (&acw[0][0])[i] = 0;
-  const uint32_t slot = threadIdx.x >> 3, r = threadIdx.x & 7;
-  const uint32_t c = slot / M, mcu = blockIdx.x * M + slot % M;
-  const uint32_t b = mcu * (uint32_t)g.bpm + c;
+  const uint32_t slot = threadIdx.x >> 3, r = threadIdx.x & 7, lm = slot & (kFdctGroup - 1);
+  const uint32_t unit = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t grp = unit / bpm, c = unit - grp * bpm;  // scalar
+  const uint32_t mcu = grp * kFdctGroup + lm;
+  const uint32_t b = mcu * bpm + c;
   uint32_t k = 0, bx = 0, by = 0;
   bool real = false;
-  if (c < (uint32_t)g.bpm && mcu < (uint32_t)g.nmcu) {
-    block_pos(g, b, &k, &bx, &by);
-    real = bx < (uint32_t)g.wb[k] && by < (uint32_t)g.hb[k];  // dummy blocks are made by k_len / k_pack
+  if (grp < ngroups) {
+    k = (uint32_t)g.bcomp[c];
+    const uint32_t mcux = (uint32_t)g.mcux;
+    uint32_t mx = (grp * kFdctGroup) % mcux + lm, my = (grp * kFdctGroup) / mcux;
+    while (mx >= mcux) mx -= mcux, ++my;  // once at most unless the frame is under 8 MCUs wide
+    bx = mx * (uint32_t)g.mh[k] + (uint32_t)g.bxo[c];
+    by = my * (uint32_t)g.mv[k] + (uint32_t)g.byo[c];
+    real = mcu < nmcu && bx < (uint32_t)g.wb[k] && by < (uint32_t)g.hb[k];  // dummy blocks: k_len / k_pack
   }
   const uint8_t *img = pix + F.img_off;
   if (real) {  // pass 1: row r of the block's samples
@@ -1568,16 +1549,17 @@ __global__ __launch_bounds__(256) void k_fdct(const EncFrame *fr, const EncTable
     const int real_rows = ((g.h + g.maxv - 1) / g.maxv) * g.vs[k];
     const int sy = min((int)(by * 8 + r), real_rows - 1);
     int32_t v[8];
+    const Ycc q = ycc_coefs((int)k, bgr != 0);
     if (ve == 1 && he <= 2) {  // he == 1: full-resolution line; he == 2: h2v1_downsample
-      if (he == 1) line_acc<1>(img, g.w, g.h, (int)bx * 8, sy, bgr, (int)k, v, true);
-      else line_acc<2>(img, g.w, g.h, (int)bx * 16, sy, bgr, (int)k, v, true);
+      if (he == 1) line_acc<1>(img, g.w, g.h, (int)bx * 8, sy, q, v, true);
+      else line_acc<2>(img, g.w, g.h, (int)bx * 16, sy, q, v, true);
       if (he == 2) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = (v[j] + (j & 1)) >> 1;
       }
     } else if (he == 2 && ve == 2) {  // h2v2_downsample
-      line_acc<2>(img, g.w, g.h, (int)bx * 16, 2 * sy, bgr, (int)k, v, true);
-      line_acc<2>(img, g.w, g.h, (int)bx * 16, 2 * sy + 1, bgr, (int)k, v, false);
+      line_acc<2>(img, g.w, g.h, (int)bx * 16, 2 * sy, q, v, true);
+      line_acc<2>(img, g.w, g.h, (int)bx * 16, 2 * sy + 1, q, v, false);
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = (v[j] + 1 + (j & 1)) >> 2;
     } else {
@@ -1977,8 +1959,8 @@ hipError_t dec_color(const DecFrame *fr, int n, int max_w, int max_h, const uint
 hipError_t enc_fdct(const EncFrame *fr, int n, uint32_t max_blocks, const EncTables *tab, const uint8_t *pix,
                     int16_t *dcq, uint32_t *acbits, uint32_t *acscr, int bgr, int fastdct, hipStream_t s) {
   if (n <= 0 || !max_blocks) return hipSuccess;
-  // a workgroup takes bpm * (32 / bpm) >= 27 blocks (bpm <= 10)
-  hipLaunchKernelGGL(k_fdct, dim3((max_blocks + 26) / 27, (unsigned)n), dim3(256), 0, s, fr, tab, pix, dcq, acbits,
+  // a workgroup takes 4 units of 8 blocks; a frame has ceil(nmcu / 8) * bpm <= (nblocks + 70) / 8 units
+  hipLaunchKernelGGL(k_fdct, dim3((max_blocks + 70 + 31) / 32, (unsigned)n), dim3(256), 0, s, fr, tab, pix, dcq, acbits,
                      acscr, bgr, fastdct);
   return hipGetLastError();
 }
