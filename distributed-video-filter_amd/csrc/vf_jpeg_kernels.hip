@@ -1020,52 +1020,50 @@ __constant__ uint32_t kIdctCol[8] = {  // column c: nibble i = g(8i + c)
 // before either is transformed, and the column pass's output reuses the block's LDS row (one
 // more barrier, half the LDS: 18.4 KB per workgroup for 64 blocks).  Dequantisation happens
 // on pass 1's reads, as in jidctint.c (DEQUANTIZE(inptr[DCTSIZE*k], quantptr[DCTSIZE*k])).
+// A wave takes block-in-MCU c of 8 * kIdctNb consecutive MCUs (lane group j: MCUs j and
+// j + 8), a workgroup 4 such units: the component and its geometry are wave-uniform (scalar),
+// no lane divides, and the 8 lanes of a block read the same dequantisation entries.
+constexpr uint32_t kIdctGroup = 8 * kIdctNb;  // MCUs per wave
 __global__ __launch_bounds__(256) void k_idct(const DecFrame *fr, const int16_t *coef, const int32_t *dcseq,
                                               uint8_t *planes) {
   const DecFrame &F = fr[blockIdx.y];
   const Geom &g = F.g;
-  if (blockIdx.x * kIdctBlocks >= (uint32_t)g.nblocks) return;
+  const uint32_t bpm = (uint32_t)g.bpm, nmcu = (uint32_t)g.nmcu;
+  const uint32_t ngroups = (nmcu + kIdctGroup - 1) / kIdctGroup;
+  if (blockIdx.x * 4 >= ngroups * bpm) return;
   __shared__ int32_t blkv[kIdctBlocks][72];  // coefficients (kIdctPos), then the column pass's [8][9]
   __shared__ int32_t s_q[3][72];     // dequantisation, natural order; rows 8 mod 32 dwords apart
   __shared__ uint8_t s_pos[64];      // kIdctPos
   __shared__ uint32_t s_col[8];      // kIdctCol
-  __shared__ uint32_t s_geo[kMaxBpm];  // block-in-MCU -> component | x << 8 | y << 16 (blocks)
   const uint32_t t = threadIdx.x;
   if (t < 192) s_q[t >> 6][t & 63] = F.q[t >> 6][t & 63];
   if (t < 64) s_pos[t] = kIdctPos[t];
   if (t < 8) s_col[t] = kIdctCol[t];
-  if (t < (uint32_t)g.bpm)
-    s_geo[t] = (uint32_t)g.bcomp[t] | ((uint32_t)g.bxo[t] << 8) | ((uint32_t)g.byo[t] << 16);
   __syncthreads();
-  // per-component values, uniform: picked with selects, not per-lane global loads
-  const uint32_t mh[3] = {(uint32_t)g.mh[0], (uint32_t)g.mh[1], (uint32_t)g.mh[2]};
-  const uint32_t mv[3] = {(uint32_t)g.mv[0], (uint32_t)g.mv[1], (uint32_t)g.mv[2]};
-  const uint32_t cf[3] = {(uint32_t)g.cfirst[0], (uint32_t)g.cfirst[1], (uint32_t)g.cfirst[2]};
-  const uint64_t dcb[3] = {F.dcbase[0], F.dcbase[1], F.dcbase[2]};
-  const uint64_t po[3] = {F.plane_off[0], F.plane_off[1], F.plane_off[2]};
-  const uint32_t pw[3] = {(uint32_t)g.pw[0], (uint32_t)g.pw[1], (uint32_t)g.pw[2]};
-  const uint32_t slot = t >> 3, r = t & 7;
+  const uint32_t slot = t >> 3, r = t & 7, lm = slot & 7;
+  const uint32_t unit = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(t >> 6);
+  const uint32_t grp = unit / bpm, c = unit - grp * bpm;  // scalar
+  const bool live = grp < ngroups;
+  const uint32_t k = live ? (uint32_t)g.bcomp[c] : 0u;
+  const uint32_t mh = (uint32_t)g.mh[k], mv = (uint32_t)g.mv[k], mcux = (uint32_t)g.mcux;
+  const uint32_t mx0 = (grp * kIdctGroup) % mcux, my0 = (grp * kIdctGroup) / mcux;
   bool valid[kIdctNb];
-  uint32_t kk[kIdctNb], bxs[kIdctNb], bys[kIdctNb];
+  uint32_t bxs[kIdctNb], bys[kIdctNb];
   uint4 raw[kIdctNb];
   int32_t dc[kIdctNb];
 #pragma unroll
   for (int h = 0; h < kIdctNb; ++h) {
-    const uint32_t b = blockIdx.x * kIdctBlocks + h * 32 + slot;
-    valid[h] = b < (uint32_t)g.nblocks;
-    const uint32_t mcu = b / (uint32_t)g.bpm, c = b - mcu * (uint32_t)g.bpm;
-    const uint32_t ps = valid[h] ? s_geo[c] : 0u;
-    const uint32_t k = ps & 0xFF;
-    kk[h] = k;
-    bxs[h] = (mcu % (uint32_t)g.mcux) * HuffGeom::sel(mh, k) + ((ps >> 8) & 0xFF);
-    bys[h] = (mcu / (uint32_t)g.mcux) * HuffGeom::sel(mv, k) + (ps >> 16);
+    const uint32_t mcu = grp * kIdctGroup + h * 8 + lm;
+    valid[h] = live && mcu < nmcu;
+    uint32_t mx = mx0 + h * 8 + lm, my = my0;
+    while (mx >= mcux) mx -= mcux, ++my;  // once at most unless the frame is under 16 MCUs wide
+    bxs[h] = mx * mh + (uint32_t)g.bxo[c];
+    bys[h] = my * mv + (uint32_t)g.byo[c];
     raw[h] = make_uint4(0, 0, 0, 0);
     dc[h] = 0;
     if (valid[h]) {
-      raw[h] = *reinterpret_cast<const uint4 *>(coef + (F.blk0 + b) * 64 + r * 8);
-      if (r == 0)
-        dc[h] = dcseq[HuffGeom::sel(dcb, k) + (uint64_t)mcu * (HuffGeom::sel(mh, k) * HuffGeom::sel(mv, k)) +
-                      (c - HuffGeom::sel(cf, k))];
+      raw[h] = *reinterpret_cast<const uint4 *>(coef + (F.blk0 + (uint64_t)mcu * bpm + c) * 64 + r * 8);
+      if (r == 0) dc[h] = dcseq[F.dcbase[k] + (uint64_t)mcu * (mh * mv) + (c - (uint32_t)g.cfirst[k])];
     }
   }
   const uint2 pos8 = *reinterpret_cast<const uint2 *>(&s_pos[r * 8]);  // this lane's 8 store dwords
@@ -1089,7 +1087,7 @@ __global__ __launch_bounds__(256) void k_idct(const DecFrame *fr, const int16_t 
     int32_t in[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i)
-      in[i] = blkv[h * 32 + slot][i * 8 + ((colg >> (4 * i)) & 7)] * s_q[kk[h]][i * 8 + r];
+      in[i] = blkv[h * 32 + slot][i * 8 + ((colg >> (4 * i)) & 7)] * s_q[k][i * 8 + r];
     idct_line(in, col[h], 11);
   }
   __syncthreads();
@@ -1113,8 +1111,7 @@ __global__ __launch_bounds__(256) void k_idct(const DecFrame *fr, const int16_t 
       lo |= idct_limit(out[i]) << (8 * i);
       hi |= idct_limit(out[i + 4]) << (8 * i);
     }
-    const uint32_t k = kk[h];
-    uint8_t *p = planes + HuffGeom::sel(po, k) + (uint64_t)(bys[h] * 8 + r) * HuffGeom::sel(pw, k) + bxs[h] * 8;
+    uint8_t *p = planes + F.plane_off[k] + (uint64_t)(bys[h] * 8 + r) * (uint32_t)g.pw[k] + bxs[h] * 8;
     *reinterpret_cast<uint2 *>(p) = make_uint2(lo, hi);
   }
 }
@@ -1943,7 +1940,8 @@ hipError_t dec_write(const DecFrame *fr, int n, uint32_t max_sub, const uint8_t 
 hipError_t dec_idct(const DecFrame *fr, int n, uint32_t max_blocks, const int16_t *coef, const int32_t *dcseq,
                     uint8_t *planes, hipStream_t s) {
   if (n <= 0 || !max_blocks) return hipSuccess;
-  hipLaunchKernelGGL(k_idct, dim3((max_blocks + kIdctBlocks - 1) / kIdctBlocks, (unsigned)n), dim3(256), 0, s, fr,
+  // 4 units of 16 blocks per workgroup; a frame has ceil(nmcu / 16) * bpm <= (nblocks + 150) / 16 units
+  hipLaunchKernelGGL(k_idct, dim3((max_blocks + 150 + 63) / 64, (unsigned)n), dim3(256), 0, s, fr,
                      coef, dcseq, planes);
   return hipGetLastError();
 }
