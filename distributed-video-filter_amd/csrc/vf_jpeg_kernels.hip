@@ -1444,33 +1444,51 @@ __device__ __forceinline__ uint64_t acs_idx(uint64_t gb, uint32_t i) {
   return (gb >> 6) * (64ull * kAcWords) + (uint64_t)i * 64 + (gb & 63);
 }
 
-// MSB-first bits of one lane into an LDS word image, from bit `pos` on.  Words the lane
-// shares with its neighbours (its first and its last) are OR-ed; the words in between are
-// the lane's alone and are stored.  The image is zeroed beforehand.
+// MSB-first bits of one lane into an LDS word image, from bit `pos` on.  The image is zeroed
+// beforehand and every word is OR-ed, so a lane's first and last words, shared with its
+// neighbours, need no special case.  put() has no branch: it always ORs the word the bits
+// reached -- when that word is complete, its 32 bits; otherwise the prefix of it known so far,
+// which the complete word contains (OR is idempotent on it).  acc keeps the pending n < 32
+// bits in its low end; bits above them are stale and never read (alignbit takes 32 bits).
 struct LdsBits {
   uint32_t *w;
   uint32_t wi, n;
   uint64_t acc;
-  bool first;
-  __device__ __forceinline__ LdsBits(uint32_t *words, uint32_t pos)
-      : w(words), wi(pos >> 5), n(pos & 31), acc(0), first(true) {}
+  __device__ __forceinline__ LdsBits(uint32_t *words, uint32_t pos) : w(words), wi(pos >> 5), n(pos & 31), acc(0) {}
   __device__ __forceinline__ void put(uint32_t bits, uint32_t size) {  // size <= 32
     acc = (acc << size) | bits;
     n += size;
-    if (n >= 32) {
-      n -= 32;
-      const uint32_t v = (uint32_t)(acc >> n);
-      if (first) atomicOr(w + wi, v);
-      else w[wi] = v;
-      first = false;
-      ++wi;
-      acc &= n ? ((1ull << n) - 1) : 0ull;
-    }
+    const bool full = n >= 32;
+    const uint32_t lo = (uint32_t)acc, hi = (uint32_t)(acc >> 32);
+    atomicOr(w + wi, __builtin_amdgcn_alignbit(full ? hi : lo, full ? lo : 0u, n & 31));
+    wi += full ? 1u : 0u;
+    n &= 31;
   }
-  __device__ __forceinline__ void finish() {
-    if (n) atomicOr(w + wi, (uint32_t)(acc << (32 - n)));
+  __device__ __forceinline__ void finish() {  // the pending bits of a word put() completed last
+    atomicOr(w + wi, __builtin_amdgcn_alignbit((uint32_t)acc, 0u, n));
   }
 };
+
+// Lane-group (8 lanes) primitives by DPP / swizzle instead of ds_bpermute: OR over the group,
+// inclusive prefix sum, and the group's lane 7.
+__device__ __forceinline__ uint32_t or8(uint32_t x) {
+  x |= (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+  x |= (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+  x |= (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x141, 0xF, 0xF, false);  // row_half_mirror
+  return x;
+}
+__device__ __forceinline__ uint32_t scan8(uint32_t x, uint32_t r) {  // r = lane & 7
+  uint32_t y = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x111, 0xF, 0xF, false);  // row_shr:1
+  x += r >= 1 ? y : 0u;
+  y = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x112, 0xF, 0xF, false);  // row_shr:2
+  x += r >= 2 ? y : 0u;
+  y = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x114, 0xF, 0xF, false);  // row_shr:4
+  x += r >= 4 ? y : 0u;
+  return x;
+}
+__device__ __forceinline__ uint32_t last8(uint32_t x) {  // swizzle: lane (i & 0x18) | 7
+  return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0xF8);
+}
 
 // natural (row-major) index -> zigzag position (inverse of jutils.c jpeg_natural_order)
 __constant__ uint8_t kZig[64] = {0,  1,  5,  6,  14, 15, 27, 28, 2,  4,  7,  13, 16, 26, 29, 42,
@@ -1598,10 +1616,7 @@ __global__ __launch_bounds__(256) void k_fdct(const EncFrame *fr, const EncTable
 #pragma unroll
   for (int j = 0; j < 8; ++j)
     if (vz[j] != 0 && (r | j) != 0) m8 |= 1u << j;
-  uint64_t mask = (uint64_t)m8 << (8 * r);
-  mask |= __shfl_xor(mask, 1, 8);
-  mask |= __shfl_xor(mask, 2, 8);
-  mask |= __shfl_xor(mask, 4, 8);
+  const uint64_t mask = ((uint64_t)or8(r < 4 ? 0u : m8 << (8 * (r - 4))) << 32) | or8(r < 4 ? m8 << (8 * r) : 0u);
   const uint32_t zrl = s_ac[t][0xF0], eobc = s_ac[t][0x00];
   const uint32_t zlen = zrl & 0xFF;
   const bool eob = mask == 0 || (63 - __clzll(mask)) < 63;
@@ -1620,28 +1635,24 @@ __global__ __launch_bounds__(256) void k_fdct(const EncFrame *fr, const EncTable
     // zero coefficients all read entry 0 (one broadcast address): with their own (run, 0)
     // entries they land on 2 banks, up to 8 distinct addresses each
     const uint32_t e = s_ac[t][nz ? ((run & 15) << 4) + (nb & 15) : 0u];
-    code[j] = ((e >> 8) << nb) | ((uint32_t)(v < 0 ? v - 1 : v) & ((1u << nb) - 1));
+    code[j] = nz ? ((e >> 8) << nb) | ((uint32_t)(v < 0 ? v - 1 : v) & ((1u << nb) - 1)) : 0u;  // put() ORs it
     clen[j] = nz ? (e & 0xFF) + nb : 0u;
     nzr[j] = nz ? (uint32_t)(run >> 4) : 0u;
-    nbits += nzr[j] * zlen + clen[j];
+    nbits += __umul24(nzr[j], zlen) + clen[j];
     prev = nz ? kk : prev;
   }
   if (r == 7 && eob) nbits += eobc & 0xFF;
-  uint32_t incl = nbits;
-#pragma unroll
-  for (int off = 1; off < 8; off <<= 1) {
-    const uint32_t y = __shfl_up(incl, off, 8);
-    if ((int)r >= off) incl += y;
-  }
-  const uint32_t total = __shfl(incl, 7, 8);
+  const uint32_t incl = scan8(nbits, r);
+  const uint32_t total = last8(incl);
   if (real && nbits) {
     LdsBits out(acw[slot], incl - nbits);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       for (uint32_t z = nzr[j]; z; --z) out.put(zrl >> 8, zlen);
-      if (clen[j]) out.put(code[j], clen[j]);
+      out.put(code[j], clen[j]);  // clen 0 for a zero coefficient: an idempotent OR
     }
-    if (r == 7 && eob) out.put(eobc >> 8, eobc & 0xFF);
+    const bool e = r == 7 && eob;
+    out.put(e ? eobc >> 8 : 0u, e ? eobc & 0xFF : 0u);
     out.finish();
   }
   __syncthreads();
