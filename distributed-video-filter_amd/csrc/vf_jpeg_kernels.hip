@@ -1391,47 +1391,47 @@ __device__ __forceinline__ int ycc_apply(const Ycc &q, int c0, int c1, int c2) {
   return (q.a0 * c0 + q.a1 * c1 + q.a2 * c2 + q.bias) >> 16;
 }
 
-// One component of the 8 * H pixels of row py from px, summed in groups of H into v[0..7]
-// (assigned when `first`, else added: a second row of h2v2).  Edges replicated
-// (jccolor.c on expand_right_edge / expand_bottom_edge input).  4 pixels (3 dwords) at a
-// time, so at most 12 channel values are live instead of 3 * 8 * H.
-template <int H>
-__device__ __forceinline__ void line_acc(const uint8_t *img, int w, int h, int px, int py, const Ycc &q,
-                                         int32_t v[8], bool first) {
-  py = py < h ? py : h - 1;
-  const uint8_t *row = img + (size_t)py * w * 3;
-  const uint8_t *src = row + (size_t)px * 3;
-  const bool fast = px + 8 * H <= w && ((uintptr_t)src & 3) == 0;
+// One component of the 8 * H pixels of rows py .. py + R - 1 from px, summed over groups of H
+// pixels and over the R rows into v[0..7] (R = 2: h2v2).  Edges replicated (jccolor.c on
+// expand_right_edge / expand_bottom_edge input).  Inside the image every row's words are
+// loaded before any is converted, so a lane waits for memory once, not once per 4 pixels.
+template <int H, int R>
+__device__ __forceinline__ void rows_acc(const uint8_t *img, int w, int h, int px, int py, const Ycc &q,
+                                         int32_t v[8]) {
+  const uint8_t *row[R];
+  bool fast = px + 8 * H <= w;
 #pragma unroll
-  for (int qd = 0; qd < 2 * H; ++qd) {
-    int c[4];
-    if (fast) {
-      const uint32_t *s32 = reinterpret_cast<const uint32_t *>(src) + 3 * qd;
-      const uint32_t wd[3] = {s32[0], s32[1], s32[2]};
+  for (int y = 0; y < R; ++y) {
+    row[y] = img + (size_t)min(py + y, h - 1) * w * 3;
+    fast = fast && ((reinterpret_cast<uintptr_t>(row[y]) + (uintptr_t)px * 3) & 3) == 0;
+  }
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int c0 = (int)((wd[(3 * j) / 4] >> (8 * ((3 * j) % 4))) & 0xFF);
-        const int c1 = (int)((wd[(3 * j + 1) / 4] >> (8 * ((3 * j + 1) % 4))) & 0xFF);
-        const int c2 = (int)((wd[(3 * j + 2) / 4] >> (8 * ((3 * j + 2) % 4))) & 0xFF);
-        c[j] = ycc_apply(q, c0, c1, c2);
-      }
-    } else {
+  for (int j = 0; j < 8; ++j) v[j] = 0;
+  if (fast) {
+    uint32_t wd[R][6 * H];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        int x = px + 4 * qd + j;
-        x = x < w ? x : w - 1;
-        const uint8_t *p = row + (size_t)x * 3;
-        c[j] = ycc_apply(q, p[0], p[1], p[2]);
-      }
+    for (int y = 0; y < R; ++y) {
+      const uint32_t *s32 = reinterpret_cast<const uint32_t *>(row[y] + (size_t)px * 3);
+#pragma unroll
+      for (int i = 0; i < 6 * H; ++i) wd[y][i] = s32[i];
     }
 #pragma unroll
-    for (int j = 0; j < 4 / H; ++j) {
-      const int o = qd * (4 / H) + j;
-      int sum = 0;
+    for (int y = 0; y < R; ++y)
 #pragma unroll
-      for (int e = 0; e < H; ++e) sum += c[j * H + e];
-      v[o] = first ? sum : v[o] + sum;
-    }
+      for (int x = 0; x < 8 * H; ++x) {
+        const int c0 = (int)((wd[y][(3 * x) / 4] >> (8 * ((3 * x) % 4))) & 0xFF);
+        const int c1 = (int)((wd[y][(3 * x + 1) / 4] >> (8 * ((3 * x + 1) % 4))) & 0xFF);
+        const int c2 = (int)((wd[y][(3 * x + 2) / 4] >> (8 * ((3 * x + 2) % 4))) & 0xFF);
+        v[x / H] += ycc_apply(q, c0, c1, c2);
+      }
+  } else {
+#pragma unroll
+    for (int y = 0; y < R; ++y)
+#pragma unroll
+      for (int x = 0; x < 8 * H; ++x) {
+        const uint8_t *p = row[y] + (size_t)min(px + x, w - 1) * 3;
+        v[x / H] += ycc_apply(q, p[0], p[1], p[2]);
+      }
   }
 }
 
@@ -1566,15 +1566,14 @@ __global__ __launch_bounds__(256) void k_fdct(const EncFrame *fr, const EncTable
     int32_t v[8];
     const Ycc q = ycc_coefs((int)k, bgr != 0);
     if (ve == 1 && he <= 2) {  // he == 1: full-resolution line; he == 2: h2v1_downsample
-      if (he == 1) line_acc<1>(img, g.w, g.h, (int)bx * 8, sy, q, v, true);
-      else line_acc<2>(img, g.w, g.h, (int)bx * 16, sy, q, v, true);
+      if (he == 1) rows_acc<1, 1>(img, g.w, g.h, (int)bx * 8, sy, q, v);
+      else rows_acc<2, 1>(img, g.w, g.h, (int)bx * 16, sy, q, v);
       if (he == 2) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = (v[j] + (j & 1)) >> 1;
       }
     } else if (he == 2 && ve == 2) {  // h2v2_downsample
-      line_acc<2>(img, g.w, g.h, (int)bx * 16, 2 * sy, q, v, true);
-      line_acc<2>(img, g.w, g.h, (int)bx * 16, 2 * sy + 1, q, v, false);
+      rows_acc<2, 2>(img, g.w, g.h, (int)bx * 16, 2 * sy, q, v);
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = (v[j] + 1 + (j & 1)) >> 2;
     } else {
