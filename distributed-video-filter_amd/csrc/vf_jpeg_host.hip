@@ -488,6 +488,13 @@ bool make_geom(int w, int h, int ncomp, const int *hs, const int *vs, Geom *g) {
     }
     g->bpm = b;
   }
+  for (int k = 0; k < ncomp; ++k) {  // per-component quotients the kernels would otherwise divide for
+    g->he[k] = (int8_t)(maxh / g->hs[k]);
+    g->ve[k] = (int8_t)(maxv / g->vs[k]);
+    g->dw[k] = ceil_div(w * g->hs[k], maxh);
+    g->dh[k] = ceil_div(h * g->vs[k], maxv);
+    g->rrows[k] = ceil_div(h, maxv) * g->vs[k];
+  }
   const long long nm = (long long)g->mcux * g->mcuy;
   if (nm * g->bpm > (1ll << 30)) return false;
   g->nmcu = (int32_t)nm;

@@ -1153,8 +1153,7 @@ __device__ __forceinline__ void color8(const DecFrame &F, const Geom &g, const u
     if (k >= g.ncomp) break;
     const uint8_t *p = planes + F.plane_off[k];
     const int pw = g.pw[k];
-    const int he = g.maxh / g.hs[k], ve = g.maxv / g.vs[k];
-    const int dw = (g.w * g.hs[k] + g.maxh - 1) / g.maxh, dh = (g.h * g.vs[k] + g.maxv - 1) / g.maxv;
+    const int he = g.he[k], ve = g.ve[k], dw = g.dw[k], dh = g.dh[k];
     const bool fancy = (F.flags & 1) && ((he == 2 && dw > 2) || (he == 1 && ve == 2));
     if (he == 1 && ve == 1) {
       const uint2 q = *reinterpret_cast<const uint2 *>(p + (size_t)y * pw + x0);
@@ -1275,8 +1274,7 @@ __device__ __forceinline__ int comp_at(const uint8_t *img, int w, int h, int px,
 // sample (sx, sy) of component k's downsampled plane (jcsample.c + jcprepct.c edges)
 __device__ __forceinline__ int enc_sample(const Geom &g, const uint8_t *img, int k, int sx, int sy, int ro,
                                           int bo) {
-  const int he = g.maxh / g.hs[k], ve = g.maxv / g.vs[k];
-  const int real_rows = ((g.h + g.maxv - 1) / g.maxv) * g.vs[k];
+  const int he = g.he[k], ve = g.ve[k], real_rows = g.rrows[k];
   if (sy > real_rows - 1) sy = real_rows - 1;
   if (he == 1 && ve == 1) return comp_at(img, g.w, g.h, sx, sy, k, ro, bo);
   if (he == 2 && ve == 1)
@@ -1560,8 +1558,7 @@ __global__ __launch_bounds__(256) void k_fdct(const EncFrame *fr, const EncTable
   }
   const uint8_t *img = pix + F.img_off;
   if (real) {  // pass 1: row r of the block's samples
-    const int he = g.maxh / g.hs[k], ve = g.maxv / g.vs[k];
-    const int real_rows = ((g.h + g.maxv - 1) / g.maxv) * g.vs[k];
+    const int he = g.he[k], ve = g.ve[k], real_rows = g.rrows[k];
     const int sy = min((int)(by * 8 + r), real_rows - 1);
     int32_t v[8];
     const Ycc q = ycc_coefs((int)k, bgr != 0);
