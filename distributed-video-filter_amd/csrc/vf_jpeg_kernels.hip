@@ -543,6 +543,7 @@ __global__ __launch_bounds__(256) void k_sync(const DecFrame *fr, const uint8_t 
 // Only a frame too long for k_resolve's tables, or a stream that never rejoins (corrupt
 // data), is reported unresolved; the caller then runs k_sync.
 
+__device__ __forceinline__ uint32_t nib(uint64_t row, uint32_t i) { return (uint32_t)(row >> (4 * i)) & 0xF; }
 __device__ __forceinline__ uint32_t spec_lanes(uint32_t bpm) {
   return bpm <= 1 ? 1u : bpm <= 2 ? 2u : bpm <= 4 ? 4u : bpm <= 8 ? 8u : 16u;
 }
@@ -665,16 +666,84 @@ __global__ __launch_bounds__(256) void k_spec(const DecFrame *fr, const uint8_t 
   s_X[t] = X;
   __syncthreads();
   if (VF_SYNC_STATS && t == 0) atomicAdd(B.stats + 9, (uint32_t)((clock64() - c_start) >> 10));
-  // C: one lane per entry index e walks the workgroup; walkers sit 256 / L lanes apart so
-  // their (divergent) explicit decodes run in different waves where possible
+  // C: the walks.  Walk e is trajectory e of the first subsequence followed through the links:
+  // j_k = f_k(j_{k-1}), f_k(j) = s_M[k * L + j].  While every step is a link (no explicit
+  // state), j_k = (f_k o ... o f_1)(e), and map composition is associative, so one lane per
+  // subsequence gets every walk's trajectory there from a prefix scan of the link maps (maps
+  // of <= 16 entries packed as nibbles; kLinkNone and kLinkLast are absorbing).  A walk that
+  // reaches an explicit state (a link that rejoined nothing, rare) continues serially from
+  // there, decoding as before.
+  const uint32_t nk = blockIdx.x * NS < nsub ? min(NS, nsub - blockIdx.x * NS) : 0u;  // subsequences here
+  if (nk == 0) return;  // workgroup-uniform
+  const uint32_t bpm = hg.bpm;
+  auto compose = [bpm](uint64_t later, uint64_t earlier) {  // (later o earlier)(e)
+    uint64_t r = 0;
+    for (uint32_t q = 0; q < bpm; ++q) {
+      const uint32_t a = nib(earlier, q);
+      r |= (uint64_t)(a < bpm ? nib(later, a) : a) << (4 * q);
+    }
+    return r;
+  };
+  uint64_t ident = 0;
+  for (uint32_t q = 0; q < bpm; ++q) ident |= (uint64_t)q << (4 * q);
+  uint64_t f = ident;
+  if (t > 0 && t < nk) {
+    f = 0;
+    for (uint32_t q = 0; q < bpm; ++q) f |= (uint64_t)(s_M[t * L + q] & 0xF) << (4 * q);
+  }
+  const uint32_t lane = t & 63, wv = t >> 6;
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint64_t o = __shfl_up(f, d, 64);
+    if (lane >= d) f = compose(f, o);
+  }
+  __shared__ uint64_t s_wt[4];
+  __shared__ uint64_t s_fst[kSpecLanesMax];
+  __shared__ uint32_t s_first[kSpecLanesMax];
+  if (lane == 63) s_wt[wv] = f;
+  if (t < kSpecLanesMax) s_first[t] = 0;
+  __syncthreads();
+  uint64_t pre = ident;  // the maps of the waves before this one
+  for (uint32_t q = 0; q < wv; ++q) pre = compose(s_wt[q], pre);
+  f = compose(f, pre);
+  uint64_t gp = __shfl_up(f, 1, 64);  // G_{t-1}
+  if (lane == 0) gp = pre;
+  if (t < nk) {
+    if (t == 0) {
+      for (uint32_t q = 0; q < bpm; ++q) {
+        B.tG[g0 + q] = (uint8_t)q;
+        B.tX[g0 + q] = s_E[q];
+        B.tXc[g0 + q] = s_C[q];  // trajectory count (used for the frame's first subsequence)
+      }
+    } else {
+      for (uint32_t q = 0; q < bpm; ++q) {
+        const uint32_t p = nib(gp, q);
+        if (p >= bpm) continue;  // stopped (last) or explicit (the serial walk below)
+        const uint32_t M2 = s_M[t * L + p];
+        const uint64_t st = M2 < bpm ? s_E[t * L + M2] : s_X[t * L + p];
+        B.tG[g0 + t * L + q] = (uint8_t)M2;
+        B.tX[g0 + t * L + q] = st;
+        B.tXc[g0 + t * L + q] = s_C[t * L + p];
+        if (M2 == kLinkNone) {  // walk q turns explicit here: its serial continuation starts at t + 1
+          s_first[q] = t;
+          s_fst[q] = st;
+        }
+      }
+    }
+    if (t == nk - 1)
+      for (uint32_t q = 0; q < bpm; ++q) {
+        const uint32_t j = nib(f, q);
+        if (j != kLinkNone) B.wF[(uint64_t)(F.wg0 + blockIdx.x) * kSpecLanesMax + q] = (uint8_t)(j < bpm ? j : kLinkNone);
+      }
+  }
+  __syncthreads();
+  // serial continuations, walkers 256 / L lanes apart so their divergent decodes run in
+  // different waves where possible
   const uint32_t wsp = 256 / L, e = t / wsp;
-  if (t % wsp == 0 && e < hg.bpm && blockIdx.x * NS < nsub) {
-    uint32_t j = e;  // current trajectory, or kLinkNone while explicit
-    uint64_t st = s_E[e];
-    B.tG[g0 + e] = (uint8_t)e;
-    B.tX[g0 + e] = st;
-    B.tXc[g0 + e] = s_C[e];  // trajectory count (used for the frame's first subsequence)
-    for (uint32_t k = 1; k < NS && blockIdx.x * NS + k < nsub; ++k) {
+  if (t % wsp == 0 && e < bpm && s_first[e] != 0) {
+    uint32_t j = kLinkNone;  // current trajectory, or kLinkNone while explicit
+    uint64_t st = s_fst[e];
+    for (uint32_t k = s_first[e] + 1; k < nk; ++k) {
       const uint32_t sk = blockIdx.x * NS + k;
       uint32_t cnt, M2;
       uint64_t xe = 0;
@@ -744,7 +813,6 @@ __global__ __launch_bounds__(256) void k_wglink(const DecFrame *fr, const uint8_
 // state, lane 0 decodes on until its exit state equals some column's exit (tX) there.
 constexpr uint32_t kResolveLds = 4096;  // workgroups per frame resolved here (else fallback)
 constexpr uint32_t kTraceWords = kSubBits / 32 + 6;  // one subsequence + overshoot + lookahead
-__device__ __forceinline__ uint32_t nib(uint64_t row, uint32_t i) { return (uint32_t)(row >> (4 * i)) & 0xF; }
 
 __global__ __launch_bounds__(256) void k_resolve(const DecFrame *fr, const uint8_t *us, const uint32_t *us_len,
                                                  SpecBufs B, uint32_t *unresolved) {
