@@ -82,6 +82,20 @@ struct DecFrame {
   uint16_t q[3][64];       // dequantisation per component, natural order
   HuffDec dc[3], ac[3];    // per component (kept adjacent: loaded into LDS as one block)
   HuffSync sdc[3], sac[3];  // the same, for the synchronisation decoders (adjacent too)
+  uint32_t flags;          // bit 0: fancy upsampling allowed
+  uint64_t blk0;           // first block in the batch coefficient buffer
+  uint64_t dcbase[3];      // per-component DC sequences in the DC buffer
+  uint64_t plane_off[3];   // component planes in the plane buffer
+  uint64_t out_off;        // interleaved pixels in the pixel buffer
+};
+
+// One entropy-coded segment, the unit of the unstuff / sync / write stages: a frame's whole
+// scan, or one restart interval of it.  With DRI every interval starts byte-aligned after an
+// RSTn marker with the DC predictions reset (T.81 F.1.2.3, jdhuff.c process_restart), so the
+// intervals decode as independent segments whose blocks and DC sequences tile the frame's.
+struct DecSeg {
+  uint32_t frame;          // its frame in the DecFrame array (tables, geometry)
+  uint32_t nblocks;        // blocks coded in the segment (whole MCUs)
   uint64_t in_off;         // raw entropy-coded bytes in the batch input buffer (16-aligned)
   uint32_t in_len;
   uint32_t ntiles;         // kTile tiles over the raw bytes
@@ -89,13 +103,10 @@ struct DecFrame {
   uint32_t sub0;           // first subsequence slot
   uint32_t nsub_max;       // subsequence slots (ceil(in_len * 8 / kSubBits))
   uint32_t wg0, nwg;       // speculative sync: first workgroup slot, workgroups (spec_lanes)
-  uint64_t tr0;            // speculative sync: first trajectory slot (nwg * 256 per frame)
-  uint32_t flags;          // bit 0: fancy upsampling allowed
+  uint64_t tr0;            // speculative sync: first trajectory slot (nwg * 256 per segment)
   uint64_t us_off;         // unstuffed stream in the unstuffed buffer (16-aligned)
-  uint64_t blk0;           // first block in the batch coefficient buffer
-  uint64_t dcbase[3];      // per-component DC sequences in the DC buffer
-  uint64_t plane_off[3];   // component planes in the plane buffer
-  uint64_t out_off;        // interleaved pixels in the pixel buffer
+  uint64_t blk0;           // its first block in the batch coefficient buffer
+  uint64_t dcbase[3];      // its first entries of the frame's per-component DC sequences
 };
 
 struct EncFrame {
@@ -125,11 +136,11 @@ hipError_t scan_u32(const ScanSeg *segs, int nseg, uint32_t max_tiles, const uin
 hipError_t scan_i32(const ScanSeg *segs, int nseg, uint32_t max_tiles, const int32_t *in, int32_t *out,
                     int32_t *tsum, int32_t *totals, bool inclusive, hipStream_t s);
 
-hipError_t dec_unstuff_count(const DecFrame *fr, int n, uint32_t max_tiles, const uint8_t *in,
+hipError_t dec_unstuff_count(const DecSeg *sg, int nseg, uint32_t max_tiles, const uint8_t *in,
                              uint32_t *tile_cnt, hipStream_t s);
-hipError_t dec_unstuff_write(const DecFrame *fr, int n, uint32_t max_tiles, const uint8_t *in,
+hipError_t dec_unstuff_write(const DecSeg *sg, int nseg, uint32_t max_tiles, const uint8_t *in,
                              const uint32_t *tile_off, const uint32_t *us_len, uint8_t *us, hipStream_t s);
-hipError_t dec_sync(const DecFrame *fr, int n, uint32_t max_sub, const uint8_t *us, const uint32_t *us_len,
+hipError_t dec_sync(const DecSeg *sg, const DecFrame *fr, int nseg, uint32_t max_sub, const uint8_t *us, const uint32_t *us_len,
                     const uint64_t *exit_in, uint64_t *exit_out, const uint32_t *cnt_in, uint32_t *cnt_out,
                     uint64_t *used, uint64_t *ck, uint32_t *ckrem, uint32_t *changed, int pass, hipStream_t s);
 // Speculative sync (one pass, no host round trip): k_spec decodes every subsequence from
@@ -158,10 +169,10 @@ struct SpecBufs {
 };
 constexpr int kSpecLanesMax = 16;
 inline uint32_t spec_lanes_host(int bpm) { return bpm <= 1 ? 1u : bpm <= 2 ? 2u : bpm <= 4 ? 4u : bpm <= 8 ? 8u : 16u; }
-hipError_t dec_sync_spec(const DecFrame *fr, int n, uint32_t max_wg, const uint8_t *us, const uint32_t *us_len,
+hipError_t dec_sync_spec(const DecSeg *sg, const DecFrame *fr, int nseg, uint32_t max_wg, const uint8_t *us, const uint32_t *us_len,
                          const SpecBufs &b, uint64_t *exit_out, uint32_t *cnt_out, uint32_t *unresolved,
                          hipStream_t s);
-hipError_t dec_write(const DecFrame *fr, int n, uint32_t max_sub, const uint8_t *us, const uint32_t *us_len,
+hipError_t dec_write(const DecSeg *sg, const DecFrame *fr, int nseg, uint32_t max_sub, const uint8_t *us, const uint32_t *us_len,
                      const uint64_t *exits, const uint32_t *bstart, int16_t *coef, int32_t *dcseq,
                      hipStream_t s);
 hipError_t dec_idct(const DecFrame *fr, int n, uint32_t max_blocks, const int16_t *coef, const int32_t *dcseq,

@@ -148,17 +148,19 @@ class Codec {
 
   // decode layout
   std::vector<DecFrame> dfr_;
-  int dn_ = 0, ndcseg_ = 0;
+  std::vector<DecSeg> dsg_;    // entropy-coded segments: one per frame, or one per restart interval
+  std::vector<const uint8_t *> seg_src_;  // each segment's raw bytes in the caller's JPEG
+  int dn_ = 0, dnseg_ = 0, ndcseg_ = 0;
   uint32_t dmax_tiles_ = 0, dmax_sub_ = 0, dmax_blocks_ = 0, dc_max_tiles_ = 0;
   int dmax_w_ = 0, dmax_h_ = 0;
   uint64_t dblocks_ = 0, dpix_bytes_ = 0;
-  uint32_t dmax_wg_ = 0;       // speculative sync: workgroups of the largest frame
+  uint32_t dmax_wg_ = 0;       // speculative sync: workgroups of the largest segment
   bool spec_ok_ = true;        // every frame fits the speculative resolver
   uint64_t spec_calls_ = 0, spec_fallbacks_ = 0;
   DevBuf d_tE_, d_tG_, d_tX_, d_tXc_, d_pX_, d_pC_, d_wF_, d_wck_, d_wrem_, d_wB_, d_wBC_, d_wBX_, d_rE_, d_rK_,
       d_unres_;
   int sync_passes_ = 0;
-  DevBuf d_in_, d_dfr_, d_segs_, d_tile_, d_tsum_, d_totals_, d_us_, d_exit_[2], d_cnt_[2], d_used_, d_ck_, d_ckrem_, d_bstart_,
+  DevBuf d_in_, d_dfr_, d_dsg_, d_segs_, d_tile_, d_tsum_, d_totals_, d_us_, d_exit_[2], d_cnt_[2], d_used_, d_ck_, d_ckrem_, d_bstart_,
       d_changed_, d_coef_, d_dcseq_, d_planes_, d_pix_;
 
   // encode layout
@@ -170,7 +172,7 @@ class Codec {
       d_out_, d_outsize_, d_pack_;
 
   HostBuf h_stage_, h_out_, h_flag_;  // h_flag_: the speculative sync's unresolved flag
-  HostBuf h_ddesc_, h_edesc_, h_meta_;  // pinned descriptor uploads; block totals + output sizes
+  HostBuf h_ddesc_, h_edesc_, h_meta_, h_dtot_;  // pinned descriptor uploads; output sizes; block totals
   uint64_t guess_ = 0, out_total_ = 0, fetch_refills_ = 0;
   bool waited_ = false;
   std::vector<uint64_t> out_sizes_, out_offs_;

@@ -214,6 +214,9 @@ struct Parsed {
   uint8_t dcvals[4][256] = {}, acvals[4][256] = {};
   int qdef = 0, dcdef = 0, acdef = 0;
   size_t scan_off = 0, scan_end = 0;
+  // with DRI: each RSTn marker in the scan as (end of the interval's data before it, marker
+  // number); the next interval starts 2 bytes after the data end plus any fill bytes
+  std::vector<std::pair<size_t, size_t>> rst;  // (data end, position of the marker's 0xFF)
 };
 
 // jdmarker.c restated for baseline / extended sequential Huffman, one interleaved scan
@@ -298,6 +301,7 @@ int parse(const uint8_t *b, size_t n, Parsed *P, std::string *err, bool find_sca
       P->scan_off = p + len;
       size_t q = P->scan_off;
       if (!find_scan_end) q = n;
+      P->rst.clear();
       while (q + 1 < n) {
         const void *f = std::memchr(b + q, 0xFF, n - q);
         if (!f) {
@@ -308,6 +312,12 @@ int parse(const uint8_t *b, size_t n, Parsed *P, std::string *err, bool find_sca
         if (q + 1 >= n) break;
         const uint8_t nx = b[q + 1];
         if (nx != 0x00 && !(nx >= 0xD0 && nx <= 0xD7) && nx != 0xFF) break;
+        if (nx >= 0xD0 && nx <= 0xD7) {  // RSTn: fill bytes (0xFF runs) before it are not data
+          size_t e = q;
+          const size_t lo = P->rst.empty() ? P->scan_off : P->rst.back().second + 2;
+          while (e > lo && b[e - 1] == 0xFF) --e;
+          P->rst.emplace_back(e, q);
+        }
         ++q;
       }
       P->scan_end = q + 1 < n ? q : n;
@@ -629,6 +639,7 @@ int Codec::prepare_decode(const uint8_t *const *jpegs, const size_t *sizes, int 
     return kInvalid;
   }
   dfr_.assign((size_t)n, DecFrame());
+  seg_src_.clear();
   std::vector<Parsed> parsed((size_t)n);
   uint64_t in_off = 0, us_off = 0, blk = 0, dcoff = 0, plane = 0, pix = 0;
   uint32_t tiles = 0, subs = 0, wgs = 0;
@@ -646,15 +657,24 @@ int Codec::prepare_decode(const uint8_t *const *jpegs, const size_t *sizes, int 
       return;
     }
     if (parse(jpegs[f], sizes[f], &P, &e) != 0) return;
-    if (P.restart) {
-      e = "restart intervals (DRI) are not supported by the GPU decoder yet";
-      return;
-    }
     DecFrame &F = dfr_[(size_t)f];
     if (!make_geom(P.w, P.h, P.ncomp, P.hs, P.vs, &F.g)) {
       e = "unsupported sampling geometry";
       return;
     }
+    // restart markers: one per interval boundary, numbered 0..7 cyclically (jdhuff.c
+    // process_restart / jdmarker.c read_restart_marker; libjpeg-turbo resynchronises on a
+    // missing or misnumbered one with a corrupt-data warning -- refused here)
+    const size_t nint = P.restart ? ((size_t)F.g.nmcu + P.restart - 1) / P.restart : 1;
+    if (P.rst.size() + 1 != nint) {
+      e = P.restart ? "restart markers missing or extra (corrupt JPEG)" : "RSTn marker in a scan without DRI";
+      return;
+    }
+    for (size_t i = 0; i < P.rst.size(); ++i)
+      if (jpegs[f][P.rst[i].second + 1] != 0xD0 + (i & 7)) {
+        e = "restart marker out of sequence (corrupt JPEG)";
+        return;
+      }
     for (int c = 0; c < P.ncomp; ++c) {
       std::memcpy(F.q[c], P.qt[P.tq[c]], sizeof F.q[c]);
       if (!build_tables(P.dcbits[P.td[c]], P.dcvals[P.td[c]], true, &F.dc[c], &F.sdc[c]) ||
@@ -663,36 +683,26 @@ int Codec::prepare_decode(const uint8_t *const *jpegs, const size_t *sizes, int 
         return;
       }
     }
-    const size_t len = P.scan_end - P.scan_off;
-    if (len == 0 || len > (1u << 28)) e = "empty or oversized entropy-coded segment";
+    size_t start = P.scan_off;
+    for (size_t i = 0; i <= P.rst.size(); ++i) {
+      const size_t end = i < P.rst.size() ? P.rst[i].first : P.scan_end;
+      if (end <= start || end - start > (1u << 28)) {
+        e = "empty or oversized entropy-coded segment";
+        return;
+      }
+      if (i < P.rst.size()) start = P.rst[i].second + 2;
+    }
   });
   for (int f = 0; f < n; ++f)
     if (!ferr[(size_t)f].empty()) {
       *err = "frame " + std::to_string(f) + ": " + ferr[(size_t)f];
       return kJpeg;
     }
+  dsg_.clear();
   for (int f = 0; f < n; ++f) {
     const Parsed &P = parsed[(size_t)f];
     DecFrame &F = dfr_[(size_t)f];
-    const size_t len = P.scan_end - P.scan_off;
-    F.in_off = in_off;
-    F.in_len = (uint32_t)len;
-    F.ntiles = (uint32_t)((len + kTile - 1) / kTile);
-    F.tile0 = tiles;
-    F.sub0 = subs;
-    F.nsub_max = (uint32_t)((len * 8 + kSubBits - 1) / kSubBits);
-    {  // speculative sync layout: spec_lanes(bpm) lanes per subsequence, 256 lanes per workgroup
-      const uint32_t ns = 256 / spec_lanes_host(F.g.bpm);
-      F.nwg = (F.nsub_max + ns - 1) / ns;
-      F.wg0 = wgs;
-      F.tr0 = trs;
-      wgs += F.nwg;
-      trs += (uint64_t)F.nwg * 256;
-      dmax_wg_ = std::max(dmax_wg_, F.nwg);
-      if (F.nwg > 4096) spec_ok_ = false;  // k_resolve stages at most 4096 workgroups per frame
-    }
     F.flags = (flags & kFlagFastUpsample) ? 0u : 1u;
-    F.us_off = us_off;
     F.blk0 = blk;
     for (int c = 0; c < P.ncomp; ++c) {
       F.dcbase[c] = dcoff;
@@ -702,47 +712,90 @@ int Codec::prepare_decode(const uint8_t *const *jpegs, const size_t *sizes, int 
     }
     F.out_off = pix;
     pix += align_up((size_t)P.w * P.h * 3, 256);
-    in_off += align_up(len, 16);
-    us_off += align_up(len + 64, 16);
     blk += (uint64_t)F.g.nblocks;
-    tiles += F.ntiles;
-    subs += F.nsub_max;
-    dmax_tiles_ = std::max(dmax_tiles_, F.ntiles);
-    dmax_sub_ = std::max(dmax_sub_, F.nsub_max);
+    // entropy-coded segments: the scan, or its restart intervals (whole MCUs each, the last
+    // one the remainder), with their blocks and DC sequence entries inside the frame's
+    const uint32_t nmcu = (uint32_t)F.g.nmcu, per = P.restart ? (uint32_t)P.restart : nmcu;
+    size_t start = P.scan_off;
+    for (size_t i = 0; i <= P.rst.size(); ++i) {
+      const size_t end = i < P.rst.size() ? P.rst[i].first : P.scan_end;
+      const size_t len = end - start;
+      const uint32_t m0 = (uint32_t)i * per, mc = std::min(per, nmcu - m0);
+      DecSeg S{};
+      S.frame = (uint32_t)f;
+      S.nblocks = mc * (uint32_t)F.g.bpm;
+      S.blk0 = F.blk0 + (uint64_t)m0 * F.g.bpm;
+      for (int c = 0; c < P.ncomp; ++c) S.dcbase[c] = F.dcbase[c] + (uint64_t)m0 * F.g.mh[c] * F.g.mv[c];
+      S.in_off = in_off;
+      S.in_len = (uint32_t)len;
+      S.ntiles = (uint32_t)((len + kTile - 1) / kTile);
+      S.tile0 = tiles;
+      S.sub0 = subs;
+      S.nsub_max = (uint32_t)((len * 8 + kSubBits - 1) / kSubBits);
+      {  // speculative sync layout: spec_lanes(bpm) lanes per subsequence, 256 lanes per workgroup
+        const uint32_t ns = 256 / spec_lanes_host(F.g.bpm);
+        S.nwg = (S.nsub_max + ns - 1) / ns;
+        S.wg0 = wgs;
+        S.tr0 = trs;
+        wgs += S.nwg;
+        trs += (uint64_t)S.nwg * 256;
+        dmax_wg_ = std::max(dmax_wg_, S.nwg);
+        if (S.nwg > 4096) spec_ok_ = false;  // k_resolve stages at most 4096 workgroups per segment
+      }
+      S.us_off = us_off;
+      in_off += align_up(len, 16);
+      us_off += align_up(len + 64, 16);
+      tiles += S.ntiles;
+      subs += S.nsub_max;
+      dmax_tiles_ = std::max(dmax_tiles_, S.ntiles);
+      dmax_sub_ = std::max(dmax_sub_, S.nsub_max);
+      seg_src_.push_back(jpegs[f] + start);
+      dsg_.push_back(S);
+      if (i < P.rst.size()) start = P.rst[i].second + 2;
+    }
     dmax_blocks_ = std::max(dmax_blocks_, (uint32_t)F.g.nblocks);
     dmax_w_ = std::max(dmax_w_, P.w);
     dmax_h_ = std::max(dmax_h_, P.h);
   }
   dn_ = n;
+  dnseg_ = (int)dsg_.size();
+  if (dnseg_ > 65535) {
+    *err = "more than 65535 restart intervals in one batch (split the batch)";
+    return kInvalid;
+  }
   dblocks_ = blk;
   dpix_bytes_ = pix;
-  // scan segments: [0, n) unstuff tiles, [n, 2n) subsequence counts, then DC sequences
+  // scan segments: [0, nseg) unstuff tiles, [nseg, 2 nseg) subsequence counts, then DC sequences
+  // (per entropy-coded segment and component: restart intervals reset the DC prediction)
   std::vector<ScanSeg> segs;
   uint32_t t0 = 0;
   auto add = [&](uint64_t base, uint32_t len) {
     segs.push_back(ScanSeg{base, len, t0});
     t0 += (len + kScanTile - 1) / kScanTile;
   };
-  for (auto &F : dfr_) add(F.tile0, F.ntiles);
-  for (auto &F : dfr_) add(F.sub0, F.nsub_max);
+  for (auto &S : dsg_) add(S.tile0, S.ntiles);
+  for (auto &S : dsg_) add(S.sub0, S.nsub_max);
   ndcseg_ = 0;
   dc_max_tiles_ = 0;
-  for (auto &F : dfr_)
-    for (int c = 0; c < F.g.ncomp; ++c) {
-      const uint32_t len = (uint32_t)((uint64_t)F.g.nmcu * F.g.mh[c] * F.g.mv[c]);
-      add(F.dcbase[c], len);
+  for (auto &S : dsg_) {
+    const Geom &g = dfr_[S.frame].g;
+    for (int c = 0; c < g.ncomp; ++c) {
+      const uint32_t len = S.nblocks / (uint32_t)g.bpm * (uint32_t)(g.mh[c] * g.mv[c]);
+      add(S.dcbase[c], len);
       dc_max_tiles_ = std::max(dc_max_tiles_, (len + kScanTile - 1) / kScanTile);
       ++ndcseg_;
     }
+  }
   // staging: inputs packed, then uploaded in one copy
   CK(h_stage_.ensure(in_off));
-  pool_.run(n, [&](int f) {
-    const Parsed &P = parsed[(size_t)f];
-    std::memcpy(h_stage_.as<uint8_t>() + dfr_[(size_t)f].in_off, jpegs[f] + P.scan_off, P.scan_end - P.scan_off);
+  pool_.run(dnseg_, [&](int i) {
+    const DecSeg &S = dsg_[(size_t)i];
+    std::memcpy(h_stage_.as<uint8_t>() + S.in_off, seg_src_[(size_t)i], S.in_len);
   });
   CK(hipSetDevice(device_));
   CK(d_in_.ensure(in_off));
   CK(d_dfr_.ensure(sizeof(DecFrame) * (size_t)n));
+  CK(d_dsg_.ensure(sizeof(DecSeg) * (size_t)dnseg_));
   CK(d_segs_.ensure(sizeof(ScanSeg) * segs.size()));
   CK(d_tile_.ensure(sizeof(uint32_t) * tiles));
   CK(d_tsum_.ensure(sizeof(int32_t) * (t0 + 1)));
@@ -782,28 +835,32 @@ int Codec::prepare_decode(const uint8_t *const *jpegs, const size_t *sizes, int 
   // descriptors go through pinned memory too, so every upload stays asynchronous and nothing
   // waits for the GPU before the kernels are queued (the pinned buffers are reused only by the
   // codec's next call, which starts after this one has synchronised)
-  const size_t dsz = sizeof(DecFrame) * (size_t)n, ssz = sizeof(ScanSeg) * segs.size();
-  CK(h_ddesc_.ensure(dsz + ssz));
+  const size_t dsz = sizeof(DecFrame) * (size_t)n, gsz = sizeof(DecSeg) * (size_t)dnseg_,
+               ssz = sizeof(ScanSeg) * segs.size();
+  CK(h_ddesc_.ensure(dsz + gsz + ssz));
   std::memcpy(h_ddesc_.as<uint8_t>(), dfr_.data(), dsz);
-  std::memcpy(h_ddesc_.as<uint8_t>() + dsz, segs.data(), ssz);
+  std::memcpy(h_ddesc_.as<uint8_t>() + dsz, dsg_.data(), gsz);
+  std::memcpy(h_ddesc_.as<uint8_t>() + dsz + gsz, segs.data(), ssz);
   CK(hipMemcpyAsync(d_in_.p, h_stage_.p, in_off, hipMemcpyHostToDevice, s_));
   CK(hipMemcpyAsync(d_dfr_.p, h_ddesc_.p, dsz, hipMemcpyHostToDevice, s_));
-  CK(hipMemcpyAsync(d_segs_.p, h_ddesc_.as<uint8_t>() + dsz, ssz, hipMemcpyHostToDevice, s_));
+  CK(hipMemcpyAsync(d_dsg_.p, h_ddesc_.as<uint8_t>() + dsz, gsz, hipMemcpyHostToDevice, s_));
+  CK(hipMemcpyAsync(d_segs_.p, h_ddesc_.as<uint8_t>() + dsz + gsz, ssz, hipMemcpyHostToDevice, s_));
   return kOk;
 }
 
 // Device part of the decode: unstuff -> sync passes -> write -> DC -> IDCT -> colour.
 int Codec::run_decode(int bgr, bool invert, std::string *err) {
   const DecFrame *fr = d_dfr_.as<DecFrame>();
+  const DecSeg *sg = d_dsg_.as<DecSeg>();
   const ScanSeg *segs = d_segs_.as<ScanSeg>();
-  const int n = dn_;
+  const int n = dn_, ns = dnseg_;
   CK(hipEventRecord(ev_[0], s_));
   // 1. unstuff
-  CK(dec_unstuff_count(fr, n, dmax_tiles_, d_in_.as<uint8_t>(), d_tile_.as<uint32_t>(), s_));
-  uint32_t *us_len = d_totals_.as<uint32_t>();  // totals of segments [0, n)
-  CK(scan_u32(segs, n, (dmax_tiles_ + kScanTile - 1) / kScanTile, d_tile_.as<uint32_t>(), d_tile_.as<uint32_t>(),
+  CK(dec_unstuff_count(sg, ns, dmax_tiles_, d_in_.as<uint8_t>(), d_tile_.as<uint32_t>(), s_));
+  uint32_t *us_len = d_totals_.as<uint32_t>();  // totals of scan segments [0, ns)
+  CK(scan_u32(segs, ns, (dmax_tiles_ + kScanTile - 1) / kScanTile, d_tile_.as<uint32_t>(), d_tile_.as<uint32_t>(),
               d_tsum_.as<uint32_t>(), us_len, false, s_));
-  CK(dec_unstuff_write(fr, n, dmax_tiles_, d_in_.as<uint8_t>(), d_tile_.as<uint32_t>(), us_len,
+  CK(dec_unstuff_write(sg, ns, dmax_tiles_, d_in_.as<uint8_t>(), d_tile_.as<uint32_t>(), us_len,
                        d_us_.as<uint8_t>(), s_));
   CK(hipEventRecord(ev_[1], s_));
   // 2. synchronise the subsequence entry states: speculative (one pass, one flag read), with
@@ -828,7 +885,7 @@ int Codec::run_decode(int bgr, bool invert, std::string *err) {
                 d_wrem_.as<uint32_t>(), d_wB_.as<uint8_t>(), d_wBC_.as<uint32_t>(), d_wBX_.as<uint64_t>(),
                 d_rE_.as<uint8_t>(), d_rK_.as<uint32_t>(), d_unres_.as<uint32_t>()};
     CK(hipMemsetAsync(d_unres_.p, 0, sizeof(uint32_t) * 16, s_));
-    CK(dec_sync_spec(fr, n, dmax_wg_, d_us_.as<uint8_t>(), us_len, sb, d_exit_[0].as<uint64_t>(),
+    CK(dec_sync_spec(sg, fr, ns, dmax_wg_, d_us_.as<uint8_t>(), us_len, sb, d_exit_[0].as<uint64_t>(),
                      d_cnt_[0].as<uint32_t>(), d_unres_.as<uint32_t>(), s_));
     // k_resolve reports a frame unresolved only when it has more workgroups than it stages,
     // which prepare_decode already excludes (spec_ok_), so the rest is queued without a host
@@ -846,13 +903,13 @@ int Codec::run_decode(int bgr, bool invert, std::string *err) {
       std::fprintf(stderr, "[vf_jpeg] spec: unresolved %u walker decodes %u traced workgroups %u traced subsequences "
                    "%u link misses %u (workgroups %u, subsequences %u); k_resolve kcycles summed over frames: "
                    "trace %u walk %u\n", st[0], st[1], st[2], st[3], st[4],
-                   dmax_wg_ * (uint32_t)n, dmax_sub_ * (uint32_t)n, st[5], st[6]);
+                   dmax_wg_ * (uint32_t)ns, dmax_sub_ * (uint32_t)ns, st[5], st[6]);
     }
   }
   if (flag) CK(hipMemsetAsync(d_changed_.p, 0, sizeof(uint32_t) * kMaxPasses, s_));
   for (; flag;) {
     const int a = pass & 1;
-    CK(dec_sync(fr, n, dmax_sub_, d_us_.as<uint8_t>(), us_len, d_exit_[a ^ 1].as<uint64_t>(),
+    CK(dec_sync(sg, fr, ns, dmax_sub_, d_us_.as<uint8_t>(), us_len, d_exit_[a ^ 1].as<uint64_t>(),
                 d_exit_[a].as<uint64_t>(), d_cnt_[a ^ 1].as<uint32_t>(), d_cnt_[a].as<uint32_t>(),
                 d_used_.as<uint64_t>(), d_ck_.as<uint64_t>(), d_ckrem_.as<uint32_t>(),
                 d_changed_.as<uint32_t>() + (pass % kMaxPasses), pass > 0 ? 1 : 0, s_));
@@ -877,19 +934,19 @@ int Codec::run_decode(int bgr, bool invert, std::string *err) {
                  "[vf_jpeg] sync: spec calls %llu fallbacks %llu; passes %d; rounds pass0 max %u sum %u, pass1 max %u "
                  "sum %u (WGs %u)\n",
                  (unsigned long long)spec_calls_, (unsigned long long)spec_fallbacks_, pass, st[3], st[1], st[2], st[0],
-                 (dmax_sub_ + 255) / 256 * (uint32_t)n);
+                 (dmax_sub_ + 255) / 256 * (uint32_t)ns);
   }
   CK(hipEventRecord(ev_[2], s_));
   // 3. block offsets of the subsequences, then the write pass
-  uint32_t *blocks_total = d_totals_.as<uint32_t>() + n;
-  CK(scan_u32(segs + n, n, (dmax_sub_ + kScanTile - 1) / kScanTile, d_cnt_[last].as<uint32_t>(),
+  uint32_t *blocks_total = d_totals_.as<uint32_t>() + ns;
+  CK(scan_u32(segs + ns, ns, (dmax_sub_ + kScanTile - 1) / kScanTile, d_cnt_[last].as<uint32_t>(),
               d_bstart_.as<uint32_t>(), d_tsum_.as<uint32_t>(), blocks_total, false, s_));
   CK(hipMemsetAsync(d_coef_.p, 0, dblocks_ * 128, s_));
-  CK(dec_write(fr, n, dmax_sub_, d_us_.as<uint8_t>(), us_len, d_exit_[last].as<uint64_t>(),
+  CK(dec_write(sg, fr, ns, dmax_sub_, d_us_.as<uint8_t>(), us_len, d_exit_[last].as<uint64_t>(),
                d_bstart_.as<uint32_t>(), d_coef_.as<int16_t>(), d_dcseq_.as<int32_t>(), s_));
   CK(hipEventRecord(ev_[3], s_));
   // 4. DC prediction (inclusive scan per component sequence)
-  CK(scan_i32(segs + 2 * n, ndcseg_, dc_max_tiles_, d_dcseq_.as<int32_t>(), d_dcseq_.as<int32_t>(),
+  CK(scan_i32(segs + 2 * ns, ndcseg_, dc_max_tiles_, d_dcseq_.as<int32_t>(), d_dcseq_.as<int32_t>(),
               d_tsum_.as<int32_t>(), nullptr, true, s_));
   // 5. IDCT, 6. upsample + colour (+ invert)
   CK(dec_idct(fr, n, dmax_blocks_, d_coef_.as<int16_t>(), d_dcseq_.as<int32_t>(), d_planes_.as<uint8_t>(), s_));
@@ -901,15 +958,15 @@ int Codec::run_decode(int bgr, bool invert, std::string *err) {
 
 // Queue the D2H of every frame's decoded block count (written by run_decode) into pinned memory.
 int Codec::queue_decode_check(std::string *err) {
-  CK(h_meta_.ensure(sizeof(uint64_t) * (size_t)dn_ * 2 + 64));
-  CK(hipMemcpyAsync(h_meta_.p, d_totals_.as<uint32_t>() + dn_, sizeof(uint32_t) * (size_t)dn_,
+  CK(h_dtot_.ensure(sizeof(uint32_t) * (size_t)dnseg_ + 64));
+  CK(hipMemcpyAsync(h_dtot_.p, d_totals_.as<uint32_t>() + dnseg_, sizeof(uint32_t) * (size_t)dnseg_,
                     hipMemcpyDeviceToHost, s_));
   return kOk;
 }
 
 // Check that every frame decoded all its blocks (after queue_decode_check and a synchronisation).
 int Codec::check_decode(std::string *err) {
-  const uint32_t *tot = h_meta_.as<uint32_t>();
+  const uint32_t *tot = h_dtot_.as<uint32_t>();
   if (spec_check_) {
     spec_check_ = false;
     if (*h_flag_.as<uint32_t>()) {
@@ -918,12 +975,16 @@ int Codec::check_decode(std::string *err) {
       return kJpeg;
     }
   }
-  for (int f = 0; f < dn_; ++f)
-    if (tot[(size_t)f] < (uint32_t)dfr_[(size_t)f].g.nblocks) {
-      *err = "frame " + std::to_string(f) + ": entropy-coded data ends after " + std::to_string(tot[(size_t)f]) +
-             " of " + std::to_string(dfr_[(size_t)f].g.nblocks) + " blocks (truncated or corrupt JPEG)";
+  for (int i = 0; i < dnseg_; ++i) {
+    const DecSeg &S = dsg_[(size_t)i];
+    if (tot[(size_t)i] < S.nblocks) {
+      const bool whole = S.nblocks == (uint32_t)dfr_[S.frame].g.nblocks;
+      *err = "frame " + std::to_string(S.frame) + (whole ? std::string() : " (restart interval at block " +
+             std::to_string(S.blk0 - dfr_[S.frame].blk0) + ")") + ": entropy-coded data ends after " +
+             std::to_string(tot[(size_t)i]) + " of " + std::to_string(S.nblocks) + " blocks (truncated or corrupt JPEG)";
       return kJpeg;
     }
+  }
   return kOk;
 }
 
@@ -1046,7 +1107,7 @@ int Codec::run_encode(int bgr, bool fastdct, std::string *err) {
 int Codec::queue_fetch(uint64_t guess, std::string *err) {
   const int n = en_;
   CK(h_meta_.ensure(sizeof(uint64_t) * (size_t)n * 2 + 64));
-  uint64_t *sz = h_meta_.as<uint64_t>() + n;  // [0, n) u32 block totals, then the sizes
+  uint64_t *sz = h_meta_.as<uint64_t>() + n;  // the sizes (h_dtot_ holds the decode's block totals)
   CK(hipMemcpyAsync(sz, d_outsize_.p, sizeof(uint64_t) * (size_t)n, hipMemcpyDeviceToHost, s_));
   guess = std::min<uint64_t>(guess, d_pack_.cap);
   CK(h_out_.ensure(guess));

@@ -161,8 +161,8 @@ __device__ __forceinline__ uint32_t keep_mask(const uint8_t *s, uint32_t len, ui
   return m;
 }
 
-__global__ __launch_bounds__(256) void k_unstuff_count(const DecFrame *fr, const uint8_t *in, uint32_t *cnt) {
-  const DecFrame &F = fr[blockIdx.y];
+__global__ __launch_bounds__(256) void k_unstuff_count(const DecSeg *sg, const uint8_t *in, uint32_t *cnt) {
+  const DecSeg &F = sg[blockIdx.y];
   if (blockIdx.x >= F.ntiles) return;
   __shared__ uint32_t sh[4];
   uint8_t bytes[16];
@@ -173,9 +173,9 @@ __global__ __launch_bounds__(256) void k_unstuff_count(const DecFrame *fr, const
   if (threadIdx.x == 0) cnt[F.tile0 + blockIdx.x] = tot;
 }
 
-__global__ __launch_bounds__(256) void k_unstuff_write(const DecFrame *fr, const uint8_t *in, const uint32_t *off,
+__global__ __launch_bounds__(256) void k_unstuff_write(const DecSeg *sg, const uint8_t *in, const uint32_t *off,
                                                        const uint32_t *us_len, uint8_t *us) {
-  const DecFrame &F = fr[blockIdx.y];
+  const DecSeg &F = sg[blockIdx.y];
   if (blockIdx.x >= F.ntiles) return;
   __shared__ uint32_t sh[4];
   uint8_t bytes[16];
@@ -412,7 +412,7 @@ constexpr uint64_t kNoCk = ~0ull;
 // until the workgroup is consistent.  Across workgroups the entry of a workgroup's first
 // thread is the previous pass's exit of its predecessor; a pass that changes no exit state
 // means the whole chain is consistent, and its counts were made from the final entry states.
-__global__ __launch_bounds__(256) void k_sync(const DecFrame *fr, const uint8_t *us, const uint32_t *us_len,
+__global__ __launch_bounds__(256) void k_sync(const DecSeg *sg, const DecFrame *fr, const uint8_t *us, const uint32_t *us_len,
                                               const uint64_t *exit_in, uint64_t *exit_out, const uint32_t *cnt_in,
                                               uint32_t *cnt_out, uint64_t *used, uint64_t *ck, uint32_t *ckrem,
                                               uint32_t *changed, int pass) {
@@ -420,13 +420,14 @@ __global__ __launch_bounds__(256) void k_sync(const DecFrame *fr, const uint8_t 
   __shared__ uint64_t s_exit[256];
   __shared__ uint64_t s_ck[kCk][256];
   __shared__ uint32_t s_rem[kCk][256];
-  const DecFrame &F = fr[blockIdx.y];
-  if (blockIdx.x * 256 >= F.nsub_max) return;
+  const DecSeg &S = sg[blockIdx.y];
+  const DecFrame &F = fr[S.frame];
+  if (blockIdx.x * 256 >= S.nsub_max) return;
   load_sync_tables(F, tabs);
   const HuffGeom hg(F.g);
   const uint32_t t = threadIdx.x;
   const uint32_t i = blockIdx.x * 256 + t;
-  const uint32_t gi = F.sub0 + i;
+  const uint32_t gi = S.sub0 + i;
   const uint32_t nbits = us_len[blockIdx.y] * 8u;
   const uint32_t nsub = (nbits + kSubBits - 1) / kSubBits;
   const bool live = i < nsub;
@@ -458,7 +459,7 @@ __global__ __launch_bounds__(256) void k_sync(const DecFrame *fr, const uint8_t 
     if (need) {
       decoded = true;
       BitReader br;
-      br.init(us + F.us_off, (uint32_t)(entry >> 16));
+      br.init(us + S.us_off, (uint32_t)(entry >> 16));
       uint32_t z = (entry >> 8) & 0xFF, c = entry & 0xFF, n = 0;
       int m = 0;
       while (m < kCk && base + (uint32_t)(m + 1) * kCkStep <= br.pos) s_ck[m++][t] = kNoCk;
@@ -498,7 +499,7 @@ __global__ __launch_bounds__(256) void k_sync(const DecFrame *fr, const uint8_t 
     }
     if (!__syncthreads_or(need)) break;  // also orders the s_exit reads before the next writes
   }
-  if (i < F.nsub_max) {
+  if (i < S.nsub_max) {
     exit_out[gi] = ex;
     cnt_out[gi] = cnt;
     if (live) {
@@ -585,7 +586,7 @@ __device__ __forceinline__ uint32_t spec_link(const uint32_t *words, uint32_t wo
   return last ? kLinkLast : kLinkNone;
 }
 
-__global__ __launch_bounds__(256) void k_spec(const DecFrame *fr, const uint8_t *us, const uint32_t *us_len,
+__global__ __launch_bounds__(256) void k_spec(const DecSeg *sg, const DecFrame *fr, const uint8_t *us, const uint32_t *us_len,
                                               SpecBufs B) {
   __shared__ HuffSync tabs[6];
   __shared__ uint64_t s_ck[kCk][256];
@@ -595,8 +596,9 @@ __global__ __launch_bounds__(256) void k_spec(const DecFrame *fr, const uint8_t 
   __shared__ uint32_t s_C[256];
   __shared__ uint8_t s_M[256];
   __shared__ uint32_t s_w[kSpecWords];
-  const DecFrame &F = fr[blockIdx.y];
-  if (blockIdx.x >= F.nwg) return;
+  const DecSeg &S = sg[blockIdx.y];
+  const DecFrame &F = fr[S.frame];
+  if (blockIdx.x >= S.nwg) return;
   const long long c_start = VF_SYNC_STATS ? clock64() : 0;
   const HuffGeom hg(F.g);
   const uint32_t L = spec_lanes(hg.bpm), NS = 256 / L;
@@ -605,12 +607,12 @@ __global__ __launch_bounds__(256) void k_spec(const DecFrame *fr, const uint8_t 
   const uint32_t nbits = us_len[blockIdx.y] * 8u, nsub = (nbits + kSubBits - 1) / kSubBits;
   const bool live = c0 < hg.bpm && s < nsub;
   const uint32_t base = s * kSubBits, end = (s + 1 >= nsub) ? nbits : (s + 1) * kSubBits;
-  const uint64_t g0 = F.tr0 + (uint64_t)blockIdx.x * 256, ti = g0 + t;
+  const uint64_t g0 = S.tr0 + (uint64_t)blockIdx.x * 256, ti = g0 + t;
   // the workgroup's stream words (every decode here stays within them, plus overshoot and
   // lookahead), from the frame's padded unstuffed region
   const uint32_t woff = blockIdx.x * NS * (kSubBits / 32);
-  const uint32_t fwords = (((F.in_len + 64) + 15) & ~15u) / 4;
-  const uint32_t *gw = reinterpret_cast<const uint32_t *>(us + F.us_off);
+  const uint32_t fwords = (((S.in_len + 64) + 15) & ~15u) / 4;
+  const uint32_t *gw = reinterpret_cast<const uint32_t *>(us + S.us_off);
   for (uint32_t i = t; i < NS * (kSubBits / 32) + kSpecPadWords; i += 256)
     s_w[i] = woff + i < fwords ? gw[woff + i] : 0u;
   load_sync_tables(F, tabs);  // its barrier also publishes s_w
@@ -643,7 +645,7 @@ __global__ __launch_bounds__(256) void k_spec(const DecFrame *fr, const uint8_t 
   if (live) {
     B.tE[ti] = E;
     if (sl == 0) {  // checkpoints of the first subsequence, for k_wglink
-      const uint64_t wb = ((uint64_t)(F.wg0 + blockIdx.x) * kSpecLanesMax + c0) * kCk;
+      const uint64_t wb = ((uint64_t)(S.wg0 + blockIdx.x) * kSpecLanesMax + c0) * kCk;
 #pragma unroll
       for (int m = 0; m < kCk; ++m) {
         B.wck[wb + m] = s_ck[m][t];
@@ -733,7 +735,7 @@ __global__ __launch_bounds__(256) void k_spec(const DecFrame *fr, const uint8_t 
     if (t == nk - 1)
       for (uint32_t q = 0; q < bpm; ++q) {
         const uint32_t j = nib(f, q);
-        if (j != kLinkNone) B.wF[(uint64_t)(F.wg0 + blockIdx.x) * kSpecLanesMax + q] = (uint8_t)(j < bpm ? j : kLinkNone);
+        if (j != kLinkNone) B.wF[(uint64_t)(S.wg0 + blockIdx.x) * kSpecLanesMax + q] = (uint8_t)(j < bpm ? j : kLinkNone);
       }
   }
   __syncthreads();
@@ -771,31 +773,32 @@ __global__ __launch_bounds__(256) void k_spec(const DecFrame *fr, const uint8_t 
       B.tXc[g0 + k * L + e] = cnt;
       if (j == kLinkLast) break;
     }
-    B.wF[(uint64_t)(F.wg0 + blockIdx.x) * kSpecLanesMax + e] = (uint8_t)(j < hg.bpm ? j : kLinkNone);
+    B.wF[(uint64_t)(S.wg0 + blockIdx.x) * kSpecLanesMax + e] = (uint8_t)(j < hg.bpm ? j : kLinkNone);
     if (VF_SYNC_STATS) atomicAdd(B.stats + 10, (uint32_t)((clock64() - c_start) >> 10));
   }
 }
 
 // Links across workgroup boundaries: trajectory j of the last subsequence of workgroup w-1
 // into the first subsequence of w.  16 boundaries per workgroup, one lane per j.
-__global__ __launch_bounds__(256) void k_wglink(const DecFrame *fr, const uint8_t *us, const uint32_t *us_len,
+__global__ __launch_bounds__(256) void k_wglink(const DecSeg *sg, const DecFrame *fr, const uint8_t *us, const uint32_t *us_len,
                                                 SpecBufs B) {
   __shared__ HuffSync tabs[6];
-  const DecFrame &F = fr[blockIdx.y];
-  if (blockIdx.x * 16 >= F.nwg) return;
+  const DecSeg &S = sg[blockIdx.y];
+  const DecFrame &F = fr[S.frame];
+  if (blockIdx.x * 16 >= S.nwg) return;
   load_sync_tables(F, tabs);
   const HuffGeom hg(F.g);
   const uint32_t L = spec_lanes(hg.bpm), NS = 256 / L;
   const uint32_t w = blockIdx.x * 16 + threadIdx.x / 16, j = threadIdx.x % 16;
   const uint32_t nbits = us_len[blockIdx.y] * 8u, nsub = (nbits + kSubBits - 1) / kSubBits;
   const uint32_t s = w * NS;
-  if (w == 0 || w >= F.nwg || j >= hg.bpm || s >= nsub) return;
+  if (w == 0 || w >= S.nwg || j >= hg.bpm || s >= nsub) return;
   const uint32_t base = s * kSubBits, end = (s + 1 >= nsub) ? nbits : (s + 1) * kSubBits;
-  const uint64_t X = B.tE[F.tr0 + (uint64_t)(w - 1) * 256 + (NS - 1) * L + j];
-  const uint64_t wc = (uint64_t)(F.wg0 + w) * kSpecLanesMax;
+  const uint64_t X = B.tE[S.tr0 + (uint64_t)(w - 1) * 256 + (NS - 1) * L + j];
+  const uint64_t wc = (uint64_t)(S.wg0 + w) * kSpecLanesMax;
   uint32_t C = 0;
   uint64_t xe = 0;
-  const uint32_t M = spec_link(reinterpret_cast<const uint32_t *>(us + F.us_off), 0u, X, base, end, s + 1 == nsub,
+  const uint32_t M = spec_link(reinterpret_cast<const uint32_t *>(us + S.us_off), 0u, X, base, end, s + 1 == nsub,
                                hg, tabs,
                                [&](uint32_t c2, int m) { return B.wck[(wc + c2) * kCk + m]; },
                                [&](uint32_t c2, int m) { return B.wrem[(wc + c2) * kCk + m]; }, &C, &xe);
@@ -814,17 +817,18 @@ __global__ __launch_bounds__(256) void k_wglink(const DecFrame *fr, const uint8_
 constexpr uint32_t kResolveLds = 4096;  // workgroups per frame resolved here (else fallback)
 constexpr uint32_t kTraceWords = kSubBits / 32 + 6;  // one subsequence + overshoot + lookahead
 
-__global__ __launch_bounds__(256) void k_resolve(const DecFrame *fr, const uint8_t *us, const uint32_t *us_len,
+__global__ __launch_bounds__(256) void k_resolve(const DecSeg *sg, const DecFrame *fr, const uint8_t *us, const uint32_t *us_len,
                                                  SpecBufs B, uint32_t *unresolved) {
   __shared__ uint64_t sF[kResolveLds], sB[kResolveLds];
   __shared__ uint8_t sE[kResolveLds], sK[kResolveLds], sJ[kResolveLds];
   __shared__ HuffSync tabs[6];
   __shared__ uint32_t s_tw[kTraceWords];
-  const DecFrame &F = fr[blockIdx.x];
+  const DecSeg &S = sg[blockIdx.x];
+  const DecFrame &F = fr[S.frame];
   const HuffGeom hg(F.g);
   const uint32_t bpm = hg.bpm, L = spec_lanes(bpm), NS = 256 / L;
   const uint32_t nbits = us_len[blockIdx.x] * 8u, nsub = (nbits + kSubBits - 1) / kSubBits;
-  const uint32_t nwg = min(F.nwg, (nsub + NS - 1) / NS);
+  const uint32_t nwg = min(S.nwg, (nsub + NS - 1) / NS);
   if (nwg > kResolveLds) {
     if (threadIdx.x == 0) atomicOr(unresolved, 1u);
     return;
@@ -832,7 +836,7 @@ __global__ __launch_bounds__(256) void k_resolve(const DecFrame *fr, const uint8
   load_sync_tables(F, tabs);
   for (uint32_t i = threadIdx.x; i < nwg; i += 256) {
     uint64_t fr_ = 0, br_ = 0;
-    const uint64_t row = (uint64_t)(F.wg0 + i) * kSpecLanesMax;
+    const uint64_t row = (uint64_t)(S.wg0 + i) * kSpecLanesMax;
     for (uint32_t e = 0; e < bpm; ++e) {
       fr_ |= (uint64_t)(B.wF[row + e] & 0xF) << (4 * e);
       if (i > 0) br_ |= (uint64_t)(B.wB[row + e] & 0xF) << (4 * e);
@@ -841,9 +845,9 @@ __global__ __launch_bounds__(256) void k_resolve(const DecFrame *fr, const uint8
     sB[i] = br_;
   }
   __syncthreads();
-  auto slot = [&](uint32_t w, uint32_t k, uint32_t lane) { return F.tr0 + (uint64_t)w * 256 + k * L + lane; };
-  const uint32_t fwords = (((F.in_len + 64) + 15) & ~15u) / 4;
-  const uint32_t *gw = reinterpret_cast<const uint32_t *>(us + F.us_off);
+  auto slot = [&](uint32_t w, uint32_t k, uint32_t lane) { return S.tr0 + (uint64_t)w * 256 + k * L + lane; };
+  const uint32_t fwords = (((S.in_len + 64) + 15) & ~15u) / 4;
+  const uint32_t *gw = reinterpret_cast<const uint32_t *>(us + S.us_off);
   const uint8_t kTraced = 0xFF;  // sJ: the prefix was written by the tracer
   if (threadIdx.x == 0) {
     long long c_loop = VF_SYNC_STATS ? clock64() : 0, c_trace = 0;
@@ -874,7 +878,7 @@ __global__ __launch_bounds__(256) void k_resolve(const DecFrame *fr, const uint8
       uint64_t X;
       uint32_t k = 0;
       if (jl < bpm) {  // the boundary link decoded subsequence 0 without rejoining
-        const uint64_t wb = (uint64_t)(F.wg0 + w) * kSpecLanesMax + jl;
+        const uint64_t wb = (uint64_t)(S.wg0 + w) * kSpecLanesMax + jl;
         X = B.wBX[wb];
         B.pX[slot(w, 0, 0)] = X;
         B.pC[slot(w, 0, 0)] = B.wBC[wb];
@@ -920,10 +924,10 @@ __global__ __launch_bounds__(256) void k_resolve(const DecFrame *fr, const uint8
   }
   __syncthreads();
   for (uint32_t w = threadIdx.x; w < nwg; w += 256) {
-    B.rE[F.wg0 + w] = sE[w];
-    B.rK[F.wg0 + w] = sK[w];
+    B.rE[S.wg0 + w] = sE[w];
+    B.rK[S.wg0 + w] = sK[w];
     if (sJ[w] != kTraced) {  // rejoined at the boundary: prefix record of subsequence 0
-      const uint64_t wb = (uint64_t)(F.wg0 + w) * kSpecLanesMax + sJ[w];
+      const uint64_t wb = (uint64_t)(S.wg0 + w) * kSpecLanesMax + sJ[w];
       B.pX[slot(w, 0, 0)] = sK[w] == 0 && nib(sB[w], sJ[w]) < bpm ? B.tE[slot(w, 0, sE[w])] : B.wBX[wb];
       B.pC[slot(w, 0, 0)] = B.wBC[wb];
     }
@@ -932,24 +936,25 @@ __global__ __launch_bounds__(256) void k_resolve(const DecFrame *fr, const uint8
 
 // Exit state and block count of every subsequence along the resolved path, in the layout
 // the write pass and the block-offset scan read (exit_out / cnt_out of k_sync).
-__global__ __launch_bounds__(256) void k_finalize(const DecFrame *fr, const uint32_t *us_len, SpecBufs B,
+__global__ __launch_bounds__(256) void k_finalize(const DecSeg *sg, const DecFrame *fr, const uint32_t *us_len, SpecBufs B,
                                                   uint64_t *exit_out, uint32_t *cnt_out) {
-  const DecFrame &F = fr[blockIdx.y];
-  if (blockIdx.x >= F.nwg) return;
+  const DecSeg &S = sg[blockIdx.y];
+  const DecFrame &F = fr[S.frame];
+  if (blockIdx.x >= S.nwg) return;
   const uint32_t bpm = (uint32_t)F.g.bpm, L = spec_lanes(bpm), NS = 256 / L;
   const uint32_t nbits = us_len[blockIdx.y] * 8u, nsub = (nbits + kSubBits - 1) / kSubBits;
   const uint32_t sl = threadIdx.x;
   if (sl >= NS) return;
   const uint32_t s = blockIdx.x * NS + sl;
-  if (s >= F.nsub_max) return;
-  const uint64_t gi = F.sub0 + s;
+  if (s >= S.nsub_max) return;
+  const uint64_t gi = S.sub0 + s;
   if (s >= nsub) {
     exit_out[gi] = pack_state(nbits, 0, 0);
     cnt_out[gi] = 0;
     return;
   }
-  const uint64_t g0 = F.tr0 + (uint64_t)blockIdx.x * 256;
-  const uint32_t kj = B.rK[F.wg0 + blockIdx.x], e = B.rE[F.wg0 + blockIdx.x];
+  const uint64_t g0 = S.tr0 + (uint64_t)blockIdx.x * 256;
+  const uint32_t kj = B.rK[S.wg0 + blockIdx.x], e = B.rE[S.wg0 + blockIdx.x];
   if (sl <= kj) {
     exit_out[gi] = B.pX[g0 + sl * L];
     cnt_out[gi] = B.pC[g0 + sl * L];
@@ -962,32 +967,35 @@ __global__ __launch_bounds__(256) void k_finalize(const DecFrame *fr, const uint
 // The workgroup's stream words are staged in LDS first (as k_spec does): every refill of a
 // thread's bit buffer is then an LDS read instead of a dependent global load, the chain a
 // subsequence's decode waits on (k_write has only ~3 waves per SIMD to hide it with).
-__global__ __launch_bounds__(256) void k_write(const DecFrame *fr, const uint8_t *us, const uint32_t *us_len,
+__global__ __launch_bounds__(256) void k_write(const DecSeg *sg, const DecFrame *fr, const uint8_t *us, const uint32_t *us_len,
                                                const uint64_t *exits, const uint32_t *bstart, int16_t *coef,
                                                int32_t *dcseq) {
   __shared__ HuffDec tabs[6];
   __shared__ uint32_t s_w[kSpecWords];
-  const DecFrame &F = fr[blockIdx.y];
-  if (blockIdx.x * 256 >= F.nsub_max) return;
+  const DecSeg &S = sg[blockIdx.y];
+  const DecFrame &F = fr[S.frame];
+  if (blockIdx.x * 256 >= S.nsub_max) return;
   // this workgroup's 256 subsequences of stream words, plus overshoot and lookahead, from the
   // frame's padded unstuffed region (an entry state lies at or after its subsequence's start)
   const uint32_t woff = blockIdx.x * 256 * (kSubBits / 32);
-  const uint32_t fwords = (((F.in_len + 64) + 15) & ~15u) / 4;
-  const uint32_t *gw = reinterpret_cast<const uint32_t *>(us + F.us_off);
+  const uint32_t fwords = (((S.in_len + 64) + 15) & ~15u) / 4;
+  const uint32_t *gw = reinterpret_cast<const uint32_t *>(us + S.us_off);
   for (uint32_t k = threadIdx.x; k < kSpecWords; k += 256) s_w[k] = woff + k < fwords ? gw[woff + k] : 0u;
   load_tables(F, tabs);  // its barrier also publishes s_w
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   const uint32_t nbits = us_len[blockIdx.y] * 8u;
   const uint32_t nsub = (nbits + kSubBits - 1) / kSubBits;
   if (i >= nsub) return;
-  const uint32_t gi = F.sub0 + i;
+  const uint32_t gi = S.sub0 + i;
   const uint64_t st = i == 0 ? 0 : exits[gi - 1];
   const uint32_t end = (i + 1 == nsub) ? nbits : (i + 1) * kSubBits;
   BitReader br;
   br.init_words(s_w, (uint32_t)(st >> 16), woff);
   uint32_t z = (st >> 8) & 0xFF, c = st & 0xFF, blocks = 0;
-  decode_span<true>(br, end, z, c, blocks, HuffGeom(F.g), tabs, tabs + 3, bstart[gi], coef + F.blk0 * 64, dcseq,
-                    F.dcbase);
+  HuffGeom hg(F.g);
+  hg.nblocks = S.nblocks;  // the segment's blocks (a restart interval: its whole MCUs)
+  decode_span<true>(br, end, z, c, blocks, hg, tabs, tabs + 3, bstart[gi], coef + S.blk0 * 64, dcseq,
+                    S.dcbase);
 }
 
 // ---- decoder: IDCT -------------------------------------------------------------------------
@@ -1970,44 +1978,46 @@ hipError_t scan_i32(const ScanSeg *segs, int nseg, uint32_t max_tiles, const int
   return seg_scan<int32_t>(segs, nseg, max_tiles, in, out, tsum, totals, inclusive, s);
 }
 
-hipError_t dec_unstuff_count(const DecFrame *fr, int n, uint32_t max_tiles, const uint8_t *in, uint32_t *tile_cnt,
+hipError_t dec_unstuff_count(const DecSeg *sg, int nseg, uint32_t max_tiles, const uint8_t *in, uint32_t *tile_cnt,
                              hipStream_t s) {
-  if (n <= 0 || !max_tiles) return hipSuccess;
-  hipLaunchKernelGGL(k_unstuff_count, dim3(max_tiles, (unsigned)n), dim3(256), 0, s, fr, in, tile_cnt);
+  if (nseg <= 0 || !max_tiles) return hipSuccess;
+  hipLaunchKernelGGL(k_unstuff_count, dim3(max_tiles, (unsigned)nseg), dim3(256), 0, s, sg, in, tile_cnt);
   return hipGetLastError();
 }
 
-hipError_t dec_unstuff_write(const DecFrame *fr, int n, uint32_t max_tiles, const uint8_t *in,
+hipError_t dec_unstuff_write(const DecSeg *sg, int nseg, uint32_t max_tiles, const uint8_t *in,
                              const uint32_t *tile_off, const uint32_t *us_len, uint8_t *us, hipStream_t s) {
-  if (n <= 0 || !max_tiles) return hipSuccess;
-  hipLaunchKernelGGL(k_unstuff_write, dim3(max_tiles, (unsigned)n), dim3(256), 0, s, fr, in, tile_off, us_len, us);
+  if (nseg <= 0 || !max_tiles) return hipSuccess;
+  hipLaunchKernelGGL(k_unstuff_write, dim3(max_tiles, (unsigned)nseg), dim3(256), 0, s, sg, in, tile_off, us_len, us);
   return hipGetLastError();
 }
 
-hipError_t dec_sync(const DecFrame *fr, int n, uint32_t max_sub, const uint8_t *us, const uint32_t *us_len,
-                    const uint64_t *exit_in, uint64_t *exit_out, const uint32_t *cnt_in, uint32_t *cnt_out,
-                    uint64_t *used, uint64_t *ck, uint32_t *ckrem, uint32_t *changed, int pass, hipStream_t s) {
-  if (n <= 0 || !max_sub) return hipSuccess;
-  hipLaunchKernelGGL(k_sync, dim3((max_sub + 255) / 256, (unsigned)n), dim3(256), 0, s, fr, us, us_len, exit_in,
-                     exit_out, cnt_in, cnt_out, used, ck, ckrem, changed, pass);
+hipError_t dec_sync(const DecSeg *sg, const DecFrame *fr, int nseg, uint32_t max_sub, const uint8_t *us,
+                    const uint32_t *us_len, const uint64_t *exit_in, uint64_t *exit_out, const uint32_t *cnt_in,
+                    uint32_t *cnt_out, uint64_t *used, uint64_t *ck, uint32_t *ckrem, uint32_t *changed, int pass,
+                    hipStream_t s) {
+  if (nseg <= 0 || !max_sub) return hipSuccess;
+  hipLaunchKernelGGL(k_sync, dim3((max_sub + 255) / 256, (unsigned)nseg), dim3(256), 0, s, sg, fr, us, us_len,
+                     exit_in, exit_out, cnt_in, cnt_out, used, ck, ckrem, changed, pass);
   return hipGetLastError();
 }
 
-hipError_t dec_sync_spec(const DecFrame *fr, int n, uint32_t max_wg, const uint8_t *us, const uint32_t *us_len,
-                         const SpecBufs &b, uint64_t *exit_out, uint32_t *cnt_out, uint32_t *unresolved,
-                         hipStream_t s) {
-  if (n <= 0 || !max_wg) return hipSuccess;
-  hipLaunchKernelGGL(k_spec, dim3(max_wg, (unsigned)n), dim3(256), 0, s, fr, us, us_len, b);
-  hipLaunchKernelGGL(k_wglink, dim3((max_wg + 15) / 16, (unsigned)n), dim3(256), 0, s, fr, us, us_len, b);
-  hipLaunchKernelGGL(k_resolve, dim3((unsigned)n), dim3(256), 0, s, fr, us, us_len, b, unresolved);
-  hipLaunchKernelGGL(k_finalize, dim3(max_wg, (unsigned)n), dim3(256), 0, s, fr, us_len, b, exit_out, cnt_out);
+hipError_t dec_sync_spec(const DecSeg *sg, const DecFrame *fr, int nseg, uint32_t max_wg, const uint8_t *us,
+                         const uint32_t *us_len, const SpecBufs &b, uint64_t *exit_out, uint32_t *cnt_out,
+                         uint32_t *unresolved, hipStream_t s) {
+  if (nseg <= 0 || !max_wg) return hipSuccess;
+  hipLaunchKernelGGL(k_spec, dim3(max_wg, (unsigned)nseg), dim3(256), 0, s, sg, fr, us, us_len, b);
+  hipLaunchKernelGGL(k_wglink, dim3((max_wg + 15) / 16, (unsigned)nseg), dim3(256), 0, s, sg, fr, us, us_len, b);
+  hipLaunchKernelGGL(k_resolve, dim3((unsigned)nseg), dim3(256), 0, s, sg, fr, us, us_len, b, unresolved);
+  hipLaunchKernelGGL(k_finalize, dim3(max_wg, (unsigned)nseg), dim3(256), 0, s, sg, fr, us_len, b, exit_out, cnt_out);
   return hipGetLastError();
 }
 
-hipError_t dec_write(const DecFrame *fr, int n, uint32_t max_sub, const uint8_t *us, const uint32_t *us_len,
-                     const uint64_t *exits, const uint32_t *bstart, int16_t *coef, int32_t *dcseq, hipStream_t s) {
-  if (n <= 0 || !max_sub) return hipSuccess;
-  hipLaunchKernelGGL(k_write, dim3((max_sub + 255) / 256, (unsigned)n), dim3(256), 0, s, fr, us, us_len, exits,
+hipError_t dec_write(const DecSeg *sg, const DecFrame *fr, int nseg, uint32_t max_sub, const uint8_t *us,
+                     const uint32_t *us_len, const uint64_t *exits, const uint32_t *bstart, int16_t *coef,
+                     int32_t *dcseq, hipStream_t s) {
+  if (nseg <= 0 || !max_sub) return hipSuccess;
+  hipLaunchKernelGGL(k_write, dim3((max_sub + 255) / 256, (unsigned)nseg), dim3(256), 0, s, sg, fr, us, us_len, exits,
                      bstart, coef, dcseq);
   return hipGetLastError();
 }

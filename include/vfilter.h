@@ -206,7 +206,8 @@ int vf_bench_device_ring(vf_ctx *ctx, void *const *srcs, void *const *dsts, int 
  * with a gfx950 baseline-JPEG codec whose integer arithmetic is libjpeg-turbo's: outputs are
  * bit-exact with libjpeg-turbo.  Constants below are TurboJPEG's (turbojpeg.h).
  * Supported: 8-bit baseline / extended-sequential Huffman JPEG, 1 or 3 components, one
- * interleaved scan, no restart markers (decode); TJSAMP_444/422/420/GRAY/440 (encode).
+ * interleaved scan, any Huffman tables, with or without restart intervals (DRI / RSTn)
+ * (decode); TJSAMP_444/422/420/GRAY/440 (encode).
  * Anything else returns VF_E_JPEG with a message. */
 #define VF_TJPF_RGB 0
 #define VF_TJPF_BGR 1

@@ -141,6 +141,8 @@ def _x():
         lib.xc_available.restype = ci
         lib.xc_encode.argtypes = [vp, ci, ci, ci, ci, ci, ci, vp, sz]
         lib.xc_encode.restype = sz
+        lib.xc_encode_ex.argtypes = [vp, ci, ci, ci, ci, ci, ci, ci, ci, ci, vp, sz]
+        lib.xc_encode_ex.restype = sz
         lib.xc_decode.argtypes = [vp, sz, ci, ci, ci, ci, ci, vp]
         lib.xc_decode.restype = ci
         _xlib = lib
@@ -158,13 +160,16 @@ def libjpeg_available() -> Tuple[bool, str]:
 
 
 def libjpeg_encode(img: np.ndarray, quality: int = 85, pixel_format: int = TJPF_BGR,
-                   jpeg_subsample: int = TJSAMP_422, fastdct: bool = False) -> bytes:
+                   jpeg_subsample: int = TJSAMP_422, fastdct: bool = False, restart_interval: int = 0,
+                   restart_rows: int = 0, optimize: bool = False) -> bytes:
+    """libjpeg-turbo as tjCompress2 drives it, plus libjpeg options TurboJPEG leaves at their
+    defaults (restart markers, optimised Huffman tables) for decoder test inputs."""
     img = np.ascontiguousarray(img, dtype=np.uint8)
     h, w = img.shape[:2]
-    cap = _oracle().vfo_jpeg_encode_bound(w, h, jpeg_subsample)
+    cap = _oracle().vfo_jpeg_encode_bound(w, h, jpeg_subsample) + 2 * (w * h // 64 + 16) + 4096
     out = np.empty(cap, np.uint8)
-    n = _x().xc_encode(img.ctypes.data, w, h, int(pixel_format == TJPF_BGR), quality, jpeg_subsample,
-                       int(fastdct), out.ctypes.data, cap)
+    n = _x().xc_encode_ex(img.ctypes.data, w, h, int(pixel_format == TJPF_BGR), quality, jpeg_subsample,
+                          int(fastdct), restart_interval, restart_rows, int(optimize), out.ctypes.data, cap)
     if n == 0:
         raise RuntimeError("libjpeg encode failed: " + libjpeg_available()[1])
     return out[:n].tobytes()

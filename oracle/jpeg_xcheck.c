@@ -198,8 +198,19 @@ int xc_available(char *why, size_t why_len) {
 
 /* tjCompress2(pixel_format, subsamp TJSAMP_*, quality, flags -> dct) through libjpeg.
  * Returns the JPEG size (0 on failure or if it does not fit `cap`). */
+size_t xc_encode_ex(const uint8_t *img, int w, int h, int bgr, int quality, int subsamp, int fastdct,
+                    int restart_interval, int restart_in_rows, int optimize, uint8_t *out, size_t cap);
+
 size_t xc_encode(const uint8_t *img, int w, int h, int bgr, int quality, int subsamp, int fastdct,
                  uint8_t *out, size_t cap) {
+  return xc_encode_ex(img, w, h, bgr, quality, subsamp, fastdct, 0, 0, 0, out, cap);
+}
+
+/* xc_encode plus libjpeg options TurboJPEG does not set: restart_interval (MCUs) or
+ * restart_in_rows (MCU rows) -> DRI + RSTn markers (jcmarker.c / jchuff.c emit_restart), and
+ * optimize_coding -> per-image Huffman tables (jchuff.c jpeg_gen_optimal_table). */
+size_t xc_encode_ex(const uint8_t *img, int w, int h, int bgr, int quality, int subsamp, int fastdct,
+                    int restart_interval, int restart_in_rows, int optimize, uint8_t *out, size_t cap) {
   static const int samp_h[5] = {1, 2, 2, 1, 1}, samp_v[5] = {1, 1, 2, 1, 2};
   if (!xc_available(NULL, 0) || subsamp < 0 || subsamp > 4) return 0;
   cinfo_t c;
@@ -242,6 +253,9 @@ size_t xc_encode(const uint8_t *img, int w, int h, int bgr, int quality, int sub
       *(int *)(c.comp_info + k * COMP_INFO_SIZE + 8) = 1;
       *(int *)(c.comp_info + k * COMP_INFO_SIZE + 12) = 1;
     }
+  c.restart_interval = (unsigned)restart_interval;
+  c.restart_in_rows = restart_in_rows;
+  c.optimize_coding = optimize;
   p_start_compress(&c, 1);
   while (c.next_scanline < (unsigned)h) {
     unsigned char *row = (unsigned char *)img + (size_t)c.next_scanline * w * 3;

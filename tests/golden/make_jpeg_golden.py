@@ -41,6 +41,16 @@ CASES = [  # (name, kind, seed, h, w, quality, subsamp, fastdct)
     ("noise_64x48_q85_422", "noise", 7, 64, 48, 85, J.TJSAMP_422, False),
     ("noise_16x16_q100_444", "noise", 8, 16, 16, 100, J.TJSAMP_444, False),
     ("flat_1x1_q85_422", "flat", 9, 1, 1, 85, J.TJSAMP_422, False),
+    # libjpeg options TurboJPEG leaves off, which a decoder of arbitrary producers meets:
+    # restart intervals (DRI + RSTn; per MCU count or per MCU row) and optimised Huffman tables
+    ("scene_480p_q85_422_dri4", "scene", 10, 480, 640, 85, J.TJSAMP_422, False, {"restart_interval": 4}),
+    ("scene_270x360_q85_420_drirow_opt", "scene", 11, 270, 360, 85, J.TJSAMP_420, False,
+     {"restart_rows": 1, "optimize": True}),
+    ("scene_120x160_q85_gray_dri1", "scene", 12, 120, 160, 85, J.TJSAMP_GRAY, False, {"restart_interval": 1}),
+    ("noise_64x48_q90_444_dri7_opt", "noise", 13, 64, 48, 90, J.TJSAMP_444, False,
+     {"restart_interval": 7, "optimize": True}),
+    ("scene_96x128_q75_440_opt", "scene", 14, 96, 128, 75, J.TJSAMP_440, False, {"optimize": True}),
+    ("scene_33x9_q85_422_dri2", "scene", 15, 33, 9, 85, J.TJSAMP_422, False, {"restart_interval": 2}),
 ]
 
 
@@ -58,9 +68,10 @@ def main():
         sys.exit(f"libjpeg-turbo not usable: {why}")
     os.makedirs(OUT, exist_ok=True)
     cases = []
-    for name, kind, seed, h, w, q, ss, fast in CASES:
+    for name, kind, seed, h, w, q, ss, fast, *opt in CASES:
+        opt = opt[0] if opt else {}
         img = frame(kind, seed, h, w)
-        jpg = J.libjpeg_encode(img, q, J.TJPF_BGR, ss, fast)
+        jpg = J.libjpeg_encode(img, q, J.TJPF_BGR, ss, fast, **opt)
         dec = J.libjpeg_decode(jpg, J.TJPF_BGR)
         inv = J.libjpeg_encode(np.bitwise_not(dec), 85, J.TJPF_BGR, J.TJSAMP_422, False)
         rec = J.libjpeg_encode(dec, 85, J.TJPF_BGR, J.TJSAMP_422, False)
@@ -69,7 +80,7 @@ def main():
             f.write(jpg)
         cases.append({
             "file": fn, "kind": kind, "seed": seed, "shape": [h, w, 3], "quality": q, "subsamp": ss,
-            "fastdct": fast,
+            "fastdct": fast, "libjpeg_options": opt,
             "source_sha256": hashlib.sha256(img.tobytes()).hexdigest(),
             "jpeg_sha256": hashlib.sha256(jpg).hexdigest(),
             "decoded_sha256": hashlib.sha256(dec.tobytes()).hexdigest(),

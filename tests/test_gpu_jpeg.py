@@ -197,6 +197,69 @@ def test_sync_modes_on_hard_content(tj, monkeypatch, mode, subsamp, quality):
         assert g == J.invert_jpeg(j)
 
 
+@pytest.mark.parametrize("mode", ["spec", "pass"])
+def test_custom_tables_long_codes(tj, monkeypatch, mode):
+    """Frames whose Huffman tables are not Annex K (tests/jpeg_recode.py): many codes longer
+    than the decoder's 9-bit lookahead (decoded by the lim / valoff / vals path), codes of up
+    to 16 bits, tables shared by all components, and Annex K frames in the same batch.
+    Bit-exact with the oracle, both sync paths."""
+    import jpeg_recode as R
+    monkeypatch.setenv("VF_JPEG_SYNC", mode)
+    rng = np.random.default_rng(7)
+    srcs = [J.encode(rng.integers(0, 256, (64, 96, 3), dtype=np.uint8), 90, J.TJPF_BGR, J.TJSAMP_422),
+            J.encode(_img("scene", 5, 120, 160), 85, J.TJPF_BGR, J.TJSAMP_420),
+            J.encode(_img("scene", 6, 40, 56), 85, J.TJPF_BGR, J.TJSAMP_GRAY)]
+    jpgs = []
+    for j in srcs:
+        jpgs += [R.recode(j), R.recode(j, dc_long=11, ac_long=10), R.recode(j, ac_long=16, share=True)]
+    jpgs.append(srcs[1])
+    for j in jpgs:
+        assert np.array_equal(tj.decode(j), J.decode(j))
+    assert [bytes(g) for g in tj.invert_batch(jpgs)] == [J.invert_jpeg(j) for j in jpgs]
+
+
+@pytest.mark.parametrize("mode", ["spec", "pass"])
+@pytest.mark.parametrize("subsamp", [0, 1, 2, 3, 4])
+def test_restart_intervals(tj, monkeypatch, mode, subsamp):
+    """DRI streams (restart interval every 1, 2 or 5 MCUs, or every MCU row, with and without
+    optimised tables; made by the image's libjpeg-turbo): each interval is decoded as its own
+    entropy-coded segment, DC prediction reset per interval.  Frames with and without DRI share
+    a batch.  Bit-exact with the oracle (pinned to libjpeg-turbo's DRI decode in
+    tests/test_jpeg_oracle.py), both sync paths."""
+    if not J.libjpeg_available()[0]:
+        pytest.skip("libjpeg-turbo (libjpeg.so.8) not loadable: " + J.libjpeg_available()[1])
+    monkeypatch.setenv("VF_JPEG_SYNC", mode)
+    jpgs = []
+    for i, (h, w) in enumerate([(17, 13), (64, 48), (130, 66), (480, 640)]):
+        img = _img("noise" if i == 1 else "scene", 60 + i, h, w)
+        for k, opt in enumerate([{"restart_interval": 1}, {"restart_interval": 2, "optimize": True},
+                                 {"restart_interval": 5}, {"restart_rows": 1}]):
+            jpgs.append(J.libjpeg_encode(img, 80 + 4 * k, J.TJPF_BGR, subsamp, False, **opt))
+        jpgs.append(J.encode(img, 85, J.TJPF_BGR, subsamp))
+    assert all(J.info(j)["restart_interval"] for j in jpgs[:4])
+    for j in jpgs:
+        assert np.array_equal(tj.decode(j), J.decode(j))
+    assert [bytes(g) for g in tj.invert_batch(jpgs)] == [J.invert_jpeg(j) for j in jpgs]
+
+
+def test_restart_marker_errors(tj, golden_dir):
+    """A DRI stream with a missing, an extra or a misnumbered RSTn is refused (VF_E_JPEG), never
+    decoded into a wrong picture; the same batch position decodes once the stream is intact."""
+    jpg = open(os.path.join(golden_dir, "jpeg", "scene_480p_q85_422_dri4.jpg"), "rb").read()
+    pos = [i for i in range(len(jpg) - 1) if jpg[i] == 0xFF and 0xD0 <= jpg[i + 1] <= 0xD7]
+    assert len(pos) > 10
+    missing = jpg[:pos[5]] + jpg[pos[5] + 2:]
+    renumbered = bytearray(jpg)
+    renumbered[pos[5] + 1] = 0xD0 + ((renumbered[pos[5] + 1] - 0xD0 + 3) & 7)
+    no_dri = bytearray(jpg)
+    d = jpg.index(b"\xff\xdd")
+    no_dri[d + 4:d + 6] = b"\x00\x00"  # DRI 0: markers in a scan without restarts
+    for bad in (missing, bytes(renumbered), bytes(no_dri)):
+        with pytest.raises(VFilterError):
+            tj.decode(bad)
+    assert np.array_equal(tj.decode(jpg), J.decode(jpg))
+
+
 def test_async_submit_keeps_batches_in_flight(tj, vf_ctx):
     """vf_jpeg_invert_submit / _query / _wait / _fetch (the worker's form): batches submitted
     back to back from one thread come back bit-exact, in any collection order; a stream the
