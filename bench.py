@@ -625,8 +625,8 @@ def main():
             torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
-        if have_gpu:
-            torch.cuda.synchronize()
+            if have_gpu:
+                torch.cuda.synchronize()
 
     ctx = Context(device, max_frame_bytes=FRAME_BYTES, max_batch=args.batch)
     srcs, dsts, batch_bytes, host_batch = make_ring(ctx, args.batch, args.ring_gb, np, rank, world)
@@ -637,8 +637,7 @@ def main():
     barrier_sync()
     t0 = time.perf_counter()
     # the K steps, back to back on one stream; a hipEvent pair brackets them on that stream
-    region_ms, _ = ctx.bench_device_ring(srcs, dsts, batch_bytes, args.steps)
-    ctx.sync()
+    region_ms, _ = ctx.bench_device_ring(srcs, dsts, batch_bytes, args.steps)  # returns synchronised
     barrier_sync()
     elapsed = time.perf_counter() - t0
     # untimed: isolated per-launch durations (event pair around each launch) for reference

@@ -75,6 +75,8 @@ struct vf_ctx {
   // submitted vf_jpeg_invert_submit batches: ticket -> the codec that holds it until fetched
   std::map<uint64_t, vf::jpeg::Codec *> jpeg_jobs;
   uint64_t jpeg_next_ticket = 1;
+  // vf_bench_device_ring's region events, created once (not inside a caller's timed region)
+  hipEvent_t bench_ev[2] = {nullptr, nullptr};
 };
 
 namespace {
@@ -250,6 +252,8 @@ VF_EXPORT int vf_destroy(vf_ctx *ctx) {
   if (!ctx) return VF_OK;
   for (vf::jpeg::Codec *c : ctx->jpeg_all) delete c;  // each synchronises its stream first
   delete ctx->engine;  // finishes queued jobs first
+  for (hipEvent_t e : ctx->bench_ev)
+    if (e) (void)hipEventDestroy(e);
   delete ctx;
   return VF_OK;
 }
@@ -484,13 +488,20 @@ VF_EXPORT int vf_bench_device_ring(vf_ctx *ctx, void *const *srcs, void *const *
   VF_HIP(ctx, hipSetDevice(ctx->device));
   hipStream_t st = (hipStream_t)stream;
   const bool each = per_launch_ms != nullptr;
-  std::vector<hipEvent_t> ev((each ? 2 * (size_t)steps : 0) + 2, nullptr);
+  std::vector<hipEvent_t> ev(each ? 2 * (size_t)steps : 0, nullptr);
   int rc = VF_OK;
   for (auto &e : ev) {
     hipError_t h = hipEventCreate(&e);
     if (h != hipSuccess) { rc = fail_hip(ctx, h, "hipEventCreate", __LINE__); break; }
   }
-  hipEvent_t r0 = ev[ev.size() - 2], r1 = ev[ev.size() - 1];
+  // the region pair is the context's, created by the first call (the warm-up): a timed call
+  // then only records, launches and synchronises
+  for (hipEvent_t &e : ctx->bench_ev) {
+    if (rc != VF_OK || e) continue;
+    hipError_t h = hipEventCreate(&e);
+    if (h != hipSuccess) rc = fail_hip(ctx, h, "hipEventCreate", __LINE__);
+  }
+  hipEvent_t r0 = ctx->bench_ev[0], r1 = ctx->bench_ev[1];
   if (rc == VF_OK) {
     hipError_t h = hipEventRecord(r0, st);
     if (h != hipSuccess) rc = fail_hip(ctx, h, "hipEventRecord", __LINE__);
