@@ -389,19 +389,21 @@ def jpeg_mode(ctx, batch, iters=20):
         list(ex.map(lambda _: tj.invert_batch(jpgs), range(10)))
         h2h_pipe = (time.perf_counter() - t0) / 10
     # the worker's form (InverterWorker in JPEG mode): one thread, three batches in flight
-    depth = 3
-    for _ in range(2):  # warm the codecs (a codec's first batch allocates its buffers)
-        ts = [tj.invert_batch_submit(jpgs) for _ in range(depth)]
-        for t in ts:
+    def worker_form(frames, depth=3, reps=21):
+        for _ in range(2):  # warm the codecs (a codec's first batch allocates its buffers)
+            ts = [tj.invert_batch_submit(frames) for _ in range(depth)]
+            for t in ts:
+                tj.invert_batch_result(t)
+        t0 = time.perf_counter()
+        q = [tj.invert_batch_submit(frames) for _ in range(depth - 1)]
+        for _ in range(reps):
+            q.append(tj.invert_batch_submit(frames))
+            tj.invert_batch_result(q.pop(0))
+        for t in q:
             tj.invert_batch_result(t)
-    t0 = time.perf_counter()
-    q = [tj.invert_batch_submit(jpgs) for _ in range(depth - 1)]
-    for _ in range(21):
-        q.append(tj.invert_batch_submit(jpgs))
-        tj.invert_batch_result(q.pop(0))
-    for t in q:
-        tj.invert_batch_result(t)
-    h2h_async = (time.perf_counter() - t0) / (20 + depth)
+        return (time.perf_counter() - t0) / (reps - 1 + depth)
+    h2h_async = worker_form(jpgs)
+    h2h_async2x = worker_form(jpgs + jpgs, reps=11)  # the worker CLI's batch of 64 frames
     outs = tj.invert_batch(jpgs)
     passes = stages.pop("sync_passes", 0.0)
     return {"workload": f"1080p JPEG (q85 4:2:2) decode -> bitwise_not -> encode, batch {batch}",
@@ -412,6 +414,7 @@ def jpeg_mode(ctx, batch, iters=20):
             "host_to_host_fps": round(batch / h2h, 1),
             "host_to_host_2threads_fps": round(batch / h2h_pipe, 1),
             "host_to_host_worker_fps": round(batch / h2h_async, 1),
+            f"host_to_host_worker_batch{2 * batch}_fps": round(2 * batch / h2h_async2x, 1),
             "host_to_host_note": "1 call at a time | 2 host threads | the worker's form: 1 thread, 3 batches "
                                  "in flight (vf_jpeg_invert_submit / _wait / _fetch)",
             "jpeg_bytes_mean": round(sum(len(j) for j in jpgs) / batch)}, jpgs

@@ -213,7 +213,10 @@ def main(argv=None):
                     help="raw H x W x 3 frames (use_jpeg=False); default JPEG frames, as the reference CLI")
     ap.add_argument("--jpeg", action="store_true", help=argparse.SUPPRESS)  # the default; kept for old scripts
     ap.add_argument("--device", type=int, default=None, help="GPU ordinal (default: VF_DEVICE / LOCAL_RANK / 0)")
-    ap.add_argument("--batch", type=int, default=8, help="frames per request (protocol v1)")
+    ap.add_argument("--batch", type=int, default=32,
+                    help="frames per request (protocol v1; default 32, the batch every distributor "
+                         "leg of bench.py measures; 64 moves 1080p JPEG through the system by no more "
+                         "than run-to-run spread: profiles/r02_pipeline_jpeg_batch64.txt)")
     ap.add_argument("--inflight", type=int, default=None,
                     help="batches in progress at once (protocol v1; default 3 for JPEG, 2 for raw)")
     ap.add_argument("--protocol", choices=("v0", "v1"), default="v1",

@@ -70,7 +70,7 @@ def run(size, mode, batch=32, reps=24):
 if __name__ == "__main__":
     size = sys.argv[1] if len(sys.argv) > 1 else "1080p"
     if len(sys.argv) > 2:
-        run(size, sys.argv[2])
+        run(size, sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 32)
     else:
         for mode in ("1thread", "2threads", "async"):
             env = dict(os.environ)
