@@ -377,17 +377,17 @@ def jpeg_mode(ctx, batch, iters=20):
     ctx.jpeg_bench_invert(jpgs, 85, 1, 0, iters=2)
     ms, stages = ctx.jpeg_bench_invert(jpgs, 85, 1, 0, iters=iters)
     tj.invert_batch(jpgs)
-    reps = 5
+    reps = 15
     t0 = time.perf_counter()
     for _ in range(reps):
         tj.invert_batch(jpgs)
     h2h = (time.perf_counter() - t0) / reps
     from concurrent.futures import ThreadPoolExecutor
     with ThreadPoolExecutor(2) as ex:  # two host threads, one call each at a time
-        list(ex.map(lambda _: tj.invert_batch(jpgs), range(2)))
+        list(ex.map(lambda _: tj.invert_batch(jpgs), range(4)))
         t0 = time.perf_counter()
-        list(ex.map(lambda _: tj.invert_batch(jpgs), range(10)))
-        h2h_pipe = (time.perf_counter() - t0) / 10
+        list(ex.map(lambda _: tj.invert_batch(jpgs), range(30)))
+        h2h_pipe = (time.perf_counter() - t0) / 30
     # the worker's form (InverterWorker in JPEG mode): one thread, three batches in flight
     def worker_form(frames, depth=3, reps=21):
         for _ in range(2):  # warm the codecs (a codec's first batch allocates its buffers)
