@@ -13,4 +13,4 @@ VF_DEVICE=0 BENCH_DIST_BACKEND=gloo timeout -k 10 600 python -m torch.distribute
 cut -c1-400 gpurun_out/r2_bench_n2_rehearsal.json
 rm -rf gpurun_out/prof_bench
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_bench -o bench -- python3 bench.py --steps 300 --warmup 30 --no-traffic --no-e2e --no-jpeg --no-distributor --no-sizes --no-sweep --cpu-seconds 0 > gpurun_out/r2_bench_under_rocprof.json 2> gpurun_out/r2_bench_rocprof.log || { echo ROCPROF_FAILED; tail -20 gpurun_out/r2_bench_rocprof.log; exit 1; }
-grep -h invert_stream gpurun_out/prof_bench/*/*kernel_stats.csv gpurun_out/prof_bench/*kernel_stats.csv 2>/dev/null | cut -c1-300
+grep -h invert_stream gpurun_out/prof_bench/bench_kernel_stats.csv | cut -c1-300
