@@ -666,6 +666,9 @@ int Codec::prepare_decode(const uint8_t *const *jpegs, const size_t *sizes, int 
     // process_restart / jdmarker.c read_restart_marker; libjpeg-turbo resynchronises on a
     // missing or misnumbered one with a corrupt-data warning -- refused here)
     const size_t nint = P.restart ? ((size_t)F.g.nmcu + P.restart - 1) / P.restart : 1;
+    // a marker after the last interval with nothing behind it (some encoders end the scan
+    // with one) closes an empty interval: dropped, as libjpeg-turbo skips it
+    while (P.rst.size() + 1 > nint && P.rst.back().second + 2 >= P.scan_end) P.rst.pop_back();
     if (P.rst.size() + 1 != nint) {
       e = P.restart ? "restart markers missing or extra (corrupt JPEG)" : "RSTn marker in a scan without DRI";
       return;

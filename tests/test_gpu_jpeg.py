@@ -258,6 +258,11 @@ def test_restart_marker_errors(tj, golden_dir):
         with pytest.raises(VFilterError):
             tj.decode(bad)
     assert np.array_equal(tj.decode(jpg), J.decode(jpg))
+    # a trailing RSTn with no interval behind it (written by some encoders) is skipped
+    eoi = jpg.rindex(b"\xff\xd9")
+    k = (len(pos)) & 7
+    trailing = jpg[:eoi] + bytes([0xFF, 0xD0 + k]) + jpg[eoi:]
+    assert np.array_equal(tj.decode(trailing), J.decode(jpg))
 
 
 def test_async_submit_keeps_batches_in_flight(tj, vf_ctx):
