@@ -175,6 +175,10 @@ hipError_t dec_sync_spec(const DecSeg *sg, const DecFrame *fr, int nseg, uint32_
 hipError_t dec_write(const DecSeg *sg, const DecFrame *fr, int nseg, uint32_t max_sub, const uint8_t *us, const uint32_t *us_len,
                      const uint64_t *exits, const uint32_t *bstart, int16_t *coef, int32_t *dcseq,
                      hipStream_t s);
+// the write pass with 4 lanes per subsequence from the pass-based sync's converged checkpoints
+hipError_t dec_write4(const DecSeg *sg, const DecFrame *fr, int nseg, uint32_t max_sub, const uint8_t *us,
+                      const uint32_t *us_len, const uint64_t *exits, const uint32_t *cnt, const uint64_t *ck,
+                      const uint32_t *ckrem, const uint32_t *bstart, int16_t *coef, int32_t *dcseq, hipStream_t s);
 hipError_t dec_idct(const DecFrame *fr, int n, uint32_t max_blocks, const int16_t *coef, const int32_t *dcseq,
                     uint8_t *planes, hipStream_t s);
 hipError_t dec_color(const DecFrame *fr, int n, int max_w, int max_h, const uint8_t *planes, uint8_t *pix,

@@ -945,8 +945,19 @@ int Codec::run_decode(int bgr, bool invert, std::string *err) {
   CK(scan_u32(segs + ns, ns, (dmax_sub_ + kScanTile - 1) / kScanTile, d_cnt_[last].as<uint32_t>(),
               d_bstart_.as<uint32_t>(), d_tsum_.as<uint32_t>(), blocks_total, false, s_));
   CK(hipMemsetAsync(d_coef_.p, 0, dblocks_ * 128, s_));
-  CK(dec_write(sg, fr, ns, dmax_sub_, d_us_.as<uint8_t>(), us_len, d_exit_[last].as<uint64_t>(),
-               d_bstart_.as<uint32_t>(), d_coef_.as<int16_t>(), d_dcseq_.as<int32_t>(), s_));
+  // after the pass-based sync, every subsequence's checkpoints are states of the true path: the
+  // write pass runs 4 lanes per subsequence from them (VF_JPEG_WRITE4=0: one lane)
+  const bool write4 = [] {  // read per call: tests switch it inside one process
+    const char *v = std::getenv("VF_JPEG_WRITE4");
+    return !(v && std::strcmp(v, "0") == 0);
+  }();
+  if (!use_spec && write4)
+    CK(dec_write4(sg, fr, ns, dmax_sub_, d_us_.as<uint8_t>(), us_len, d_exit_[last].as<uint64_t>(),
+                  d_cnt_[last].as<uint32_t>(), d_ck_.as<uint64_t>(), d_ckrem_.as<uint32_t>(),
+                  d_bstart_.as<uint32_t>(), d_coef_.as<int16_t>(), d_dcseq_.as<int32_t>(), s_));
+  else
+    CK(dec_write(sg, fr, ns, dmax_sub_, d_us_.as<uint8_t>(), us_len, d_exit_[last].as<uint64_t>(),
+                 d_bstart_.as<uint32_t>(), d_coef_.as<int16_t>(), d_dcseq_.as<int32_t>(), s_));
   CK(hipEventRecord(ev_[3], s_));
   // 4. DC prediction (inclusive scan per component sequence)
   CK(scan_i32(segs + 2 * ns, ndcseg_, dc_max_tiles_, d_dcseq_.as<int32_t>(), d_dcseq_.as<int32_t>(),

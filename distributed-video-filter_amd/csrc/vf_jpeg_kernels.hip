@@ -998,6 +998,59 @@ __global__ __launch_bounds__(256) void k_write(const DecSeg *sg, const DecFrame 
                     S.dcbase);
 }
 
+// The write pass with 4 lanes per subsequence, for the pass-based sync (k_sync), whose
+// converged checkpoints are states of the true path: ck[m] = (pos, z, c) at the first symbol
+// boundary at or past mark m, ckrem[m] = blocks completed from there to the subsequence's end
+// (kNoCk where the entry state lies past the mark).  Lane q decodes from checkpoint q - 1 (lane
+// 0 from the entry state) up to the next lane's start: the decode of a subsequence, a chain of
+// dependent table lookups, runs as 4 shorter chains side by side.  A lane whose checkpoint is
+// missing idles and the lane before it decodes on.
+__global__ __launch_bounds__(256) void k_write4(const DecSeg *sg, const DecFrame *fr, const uint8_t *us,
+                                                const uint32_t *us_len, const uint64_t *exits, const uint32_t *cnt,
+                                                const uint64_t *ck, const uint32_t *ckrem, const uint32_t *bstart,
+                                                int16_t *coef, int32_t *dcseq) {
+  static_assert(kCk + 1 == 4, "one lane per checkpoint-delimited quarter");
+  constexpr uint32_t kSubsPerWg = 64, kW4Words = kSubsPerWg * (kSubBits / 32) + kSpecPadWords;
+  __shared__ HuffDec tabs[6];
+  __shared__ uint32_t s_w[kW4Words];
+  const DecSeg &S = sg[blockIdx.y];
+  const DecFrame &F = fr[S.frame];
+  if (blockIdx.x * kSubsPerWg >= S.nsub_max) return;
+  const uint32_t woff = blockIdx.x * kSubsPerWg * (kSubBits / 32);
+  const uint32_t fwords = (((S.in_len + 64) + 15) & ~15u) / 4;
+  const uint32_t *gw = reinterpret_cast<const uint32_t *>(us + S.us_off);
+  for (uint32_t k = threadIdx.x; k < kW4Words; k += 256) s_w[k] = woff + k < fwords ? gw[woff + k] : 0u;
+  load_tables(F, tabs);  // its barrier also publishes s_w
+  const uint32_t i = blockIdx.x * kSubsPerWg + (threadIdx.x >> 2), q = threadIdx.x & 3;
+  const uint32_t nbits = us_len[blockIdx.y] * 8u;
+  const uint32_t nsub = (nbits + kSubBits - 1) / kSubBits;
+  if (i >= nsub) return;
+  const uint32_t gi = S.sub0 + i;
+  const uint64_t *cki = ck + (uint64_t)gi * kCk;
+  uint64_t st;
+  uint32_t before = 0;
+  if (q == 0) {
+    st = i == 0 ? 0 : exits[gi - 1];
+  } else {
+    st = cki[q - 1];
+    if (st == kNoCk) return;
+    before = cnt[gi] - ckrem[(uint64_t)gi * kCk + q - 1];
+  }
+  uint32_t stop = (i + 1 == nsub) ? nbits : (i + 1) * kSubBits;
+  for (uint32_t m = q; m < kCk; ++m)
+    if (cki[m] != kNoCk) {
+      stop = (uint32_t)(cki[m] >> 16);
+      break;
+    }
+  BitReader br;
+  br.init_words(s_w, (uint32_t)(st >> 16), woff);
+  uint32_t z = (st >> 8) & 0xFF, c = st & 0xFF, blocks = 0;
+  HuffGeom hg(F.g);
+  hg.nblocks = S.nblocks;
+  decode_span<true>(br, stop, z, c, blocks, hg, tabs, tabs + 3, bstart[gi] + before, coef + S.blk0 * 64, dcseq,
+                    S.dcbase);
+}
+
 // ---- decoder: IDCT -------------------------------------------------------------------------
 
 #define FIX_0_298631336 2446
@@ -2019,6 +2072,15 @@ hipError_t dec_write(const DecSeg *sg, const DecFrame *fr, int nseg, uint32_t ma
   if (nseg <= 0 || !max_sub) return hipSuccess;
   hipLaunchKernelGGL(k_write, dim3((max_sub + 255) / 256, (unsigned)nseg), dim3(256), 0, s, sg, fr, us, us_len, exits,
                      bstart, coef, dcseq);
+  return hipGetLastError();
+}
+
+hipError_t dec_write4(const DecSeg *sg, const DecFrame *fr, int nseg, uint32_t max_sub, const uint8_t *us,
+                      const uint32_t *us_len, const uint64_t *exits, const uint32_t *cnt, const uint64_t *ck,
+                      const uint32_t *ckrem, const uint32_t *bstart, int16_t *coef, int32_t *dcseq, hipStream_t s) {
+  if (nseg <= 0 || !max_sub) return hipSuccess;
+  hipLaunchKernelGGL(k_write4, dim3((max_sub + 63) / 64, (unsigned)nseg), dim3(256), 0, s, sg, fr, us, us_len, exits,
+                     cnt, ck, ckrem, bstart, coef, dcseq);
   return hipGetLastError();
 }
 

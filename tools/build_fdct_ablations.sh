@@ -1,8 +1,8 @@
-# Timing-only ablations of k_fdct, built from patched copies in a temp dir (the product source
+# Timing-only ablations of k_fdct / k_write (ABL_VARIANTS: nopix noac nocoef), built from patched copies in a temp dir (the product source
 # is not touched): tools/libv_abl_{nopix,noac,nopack}.so.  Outputs are NOT valid JPEGs.
 set -e
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
-for v in nopix noac; do
+for v in ${ABL_VARIANTS:-nopix noac}; do
   T=$(mktemp -d)
   mkdir -p "$T/distributed-video-filter_amd"
   cp -r "$ROOT/distributed-video-filter_amd/csrc" "$T/distributed-video-filter_amd/"
@@ -18,6 +18,10 @@ if v == "nopix":   # pass 1 without pixel loads / colour conversion: a synthetic
 if v == "noac":    # no AC coding: DC and an empty AC stream per block
     a = "  // AC Huffman coding; every lane of the wave takes part in the 8-lane shuffles\n"
     b = a + "  if (real && r == 0) { dcq[F.blk0 + b] = qo[slot][qo_at(slot, 0)]; acbits[F.blk0 + b] = 0; }\n  return;\n"
+    assert s.count(a) == 1; s = s.replace(a, b)
+if v == "nocoef":  # Huffman write without the coefficient stores (DC sequence still written)
+    a = "        if (WRITE) coef[(uint64_t)blk * 64 + (z < 63 ? z : 63)] = (int16_t)v;"
+    b = "        if (WRITE && v == 0x7fffffff) coef[(uint64_t)blk * 64 + (z < 63 ? z : 63)] = (int16_t)v;"
     assert s.count(a) == 1; s = s.replace(a, b)
 open(p, "w").write(s)
 PY
