@@ -188,7 +188,9 @@ int vf_last_timeline(const vf_ctx *ctx, float *out4, size_t *chunk_bytes, int ma
  * pointers) back to back on `stream`, then synchronise.  A hipEvent pair brackets the whole
  * sequence; its duration (ms) goes to *region_ms (may be NULL).  If per_launch_ms is not
  * NULL, an extra event pair is recorded around every launch and each launch's duration goes
- * to per_launch_ms[s] (the pairs add a few microseconds of gap per launch). */
+ * to per_launch_ms[s] (the pairs add a few microseconds of gap per launch).  The region pair
+ * belongs to the context and is created by its first call (so a timed call only records,
+ * launches and synchronises): calls on one context must not overlap. */
 int vf_bench_device_ring(vf_ctx *ctx, void *const *srcs, void *const *dsts, int nbuf,
                          size_t nbytes, int steps, void *stream, float *per_launch_ms,
                          float *region_ms);
