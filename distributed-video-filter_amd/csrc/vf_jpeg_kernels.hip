@@ -193,11 +193,15 @@ __global__ __launch_bounds__(256) void k_unstuff_write(const DecSeg *sg, const u
 
 // ---- decoder: Huffman ------------------------------------------------------------------------
 
+// The next word is loaded one refill ahead (nxt), so a refill costs no memory wait of its
+// own: the load is in flight with the symbol lookups that follow it, and LDS completes in
+// order.  A reader therefore reads up to 3 words past its position.
 struct BitReader {
   const uint32_t *w;  // words of the stream from word `woff` on (global memory or an LDS copy)
   uint64_t buf;  // next bits, left-aligned
   uint32_t nb;   // valid bits in buf
-  uint32_t wi;   // next word to load (minus woff)
+  uint32_t wi;   // index of nxt (minus woff)
+  uint32_t nxt;  // the next word, loaded ahead
   uint32_t pos;  // bit position of the next unread bit
   __device__ __forceinline__ void init(const uint8_t *base, uint32_t p) {
     init_words(reinterpret_cast<const uint32_t *>(base), p, 0);
@@ -207,6 +211,7 @@ struct BitReader {
     wi = (p >> 5) - woff;
     buf = ((uint64_t)bswap32(w[wi]) << 32) | bswap32(w[wi + 1]);
     wi += 2;
+    nxt = w[wi];
     const uint32_t sk = p & 31;
     buf <<= sk;
     nb = 64 - sk;
@@ -214,8 +219,9 @@ struct BitReader {
   }
   __device__ __forceinline__ void refill() {  // afterwards nb >= 33
     if (nb <= 32) {
-      buf |= (uint64_t)bswap32(w[wi++]) << (32 - nb);
+      buf |= (uint64_t)bswap32(nxt) << (32 - nb);
       nb += 32;
+      nxt = w[++wi];
     }
   }
   __device__ __forceinline__ uint32_t peek(uint32_t n) const { return (uint32_t)(buf >> (64 - n)); }
@@ -897,7 +903,7 @@ __global__ __launch_bounds__(256) void k_resolve(const DecSeg *sg, const DecFram
         BitReader br;
         br.init_words(s_tw, (uint32_t)(X >> 16), w0);
         uint32_t z = (X >> 8) & 0xFF, c = X & 0xFF, n = 0;
-        const uint32_t lim = min(ek, (w0 + kTraceWords - 3) * 32u);  // stays inside s_tw (binds only on corrupt data)
+        const uint32_t lim = min(ek, (w0 + kTraceWords - 4) * 32u);  // stays inside s_tw (binds only on corrupt data)
         while (br.pos < lim) sync_step(br, z, c, n, hg, tabs, tabs + 3);
         X = pack_state(br.pos, z, c);
         B.pX[slot(w, k, 0)] = X;
