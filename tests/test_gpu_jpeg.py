@@ -179,13 +179,16 @@ def test_concurrent_calls_lease_separate_codecs(tj):
     assert not errors, errors[:3]
 
 
-@pytest.mark.parametrize("mode", ["spec", "pass"])
+@pytest.mark.parametrize("mode", ["spec", "pass", "pass-1lane"])
 @pytest.mark.parametrize("subsamp,quality", [(J.TJSAMP_420, 95), (J.TJSAMP_444, 90), (J.TJSAMP_422, 85)])
 def test_sync_modes_on_hard_content(tj, monkeypatch, mode, subsamp, quality):
     """Both Huffman synchronisation paths (speculative trajectories + links, and the
-    pass-based chain) on content with long blocks (noise: links rejoin late, walkers and the
-    resolver decode explicit states) and a mixed batch, bit-exact with the oracle."""
-    monkeypatch.setenv("VF_JPEG_SYNC", mode)
+    pass-based chain, whose write pass runs 4 lanes per subsequence from the converged
+    checkpoints, or one with VF_JPEG_WRITE4=0) on content with long blocks (noise: links rejoin
+    late, walkers and the resolver decode explicit states) and a mixed batch, bit-exact with
+    the oracle."""
+    monkeypatch.setenv("VF_JPEG_SYNC", mode.split("-")[0])
+    monkeypatch.setenv("VF_JPEG_WRITE4", "0" if mode == "pass-1lane" else "1")
     rng = np.random.default_rng(quality)
     imgs = [rng.integers(0, 256, (256, 320, 3), dtype=np.uint8),
             _img("scene", 3, 480, 640),
