@@ -1777,10 +1777,19 @@ __global__ __launch_bounds__(256) void k_fdct(const EncFrame *fr, const EncTable
   const uint32_t total = last8(incl);
   if (real && nbits) {
     LdsBits out(acw[slot], incl - nbits);
+    // codes in pairs: one put for codes j and j + 1 when no ZRL comes between them and they fit
+    // 32 bits together (zero coefficients have clen 0); the second put is skipped by the whole
+    // wave when every lane merged its pair
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < 8; j += 2) {
       for (uint32_t z = nzr[j]; z; --z) out.put(zrl >> 8, zlen);
-      out.put(code[j], clen[j]);  // clen 0 for a zero coefficient: an idempotent OR
+      const uint32_t l2 = clen[j] + clen[j + 1];
+      const bool m = nzr[j + 1] == 0 && l2 <= 32;
+      out.put(m ? (code[j] << clen[j + 1]) | code[j + 1] : code[j], m ? l2 : clen[j]);
+      if (__ballot(!m)) {
+        for (uint32_t z = nzr[j + 1]; z; --z) out.put(zrl >> 8, zlen);
+        out.put(m ? 0u : code[j + 1], m ? 0u : clen[j + 1]);  // clen 0: an idempotent OR
+      }
     }
     const bool e = r == 7 && eob;
     out.put(e ? eobc >> 8 : 0u, e ? eobc & 0xFF : 0u);
