@@ -1777,22 +1777,34 @@ __global__ __launch_bounds__(256) void k_fdct(const EncFrame *fr, const EncTable
   const uint32_t total = last8(incl);
   if (real && nbits) {
     LdsBits out(acw[slot], incl - nbits);
-    // codes in pairs: one put for codes j and j + 1 when no ZRL comes between them and they fit
-    // 32 bits together (zero coefficients have clen 0); the second put is skipped by the whole
-    // wave when every lane merged its pair
-#pragma unroll
-    for (int j = 0; j < 8; j += 2) {
-      for (uint32_t z = nzr[j]; z; --z) out.put(zrl >> 8, zlen);
-      const uint32_t l2 = clen[j] + clen[j + 1];
-      const bool m = nzr[j + 1] == 0 && l2 <= 32;
-      out.put(m ? (code[j] << clen[j + 1]) | code[j + 1] : code[j], m ? l2 : clen[j]);
-      if (__ballot(!m)) {
-        for (uint32_t z = nzr[j + 1]; z; --z) out.put(zrl >> 8, zlen);
-        out.put(m ? 0u : code[j + 1], m ? 0u : clen[j + 1]);  // clen 0: an idempotent OR
-      }
-    }
     const bool e = r == 7 && eob;
-    out.put(e ? eobc >> 8 : 0u, e ? eobc & 0xFF : 0u);
+    // A lane whose bits (no ZRL) fit 64 concatenates its codes (and the EOB) in a register and
+    // writes them with two puts; the other lanes write codes in pairs (one put for codes j and
+    // j + 1 when no ZRL comes between them and they fit 32 bits), the second put of a pair
+    // skipped wave-wide when every lane merged it.  Zero coefficients have clen 0, and a
+    // zero-length put is an idempotent OR.
+    const bool fast = nbits <= 64 && (nzr[0] | nzr[1] | nzr[2] | nzr[3] | nzr[4] | nzr[5] | nzr[6] | nzr[7]) == 0;
+    uint64_t v = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v = (v << clen[j]) | code[j];
+    if (e) v = (v << (eobc & 0xFF)) | (eobc >> 8);
+    const bool two = fast && nbits > 32;
+    out.put(fast ? (uint32_t)(two ? v >> 32 : v) : 0u, fast ? (two ? nbits - 32 : nbits) : 0u);
+    out.put(two ? (uint32_t)v : 0u, two ? 32u : 0u);
+    if (__ballot(!fast)) {
+#pragma unroll
+      for (int j = 0; j < 8; j += 2) {
+        for (uint32_t z = fast ? 0u : nzr[j]; z; --z) out.put(zrl >> 8, zlen);
+        const uint32_t l2 = clen[j] + clen[j + 1];
+        const bool m = nzr[j + 1] == 0 && l2 <= 32;
+        out.put(fast ? 0u : m ? (code[j] << clen[j + 1]) | code[j + 1] : code[j], fast ? 0u : m ? l2 : clen[j]);
+        if (__ballot(!fast && !m)) {
+          for (uint32_t z = fast ? 0u : nzr[j + 1]; z; --z) out.put(zrl >> 8, zlen);
+          out.put(fast || m ? 0u : code[j + 1], fast || m ? 0u : clen[j + 1]);
+        }
+      }
+      out.put(!fast && e ? eobc >> 8 : 0u, !fast && e ? eobc & 0xFF : 0u);
+    }
     out.finish();
   }
   __syncthreads();
