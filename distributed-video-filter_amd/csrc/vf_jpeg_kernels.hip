@@ -304,41 +304,34 @@ __device__ __forceinline__ void decode_span(BitReader &br, uint32_t end, uint32_
 #pragma unroll
     for (int k = 0; k < 3; ++k) dcb[k] = dcbase[k];
   }
+  // One path for DC and AC symbols (a wave's lanes are at different places in their blocks;
+  // two paths meant both ran every step), and the MCU index kept as a counter instead of a
+  // division per DC symbol.
+  uint32_t mcu = blk / g.bpm;
   while (br.pos < end) {
     if (WRITE && blk >= g.nblocks) break;
     br.refill();
     const uint32_t k = g.comp(c);
-    if (z == 0) {
-      uint32_t s = huff_sym(br, dcT[k]);
-      int v = 0;
-      if (s) {
-        if (s > 16) s = 16;  // corrupt table
-        v = extend(br.peek(s), s);
-        br.skip(s);
-      }
-      if (WRITE) {
-        const uint32_t mcu = blk / g.bpm;
-        dcseq[HuffGeom::sel(dcb, k) + (uint64_t)mcu * HuffGeom::sel(g.bpc, k) + (c - HuffGeom::sel(g.cfirst, k))] = v;
-      }
-      z = 1;
-    } else {
-      const uint32_t rs = huff_sym(br, acT[k]);
-      const uint32_t r = rs >> 4, s = rs & 15;
-      if (s) {
-        z += r;
-        const int v = extend(br.peek(s), s);
-        br.skip(s);
-        if (WRITE) coef[(uint64_t)blk * 64 + (z < 63 ? z : 63)] = (int16_t)v;
-        z++;
-      } else if (r == 15) {
-        z += 16;
-      } else {
-        z = 64;
-      }
+    const bool dc = z == 0;
+    const uint32_t sym = huff_sym(br, dc ? dcT[k] : acT[k]);
+    const uint32_t r = dc ? 0u : sym >> 4;
+    const uint32_t s = dc ? (sym > 16 ? 16u : sym) : (sym & 15);  // DC > 16: corrupt table
+    int v = 0;
+    if (s) {
+      v = extend(br.peek(s), s);
+      br.skip(s);
     }
+    if (WRITE) {
+      if (dc)
+        dcseq[HuffGeom::sel(dcb, k) + (uint64_t)mcu * HuffGeom::sel(g.bpc, k) + (c - HuffGeom::sel(g.cfirst, k))] = v;
+      else if (s)
+        coef[(uint64_t)blk * 64 + (z + r < 63 ? z + r : 63)] = (int16_t)v;
+    }
+    z = dc ? 1u : s ? z + r + 1 : r == 15 ? z + 16 : 64u;
     if (z >= 64) {
       z = 0;
       c = (c + 1 == g.bpm) ? 0 : c + 1;
+      mcu += c == 0 ? 1u : 0u;
       ++blocks;
       ++blk;
     }
