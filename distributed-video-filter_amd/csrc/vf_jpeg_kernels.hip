@@ -1814,42 +1814,6 @@ __global__ __launch_bounds__(256) void k_fdct(const EncFrame *fr, const EncTable
 
 // ---- encoder: DC coding, bit offsets, packing --------------------------------------------------
 
-// Quantised DC of block-in-MCU c of MCU `mcu`, following jccoefct.c for dummy blocks: a dummy
-// block at the right edge takes its left neighbour's DC, a dummy row at the bottom the DC of
-// the component's last block in the row above (within the MCU).
-__device__ __forceinline__ int enc_dc_of(const Geom &g, const int16_t *dcq, uint32_t mcu, uint32_t c) {
-  const int k = g.bcomp[c];
-  int xi = g.bxo[c], yi = g.byo[c];
-  const int mx = (int)(mcu % (uint32_t)g.mcux), my = (int)(mcu / (uint32_t)g.mcux);
-  for (;;) {
-    const int bx = mx * g.mh[k] + xi, by = my * g.mv[k] + yi;
-    if (by >= g.hb[k]) {
-      yi -= 1;
-      xi = g.mh[k] - 1;
-      continue;
-    }
-    if (bx >= g.wb[k]) {
-      xi -= 1;
-      continue;
-    }
-    return dcq[(uint64_t)mcu * g.bpm + (uint32_t)(g.cfirst[k] + yi * g.mh[k] + xi)];
-  }
-}
-
-// DC difference of block b (jchuff.c: diff to the previous block of the same component in
-// scan order) and whether b is a dummy edge block
-__device__ __forceinline__ int enc_dc_diff(const Geom &g, const int16_t *dcq, uint32_t b, bool *dummy) {
-  const uint32_t mcu = b / (uint32_t)g.bpm, c = b % (uint32_t)g.bpm;
-  const int k = g.bcomp[c];
-  const int dc = enc_dc_of(g, dcq, mcu, c);
-  int pred = 0;
-  if ((int)c > g.cfirst[k]) pred = enc_dc_of(g, dcq, mcu, c - 1);
-  else if (mcu > 0) pred = enc_dc_of(g, dcq, mcu - 1, (uint32_t)(g.cfirst[k] + g.mh[k] * g.mv[k] - 1));
-  const int mx = (int)(mcu % (uint32_t)g.mcux), my = (int)(mcu / (uint32_t)g.mcux);
-  *dummy = mx * g.mh[k] + g.bxo[c] >= g.wb[k] || my * g.mv[k] + g.byo[c] >= g.hb[k];
-  return dc - pred;
-}
-
 struct BitSink {  // MSB-first bits into big-endian words at a bit offset
   uint32_t *w;
   uint32_t wi;
@@ -1886,19 +1850,55 @@ __device__ __forceinline__ uint32_t dc_category(int diff) {
 // bits << 5) | their length (<= 16 + 11 bits), and for a dummy block acbits = kDummyAc |
 // (EOB code << 5) | EOB length (k_fdct never writes a dummy block's acbits).
 constexpr uint32_t kDummyAc = 0x80000000u;
+// A wave takes block-in-MCU c of 64 consecutive MCUs (as k_fdct groups them): the component,
+// its geometry and its tables are wave-uniform (scalar), and each lane locates its MCU with
+// one division instead of several per DC lookup.
+__device__ __forceinline__ int enc_dc_at(const Geom &g, const int16_t *dcq, int mx, int my, int xi, int yi, int mh,
+                                         int mv, int wb, int hb, int cf) {
+  for (;;) {  // jccoefct.c dummy blocks: the left neighbour, or the last block of the row above
+    const int bx = mx * mh + xi, by = my * mv + yi;
+    if (by >= hb) {
+      yi -= 1;
+      xi = mh - 1;
+      continue;
+    }
+    if (bx >= wb) {
+      xi -= 1;
+      continue;
+    }
+    return dcq[((uint64_t)my * (uint32_t)g.mcux + (uint32_t)mx) * (uint32_t)g.bpm + (uint32_t)(cf + yi * mh + xi)];
+  }
+}
+
 __global__ __launch_bounds__(256) void k_len(const EncFrame *fr, const EncTables *tab, const int16_t *dcq,
                                              uint32_t *acbits, uint32_t *bits, uint32_t *pre) {
   const EncFrame &F = fr[blockIdx.y];
   const Geom &g = F.g;
-  const uint32_t b = blockIdx.x * 256 + threadIdx.x;
-  if (b >= (uint32_t)g.nblocks) return;
-  bool dummy;
-  const int diff = enc_dc_diff(g, dcq + F.blk0, b, &dummy);
-  const int t = g.bcomp[b % (uint32_t)g.bpm] > 0;
+  const uint32_t bpm = (uint32_t)g.bpm, nmcu = (uint32_t)g.nmcu, mcux = (uint32_t)g.mcux;
+  const uint32_t ngroups = (nmcu + 63) / 64;
+  const uint32_t unit = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (unit >= ngroups * bpm) return;
+  const uint32_t grp = unit / bpm, c = unit - grp * bpm;  // scalar
+  const uint32_t mcu = grp * 64 + (threadIdx.x & 63);
+  if (mcu >= nmcu) return;
+  const int k = g.bcomp[c], mh = g.mh[k], mv = g.mv[k], wb = g.wb[k], hb = g.hb[k], cf = g.cfirst[k];
+  int mx = (int)((grp * 64) % mcux + (threadIdx.x & 63)), my = (int)((grp * 64) / mcux);
+  while (mx >= (int)mcux) mx -= (int)mcux, ++my;  // once at most unless the frame is under 64 MCUs wide
+  const int dc = enc_dc_at(g, dcq + F.blk0, mx, my, g.bxo[c], g.byo[c], mh, mv, wb, hb, cf);
+  int pred = 0;  // jchuff.c: the previous block of the same component in scan order
+  if ((int)c > cf) {
+    pred = enc_dc_at(g, dcq + F.blk0, mx, my, g.bxo[c - 1], g.byo[c - 1], mh, mv, wb, hb, cf);
+  } else if (mcu > 0) {
+    const int pmx = mx > 0 ? mx - 1 : (int)mcux - 1, pmy = mx > 0 ? my : my - 1;
+    pred = enc_dc_at(g, dcq + F.blk0, pmx, pmy, mh - 1, mv - 1, mh, mv, wb, hb, cf);
+  }
+  const bool dummy = mx * mh + g.bxo[c] >= wb || my * mv + g.byo[c] >= hb;
+  const int diff = dc - pred;
+  const int t = k > 0;
   const uint32_t nb = dc_category(diff);
   const uint32_t e = tab->dc[t][nb];
   const uint32_t extra = nb ? ((uint32_t)(diff < 0 ? diff - 1 : diff) & ((1u << nb) - 1)) : 0u;
-  const uint64_t gb = F.blk0 + b;
+  const uint64_t gb = F.blk0 + (uint64_t)mcu * bpm + c;
   pre[gb] = ((((e >> 8) << nb) | extra) << 5) | ((e & 0xFF) + nb);
   uint32_t ac;
   if (dummy) {
@@ -2133,8 +2133,9 @@ hipError_t enc_fdct(const EncFrame *fr, int n, uint32_t max_blocks, const EncTab
 hipError_t enc_len(const EncFrame *fr, int n, uint32_t max_blocks, const EncTables *tab, const int16_t *dcq,
                    uint32_t *acbits, uint32_t *bits, uint32_t *pre, hipStream_t s) {
   if (n <= 0 || !max_blocks) return hipSuccess;
-  hipLaunchKernelGGL(k_len, dim3((max_blocks + 255) / 256, (unsigned)n), dim3(256), 0, s, fr, tab, dcq, acbits, bits,
-                     pre);
+  // 4 units of 64 MCUs per workgroup; a frame has ceil(nmcu / 64) * bpm <= nblocks / 64 + 10 units
+  hipLaunchKernelGGL(k_len, dim3((max_blocks / 64 + 10 + 3) / 4, (unsigned)n), dim3(256), 0, s, fr, tab, dcq, acbits,
+                     bits, pre);
   return hipGetLastError();
 }
 
