@@ -781,26 +781,44 @@ __global__ __launch_bounds__(256) void k_spec(const DecSeg *sg, const DecFrame *
 // into the first subsequence of w.  16 boundaries per workgroup, one lane per j.
 __global__ __launch_bounds__(256) void k_wglink(const DecSeg *sg, const DecFrame *fr, const uint8_t *us, const uint32_t *us_len,
                                                 SpecBufs B) {
+  constexpr uint32_t kLinkWords = kSubBits / 32 + kSpecPadWords;  // as k_spec's window for one subsequence
   __shared__ HuffSync tabs[6];
+  __shared__ uint32_t s_lw[16][kLinkWords];
+  __shared__ uint64_t s_ck[16][kSpecLanesMax * kCk];
+  __shared__ uint32_t s_rem[16][kSpecLanesMax * kCk];
   const DecSeg &S = sg[blockIdx.y];
   const DecFrame &F = fr[S.frame];
   if (blockIdx.x * 16 >= S.nwg) return;
-  load_sync_tables(F, tabs);
   const HuffGeom hg(F.g);
   const uint32_t L = spec_lanes(hg.bpm), NS = 256 / L;
-  const uint32_t w = blockIdx.x * 16 + threadIdx.x / 16, j = threadIdx.x % 16;
+  const uint32_t wl = threadIdx.x / 16, w = blockIdx.x * 16 + wl, j = threadIdx.x % 16;
   const uint32_t nbits = us_len[blockIdx.y] * 8u, nsub = (nbits + kSubBits - 1) / kSubBits;
   const uint32_t s = w * NS;
-  if (w == 0 || w >= S.nwg || j >= hg.bpm || s >= nsub) return;
+  const bool live = w > 0 && w < S.nwg && s < nsub;
+  // Stage each boundary's stream words and the checkpoints it compares against (all loads
+  // issued before the decode, instead of one dependent global load per refill and per mark)
+  const uint64_t wc = (uint64_t)(S.wg0 + w) * kSpecLanesMax;
+  if (live) {
+    const uint32_t fwords = (((S.in_len + 64) + 15) & ~15u) / 4, woff = s * (kSubBits / 32);
+    const uint32_t *gw = reinterpret_cast<const uint32_t *>(us + S.us_off);
+    for (uint32_t i = j; i < kLinkWords; i += 16) s_lw[wl][i] = woff + i < fwords ? gw[woff + i] : 0u;
+    if (j < hg.bpm) {
+#pragma unroll
+      for (int m = 0; m < kCk; ++m) {
+        s_ck[wl][j * kCk + m] = B.wck[(wc + j) * kCk + m];
+        s_rem[wl][j * kCk + m] = B.wrem[(wc + j) * kCk + m];
+      }
+    }
+  }
+  load_sync_tables(F, tabs);  // its barrier also publishes the staged words and checkpoints
+  if (!live || j >= hg.bpm) return;
   const uint32_t base = s * kSubBits, end = (s + 1 >= nsub) ? nbits : (s + 1) * kSubBits;
   const uint64_t X = B.tE[S.tr0 + (uint64_t)(w - 1) * 256 + (NS - 1) * L + j];
-  const uint64_t wc = (uint64_t)(S.wg0 + w) * kSpecLanesMax;
   uint32_t C = 0;
   uint64_t xe = 0;
-  const uint32_t M = spec_link(reinterpret_cast<const uint32_t *>(us + S.us_off), 0u, X, base, end, s + 1 == nsub,
-                               hg, tabs,
-                               [&](uint32_t c2, int m) { return B.wck[(wc + c2) * kCk + m]; },
-                               [&](uint32_t c2, int m) { return B.wrem[(wc + c2) * kCk + m]; }, &C, &xe);
+  const uint32_t M = spec_link(s_lw[wl], s * (kSubBits / 32), X, base, end, s + 1 == nsub, hg, tabs,
+                               [&](uint32_t c2, int m) { return s_ck[wl][c2 * kCk + m]; },
+                               [&](uint32_t c2, int m) { return s_rem[wl][c2 * kCk + m]; }, &C, &xe);
   const uint64_t wb = wc + j;
   B.wB[wb] = (uint8_t)M;
   B.wBC[wb] = C;
