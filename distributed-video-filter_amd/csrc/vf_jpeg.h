@@ -82,7 +82,8 @@ struct DecFrame {
   uint16_t q[3][64];       // dequantisation per component, natural order
   HuffDec dc[3], ac[3];    // per component (kept adjacent: loaded into LDS as one block)
   HuffSync sdc[3], sac[3];  // the same, for the synchronisation decoders (adjacent too)
-  uint32_t flags;          // bit 0: fancy upsampling allowed
+  uint32_t flags;          // bit 0: fancy upsampling allowed; bits 1-2: k_color layout (0 other,
+                           // 1 4:4:4, 2 chroma 2x1, 3 chroma 2x2; three components, full-size luma)
   uint64_t blk0;           // first block in the batch coefficient buffer
   uint64_t dcbase[3];      // per-component DC sequences in the DC buffer
   uint64_t plane_off[3];   // component planes in the plane buffer

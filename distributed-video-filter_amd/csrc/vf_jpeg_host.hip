@@ -706,6 +706,13 @@ int Codec::prepare_decode(const uint8_t *const *jpegs, const size_t *sizes, int 
     const Parsed &P = parsed[(size_t)f];
     DecFrame &F = dfr_[(size_t)f];
     F.flags = (flags & kFlagFastUpsample) ? 0u : 1u;
+    {  // k_color's layout (vf_jpeg.h DecFrame.flags), read as one scalar word on the device
+      const Geom &g = F.g;
+      uint32_t cm = 0;
+      if (g.ncomp == 3 && g.he[0] == 1 && g.ve[0] == 1 && g.he[1] == g.he[2] && g.ve[1] == g.ve[2])
+        cm = g.he[1] == 1 && g.ve[1] == 1 ? 1u : g.he[1] == 2 && g.ve[1] == 1 ? 2u : g.he[1] == 2 && g.ve[1] == 2 ? 3u : 0u;
+      F.flags |= cm << 1;
+    }
     F.blk0 = blk;
     for (int c = 0; c < P.ncomp; ++c) {
       F.dcbase[c] = dcoff;

@@ -1287,6 +1287,56 @@ __device__ __forceinline__ int up_sample(const uint8_t *p, int pw, int dw, int d
 
 __device__ __forceinline__ uint32_t clamp255(int v) { return (uint32_t)(v < 0 ? 0 : v > 255 ? 255 : v); }
 
+// 8 output samples of a 2x horizontally subsampled row from chroma samples i0-1 .. i0+4
+// (cs, edge-clamped column values; for h2v2 already 3 * nearer row + further row)
+__device__ __forceinline__ void up2(const int cs[6], int i0, int dw, bool fancy, int ve, int out[8]) {
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj) {
+    const int i = i0 + jj, c = cs[jj + 1];
+    int a, b;
+    if (!fancy) {
+      a = b = c;
+    } else if (ve == 1) {  // h2v1_fancy_upsample
+      a = i == 0 ? c : (3 * c + cs[jj] + 1) >> 2;
+      b = i == dw - 1 ? c : (3 * c + cs[jj + 2] + 2) >> 2;
+    } else {  // h2v2_fancy_upsample
+      a = i == 0 ? (4 * c + 8) >> 4 : (3 * c + cs[jj] + 8) >> 4;
+      b = i == dw - 1 ? (4 * c + 7) >> 4 : (3 * c + cs[jj + 2] + 7) >> 4;
+    }
+    out[2 * jj] = a;
+    out[2 * jj + 1] = b;
+  }
+}
+
+// jdcolor.c ycc_rgb_convert (grayscale: replicated) of 8 pixels, inverted when asked
+__device__ __forceinline__ void ycc8(const int v[3][8], int ncomp, int bgr, int invert, uint8_t o[24]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    uint32_t r, gg, b;
+    if (ncomp == 1) {
+      r = gg = b = (uint32_t)v[0][j];
+    } else {
+      const int xcr = v[2][j] - 128, xcb = v[1][j] - 128;
+      r = clamp255(v[0][j] + ((91881 * xcr + 32768) >> 16));
+      gg = clamp255(v[0][j] + ((-22554 * xcb + 32768 - 46802 * xcr) >> 16));
+      b = clamp255(v[0][j] + ((116130 * xcb + 32768) >> 16));
+    }
+    if (invert) {
+      r ^= 0xFF;
+      gg ^= 0xFF;
+      b ^= 0xFF;
+    }
+    o[3 * j] = (uint8_t)(bgr ? b : r);
+    o[3 * j + 1] = (uint8_t)gg;
+    o[3 * j + 2] = (uint8_t)(bgr ? r : b);
+  }
+}
+
+__device__ __forceinline__ void unpack8(uint2 q, int v[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = (int)(((j < 4 ? q.x : q.y) >> (8 * (j & 3))) & 0xFF);
+}
+
 // 8 horizontally adjacent output pixels per thread: one 8-byte load per full-size plane,
 // the chroma samples they need (+1 neighbour each side) for 2x horizontal subsampling, and
 // three 8-byte stores of interleaved output when the row is 8-byte aligned.
@@ -1323,48 +1373,14 @@ __device__ __forceinline__ void color8(const DecFrame &F, const Geom &g, const u
 #pragma unroll
         for (int m = 0; m < 6; ++m) cs[m] = r0[min(max(i0 - 1 + m, 0), dw - 1)];
       }
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
-        const int i = i0 + jj, c = cs[jj + 1];
-        int a, b;
-        if (!fancy) {
-          a = b = c;
-        } else if (ve == 1) {  // h2v1_fancy_upsample
-          a = i == 0 ? c : (3 * c + cs[jj] + 1) >> 2;
-          b = i == dw - 1 ? c : (3 * c + cs[jj + 2] + 2) >> 2;
-        } else {  // h2v2_fancy_upsample
-          a = i == 0 ? (4 * c + 8) >> 4 : (3 * c + cs[jj] + 8) >> 4;
-          b = i == dw - 1 ? (4 * c + 7) >> 4 : (3 * c + cs[jj + 2] + 7) >> 4;
-        }
-        v[k][2 * jj] = a;
-        v[k][2 * jj + 1] = b;
-      }
+      up2(cs, i0, dw, fancy, ve, v[k]);
     } else {
 #pragma unroll
       for (int j = 0; j < 8; ++j)
         v[k][j] = up_sample(p, pw, dw, dh, he, ve, fancy && he <= 2 && ve <= 2, min(x0 + j, g.w - 1), y);
     }
   }
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    uint32_t r, gg, b;
-    if (g.ncomp == 1) {
-      r = gg = b = (uint32_t)v[0][j];
-    } else {  // jdcolor.c ycc_rgb_convert
-      const int xcr = v[2][j] - 128, xcb = v[1][j] - 128;
-      r = clamp255(v[0][j] + ((91881 * xcr + 32768) >> 16));
-      gg = clamp255(v[0][j] + ((-22554 * xcb + 32768 - 46802 * xcr) >> 16));
-      b = clamp255(v[0][j] + ((116130 * xcb + 32768) >> 16));
-    }
-    if (invert) {
-      r ^= 0xFF;
-      gg ^= 0xFF;
-      b ^= 0xFF;
-    }
-    o[3 * j] = (uint8_t)(bgr ? b : r);
-    o[3 * j + 1] = (uint8_t)gg;
-    o[3 * j + 2] = (uint8_t)(bgr ? r : b);
-  }
+  ycc8(v, g.ncomp, bgr, invert, o);
 }
 
 __device__ __forceinline__ void color8_store(const DecFrame &F, const Geom &g, uint8_t *__restrict__ pix, int y,
@@ -1388,6 +1404,85 @@ __device__ __forceinline__ void color8_store(const DecFrame &F, const Geom &g, u
   }
 }
 
+// Rows y0 and y0 + 1 (y0 even) for three components with full-size luma and both chroma
+// planes 1x1 (MODE 0), 2x1 (MODE 1) or 2x2 (MODE 2) subsampled: the same arithmetic as color8,
+// with every plane load of both rows issued before any is used (color8's per-component
+// branches leave the compiler waiting on each component's loads in turn: six round trips per
+// thread at 4:2:0).  4:2:0 reads chroma rows iy - 1, iy, iy + 1 once for both output rows.
+template <int MODE>
+__device__ __forceinline__ void color_rows(const DecFrame &F, const Geom &g, const uint8_t *__restrict__ planes,
+                                           uint8_t *__restrict__ pix, int y0, int x0, bool two, int bgr, int invert) {
+  const int y1 = two ? y0 + 1 : y0;
+  int v0[3][8], v1[3][8];
+  if constexpr (MODE == 0) {
+    uint2 q[3][2];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const uint8_t *p = planes + F.plane_off[k];
+      q[k][0] = *reinterpret_cast<const uint2 *>(p + (size_t)y0 * g.pw[k] + x0);
+      q[k][1] = *reinterpret_cast<const uint2 *>(p + (size_t)y1 * g.pw[k] + x0);
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      unpack8(q[k][0], v0[k]);
+      unpack8(q[k][1], v1[k]);
+    }
+  } else {
+    const uint8_t *pY = planes + F.plane_off[0];
+    const uint2 qa = *reinterpret_cast<const uint2 *>(pY + (size_t)y0 * g.pw[0] + x0);
+    const uint2 qb = *reinterpret_cast<const uint2 *>(pY + (size_t)y1 * g.pw[0] + x0);
+    const int dw = g.dw[1], dh = g.dh[1], pw = g.pw[1];
+    const bool fancy = (F.flags & 1) && dw > 2;
+    const int i0 = x0 >> 1;
+    int ix[6];
+#pragma unroll
+    for (int m = 0; m < 6; ++m) ix[m] = min(max(i0 - 1 + m, 0), dw - 1);
+    constexpr int NR = MODE == 2 ? 3 : 2;
+    int rows[NR];
+    if constexpr (MODE == 2) {  // the row above, the row itself, the row below (clamped)
+      const int iy = min(y0 >> 1, dh - 1);
+      rows[0] = max(iy - 1, 0);
+      rows[1] = iy;
+      rows[2] = min(iy + 1, dh - 1);
+    } else {
+      rows[0] = min(y0, dh - 1);
+      rows[1] = min(y1, dh - 1);
+    }
+    int b[2][NR][6];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const uint8_t *p = planes + F.plane_off[k + 1];
+#pragma unroll
+      for (int rr = 0; rr < NR; ++rr)
+#pragma unroll
+        for (int m = 0; m < 6; ++m) b[k][rr][m] = p[(size_t)rows[rr] * pw + ix[m]];
+    }
+    unpack8(qa, v0[0]);
+    unpack8(qb, v1[0]);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      int c0[6], c1[6];
+#pragma unroll
+      for (int m = 0; m < 6; ++m) {
+        if constexpr (MODE == 2) {  // y0 even: its further row is above, y0 + 1's below
+          c0[m] = fancy ? 3 * b[k][1][m] + b[k][0][m] : b[k][1][m];
+          c1[m] = fancy ? 3 * b[k][1][m] + b[k][2][m] : b[k][1][m];
+        } else {
+          c0[m] = b[k][0][m];
+          c1[m] = b[k][1][m];
+        }
+      }
+      up2(c0, i0, dw, fancy, MODE == 2 ? 2 : 1, v0[k + 1]);
+      up2(c1, i0, dw, fancy, MODE == 2 ? 2 : 1, v1[k + 1]);
+    }
+  }
+  uint8_t o0[24], o1[24];
+  ycc8(v0, 3, bgr, invert, o0);
+  ycc8(v1, 3, bgr, invert, o1);
+  color8_store(F, g, pix, y0, x0, o0);
+  if (two) color8_store(F, g, pix, y1, x0, o1);
+}
+
 // Two rows per workgroup: both rows' plane loads are issued before either row is stored (the
 // kernel is bound by load latency per wave; one short row per workgroup left it exposed).
 __global__ __launch_bounds__(256) void k_color(const DecFrame *fr, const uint8_t *__restrict__ planes,
@@ -1397,6 +1492,13 @@ __global__ __launch_bounds__(256) void k_color(const DecFrame *fr, const uint8_t
   const int y0 = blockIdx.y * 2, x0 = (blockIdx.x * 256 + threadIdx.x) * 8;
   if (y0 >= g.h || x0 >= g.w) return;
   const bool two = y0 + 1 < g.h;
+  // the common layouts (classified on the host: one scalar word, where the int8 sampling
+  // fields would each be a vector load and a wait) take a path whose plane loads are all
+  // issued up front
+  const uint32_t cm = (F.flags >> 1) & 3u;
+  if (cm == 1) return color_rows<0>(F, g, planes, pix, y0, x0, two, bgr, invert);
+  if (cm == 2) return color_rows<1>(F, g, planes, pix, y0, x0, two, bgr, invert);
+  if (cm == 3) return color_rows<2>(F, g, planes, pix, y0, x0, two, bgr, invert);
   uint8_t o0[24], o1[24];
   color8(F, g, planes, y0, x0, bgr, invert, o0);
   color8(F, g, planes, two ? y0 + 1 : y0, x0, bgr, invert, o1);
