@@ -35,8 +35,10 @@ struct Geom {
   int32_t cfirst[3];     // first block-in-MCU of the component
   int32_t dw[3], dh[3];  // downsampled size in samples: ceil(w * hs / maxh), ceil(h * vs / maxv)
   int32_t rrows[3];      // encoder: sample rows from real pixel rows, ceil(h / maxv) * vs
-  int8_t bcomp[kMaxBpm], bxo[kMaxBpm], byo[kMaxBpm];  // block-in-MCU -> component, x/y (blocks)
-  int8_t he[3], ve[3];   // expansion factors maxh / hs, maxv / vs
+  // 32-bit, as every field here: a kernel reads a wave-uniform entry with one scalar load,
+  // where an 8-bit field would be a vector load and a wait
+  int32_t bcomp[kMaxBpm], bxo[kMaxBpm], byo[kMaxBpm];  // block-in-MCU -> component, x/y (blocks)
+  int32_t he[3], ve[3];  // expansion factors maxh / hs, maxv / vs
 };
 
 bool make_geom(int w, int h, int ncomp, const int *hs, const int *vs, Geom *g);

@@ -490,17 +490,17 @@ bool make_geom(int w, int h, int ncomp, const int *hs, const int *vs, Geom *g) {
       for (int yi = 0; yi < vs[k]; ++yi)
         for (int xi = 0; xi < hs[k]; ++xi) {
           if (b >= kMaxBpm) return false;
-          g->bcomp[b] = (int8_t)k;
-          g->bxo[b] = (int8_t)xi;
-          g->byo[b] = (int8_t)yi;
+          g->bcomp[b] = k;
+          g->bxo[b] = xi;
+          g->byo[b] = yi;
           ++b;
         }
     }
     g->bpm = b;
   }
   for (int k = 0; k < ncomp; ++k) {  // per-component quotients the kernels would otherwise divide for
-    g->he[k] = (int8_t)(maxh / g->hs[k]);
-    g->ve[k] = (int8_t)(maxv / g->vs[k]);
+    g->he[k] = maxh / g->hs[k];
+    g->ve[k] = maxv / g->vs[k];
     g->dw[k] = ceil_div(w * g->hs[k], maxh);
     g->dh[k] = ceil_div(h * g->vs[k], maxv);
     g->rrows[k] = ceil_div(h, maxv) * g->vs[k];

@@ -1182,10 +1182,6 @@ __global__ __launch_bounds__(256) void k_idct(const DecFrame *fr, const int16_t 
   __shared__ uint8_t s_pos[64];      // kIdctPos
   __shared__ uint32_t s_col[8];      // kIdctCol
   const uint32_t t = threadIdx.x;
-  if (t < 192) s_q[t >> 6][t & 63] = F.q[t >> 6][t & 63];
-  if (t < 64) s_pos[t] = kIdctPos[t];
-  if (t < 8) s_col[t] = kIdctCol[t];
-  __syncthreads();
   const uint32_t slot = t >> 3, r = t & 7, lm = slot & 7;
   const uint32_t unit = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(t >> 6);
   const uint32_t grp = unit / bpm, c = unit - grp * bpm;  // scalar
@@ -1205,13 +1201,19 @@ __global__ __launch_bounds__(256) void k_idct(const DecFrame *fr, const int16_t 
     while (mx >= mcux) mx -= mcux, ++my;  // once at most unless the frame is under 16 MCUs wide
     bxs[h] = mx * mh + (uint32_t)g.bxo[c];
     bys[h] = my * mv + (uint32_t)g.byo[c];
-    raw[h] = make_uint4(0, 0, 0, 0);
-    dc[h] = 0;
-    if (valid[h]) {
-      raw[h] = *reinterpret_cast<const uint4 *>(coef + (F.blk0 + (uint64_t)mcu * bpm + c) * 64 + r * 8);
-      if (r == 0) dc[h] = dcseq[F.dcbase[k] + (uint64_t)mcu * (mh * mv) + (c - (uint32_t)g.cfirst[k])];
-    }
+    // unconditional loads (an invalid block reads the frame's first block and DC): loads
+    // under a branch made the compiler wait for the first block's before issuing the second's
+    const uint64_t bi = valid[h] ? F.blk0 + (uint64_t)mcu * bpm + c : F.blk0;
+    const uint64_t di = valid[h] ? F.dcbase[k] + (uint64_t)mcu * (mh * mv) + (c - (uint32_t)g.cfirst[k]) : F.dcbase[k];
+    raw[h] = *reinterpret_cast<const uint4 *>(coef + bi * 64 + r * 8);
+    dc[h] = dcseq[di];
   }
+  // the tables after the coefficient loads: their round trips overlap instead of the
+  // coefficients waiting behind the tables' barrier
+  if (t < 192) s_q[t >> 6][t & 63] = F.q[t >> 6][t & 63];
+  if (t < 64) s_pos[t] = kIdctPos[t];
+  if (t < 8) s_col[t] = kIdctCol[t];
+  __syncthreads();
   const uint2 pos8 = *reinterpret_cast<const uint2 *>(&s_pos[r * 8]);  // this lane's 8 store dwords
   const uint32_t colg = s_col[r];
 #pragma unroll
