@@ -2093,11 +2093,15 @@ __global__ __launch_bounds__(256) void k_compact(const EncFrame *fr, const uint6
 // the 16 bytes of the packed stream at i0, the final partial byte padded with ones
 __device__ __forceinline__ uint32_t ff_bytes(const uint8_t *s, uint32_t nbytes, uint32_t tb, uint32_t i0,
                                              uint8_t *bytes) {
+  // one 16-B load: i0 is a multiple of 16 below nbytes, and a frame's stream region (256-B
+  // aligned) holds at least nbytes + 16 bytes (the host's bits_cap)
+  const uint4 q = *reinterpret_cast<const uint4 *>(s + i0);
+  const uint32_t qw[4] = {q.x, q.y, q.z, q.w};
   uint32_t n = 0;
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
     const uint32_t i = i0 + j;
-    uint8_t v = i < nbytes ? s[i] : 0;
+    uint8_t v = i < nbytes ? (uint8_t)(qw[j >> 2] >> (8 * (j & 3))) : 0;
     if (i == nbytes - 1 && (tb & 7)) v |= (uint8_t)(0xFF >> (tb & 7));
     bytes[j] = v;
     n += (i < nbytes && v == 0xFF);
@@ -2135,6 +2139,7 @@ __global__ __launch_bounds__(256) void k_ff_write(const EncFrame *fr, const uint
   const uint32_t tb = total_bits[blockIdx.y], nbytes = (tb + 7) >> 3;
   const uint32_t ntiles = (nbytes + kTile - 1) / kTile;
   __shared__ uint32_t sh[4];
+  __shared__ uint8_t s_out[2 * kTile];  // a tile's bytes after stuffing (at most every byte 0xFF)
   uint8_t *o = out + F.out_off;
   for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {  // grid-stride over the stream's tiles
     if (t == 0)
@@ -2143,12 +2148,26 @@ __global__ __launch_bounds__(256) void k_ff_write(const EncFrame *fr, const uint
     const uint32_t i0 = t * kTile + threadIdx.x * 16;
     const uint32_t n = i0 < nbytes ? ff_bytes(stream + F.bits_off, nbytes, tb, i0, bytes) : 0;
     uint32_t tot;
-    uint64_t pos = (uint64_t)F.hdr_len + i0 + off[F.tile0 + t] + wg_excl_scan(n, sh, &tot);
+    // the tile's stuffed bytes are assembled in LDS, then stored as aligned dwords (per-lane
+    // byte stores at scattered offsets were 16-32 store instructions per lane)
+    uint32_t lp = threadIdx.x * 16 + wg_excl_scan(n, sh, &tot);
     for (int j = 0; j < 16; ++j) {
       if (i0 + j >= nbytes) break;
-      o[pos++] = bytes[j];
-      if (bytes[j] == 0xFF) o[pos++] = 0;
+      s_out[lp++] = bytes[j];
+      if (bytes[j] == 0xFF) s_out[lp++] = 0;
     }
+    __syncthreads();
+    const uint32_t len = min((uint32_t)kTile, nbytes - t * kTile) + tot;
+    uint8_t *dst = o + (uint64_t)F.hdr_len + t * kTile + off[F.tile0 + t];
+    const uint32_t head = min((uint32_t)(-(uintptr_t)dst & 3), len), nw = (len - head) >> 2;
+    if (threadIdx.x < head) dst[threadIdx.x] = s_out[threadIdx.x];
+    for (uint32_t i = threadIdx.x; i < nw; i += 256) {
+      const uint32_t a = head + 4 * i;
+      reinterpret_cast<uint32_t *>(dst + head)[i] = (uint32_t)s_out[a] | ((uint32_t)s_out[a + 1] << 8) |
+                                                    ((uint32_t)s_out[a + 2] << 16) | ((uint32_t)s_out[a + 3] << 24);
+    }
+    const uint32_t tail = head + 4 * nw;
+    if (threadIdx.x < len - tail) dst[tail + threadIdx.x] = s_out[tail + threadIdx.x];
     if (t == ntiles - 1 && threadIdx.x == 0) {
       const uint64_t size = (uint64_t)F.hdr_len + nbytes + nff[blockIdx.y] + 2;
       o[size - 2] = 0xFF;
