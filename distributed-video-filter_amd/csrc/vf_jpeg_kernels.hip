@@ -150,10 +150,14 @@ hipError_t seg_scan(const ScanSeg *segs, int nseg, uint32_t max_tiles, const T *
 __device__ __forceinline__ uint32_t keep_mask(const uint8_t *s, uint32_t len, uint32_t i0, uint8_t *bytes) {
   uint32_t m = 0;
   uint8_t prev = i0 ? s[i0 - 1] : 0;
+  // one 16-B load: i0 is a multiple of 16 and the host stages each segment at a 16-B aligned
+  // offset, rounded up to 16 bytes
+  const uint4 q = i0 < len ? *reinterpret_cast<const uint4 *>(s + i0) : make_uint4(0, 0, 0, 0);
+  const uint32_t qw[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
     const uint32_t i = i0 + j;
-    const uint8_t b = i < len ? s[i] : 0;
+    const uint8_t b = i < len ? (uint8_t)(qw[j >> 2] >> (8 * (j & 3))) : 0;
     bytes[j] = b;
     if (i < len && !(b == 0 && prev == 0xFF)) m |= 1u << j;
     prev = b;
@@ -182,11 +186,24 @@ __global__ __launch_bounds__(256) void k_unstuff_write(const DecSeg *sg, const u
   const uint32_t i0 = blockIdx.x * kTile + threadIdx.x * 16;
   const uint32_t m = keep_mask(in + F.in_off, F.in_len, i0, bytes);
   uint32_t tot;
-  uint32_t pos = off[F.tile0 + blockIdx.x] + wg_excl_scan((uint32_t)__popc(m), sh, &tot);
-  uint8_t *d = us + F.us_off;
+  // the tile's kept bytes are assembled in LDS, then stored as aligned dwords
+  __shared__ uint8_t s_out[kTile];
+  uint32_t lp = wg_excl_scan((uint32_t)__popc(m), sh, &tot);
 #pragma unroll
   for (int j = 0; j < 16; ++j)
-    if (m >> j & 1) d[pos++] = bytes[j];
+    if (m >> j & 1) s_out[lp++] = bytes[j];
+  __syncthreads();
+  uint8_t *d = us + F.us_off;
+  uint8_t *dst = d + off[F.tile0 + blockIdx.x];
+  const uint32_t head = min((uint32_t)(-(uintptr_t)dst & 3), tot), nw = (tot - head) >> 2;
+  if (threadIdx.x < head) dst[threadIdx.x] = s_out[threadIdx.x];
+  for (uint32_t i = threadIdx.x; i < nw; i += 256) {
+    const uint32_t a = head + 4 * i;
+    reinterpret_cast<uint32_t *>(dst + head)[i] = (uint32_t)s_out[a] | ((uint32_t)s_out[a + 1] << 8) |
+                                                  ((uint32_t)s_out[a + 2] << 16) | ((uint32_t)s_out[a + 3] << 24);
+  }
+  const uint32_t tail = head + 4 * nw;
+  if (threadIdx.x < tot - tail) dst[tail + threadIdx.x] = s_out[tail + threadIdx.x];
   // zero tail for the bit reader (libjpeg feeds zeros past the data, jdhuff.c)
   if (blockIdx.x == F.ntiles - 1 && threadIdx.x < 32) d[us_len[blockIdx.y] + threadIdx.x] = 0;
 }
