@@ -2050,17 +2050,32 @@ __global__ __launch_bounds__(256) void k_len(const EncFrame *fr, const EncTables
   bits[gb] = (e & 0xFF) + nb + ac;
 }
 
-// every block writes its bits at its offset: DC code + extra bits (pre), then its AC words
-__global__ __launch_bounds__(256) void k_pack(const EncFrame *fr, const uint32_t *pre, const uint32_t *acbits,
-                                              const uint32_t *acscr, const uint32_t *bitoff, uint8_t *stream) {
-  const EncFrame &F = fr[blockIdx.y];
-  const uint32_t b = blockIdx.x * 256 + threadIdx.x;
-  if (b >= (uint32_t)F.g.nblocks) return;
-  const uint64_t gb = F.blk0 + b;
-  const uint32_t p = pre[gb], n = acbits[gb], off = bitoff[gb];
-  const uint32_t *aw = acscr + acs_idx(gb, 0);  // word i at aw[64 * i]
-  const uint32_t a0 = aw[0];  // issued with the other loads; unused by a dummy block
-  BitSink out(reinterpret_cast<uint32_t *>(stream + F.bits_off), off);
+// MSB-first bits into big-endian words of an LDS image, every word OR-ed (the image is
+// zeroed first, and a lane's first and last words are shared with its neighbours)
+struct LdsSink {
+  uint32_t *w;
+  uint32_t wi;
+  uint64_t acc;
+  uint32_t n;
+  __device__ __forceinline__ LdsSink(uint32_t *words, uint32_t off) : w(words), wi(off >> 5), acc(0), n(off & 31) {}
+  __device__ __forceinline__ void put(uint32_t code, uint32_t size) {  // size <= 32
+    acc = (acc << size) | code;
+    n += size;
+    if (n >= 32) {
+      n -= 32;
+      atomicOr(w + wi, bswap32((uint32_t)(acc >> n)));
+      ++wi;
+      acc &= n ? ((1ull << n) - 1) : 0ull;
+    }
+  }
+  __device__ __forceinline__ void finish() {
+    if (n) atomicOr(w + wi, bswap32((uint32_t)(acc << (32 - n))));
+  }
+};
+
+// one block's bits: DC code + extra bits (pre), then its AC words (or a dummy block's EOB)
+template <typename Sink>
+__device__ __forceinline__ void pack_block(Sink &out, uint32_t p, uint32_t n, uint32_t a0, const uint32_t *aw) {
   out.put(p >> 5, p & 31);
   if (n & kDummyAc) {
     out.put((n & ~kDummyAc) >> 5, n & 31);
@@ -2074,6 +2089,57 @@ __global__ __launch_bounds__(256) void k_pack(const EncFrame *fr, const uint32_t
     }
   }
   out.finish();
+}
+
+// Every block writes its bits at its offset.  The 64 blocks of a wave are consecutive, so
+// their bits are one contiguous span: the wave assembles it in an LDS image (LDS atomics
+// where neighbouring blocks share a word) and stores it as whole words, with global atomics
+// only on the span's first and last words (shared with the neighbouring waves).  Writing
+// each block straight to memory took two global atomics per block, most of them on words a
+// neighbouring lane of the same instruction also hit.  A span over kPackWords (very detailed
+// content) takes that direct path.
+constexpr uint32_t kPackWords = 1024;  // per wave: 64 blocks of 512 bits on average
+__global__ __launch_bounds__(256) void k_pack(const EncFrame *fr, const uint32_t *pre, const uint32_t *acbits,
+                                              const uint32_t *acscr, const uint32_t *bitoff, uint8_t *stream) {
+  __shared__ uint32_t s_img[4][kPackWords];
+  const EncFrame &F = fr[blockIdx.y];
+  const uint32_t nblocks = (uint32_t)F.g.nblocks, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t bw0 = blockIdx.x * 256 + wv * 64;  // the wave's first block (uniform)
+  if (bw0 >= nblocks) return;
+  const uint32_t last = min(63u, nblocks - 1 - bw0), b = bw0 + lane;
+  const bool valid = lane <= last;
+  const uint64_t gb = F.blk0 + (valid ? b : bw0);
+  const uint32_t p = pre[gb], n = acbits[gb], off = bitoff[gb];
+  const uint32_t *aw = acscr + acs_idx(gb, 0);  // word i at aw[64 * i]
+  const uint32_t a0 = aw[0];  // issued with the other loads; unused by a dummy block
+  uint32_t *words = reinterpret_cast<uint32_t *>(stream + F.bits_off);
+  const uint32_t len = (p & 31) + ((n & kDummyAc) ? (n & 31) : n);
+  const uint32_t w0 = __shfl(off, 0) >> 5, w1 = (__shfl(off + len, (int)last) + 31) >> 5;  // words [w0, w1)
+  const uint32_t nw = w1 - w0;
+  if (nw > kPackWords) {  // wave-uniform
+    if (valid) {
+      BitSink out(words, off);
+      pack_block(out, p, n, a0, aw);
+    }
+    return;
+  }
+  uint32_t *img = s_img[wv];
+  for (uint32_t i = lane; i < nw; i += 64) img[i] = 0;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if (valid) {
+    LdsSink out(img, off - w0 * 32);
+    pack_block(out, p, n, a0, aw);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  for (uint32_t i = lane; i < nw; i += 64) {
+    const uint32_t v = img[i];
+    if (i == 0 || i == nw - 1) atomicOr(words + w0 + i, v);
+    else words[w0 + i] = v;
+  }
 }
 
 // zero the words the packed stream of each frame will occupy (boundary words are OR-ed)
