@@ -165,8 +165,8 @@ __device__ __forceinline__ uint32_t keep_mask(const uint8_t *s, uint32_t len, ui
   return m;
 }
 
-__global__ __launch_bounds__(256) void k_unstuff_count(const DecSeg *sg, const uint8_t *in, uint32_t *cnt) {
-  const DecSeg &F = sg[blockIdx.y];
+__global__ __launch_bounds__(256) void k_unstuff_count(const DecSeg *__restrict__ sg, const uint8_t *in, uint32_t *cnt) {
+  const DecSeg F = sg[blockIdx.y];  // by value: see k_spec
   if (blockIdx.x >= F.ntiles) return;
   __shared__ uint32_t sh[4];
   uint8_t bytes[16];
@@ -177,9 +177,9 @@ __global__ __launch_bounds__(256) void k_unstuff_count(const DecSeg *sg, const u
   if (threadIdx.x == 0) cnt[F.tile0 + blockIdx.x] = tot;
 }
 
-__global__ __launch_bounds__(256) void k_unstuff_write(const DecSeg *sg, const uint8_t *in, const uint32_t *off,
+__global__ __launch_bounds__(256) void k_unstuff_write(const DecSeg *__restrict__ sg, const uint8_t *in, const uint32_t *off,
                                                        const uint32_t *us_len, uint8_t *us) {
-  const DecSeg &F = sg[blockIdx.y];
+  const DecSeg F = sg[blockIdx.y];  // by value: see k_spec
   if (blockIdx.x >= F.ntiles) return;
   __shared__ uint32_t sh[4];
   uint8_t bytes[16];
@@ -428,7 +428,7 @@ constexpr uint64_t kNoCk = ~0ull;
 // until the workgroup is consistent.  Across workgroups the entry of a workgroup's first
 // thread is the previous pass's exit of its predecessor; a pass that changes no exit state
 // means the whole chain is consistent, and its counts were made from the final entry states.
-__global__ __launch_bounds__(256) void k_sync(const DecSeg *sg, const DecFrame *fr, const uint8_t *us, const uint32_t *us_len,
+__global__ __launch_bounds__(256) void k_sync(const DecSeg *__restrict__ sg, const DecFrame *__restrict__ fr, const uint8_t *us, const uint32_t *us_len,
                                               const uint64_t *exit_in, uint64_t *exit_out, const uint32_t *cnt_in,
                                               uint32_t *cnt_out, uint64_t *used, uint64_t *ck, uint32_t *ckrem,
                                               uint32_t *changed, int pass) {
@@ -436,7 +436,7 @@ __global__ __launch_bounds__(256) void k_sync(const DecSeg *sg, const DecFrame *
   __shared__ uint64_t s_exit[256];
   __shared__ uint64_t s_ck[kCk][256];
   __shared__ uint32_t s_rem[kCk][256];
-  const DecSeg &S = sg[blockIdx.y];
+  const DecSeg S = sg[blockIdx.y];  // by value: held in scalar registers
   const DecFrame &F = fr[S.frame];
   if (blockIdx.x * 256 >= S.nsub_max) return;
   load_sync_tables(F, tabs);
@@ -602,7 +602,7 @@ __device__ __forceinline__ uint32_t spec_link(const uint32_t *words, uint32_t wo
   return last ? kLinkLast : kLinkNone;
 }
 
-__global__ __launch_bounds__(256) void k_spec(const DecSeg *sg, const DecFrame *fr, const uint8_t *us, const uint32_t *us_len,
+__global__ __launch_bounds__(256) void k_spec(const DecSeg *__restrict__ sg, const DecFrame *__restrict__ fr, const uint8_t *us, const uint32_t *us_len,
                                               SpecBufs B) {
   __shared__ HuffSync tabs[6];
   __shared__ uint64_t s_ck[kCk][256];
@@ -612,7 +612,7 @@ __global__ __launch_bounds__(256) void k_spec(const DecSeg *sg, const DecFrame *
   __shared__ uint32_t s_C[256];
   __shared__ uint8_t s_M[256];
   __shared__ uint32_t s_w[kSpecWords];
-  const DecSeg &S = sg[blockIdx.y];
+  const DecSeg S = sg[blockIdx.y];  // by value: held in scalar registers
   const DecFrame &F = fr[S.frame];
   if (blockIdx.x >= S.nwg) return;
   const long long c_start = VF_SYNC_STATS ? clock64() : 0;
@@ -796,14 +796,14 @@ __global__ __launch_bounds__(256) void k_spec(const DecSeg *sg, const DecFrame *
 
 // Links across workgroup boundaries: trajectory j of the last subsequence of workgroup w-1
 // into the first subsequence of w.  16 boundaries per workgroup, one lane per j.
-__global__ __launch_bounds__(256) void k_wglink(const DecSeg *sg, const DecFrame *fr, const uint8_t *us, const uint32_t *us_len,
+__global__ __launch_bounds__(256) void k_wglink(const DecSeg *__restrict__ sg, const DecFrame *__restrict__ fr, const uint8_t *us, const uint32_t *us_len,
                                                 SpecBufs B) {
   constexpr uint32_t kLinkWords = kSubBits / 32 + kSpecPadWords;  // as k_spec's window for one subsequence
   __shared__ HuffSync tabs[6];
   __shared__ uint32_t s_lw[16][kLinkWords];
   __shared__ uint64_t s_ck[16][kSpecLanesMax * kCk];
   __shared__ uint32_t s_rem[16][kSpecLanesMax * kCk];
-  const DecSeg &S = sg[blockIdx.y];
+  const DecSeg S = sg[blockIdx.y];  // by value: held in scalar registers
   const DecFrame &F = fr[S.frame];
   if (blockIdx.x * 16 >= S.nwg) return;
   const HuffGeom hg(F.g);
@@ -851,13 +851,13 @@ __global__ __launch_bounds__(256) void k_wglink(const DecSeg *sg, const DecFrame
 constexpr uint32_t kResolveLds = 4096;  // workgroups per frame resolved here (else fallback)
 constexpr uint32_t kTraceWords = kSubBits / 32 + 6;  // one subsequence + overshoot + lookahead
 
-__global__ __launch_bounds__(256) void k_resolve(const DecSeg *sg, const DecFrame *fr, const uint8_t *us, const uint32_t *us_len,
+__global__ __launch_bounds__(256) void k_resolve(const DecSeg *__restrict__ sg, const DecFrame *__restrict__ fr, const uint8_t *us, const uint32_t *us_len,
                                                  SpecBufs B, uint32_t *unresolved) {
   __shared__ uint64_t sF[kResolveLds], sB[kResolveLds];
   __shared__ uint8_t sE[kResolveLds], sK[kResolveLds], sJ[kResolveLds];
   __shared__ HuffSync tabs[6];
   __shared__ uint32_t s_tw[kTraceWords];
-  const DecSeg &S = sg[blockIdx.x];
+  const DecSeg S = sg[blockIdx.x];  // by value: held in scalar registers
   const DecFrame &F = fr[S.frame];
   const HuffGeom hg(F.g);
   const uint32_t bpm = hg.bpm, L = spec_lanes(bpm), NS = 256 / L;
@@ -970,9 +970,9 @@ __global__ __launch_bounds__(256) void k_resolve(const DecSeg *sg, const DecFram
 
 // Exit state and block count of every subsequence along the resolved path, in the layout
 // the write pass and the block-offset scan read (exit_out / cnt_out of k_sync).
-__global__ __launch_bounds__(256) void k_finalize(const DecSeg *sg, const DecFrame *fr, const uint32_t *us_len, SpecBufs B,
+__global__ __launch_bounds__(256) void k_finalize(const DecSeg *__restrict__ sg, const DecFrame *__restrict__ fr, const uint32_t *us_len, SpecBufs B,
                                                   uint64_t *exit_out, uint32_t *cnt_out) {
-  const DecSeg &S = sg[blockIdx.y];
+  const DecSeg S = sg[blockIdx.y];  // by value: held in scalar registers
   const DecFrame &F = fr[S.frame];
   if (blockIdx.x >= S.nwg) return;
   const uint32_t bpm = (uint32_t)F.g.bpm, L = spec_lanes(bpm), NS = 256 / L;
@@ -1001,12 +1001,12 @@ __global__ __launch_bounds__(256) void k_finalize(const DecSeg *sg, const DecFra
 // The workgroup's stream words are staged in LDS first (as k_spec does): every refill of a
 // thread's bit buffer is then an LDS read instead of a dependent global load, the chain a
 // subsequence's decode waits on (k_write has only ~3 waves per SIMD to hide it with).
-__global__ __launch_bounds__(256) void k_write(const DecSeg *sg, const DecFrame *fr, const uint8_t *us, const uint32_t *us_len,
+__global__ __launch_bounds__(256) void k_write(const DecSeg *__restrict__ sg, const DecFrame *__restrict__ fr, const uint8_t *us, const uint32_t *us_len,
                                                const uint64_t *exits, const uint32_t *bstart, int16_t *coef,
                                                int32_t *dcseq) {
   __shared__ HuffDec tabs[6];
   __shared__ uint32_t s_w[kSpecWords];
-  const DecSeg &S = sg[blockIdx.y];
+  const DecSeg S = sg[blockIdx.y];  // by value: held in scalar registers
   const DecFrame &F = fr[S.frame];
   if (blockIdx.x * 256 >= S.nsub_max) return;
   // this workgroup's 256 subsequences of stream words, plus overshoot and lookahead, from the
@@ -1039,7 +1039,7 @@ __global__ __launch_bounds__(256) void k_write(const DecSeg *sg, const DecFrame 
 // 0 from the entry state) up to the next lane's start: the decode of a subsequence, a chain of
 // dependent table lookups, runs as 4 shorter chains side by side.  A lane whose checkpoint is
 // missing idles and the lane before it decodes on.
-__global__ __launch_bounds__(256) void k_write4(const DecSeg *sg, const DecFrame *fr, const uint8_t *us,
+__global__ __launch_bounds__(256) void k_write4(const DecSeg *__restrict__ sg, const DecFrame *__restrict__ fr, const uint8_t *us,
                                                 const uint32_t *us_len, const uint64_t *exits, const uint32_t *cnt,
                                                 const uint64_t *ck, const uint32_t *ckrem, const uint32_t *bstart,
                                                 int16_t *coef, int32_t *dcseq) {
@@ -1047,7 +1047,7 @@ __global__ __launch_bounds__(256) void k_write4(const DecSeg *sg, const DecFrame
   constexpr uint32_t kSubsPerWg = 64, kW4Words = kSubsPerWg * (kSubBits / 32) + kSpecPadWords;
   __shared__ HuffDec tabs[6];
   __shared__ uint32_t s_w[kW4Words];
-  const DecSeg &S = sg[blockIdx.y];
+  const DecSeg S = sg[blockIdx.y];  // by value: held in scalar registers
   const DecFrame &F = fr[S.frame];
   if (blockIdx.x * kSubsPerWg >= S.nsub_max) return;
   const uint32_t woff = blockIdx.x * kSubsPerWg * (kSubBits / 32);
@@ -1187,7 +1187,7 @@ __constant__ uint32_t kIdctCol[8] = {  // column c: nibble i = g(8i + c)
 // j + 8), a workgroup 4 such units: the component and its geometry are wave-uniform (scalar),
 // no lane divides, and the 8 lanes of a block read the same dequantisation entries.
 constexpr uint32_t kIdctGroup = 8 * kIdctNb;  // MCUs per wave
-__global__ __launch_bounds__(256) void k_idct(const DecFrame *fr, const int16_t *coef, const int32_t *dcseq,
+__global__ __launch_bounds__(256) void k_idct(const DecFrame *__restrict__ fr, const int16_t *coef, const int32_t *dcseq,
                                               uint8_t *planes) {
   const DecFrame &F = fr[blockIdx.y];
   const Geom &g = F.g;
@@ -1231,6 +1231,9 @@ __global__ __launch_bounds__(256) void k_idct(const DecFrame *fr, const int16_t 
   if (t < 64) s_pos[t] = kIdctPos[t];
   if (t < 8) s_col[t] = kIdctCol[t];
   __syncthreads();
+  // read before the first store (through F after a store, they were re-loaded with a wait)
+  uint8_t *const plane = planes + F.plane_off[k];
+  const uint32_t pw = (uint32_t)g.pw[k];
   const uint2 pos8 = *reinterpret_cast<const uint2 *>(&s_pos[r * 8]);  // this lane's 8 store dwords
   const uint32_t colg = s_col[r];
 #pragma unroll
@@ -1276,7 +1279,7 @@ __global__ __launch_bounds__(256) void k_idct(const DecFrame *fr, const int16_t 
       lo |= idct_limit(out[i]) << (8 * i);
       hi |= idct_limit(out[i + 4]) << (8 * i);
     }
-    uint8_t *p = planes + F.plane_off[k] + (uint64_t)(bys[h] * 8 + r) * (uint32_t)g.pw[k] + bxs[h] * 8;
+    uint8_t *p = plane + (uint64_t)(bys[h] * 8 + r) * pw + bxs[h] * 8;
     *reinterpret_cast<uint2 *>(p) = make_uint2(lo, hi);
   }
 }
@@ -1402,10 +1405,9 @@ __device__ __forceinline__ void color8(const DecFrame &F, const Geom &g, const u
   ycc8(v, g.ncomp, bgr, invert, o);
 }
 
-__device__ __forceinline__ void color8_store(const DecFrame &F, const Geom &g, uint8_t *__restrict__ pix, int y,
-                                             int x0, const uint8_t o[24]) {
-  uint8_t *dst = pix + F.out_off + ((size_t)y * g.w + x0) * 3;
-  if (x0 + 8 <= g.w && ((uintptr_t)dst & 7) == 0) {
+// 8 pixels (24 bytes of o) to dst, of which `left` are inside the row
+__device__ __forceinline__ void store24(uint8_t *dst, int left, const uint8_t o[24]) {
+  if (left >= 8 && ((uintptr_t)dst & 7) == 0) {
     uint2 *d2 = reinterpret_cast<uint2 *>(dst);
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
@@ -1418,10 +1420,11 @@ __device__ __forceinline__ void color8_store(const DecFrame &F, const Geom &g, u
       d2[q] = make_uint2(lo, hi);
     }
   } else {
-    const int n = min(8, g.w - x0) * 3;
+    const int n = min(8, left) * 3;
     for (int j = 0; j < n; ++j) dst[j] = o[j];
   }
 }
+
 
 // Rows y0 and y0 + 1 (y0 even) for three components with full-size luma and both chroma
 // planes 1x1 (MODE 0), 2x1 (MODE 1) or 2x2 (MODE 2) subsampled: the same arithmetic as color8,
@@ -1498,13 +1501,16 @@ __device__ __forceinline__ void color_rows(const DecFrame &F, const Geom &g, con
   uint8_t o0[24], o1[24];
   ycc8(v0, 3, bgr, invert, o0);
   ycc8(v1, 3, bgr, invert, o1);
-  color8_store(F, g, pix, y0, x0, o0);
-  if (two) color8_store(F, g, pix, y1, x0, o1);
+  // both destinations before the first store (after it, F's fields were re-loaded with a wait)
+  const int w = g.w;
+  uint8_t *const d0 = pix + F.out_off + ((size_t)y0 * w + x0) * 3, *const d1 = d0 + (size_t)w * 3;
+  store24(d0, w - x0, o0);
+  if (two) store24(d1, w - x0, o1);
 }
 
 // Two rows per workgroup: both rows' plane loads are issued before either row is stored (the
 // kernel is bound by load latency per wave; one short row per workgroup left it exposed).
-__global__ __launch_bounds__(256) void k_color(const DecFrame *fr, const uint8_t *__restrict__ planes,
+__global__ __launch_bounds__(256) void k_color(const DecFrame *__restrict__ fr, const uint8_t *__restrict__ planes,
                                                uint8_t *__restrict__ pix, int bgr, int invert) {
   const DecFrame &F = fr[blockIdx.z];
   const Geom &g = F.g;
@@ -1521,8 +1527,10 @@ __global__ __launch_bounds__(256) void k_color(const DecFrame *fr, const uint8_t
   uint8_t o0[24], o1[24];
   color8(F, g, planes, y0, x0, bgr, invert, o0);
   color8(F, g, planes, two ? y0 + 1 : y0, x0, bgr, invert, o1);
-  color8_store(F, g, pix, y0, x0, o0);
-  if (two) color8_store(F, g, pix, y0 + 1, x0, o1);
+  const int w = g.w;
+  uint8_t *const d0 = pix + F.out_off + ((size_t)y0 * w + x0) * 3;
+  store24(d0, w - x0, o0);
+  if (two) store24(d0 + (size_t)w * 3, w - x0, o1);
 }
 
 // ---- encoder: colour + downsampling + FDCT + quantisation -----------------------------------
@@ -1785,7 +1793,7 @@ __device__ __forceinline__ uint32_t qo_at(uint32_t slot, uint32_t zz) {
 // register accumulator into an LDS image of the block's AC stream that is then copied out.
 // Outputs per block: quantised DC, AC bit count, AC bits (MSB-first words).
 constexpr uint32_t kFdctGroup = 8;  // MCUs per wave
-__global__ __launch_bounds__(256) void k_fdct(const EncFrame *fr, const EncTables *tab, const uint8_t *pix,
+__global__ __launch_bounds__(256) void k_fdct(const EncFrame *__restrict__ fr, const EncTables *tab, const uint8_t *pix,
                                               int16_t *dcq, uint32_t *acbits, uint32_t *acscr, int bgr,
                                               int fastdct) {
   const EncFrame &F = fr[blockIdx.y];
@@ -2009,7 +2017,7 @@ __device__ __forceinline__ int enc_dc_at(const Geom &g, const int16_t *dcq, int 
   }
 }
 
-__global__ __launch_bounds__(256) void k_len(const EncFrame *fr, const EncTables *tab, const int16_t *dcq,
+__global__ __launch_bounds__(256) void k_len(const EncFrame *__restrict__ fr, const EncTables *tab, const int16_t *dcq,
                                              uint32_t *acbits, uint32_t *bits, uint32_t *pre) {
   const EncFrame &F = fr[blockIdx.y];
   const Geom &g = F.g;
@@ -2099,7 +2107,7 @@ __device__ __forceinline__ void pack_block(Sink &out, uint32_t p, uint32_t n, ui
 // neighbouring lane of the same instruction also hit.  A span over kPackWords (very detailed
 // content) takes that direct path.
 constexpr uint32_t kPackWords = 1024;  // per wave: 64 blocks of 512 bits on average
-__global__ __launch_bounds__(256) void k_pack(const EncFrame *fr, const uint32_t *pre, const uint32_t *acbits,
+__global__ __launch_bounds__(256) void k_pack(const EncFrame *__restrict__ fr, const uint32_t *pre, const uint32_t *acbits,
                                               const uint32_t *acscr, const uint32_t *bitoff, uint8_t *stream) {
   __shared__ uint32_t s_img[4][kPackWords];
   const EncFrame &F = fr[blockIdx.y];
@@ -2143,7 +2151,7 @@ __global__ __launch_bounds__(256) void k_pack(const EncFrame *fr, const uint32_t
 }
 
 // zero the words the packed stream of each frame will occupy (boundary words are OR-ed)
-__global__ __launch_bounds__(256) void k_zero_stream(const EncFrame *fr, const uint32_t *total_bits, uint8_t *stream) {
+__global__ __launch_bounds__(256) void k_zero_stream(const EncFrame *__restrict__ fr, const uint32_t *total_bits, uint8_t *stream) {
   const EncFrame &F = fr[blockIdx.y];
   const uint32_t nw = (total_bits[blockIdx.y] >> 5) + 2;
   uint32_t *w = reinterpret_cast<uint32_t *>(stream + F.bits_off);
@@ -2152,7 +2160,7 @@ __global__ __launch_bounds__(256) void k_zero_stream(const EncFrame *fr, const u
 
 // Frame f's JPEG to pack + sum over g < f of align64(size g): the host then fetches the batch
 // with one copy of the packed total instead of one copy per frame (~10 us of DMA set-up each).
-__global__ __launch_bounds__(256) void k_compact(const EncFrame *fr, const uint64_t *out_size, const uint8_t *out,
+__global__ __launch_bounds__(256) void k_compact(const EncFrame *__restrict__ fr, const uint64_t *out_size, const uint8_t *out,
                                                  uint8_t *pack) {
   const uint32_t f = blockIdx.y;
   uint64_t off = 0;
@@ -2192,44 +2200,50 @@ __device__ __forceinline__ uint32_t ff_bytes(const uint8_t *s, uint32_t nbytes, 
   return n;
 }
 
-__global__ __launch_bounds__(256) void k_ff_count(const EncFrame *fr, const uint32_t *total_bits,
+__global__ __launch_bounds__(256) void k_ff_count(const EncFrame *__restrict__ fr, const uint32_t *total_bits,
                                                   const uint8_t *stream, uint32_t *cnt) {
   // Grid-stride over the frame's worst-case tiles: the stream fills only the first few (a
   // 1080p q85 frame ~45 of ~1,500), so one workgroup per tile launched ~48 k workgroups per
   // batch that mostly wrote a zero.  Tiles past the stream's end get their zero count here.
-  const EncFrame &F = fr[blockIdx.y];
+  // the frame's fields in registers: read through the reference after a store, they were
+  // re-loaded from memory (with a wait) on every iteration
+  const uint32_t ntiles_max = fr[blockIdx.y].ntiles_max, tile0 = fr[blockIdx.y].tile0;
+  const uint8_t *src = stream + fr[blockIdx.y].bits_off;
   __shared__ uint32_t sh[4];
   const uint32_t tb = total_bits[blockIdx.y], nbytes = (tb + 7) >> 3;
-  for (uint32_t t = blockIdx.x; t < F.ntiles_max; t += gridDim.x) {  // t is uniform
+  for (uint32_t t = blockIdx.x; t < ntiles_max; t += gridDim.x) {  // t is uniform
     if (t * kTile < nbytes) {
       uint8_t bytes[16];
       const uint32_t i0 = t * kTile + threadIdx.x * 16;
-      const uint32_t n = i0 < nbytes ? ff_bytes(stream + F.bits_off, nbytes, tb, i0, bytes) : 0;
+      const uint32_t n = i0 < nbytes ? ff_bytes(src, nbytes, tb, i0, bytes) : 0;
       uint32_t tot;
       (void)wg_excl_scan(n, sh, &tot);
-      if (threadIdx.x == 0) cnt[F.tile0 + t] = tot;
+      if (threadIdx.x == 0) cnt[tile0 + t] = tot;
       __syncthreads();  // sh is reused by the next tile's scan
     } else if (threadIdx.x == 0) {
-      cnt[F.tile0 + t] = 0;
+      cnt[tile0 + t] = 0;
     }
   }
 }
 
-__global__ __launch_bounds__(256) void k_ff_write(const EncFrame *fr, const uint32_t *total_bits,
+__global__ __launch_bounds__(256) void k_ff_write(const EncFrame *__restrict__ fr, const uint32_t *total_bits,
                                                   const uint8_t *stream, const uint32_t *off, const uint32_t *nff,
                                                   const uint8_t *hdr, uint8_t *out, uint64_t *out_size) {
   const EncFrame &F = fr[blockIdx.y];
+  // the frame's fields in registers (k_ff_count)
+  const uint32_t hdr_len = F.hdr_len, hdr_off = F.hdr_off, tile0 = F.tile0;
+  const uint8_t *src = stream + F.bits_off;
+  uint8_t *o = out + F.out_off;
   const uint32_t tb = total_bits[blockIdx.y], nbytes = (tb + 7) >> 3;
   const uint32_t ntiles = (nbytes + kTile - 1) / kTile;
   __shared__ uint32_t sh[4];
   __shared__ uint8_t s_out[2 * kTile];  // a tile's bytes after stuffing (at most every byte 0xFF)
-  uint8_t *o = out + F.out_off;
   for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {  // grid-stride over the stream's tiles
     if (t == 0)
-      for (uint32_t j = threadIdx.x; j < F.hdr_len; j += 256) o[j] = hdr[F.hdr_off + j];
+      for (uint32_t j = threadIdx.x; j < hdr_len; j += 256) o[j] = hdr[hdr_off + j];
     uint8_t bytes[16];
     const uint32_t i0 = t * kTile + threadIdx.x * 16;
-    const uint32_t n = i0 < nbytes ? ff_bytes(stream + F.bits_off, nbytes, tb, i0, bytes) : 0;
+    const uint32_t n = i0 < nbytes ? ff_bytes(src, nbytes, tb, i0, bytes) : 0;
     uint32_t tot;
     // the tile's stuffed bytes are assembled in LDS, then stored as aligned dwords (per-lane
     // byte stores at scattered offsets were 16-32 store instructions per lane)
@@ -2241,7 +2255,7 @@ __global__ __launch_bounds__(256) void k_ff_write(const EncFrame *fr, const uint
     }
     __syncthreads();
     const uint32_t len = min((uint32_t)kTile, nbytes - t * kTile) + tot;
-    uint8_t *dst = o + (uint64_t)F.hdr_len + t * kTile + off[F.tile0 + t];
+    uint8_t *dst = o + (uint64_t)hdr_len + t * kTile + off[tile0 + t];
     const uint32_t head = min((uint32_t)(-(uintptr_t)dst & 3), len), nw = (len - head) >> 2;
     if (threadIdx.x < head) dst[threadIdx.x] = s_out[threadIdx.x];
     for (uint32_t i = threadIdx.x; i < nw; i += 256) {
@@ -2252,7 +2266,7 @@ __global__ __launch_bounds__(256) void k_ff_write(const EncFrame *fr, const uint
     const uint32_t tail = head + 4 * nw;
     if (threadIdx.x < len - tail) dst[tail + threadIdx.x] = s_out[tail + threadIdx.x];
     if (t == ntiles - 1 && threadIdx.x == 0) {
-      const uint64_t size = (uint64_t)F.hdr_len + nbytes + nff[blockIdx.y] + 2;
+      const uint64_t size = (uint64_t)hdr_len + nbytes + nff[blockIdx.y] + 2;
       o[size - 2] = 0xFF;
       o[size - 1] = 0xD9;
       out_size[blockIdx.y] = size;
@@ -2275,21 +2289,21 @@ hipError_t scan_i32(const ScanSeg *segs, int nseg, uint32_t max_tiles, const int
   return seg_scan<int32_t>(segs, nseg, max_tiles, in, out, tsum, totals, inclusive, s);
 }
 
-hipError_t dec_unstuff_count(const DecSeg *sg, int nseg, uint32_t max_tiles, const uint8_t *in, uint32_t *tile_cnt,
+hipError_t dec_unstuff_count(const DecSeg *__restrict__ sg, int nseg, uint32_t max_tiles, const uint8_t *in, uint32_t *tile_cnt,
                              hipStream_t s) {
   if (nseg <= 0 || !max_tiles) return hipSuccess;
   hipLaunchKernelGGL(k_unstuff_count, dim3(max_tiles, (unsigned)nseg), dim3(256), 0, s, sg, in, tile_cnt);
   return hipGetLastError();
 }
 
-hipError_t dec_unstuff_write(const DecSeg *sg, int nseg, uint32_t max_tiles, const uint8_t *in,
+hipError_t dec_unstuff_write(const DecSeg *__restrict__ sg, int nseg, uint32_t max_tiles, const uint8_t *in,
                              const uint32_t *tile_off, const uint32_t *us_len, uint8_t *us, hipStream_t s) {
   if (nseg <= 0 || !max_tiles) return hipSuccess;
   hipLaunchKernelGGL(k_unstuff_write, dim3(max_tiles, (unsigned)nseg), dim3(256), 0, s, sg, in, tile_off, us_len, us);
   return hipGetLastError();
 }
 
-hipError_t dec_sync(const DecSeg *sg, const DecFrame *fr, int nseg, uint32_t max_sub, const uint8_t *us,
+hipError_t dec_sync(const DecSeg *__restrict__ sg, const DecFrame *__restrict__ fr, int nseg, uint32_t max_sub, const uint8_t *us,
                     const uint32_t *us_len, const uint64_t *exit_in, uint64_t *exit_out, const uint32_t *cnt_in,
                     uint32_t *cnt_out, uint64_t *used, uint64_t *ck, uint32_t *ckrem, uint32_t *changed, int pass,
                     hipStream_t s) {
@@ -2299,7 +2313,7 @@ hipError_t dec_sync(const DecSeg *sg, const DecFrame *fr, int nseg, uint32_t max
   return hipGetLastError();
 }
 
-hipError_t dec_sync_spec(const DecSeg *sg, const DecFrame *fr, int nseg, uint32_t max_wg, const uint8_t *us,
+hipError_t dec_sync_spec(const DecSeg *__restrict__ sg, const DecFrame *__restrict__ fr, int nseg, uint32_t max_wg, const uint8_t *us,
                          const uint32_t *us_len, const SpecBufs &b, uint64_t *exit_out, uint32_t *cnt_out,
                          uint32_t *unresolved, hipStream_t s) {
   if (nseg <= 0 || !max_wg) return hipSuccess;
@@ -2310,7 +2324,7 @@ hipError_t dec_sync_spec(const DecSeg *sg, const DecFrame *fr, int nseg, uint32_
   return hipGetLastError();
 }
 
-hipError_t dec_write(const DecSeg *sg, const DecFrame *fr, int nseg, uint32_t max_sub, const uint8_t *us,
+hipError_t dec_write(const DecSeg *__restrict__ sg, const DecFrame *__restrict__ fr, int nseg, uint32_t max_sub, const uint8_t *us,
                      const uint32_t *us_len, const uint64_t *exits, const uint32_t *bstart, int16_t *coef,
                      int32_t *dcseq, hipStream_t s) {
   if (nseg <= 0 || !max_sub) return hipSuccess;
@@ -2319,7 +2333,7 @@ hipError_t dec_write(const DecSeg *sg, const DecFrame *fr, int nseg, uint32_t ma
   return hipGetLastError();
 }
 
-hipError_t dec_write4(const DecSeg *sg, const DecFrame *fr, int nseg, uint32_t max_sub, const uint8_t *us,
+hipError_t dec_write4(const DecSeg *__restrict__ sg, const DecFrame *__restrict__ fr, int nseg, uint32_t max_sub, const uint8_t *us,
                       const uint32_t *us_len, const uint64_t *exits, const uint32_t *cnt, const uint64_t *ck,
                       const uint32_t *ckrem, const uint32_t *bstart, int16_t *coef, int32_t *dcseq, hipStream_t s) {
   if (nseg <= 0 || !max_sub) return hipSuccess;
@@ -2328,7 +2342,7 @@ hipError_t dec_write4(const DecSeg *sg, const DecFrame *fr, int nseg, uint32_t m
   return hipGetLastError();
 }
 
-hipError_t dec_idct(const DecFrame *fr, int n, uint32_t max_blocks, const int16_t *coef, const int32_t *dcseq,
+hipError_t dec_idct(const DecFrame *__restrict__ fr, int n, uint32_t max_blocks, const int16_t *coef, const int32_t *dcseq,
                     uint8_t *planes, hipStream_t s) {
   if (n <= 0 || !max_blocks) return hipSuccess;
   // 4 units of 16 blocks per workgroup; a frame has ceil(nmcu / 16) * bpm <= (nblocks + 150) / 16 units
@@ -2337,7 +2351,7 @@ hipError_t dec_idct(const DecFrame *fr, int n, uint32_t max_blocks, const int16_
   return hipGetLastError();
 }
 
-hipError_t dec_color(const DecFrame *fr, int n, int max_w, int max_h, const uint8_t *planes, uint8_t *pix, int bgr,
+hipError_t dec_color(const DecFrame *__restrict__ fr, int n, int max_w, int max_h, const uint8_t *planes, uint8_t *pix, int bgr,
                      int invert, hipStream_t s) {
   if (n <= 0 || max_w <= 0 || max_h <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_color, dim3((unsigned)((max_w + 2047) / 2048), (unsigned)((max_h + 1) / 2), (unsigned)n), dim3(256), 0, s,
@@ -2345,7 +2359,7 @@ hipError_t dec_color(const DecFrame *fr, int n, int max_w, int max_h, const uint
   return hipGetLastError();
 }
 
-hipError_t enc_fdct(const EncFrame *fr, int n, uint32_t max_blocks, const EncTables *tab, const uint8_t *pix,
+hipError_t enc_fdct(const EncFrame *__restrict__ fr, int n, uint32_t max_blocks, const EncTables *tab, const uint8_t *pix,
                     int16_t *dcq, uint32_t *acbits, uint32_t *acscr, int bgr, int fastdct, hipStream_t s) {
   if (n <= 0 || !max_blocks) return hipSuccess;
   // a workgroup takes 4 units of 8 blocks; a frame has ceil(nmcu / 8) * bpm <= (nblocks + 70) / 8 units
@@ -2354,7 +2368,7 @@ hipError_t enc_fdct(const EncFrame *fr, int n, uint32_t max_blocks, const EncTab
   return hipGetLastError();
 }
 
-hipError_t enc_len(const EncFrame *fr, int n, uint32_t max_blocks, const EncTables *tab, const int16_t *dcq,
+hipError_t enc_len(const EncFrame *__restrict__ fr, int n, uint32_t max_blocks, const EncTables *tab, const int16_t *dcq,
                    uint32_t *acbits, uint32_t *bits, uint32_t *pre, hipStream_t s) {
   if (n <= 0 || !max_blocks) return hipSuccess;
   // 4 units of 64 MCUs per workgroup; a frame has ceil(nmcu / 64) * bpm <= nblocks / 64 + 10 units
@@ -2363,7 +2377,7 @@ hipError_t enc_len(const EncFrame *fr, int n, uint32_t max_blocks, const EncTabl
   return hipGetLastError();
 }
 
-hipError_t enc_pack(const EncFrame *fr, int n, uint32_t max_blocks, const uint32_t *pre, const uint32_t *acbits,
+hipError_t enc_pack(const EncFrame *__restrict__ fr, int n, uint32_t max_blocks, const uint32_t *pre, const uint32_t *acbits,
                     const uint32_t *acscr, const uint32_t *bitoff, const uint32_t *total_bits, uint8_t *stream,
                     hipStream_t s) {
   if (n <= 0 || !max_blocks) return hipSuccess;
@@ -2375,7 +2389,7 @@ hipError_t enc_pack(const EncFrame *fr, int n, uint32_t max_blocks, const uint32
 
 constexpr uint32_t kFFGrid = 64;  // stuffing workgroups per frame (grid-stride over tiles)
 
-hipError_t enc_ff_count(const EncFrame *fr, int n, uint32_t max_tiles, const uint32_t *total_bits,
+hipError_t enc_ff_count(const EncFrame *__restrict__ fr, int n, uint32_t max_tiles, const uint32_t *total_bits,
                         const uint8_t *stream, uint32_t *tile_cnt, hipStream_t s) {
   if (n <= 0 || !max_tiles) return hipSuccess;
   hipLaunchKernelGGL(k_ff_count, dim3(max_tiles < kFFGrid ? max_tiles : kFFGrid, (unsigned)n), dim3(256), 0, s, fr,
@@ -2383,7 +2397,7 @@ hipError_t enc_ff_count(const EncFrame *fr, int n, uint32_t max_tiles, const uin
   return hipGetLastError();
 }
 
-hipError_t enc_ff_write(const EncFrame *fr, int n, uint32_t max_tiles, const uint32_t *total_bits,
+hipError_t enc_ff_write(const EncFrame *__restrict__ fr, int n, uint32_t max_tiles, const uint32_t *total_bits,
                         const uint8_t *stream, const uint32_t *tile_off, const uint32_t *nff, const uint8_t *hdr,
                         uint8_t *out, uint64_t *out_size, hipStream_t s) {
   if (n <= 0 || !max_tiles) return hipSuccess;
@@ -2392,7 +2406,7 @@ hipError_t enc_ff_write(const EncFrame *fr, int n, uint32_t max_tiles, const uin
   return hipGetLastError();
 }
 
-hipError_t enc_compact(const EncFrame *fr, int n, const uint64_t *out_size, const uint8_t *out, uint8_t *pack,
+hipError_t enc_compact(const EncFrame *__restrict__ fr, int n, const uint64_t *out_size, const uint8_t *out, uint8_t *pack,
                        hipStream_t s) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_compact, dim3(32, (unsigned)n), dim3(256), 0, s, fr, out_size, out, pack);
