@@ -1471,13 +1471,32 @@ __device__ __forceinline__ void color_rows(const DecFrame &F, const Geom &g, con
       rows[1] = min(y1, dh - 1);
     }
     int b[2][NR][6];
+    // Away from the right edge, samples i0 .. i0 + 3 are one aligned dword (i0 is a multiple
+    // of 4; rows are pw bytes, a multiple of 8, from 256-B aligned planes) and only the two
+    // neighbours are byte loads: 3 loads per chroma row instead of 6.
+    if (i0 + 4 <= dw - 1) {
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const uint8_t *p = planes + F.plane_off[k + 1];
+      for (int k = 0; k < 2; ++k) {
+        const uint8_t *p = planes + F.plane_off[k + 1];
 #pragma unroll
-      for (int rr = 0; rr < NR; ++rr)
+        for (int rr = 0; rr < NR; ++rr) {
+          const uint8_t *r = p + (size_t)rows[rr] * pw;
+          const uint32_t mid = *reinterpret_cast<const uint32_t *>(r + i0);
+          b[k][rr][0] = r[ix[0]];
 #pragma unroll
-        for (int m = 0; m < 6; ++m) b[k][rr][m] = p[(size_t)rows[rr] * pw + ix[m]];
+          for (int m = 1; m < 5; ++m) b[k][rr][m] = (int)((mid >> (8 * (m - 1))) & 0xFF);
+          b[k][rr][5] = r[i0 + 4];
+        }
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const uint8_t *p = planes + F.plane_off[k + 1];
+#pragma unroll
+        for (int rr = 0; rr < NR; ++rr)
+#pragma unroll
+          for (int m = 0; m < 6; ++m) b[k][rr][m] = p[(size_t)rows[rr] * pw + ix[m]];
+      }
     }
     unpack8(qa, v0[0]);
     unpack8(qb, v1[0]);
