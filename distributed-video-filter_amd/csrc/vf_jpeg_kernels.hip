@@ -1471,31 +1471,26 @@ __device__ __forceinline__ void color_rows(const DecFrame &F, const Geom &g, con
       rows[1] = min(y1, dh - 1);
     }
     int b[2][NR][6];
-    // Away from the right edge, samples i0 .. i0 + 3 are one aligned dword (i0 is a multiple
-    // of 4; rows are pw bytes, a multiple of 8, from 256-B aligned planes) and only the two
-    // neighbours are byte loads: 3 loads per chroma row instead of 6.
-    if (i0 + 4 <= dw - 1) {
+    // Samples i0 .. i0 + 3 are one aligned dword (i0 is a multiple of 4 and below dw <= pw;
+    // rows are pw bytes, a multiple of 8, from 256-B aligned planes) and only the two
+    // neighbours are byte loads: 3 loads per chroma row instead of 6.  At the right edge the
+    // dword's bytes past dw - 1 are replaced by byte dw - 1 - i0 (the edge clamp), so no lane
+    // takes another path.
+    const int e = min(dw - 1 - i0, 3);
+    int sh[4];
 #pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const uint8_t *p = planes + F.plane_off[k + 1];
+    for (int m = 0; m < 4; ++m) sh[m] = 8 * min(m, e);
 #pragma unroll
-        for (int rr = 0; rr < NR; ++rr) {
-          const uint8_t *r = p + (size_t)rows[rr] * pw;
-          const uint32_t mid = *reinterpret_cast<const uint32_t *>(r + i0);
-          b[k][rr][0] = r[ix[0]];
+    for (int k = 0; k < 2; ++k) {
+      const uint8_t *p = planes + F.plane_off[k + 1];
 #pragma unroll
-          for (int m = 1; m < 5; ++m) b[k][rr][m] = (int)((mid >> (8 * (m - 1))) & 0xFF);
-          b[k][rr][5] = r[i0 + 4];
-        }
-      }
-    } else {
+      for (int rr = 0; rr < NR; ++rr) {
+        const uint8_t *r = p + (size_t)rows[rr] * pw;
+        const uint32_t mid = *reinterpret_cast<const uint32_t *>(r + i0);
+        b[k][rr][0] = r[ix[0]];
 #pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const uint8_t *p = planes + F.plane_off[k + 1];
-#pragma unroll
-        for (int rr = 0; rr < NR; ++rr)
-#pragma unroll
-          for (int m = 0; m < 6; ++m) b[k][rr][m] = p[(size_t)rows[rr] * pw + ix[m]];
+        for (int m = 1; m < 5; ++m) b[k][rr][m] = (int)((mid >> sh[m - 1]) & 0xFF);
+        b[k][rr][5] = r[ix[5]];
       }
     }
     unpack8(qa, v0[0]);
