@@ -603,18 +603,25 @@ bool Engine::step_mapped_retire() {
   return true;
 }
 
+// Called from the engine thread and from run_now on the caller's thread (a synchronous
+// zero-copy call while async jobs are in flight), so the free list is locked.
 hipEvent_t Engine::take_event() {
-  if (!free_events_.empty()) {
-    hipEvent_t e = free_events_.back();
-    free_events_.pop_back();
-    return e;
+  {
+    std::lock_guard<std::mutex> lk(ev_mu_);
+    if (!free_events_.empty()) {
+      hipEvent_t e = free_events_.back();
+      free_events_.pop_back();
+      return e;
+    }
   }
   hipEvent_t e = nullptr;
   return hipEventCreate(&e) == hipSuccess ? e : nullptr;
 }
 
 void Engine::give_event(hipEvent_t e) {
-  if (e) free_events_.push_back(e);
+  if (!e) return;
+  std::lock_guard<std::mutex> lk(ev_mu_);
+  free_events_.push_back(e);
 }
 
 int Engine::busy_slots() const {

@@ -172,6 +172,7 @@ class Engine {
   std::vector<Slot> slots_;
   size_t fill_ = 0, d2h_ = 0, retire_ = 0;
   std::unique_ptr<CopyPool> pool_;
+  std::mutex ev_mu_;             // free_events_: the engine thread and run_now's caller both take and give
   std::vector<hipEvent_t> free_events_;
 
   std::mutex mu_;  // guards everything below

@@ -199,6 +199,7 @@ class Distributor:
         self.departures = 0
         self.results_received = 0
         self.result_errors = 0
+        self.quarantine_expired = 0   # slots of evicted workers' frames freed after the grace period
         # threads (distributor.py:42-51)
         self.running = False
         self.distribute_thread = threading.Thread(target=self.handle_distribute_requests, daemon=True)
@@ -860,7 +861,7 @@ class Distributor:
             ring = None
             use_ring = p.shm and any(it["slot"] is not None for it in items)
             if use_ring:
-                sid = items[0]["slot"] // self.ring_slots
+                sid = next(it["slot"] for it in items if it["slot"] is not None) // self.ring_slots
                 ring = {"name": self._slices[sid].ring.name, "slot_bytes": self._slices[sid].ring.slot_bytes}
             metas, payloads = [], []
             for it in items:
@@ -916,6 +917,8 @@ class Distributor:
         now = time.monotonic()
         with self._cv:
             for p in list(self._peers.values()):
+                if p.quarantine:
+                    self._expire_quarantine(p, now)
                 if not p.alive:
                     continue
                 if p.batches and now - p.batches[0][0] > self.batch_timeout:
@@ -929,6 +932,18 @@ class Distributor:
                     p.waiting_since = now
                 elif now - p.waiting_since > self.batch_timeout:
                     self._evict(p, f"frames waiting, no request for {self.batch_timeout:g} s")
+
+    def _expire_quarantine(self, p: _Peer, now: float) -> None:
+        """Slots of frames an evicted worker still held come back after a grace period of one
+        more ``batch_timeout``: ZeroMQ reports no disconnects, so a worker that died or hung
+        would otherwise keep them out of use for ever and every eviction would shrink the ring
+        (ADVICE r02).  A result that still arrives later finds no dispatch record and is
+        dropped (``_find_copy``), so it cannot be mistaken for the slot's next frame."""
+        for idx in [i for i, it in p.quarantine.items() if now - it.get("_evicted_at", now) > self.batch_timeout]:
+            it = p.quarantine.pop(idx)
+            self._free_slot(it.get("slot"))
+            self._copy_done(it["frame_index"])
+            self.quarantine_expired += 1
 
     def _evict(self, p: _Peer, reason: str, gone: bool = False) -> None:
         """Take ``p`` out of service: re-queue (or lose, after ``max_attempts``) what it holds."""
@@ -948,6 +963,7 @@ class Distributor:
         for idx in sorted(p.inflight):
             it = p.inflight[idx]
             it.pop("_batch", None)
+            it["_evicted_at"] = time.monotonic()
             p.quarantine[idx] = it          # its slot stays out of use until a result frees it
             if self.policy == "latest" or it["attempts"] >= self.max_attempts:
                 self._lose(idx)

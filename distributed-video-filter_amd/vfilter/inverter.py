@@ -32,7 +32,7 @@ import numpy as np
 from . import wire
 from ._lib import Context, default_device
 from .jpeg import TurboJPEG
-from .worker import Worker
+from .worker import Worker, WorkerFailed
 
 
 class InverterWorker(Worker):
@@ -229,6 +229,9 @@ def main(argv=None):
                             protocol=args.protocol, transport=args.transport, verbose=args.verbose)
     try:
         worker.start()
+    except WorkerFailed as e:  # a fresh process, not a re-exec: let the supervisor restart it
+        print(f"Inverter worker: giving up: {e}")
+        raise SystemExit(3)
     finally:
         worker.close()
 

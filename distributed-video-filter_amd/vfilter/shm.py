@@ -157,10 +157,20 @@ def _attach(name: str) -> shared_memory.SharedMemory:
     registers every attach and would unlink the owner's segment when this process exits
     (bpo-38119); unregistering afterwards instead removes the owner's own registration when
     the tracker is shared (multiprocessing "spawn" children share their parent's)."""
+    import sys
+    if sys.version_info >= (3, 13):
+        return shared_memory.SharedMemory(name=name, track=False)
     from multiprocessing import resource_tracker
+    skip = {name, "/" + name.lstrip("/")}
     with _attach_lock:
         reg = resource_tracker.register
-        resource_tracker.register = lambda *a, **k: None
+
+        def register(rname, rtype):  # only this attach is skipped: another thread creating a
+            if rtype == "shared_memory" and rname in skip:  # segment meanwhile still registers it
+                return None
+            return reg(rname, rtype)
+
+        resource_tracker.register = register
         try:
             return shared_memory.SharedMemory(name=name)
         finally:

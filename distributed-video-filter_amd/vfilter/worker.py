@@ -32,6 +32,12 @@ from . import wire
 from .shm import FrameRing
 
 
+class WorkerFailed(RuntimeError):
+    """Raised out of ``Worker.start`` after ``max_job_failures`` consecutive batches could not
+    be collected (e.g. a sticky device error): the process should exit non-zero so that a
+    supervisor starts a fresh one (the distributor re-queues the frames it never got back)."""
+
+
 def _same_buffer(r, o) -> bool:
     """True when result ``r`` was written in place at the start of ring output view ``o``
     (the whole view, or, for a plugin whose results have their own size, a prefix of it)."""
@@ -44,6 +50,8 @@ class Worker:
     # True for a plugin whose results have their own size (a re-encoded JPEG): ring frames then
     # get their slot's whole output half to write into, and the result carries its length
     sized_results = False
+    # consecutive batches whose collection raised before the loop gives up (WorkerFailed)
+    max_job_failures = 8
 
     def __init__(self, host: str = "localhost", distribute_port: int = 5555, collect_port: int = 5556, *,
                  transport: str = "auto", protocol: str = "v1", batch: int = 1, depth: int = 0,
@@ -265,6 +273,38 @@ class Worker:
         self.frames_processed += len(metas)
         return True
 
+    def _fail_job(self, job, exc: Exception) -> None:
+        """A batch whose collection raised: report every frame of it as failed (so an in-order
+        consumer does not wait for them) and drop the job."""
+        d, start_time = job[0], job[1]
+        metas = [wire.FrameMeta(index=m.index, nbytes=m.nbytes, shape=m.shape, slot=m.slot,
+                                start=start_time, end=time.time(), error=f"{type(exc).__name__}: {exc}")
+                 for m in d.metas]
+        self.errors += len(metas)
+        print(f"Error in worker: batch {[m.index for m in d.metas]}: {type(exc).__name__}: {exc}")
+        try:
+            self.collect_socket.send(wire.encode_result(self.process_id, metas, [None] * len(metas), [],
+                                                        wid=self.wid))
+        except Exception as e:  # the distributor re-queues frames whose result never arrives
+            print(f"Error in worker: could not report the failed batch: {e}")
+
+    def _collect_jobs(self, jobs, block_when: int) -> None:
+        """Finish jobs at the head of ``jobs`` in arrival order.  A job whose collection raises
+        is popped and reported as failed (not retried); after ``max_job_failures`` in a row the
+        loop raises WorkerFailed."""
+        while jobs:
+            try:
+                if not self._finish_job(jobs[0], block=len(jobs) >= block_when):
+                    return
+                jobs.popleft()
+                self._job_failures = 0
+            except Exception as e:
+                self._fail_job(jobs.popleft(), e)
+                self._job_failures = getattr(self, "_job_failures", 0) + 1
+                if self._job_failures >= self.max_job_failures:
+                    raise WorkerFailed(f"{self._job_failures} batches in a row failed; last: "
+                                       f"{type(e).__name__}: {e}") from e
+
     def _loop_v1(self, max_frames):
         """Credit loop: ``depth`` requests outstanding; up to ``inflight`` received batches
         in progress at once (a GPU plugin submits them asynchronously, so the device works
@@ -278,8 +318,7 @@ class Worker:
                 while outstanding < self.depth:
                     self.dealer_socket.send(wire.encode_request(self.batch, shm=True, wid=self.wid, numa=numa))
                     outstanding += 1
-                while jobs and self._finish_job(jobs[0], block=len(jobs) >= self.inflight):
-                    jobs.popleft()
+                self._collect_jobs(jobs, self.inflight)
                 if len(jobs) >= self.inflight:
                     continue
                 if not self.dealer_socket.poll(1 if jobs else 10):
@@ -294,12 +333,15 @@ class Worker:
                 if d.version == 1:
                     outstanding -= 1
                 jobs.append(self._start_job(d, start_time))
+            except WorkerFailed:
+                raise
             except Exception as e:  # worker.py:74-76: report and keep serving
                 self.errors += 1
                 print(f"Error in worker: {type(e).__name__}: {e}")
                 time.sleep(0.01)
         while jobs:  # finish what was accepted before stopping
+            job = jobs.popleft()
             try:
-                self._finish_job(jobs.popleft(), block=True)
+                self._finish_job(job, block=True)
             except Exception as e:
-                print(f"Error in worker: {type(e).__name__}: {e}")
+                self._fail_job(job, e)

@@ -298,6 +298,67 @@ def test_hbm_resident_sweep_point_batch256(vf_ctx):
             vf_ctx.free_device(p)
 
 
+def _digests_1080p(golden_dir):
+    with open(os.path.join(golden_dir, "seeded_digests.json")) as f:
+        recs = {r["seed"]: r for r in json.load(f)["frames"] if r["size"] == "1080p"}
+    return ([recs[s]["input_sha256"] for s in range(4)], [recs[s]["expected_sha256"] for s in range(4)])
+
+
+def test_hbm_resident_sweep_top_batch4096(vf_ctx, golden_dir):
+    """configs[4] top point: 4096 x 1080p = 25.48 GB resident in, the same out, ONE
+    vf_invert_device call (the bench's configs4_sweep shape), then ~~x over the whole buffer.
+
+    Every frame of both outputs is checked by sha256 against the golden seeded digests
+    (frame f holds seed f % 4).  Byte offsets cross 2^32, 2^33 and 2^34: the frames that
+    straddle them are named and checked first, so a 32-bit offset bug in launch_stream's
+    sub-launch arithmetic (vf_stream.h) shows up as a named frame, not a count."""
+    import concurrent.futures as cf
+    n_frames = 4096
+    total = n_frames * FB_1080
+    in_sha, out_sha = _digests_1080p(golden_dir)
+    base = [oracle.synthetic_frame(s, 1080, 1920).reshape(-1) for s in range(4)]
+    for s in range(4):
+        assert hashlib.sha256(base[s]).hexdigest() == in_sha[s]
+    straddle = {k: (1 << k) // FB_1080 for k in (32, 33, 34)}
+    for k, f in straddle.items():
+        assert f * FB_1080 < (1 << k) < (f + 1) * FB_1080
+    piece = 160  # frames per host piece (995 MB); a multiple of 4 keeps the seed pattern
+    chunk = np.concatenate([base[f % 4] for f in range(piece)])
+    ds, d1, d2 = (vf_ctx.alloc_device(total) for _ in range(3))
+    pool = cf.ThreadPoolExecutor(16)  # hashlib releases the GIL on large buffers
+    try:
+        for f0 in range(0, n_frames, piece):
+            nf = min(piece, n_frames - f0)
+            vf_ctx.upload(ds + f0 * FB_1080, chunk, nf * FB_1080)
+        vf_ctx.sync()
+        vf_ctx.invert_device(ds, d1, total)  # one call: 25.48 GB, ~100 sub-launches
+        vf_ctx.invert_device(d1, d2, total)
+        vf_ctx.sync()
+        y = np.empty(FB_1080, np.uint8)
+        for k, f in straddle.items():
+            vf_ctx.download(y, d1 + f * FB_1080, FB_1080)
+            vf_ctx.sync()
+            assert hashlib.sha256(y).hexdigest() == out_sha[f % 4], f"frame {f} straddling 2^{k}"
+            vf_ctx.download(y, d2 + f * FB_1080, FB_1080)
+            vf_ctx.sync()
+            assert hashlib.sha256(y).hexdigest() == in_sha[f % 4], f"frame {f} straddling 2^{k} (~~x)"
+        host = np.empty(piece * FB_1080, np.uint8)
+        for dev, want in ((d1, out_sha), (d2, in_sha)):
+            bad = []
+            for f0 in range(0, n_frames, piece):
+                nf = min(piece, n_frames - f0)
+                vf_ctx.download(host, dev + f0 * FB_1080, nf * FB_1080)
+                vf_ctx.sync()
+                views = [host[i * FB_1080:(i + 1) * FB_1080] for i in range(nf)]
+                got = list(pool.map(lambda v: hashlib.sha256(v).hexdigest(), views))
+                bad += [f0 + i for i in range(nf) if got[i] != want[(f0 + i) % 4]]
+            assert not bad, f"{len(bad)} frames differ, first {bad[:8]}"
+    finally:
+        pool.shutdown()
+        for p in (ds, d1, d2):
+            vf_ctx.free_device(p)
+
+
 def test_timeline_chunks_cover_the_call(vf_ctx):
     """vf_last_timeline: one record per chunk, bytes sum to the call, H2D <= kernel <= D2H."""
     x = np.random.default_rng(1).integers(0, 256, 3 * (16 << 20) + 123, dtype=np.uint8)
@@ -351,6 +412,34 @@ def test_async_frames_on_pinned_memory(vf_ctx):
             vf_ctx.wait(10 ** 9)
         y = oracle.synthetic_frame(77, 480, 640)  # sync path after async work
         assert np.array_equal(vfilter.bitwise_not(y, ctx=vf_ctx), oracle.invert(y))
+    finally:
+        for p in ps + pd:
+            vf_ctx.free_host(p)
+
+
+def test_sync_zero_copy_while_async_in_flight(vf_ctx):
+    """A synchronous zero-copy call (Engine::run_now, on the caller's thread) while async jobs
+    are in flight on the engine thread: both take and give events from the same free list
+    (vfilter.h allows async submits followed by a sync call on one thread).
+    200 rounds of three async jobs + one sync call; every byte exact."""
+    n = 1 << 20
+    ps = [vf_ctx.alloc_host(n) for _ in range(5)]
+    pd = [vf_ctx.alloc_host(n) for _ in range(5)]
+    try:
+        hs = [np.ctypeslib.as_array((ctypes.c_uint8 * n).from_address(p)) for p in ps]
+        hd = [np.ctypeslib.as_array((ctypes.c_uint8 * n).from_address(p)) for p in pd]
+        for i, h in enumerate(hs):
+            h[:] = np.random.default_rng(100 + i).integers(0, 256, n, dtype=np.uint8)
+        for r in range(200):
+            ts = [vf_ctx.invert_frames_async([ps[k]], [pd[k]], [n]) for k in range(3)]
+            hd[4][:16] = 0
+            vf_ctx.invert_host(ps[4], pd[4], n)
+            assert _zero_copy(vf_ctx.last_timeline())
+            assert np.array_equal(hd[4], ~hs[4]), r
+            for t in ts:
+                vf_ctx.wait(t)
+        for k in range(5):
+            assert np.array_equal(hd[k], ~hs[k]), k
     finally:
         for p in ps + pd:
             vf_ctx.free_host(p)

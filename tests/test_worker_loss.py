@@ -337,3 +337,100 @@ def test_worker_that_stops_asking_is_evicted():
         a.close()
         b.close()
         d.cleanup()
+
+
+def _sticky_worker(dport, cport):
+    from _plumbing import OracleWorker
+
+    class W(OracleWorker):  # batches that can never be collected: a sticky device error
+        def submit_batch(self, frames, metas, outs):
+            return ("sticky", len(frames))
+
+        def poll_batch(self, handle, block):
+            raise RuntimeError("hipErrorIllegalAddress (sticky)")
+
+    return W("127.0.0.1", dport, cport, batch=2, protocol="v1", transport="tcp", inflight=1)
+
+
+@pytest.mark.timeout(60)
+def test_uncollectable_batches_are_reported_then_the_worker_exits():
+    """a batch whose collection raises is popped and reported as failed (every
+    frame an error result, so the in-order consumer skips it) instead of being retried every
+    10 ms forever; after max_job_failures in a row the loop raises WorkerFailed, which the
+    worker CLI turns into a non-zero exit for a supervisor to restart."""
+    from vfilter.worker import WorkerFailed
+    d = _dist(policy="pull", reassembly="ordered", queue_size=64)
+    w = _sticky_worker(d.distribute_port, d.collect_port)
+    failed = []
+
+    def run():
+        try:
+            w.start()
+        except WorkerFailed as e:
+            failed.append(e)
+
+    th = threading.Thread(target=run, daemon=True)
+    th.start()
+    try:
+        _wait_workers(d, 1)
+        for i in range(40):
+            d.add_frame_for_distribution(oracle.synthetic_frame(i, 4, 4))
+        th.join(30)
+        assert not th.is_alive() and failed, "the worker kept retrying"
+        assert w.max_job_failures == 8
+        t0 = time.time()
+        while d.result_errors < 16 and time.time() - t0 < 10:
+            time.sleep(0.02)
+        assert d.result_errors >= 16  # 8 batches x 2 frames, each reported as an error result
+    finally:
+        w.close()
+        d.cleanup()
+
+
+@pytest.mark.timeout(60)
+def test_evicted_workers_slots_come_back_after_the_grace_period():
+    """ZeroMQ reports no disconnects, so a worker that hangs is evicted without
+    ``gone`` and its in-flight frames' ring slots stay quarantined.  After one more
+    ``batch_timeout`` they are freed (the ring does not shrink per eviction); a result that
+    still arrives later is dropped."""
+    d = Distributor(0, 0, policy="pull", reassembly="ordered", queue_size=16, transport="tcp",
+                    host="127.0.0.1", verbose=False, batch_timeout=0.3, ring_slots=4, ring_slot_bytes=64)
+    d.running = True
+    a, b = _ManualWorker(d, "A"), _ManualWorker(d, "B")
+    coll = threading.Thread(target=d.check_inverter_output, daemon=True)
+    coll.start()
+    try:
+        a.request()
+        _step_until(d, lambda: d.num_workers() == 1)
+        frames = [bytes([i]) * 8 for i in range(4)]
+        for f in frames:
+            d.add_frame_for_distribution(f)
+        d.dispatch_step(0)
+        da = a.recv()
+        assert [m.index for m in da.metas] == [0, 1, 2, 3]
+        b.request()
+        _step_until(d, lambda: d.num_workers() == 2)
+        total = d.total_slots()
+        time.sleep(0.35)
+        d.dispatch_step(0)                                  # A evicted (hung), not gone
+        assert d.ordering_stats()["evictions"] == 1
+        b.request()
+        _step_until(d, lambda: b.dealer.poll(0))
+        db = b.recv()
+        b.answer(db)
+        for i in range(4):
+            item = d.get_next_frame(timeout=5)
+            assert item is not None and item[0] == i and bytes(item[1]) == oracle.invert_bytes(frames[i])
+        assert d.free_slots() == total - 4                  # A's copies still quarantined
+        time.sleep(0.35)
+        _step_until(d, lambda: d.free_slots() == total)     # grace period over: slots back
+        assert d.quarantine_expired == 4
+        a.answer(da)                                        # far too late: dropped
+        time.sleep(0.2)
+        assert d.free_slots() == total and d.ordering_stats()["released"] == 4
+    finally:
+        d.running = False
+        coll.join(2)
+        a.close()
+        b.close()
+        d.cleanup()
