@@ -15,7 +15,7 @@ all: lib oracle
 lib: $(LIB)
 
 SRCS := $(CSRC)/vf_kernels.hip $(CSRC)/vf_engine.hip $(CSRC)/vf_api.hip $(CSRC)/vf_jpeg_kernels.hip $(CSRC)/vf_jpeg_host.hip
-HDRS := $(CSRC)/vf_internal.h $(CSRC)/vf_stream.h $(CSRC)/vf_host_mem.h $(CSRC)/vf_jpeg.h $(CSRC)/vf_jpeg_codec.h include/vfilter.h
+HDRS := $(CSRC)/vf_internal.h $(CSRC)/vf_stream.h $(CSRC)/vf_host_mem.h $(CSRC)/vf_jpeg.h $(CSRC)/vf_jpeg_types.h $(CSRC)/vf_jpeg_parse.h $(CSRC)/vf_jpeg_codec.h include/vfilter.h
 
 $(LIB): $(SRCS) $(HDRS)
 	$(HIPCC) $(HIPFLAGS) $(LDFLAGS) -pthread $(SRCS) -o $@

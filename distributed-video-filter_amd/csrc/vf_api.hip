@@ -16,11 +16,11 @@
 
 #include <algorithm>
 #include <array>
+#include <atomic>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <algorithm>
 #include <condition_variable>
 #include <map>
 #include <mutex>
@@ -75,6 +75,8 @@ struct vf_ctx {
   // submitted vf_jpeg_invert_submit batches: ticket -> the codec that holds it until fetched
   std::map<uint64_t, vf::jpeg::Codec *> jpeg_jobs;
   uint64_t jpeg_next_ticket = 1;
+  // decoder frame-size limit (vf_jpeg_set_max_pixels), applied to a codec whenever it is leased
+  std::atomic<uint64_t> jpeg_max_pixels{vf::jpeg::kDefaultMaxPixels};
   // vf_bench_device_ring's region events, created once (not inside a caller's timed region)
   hipEvent_t bench_ev[2] = {nullptr, nullptr};
 };
@@ -553,6 +555,7 @@ class CodecLease {
       c_ = new (std::nothrow) vf::jpeg::Codec(ctx->device, gated ? &ctx->jpeg_gate : nullptr);
       if (c_) ctx->jpeg_all.push_back(c_);
     }
+    if (c_) c_->set_max_pixels(ctx->jpeg_max_pixels.load());
   }
   ~CodecLease() {
     if (!c_) return;
@@ -577,15 +580,16 @@ class CodecLease {
 constexpr size_t kMaxJpegJobs = 8;
 vf::jpeg::Codec *lease_nowait(vf_ctx *ctx) {
   std::lock_guard<std::mutex> lk(ctx->jpeg_mu);
+  vf::jpeg::Codec *c = nullptr;
   if (!ctx->jpeg_free.empty()) {
-    vf::jpeg::Codec *c = ctx->jpeg_free.back();
+    c = ctx->jpeg_free.back();
     ctx->jpeg_free.pop_back();
-    return c;
+  } else if (ctx->jpeg_all.size() < kMaxJpegJobs) {
+    static const bool gated = env_size("VF_JPEG_GATE", 0) != 0;
+    c = new (std::nothrow) vf::jpeg::Codec(ctx->device, gated ? &ctx->jpeg_gate : nullptr);
+    if (c) ctx->jpeg_all.push_back(c);
   }
-  if (ctx->jpeg_all.size() >= kMaxJpegJobs) return nullptr;
-  static const bool gated = env_size("VF_JPEG_GATE", 0) != 0;
-  vf::jpeg::Codec *c = new (std::nothrow) vf::jpeg::Codec(ctx->device, gated ? &ctx->jpeg_gate : nullptr);
-  if (c) ctx->jpeg_all.push_back(c);
+  if (c) c->set_max_pixels(ctx->jpeg_max_pixels.load());
   return c;
 }
 
@@ -636,6 +640,12 @@ VF_EXPORT int vf_jpeg_header(const uint8_t *jpeg, size_t size, int *width, int *
   std::string err;
   const int rc = vf::jpeg::header_info(jpeg, size, width, height, subsamp, colorspace, &err);
   return rc == VF_OK ? VF_OK : set_err(nullptr, rc, 0, "vf_jpeg_header: %s", err.c_str());
+}
+
+VF_EXPORT int vf_jpeg_set_max_pixels(vf_ctx *ctx, uint64_t max_pixels) {
+  if (!ctx) return set_err(nullptr, VF_E_INVALID, 0, "vf_jpeg_set_max_pixels: NULL context");
+  ctx->jpeg_max_pixels.store(max_pixels ? max_pixels : vf::jpeg::kDefaultMaxPixels);
+  return VF_OK;
 }
 
 VF_EXPORT size_t vf_jpeg_buffer_size(int width, int height, int subsamp) {

@@ -118,6 +118,8 @@ class Codec {
   // sizes[f] = its size either way, *placed = how many were copied; the batch stays fetchable
   int scatter_invert(uint8_t *const *outs, const size_t *caps, size_t *sizes, int *placed);
   uint64_t fetch_refills() const { return fetch_refills_; }
+  // frames whose SOF claims more pixels are refused before anything is sized from them
+  void set_max_pixels(uint64_t v) { max_pixels_ = v ? v : kDefaultMaxPixels; }
   bool waited() const { return waited_; }
   // wait for anything still queued on the codec's stream (after a failed call, before the codec
   // and its pinned buffers go to the next caller)
@@ -142,6 +144,7 @@ class Codec {
 
   int device_;
   ComputeGate *gate_;
+  uint64_t max_pixels_ = kDefaultMaxPixels;
   hipStream_t s_ = nullptr;
   hipEvent_t ev_[10] = {};
   hipEvent_t done_ = nullptr;  // the last call's downloads have landed

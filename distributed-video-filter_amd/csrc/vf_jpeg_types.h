@@ -1,0 +1,139 @@
+// vf_jpeg_types.h — the JPEG batch descriptors and table layouts shared by the kernels
+// (vf_jpeg_kernels.hip), their host side (vf_jpeg_host.hip) and the host parse
+// (vf_jpeg_parse.h).  Plain C++ (no HIP), so the parse builds under g++ with sanitizers.
+// Not installed.
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+namespace vf {
+namespace jpeg {
+
+// libjpeg's JPEG_MAX_DIMENSION (jmorecfg.h): jdinput.c initial_setup refuses larger frames
+// with JERR_IMAGE_TOO_BIG
+constexpr int kMaxDimension = 65500;
+// default per-frame pixel limit of a context's decoder (vf_jpeg_set_max_pixels): 8192 x 8192
+constexpr uint64_t kDefaultMaxPixels = 8192ull * 8192ull;
+
+constexpr int kMaxBpm = 10;     // blocks per MCU (T.81 B.2.3)
+constexpr int kSubBits = 256;  // bits per Huffman-decoding subsequence
+constexpr int kTile = 4096;     // bytes per (un)stuffing tile
+constexpr int kMaxPasses = 64;  // sync-pass flags kept on the device
+#ifndef VF_KLOOK
+#define VF_KLOOK 9
+#endif
+constexpr int kLook = VF_KLOOK;        // Huffman lookahead bits
+constexpr int kAcScratchWords = 52;  // per-block AC bit scratch (63 codes of <= 26 bits + EOB)
+constexpr int kCkStep = kSubBits / 8 < 64 ? 64 : kSubBits / 8;  // Huffman-sync checkpoint spacing (bits)
+constexpr int kCk = kSubBits / kCkStep - 1;                       // checkpoints per subsequence
+
+// MCU geometry of one frame (libjpeg jdinput.c / jcmaster.c per-scan setup, restated)
+struct Geom {
+  int32_t w, h, ncomp, bpm;
+  int32_t maxh, maxv, mcux, mcuy, nmcu, nblocks;
+  int32_t hs[3], vs[3];  // sampling factors
+  int32_t mh[3], mv[3];  // blocks of the component per MCU (1x1 in a single-component scan)
+  int32_t wb[3], hb[3];  // width/height_in_blocks (real blocks)
+  int32_t pw[3], ph[3];  // component plane in samples (whole MCUs)
+  int32_t cfirst[3];     // first block-in-MCU of the component
+  int32_t dw[3], dh[3];  // downsampled size in samples: ceil(w * hs / maxh), ceil(h * vs / maxv)
+  int32_t rrows[3];      // encoder: sample rows from real pixel rows, ceil(h / maxv) * vs
+  // 32-bit, as every field here: a kernel reads a wave-uniform entry with one scalar load,
+  // where an 8-bit field would be a vector load and a wait
+  int32_t bcomp[kMaxBpm], bxo[kMaxBpm], byo[kMaxBpm];  // block-in-MCU -> component, x/y (blocks)
+  int32_t he[3], ve[3];  // expansion factors maxh / hs, maxv / vs
+};
+
+
+// Encoder tables: jcdctmgr.c reciprocal divisors, jchuff.c derived code tables
+struct EncTables {
+  uint16_t recip[2][64];  // natural order; [0] luma, [1] chroma
+  uint16_t corr[2][64];
+  int16_t shift[2][64];
+  uint32_t dc[2][16];   // (code << 8) | size by magnitude category
+  uint32_t ac[2][256];  // (code << 8) | size by run/size symbol
+};
+
+// Codes longer than kLook bits: lim[i] = (maxcode[l] + 1) << (16 - l) for l = kLook + 1 + i,
+// running maximum over i (lim[7] unused).  The length of the code starting the next 16 bits
+// c16 is kLook + 1 + #{i : c16 >= lim[i]} (17 = no code: jdhuff.c's corrupt-data case), the
+// same as jdhuff.c jpeg_huff_decode's length-by-length maxcode walk, in one 32-B LDS read.
+static_assert(kLook >= 9 && kLook <= 15, "lim[] holds code lengths kLook + 1 .. 16 (at most 7)");
+
+// Huffman decoding table: jdhuff.c derived table plus a kLook-bit lookahead
+struct HuffDec {
+  alignas(16) uint32_t lim[8];
+  uint16_t fast[1 << kLook];  // (length << 8) | symbol for codes of <= kLook bits, else 0
+  int32_t maxcode[18];
+  int32_t valoff[18];
+  uint8_t vals[256];
+};
+
+// The same table for the synchronisation decoders, which only need how far each symbol moves:
+// sfast[next kLook bits] = (zigzag advance << 8) | (code length + extra bits) for codes of
+// <= kLook bits (advance 1 for a DC symbol, run + 1 for an AC coefficient, 16 for ZRL, 64 for
+// EOB), 0 for longer codes (decoded through maxcode / valoff / vals).
+struct HuffSync {
+  alignas(16) uint32_t lim[8];
+  uint16_t sfast[1 << kLook];
+  int32_t maxcode[18];
+  int32_t valoff[18];
+  uint8_t vals[256];
+};
+
+struct DecFrame {
+  Geom g;
+  uint16_t q[3][64];       // dequantisation per component, natural order
+  HuffDec dc[3], ac[3];    // per component (kept adjacent: loaded into LDS as one block)
+  HuffSync sdc[3], sac[3];  // the same, for the synchronisation decoders (adjacent too)
+  uint32_t flags;          // bit 0: fancy upsampling allowed; bits 1-2: k_color layout (0 other,
+                           // 1 4:4:4, 2 chroma 2x1, 3 chroma 2x2; three components, full-size luma)
+  uint64_t blk0;           // first block in the batch coefficient buffer
+  uint64_t dcbase[3];      // per-component DC sequences in the DC buffer
+  uint64_t plane_off[3];   // component planes in the plane buffer
+  uint64_t out_off;        // interleaved pixels in the pixel buffer
+};
+
+// One entropy-coded segment, the unit of the unstuff / sync / write stages: a frame's whole
+// scan, or one restart interval of it.  With DRI every interval starts byte-aligned after an
+// RSTn marker with the DC predictions reset (T.81 F.1.2.3, jdhuff.c process_restart), so the
+// intervals decode as independent segments whose blocks and DC sequences tile the frame's.
+struct DecSeg {
+  uint32_t frame;          // its frame in the DecFrame array (tables, geometry)
+  uint32_t nblocks;        // blocks coded in the segment (whole MCUs)
+  uint64_t in_off;         // raw entropy-coded bytes in the batch input buffer (16-aligned)
+  uint32_t in_len;
+  uint32_t ntiles;         // kTile tiles over the raw bytes
+  uint32_t tile0;          // first tile slot
+  uint32_t sub0;           // first subsequence slot
+  uint32_t nsub_max;       // subsequence slots (ceil(in_len * 8 / kSubBits))
+  uint32_t wg0, nwg;       // speculative sync: first workgroup slot, workgroups (spec_lanes)
+  uint64_t tr0;            // speculative sync: first trajectory slot (nwg * 256 per segment)
+  uint64_t us_off;         // unstuffed stream in the unstuffed buffer (16-aligned)
+  uint64_t blk0;           // its first block in the batch coefficient buffer
+  uint64_t dcbase[3];      // its first entries of the frame's per-component DC sequences
+};
+
+struct EncFrame {
+  Geom g;
+  uint64_t img_off;     // interleaved input pixels in the pixel buffer
+  uint64_t blk0;        // first block in the batch coefficient buffer
+  uint64_t bits_off;    // packed bitstream (bytes, 16-aligned) in the bit buffer
+  uint64_t out_off;     // finished JPEG in the output buffer
+  uint32_t hdr_off, hdr_len;  // header bytes in the header buffer
+  uint32_t tile0, ntiles_max;  // stuffing tiles
+};
+
+// Segmented scans over per-frame arrays (Huffman bit offsets, block counts, DC prediction,
+// tile counts): segment s covers elements [base, base + len) and owns tile-sum slots
+// [tile0, tile0 + ceil(len / kScanTile)).
+constexpr int kScanPerThread = 8;
+constexpr int kScanTile = 256 * kScanPerThread;
+struct ScanSeg {
+  uint64_t base;
+  uint32_t len;
+  uint32_t tile0;
+};
+
+}  // namespace jpeg
+}  // namespace vf

@@ -18,7 +18,7 @@ from typing import Optional, Sequence
 import numpy as np
 
 LIB_NAME = "libvfilter_hip.so"
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 VF_OK = 0
 VF_E_INVALID = -1
@@ -67,6 +67,7 @@ SIGNATURES = {
     "vf_bench_device_ring": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_int, _sz, ctypes.c_int, _vp, _c_float_p,
                                             _c_float_p]),
     "vf_jpeg_header": (ctypes.c_int, [_vp, _sz, _c_int_p, _c_int_p, _c_int_p, _c_int_p]),
+    "vf_jpeg_set_max_pixels": (ctypes.c_int, [_vp, ctypes.c_uint64]),
     "vf_jpeg_buffer_size": (_sz, [ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "vf_jpeg_encode": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                       ctypes.c_int, _vp, _vp, _vp]),
@@ -337,6 +338,10 @@ class Context:
     def _ptrs(bufs):
         arrs = [b if isinstance(b, np.ndarray) else np.frombuffer(b, dtype=np.uint8) for b in bufs]
         return arrs, (ctypes.c_void_p * len(arrs))(*[a.ctypes.data for a in arrs])
+
+    def jpeg_set_max_pixels(self, max_pixels: int) -> None:
+        """Decoder frame-size limit (vf_jpeg_set_max_pixels; 0 = the default, 8192 x 8192)."""
+        self._check(self._lib.vf_jpeg_set_max_pixels(self._ctx, int(max_pixels)))
 
     def jpeg_encode(self, imgs: Sequence[np.ndarray], pixel_format: int, quality: int, subsamp: int,
                     flags: int = 0) -> list:

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define VF_ABI_VERSION 2
+#define VF_ABI_VERSION 3
 
 /* status codes */
 #define VF_OK           0
@@ -226,6 +226,14 @@ int vf_bench_device_ring(vf_ctx *ctx, void *const *srcs, void *const *dsts, int 
  * (-1 if none matches), *colorspace = TJCS_YCbCr (1) or TJCS_GRAY (2). */
 int vf_jpeg_header(const uint8_t *jpeg, size_t size, int *width, int *height, int *subsamp,
                    int *colorspace);
+
+/* Decoder frame-size limit of the context: a JPEG whose SOF claims more than max_pixels
+ * (width x height) is refused with VF_E_JPEG before anything is sized from it, as is any side
+ * above 65500 (libjpeg's JPEG_MAX_DIMENSION, jdinput.c initial_setup).  0 restores the
+ * default, 8192 x 8192.  The frames a worker decodes come off the network
+ * (inverter.py:31-32): without a limit, a few hundred bytes of header could ask the codec for
+ * tens of GB.  Replaces no reference call (libjpeg-turbo applies only the per-side limit). */
+int vf_jpeg_set_max_pixels(vf_ctx *ctx, uint64_t max_pixels);
 
 /* Worst-case size of a vf_jpeg_encode output (tjBufSize); 0 for bad arguments. */
 size_t vf_jpeg_buffer_size(int width, int height, int subsamp);

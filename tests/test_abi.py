@@ -51,7 +51,7 @@ def test_library_is_gfx950_code_object():
 
 def test_abi_version_and_status_strings():
     lib = _lib.load_library()
-    assert lib.vf_get_abi_version() == _lib.ABI_VERSION == 2
+    assert lib.vf_get_abi_version() == _lib.ABI_VERSION == 3
     assert lib.vf_status_string(0) == b"VF_OK"
     assert b"gfx950" in lib.vf_status_string(_lib.VF_E_NODEVICE)
     assert lib.vf_status_string(-99) == b"unknown vfilter status"

@@ -1,0 +1,55 @@
+"""The JPEG host parse under AddressSanitizer + UndefinedBehaviorSanitizer (CPU).
+
+The default worker decodes JPEG bytes that arrive from the network (inverter.py:31-32; the
+reference swallows decoder failures at worker.py:74-76).  ``csrc/vf_jpeg_parse.h`` -- the
+marker parse, Huffman table construction, MCU geometry and restart-interval layout that
+libvfilter_hip.so runs on those bytes -- is host-only C++, so g++ builds it here with
+``-fsanitize=address,undefined`` into a fixed-seed mutation fuzzer (bit flips, interesting
+bytes, truncations, length fields, segment deletion / duplication, cross-stream splices, SOF
+dimension and sampling changes, RSTn and DRI injection) over the libjpeg-made fixtures in
+``tests/golden/jpeg/``.  Every case must be refused or parse into byte ranges inside the buffer
+(sanitizers on the C-ABI host code in CPU tests).  The size limits are
+checked on the way: a frame's own pixel count passes, one less is refused, and SOF dimensions
+past libjpeg's JPEG_MAX_DIMENSION (65500) or the default 8192 x 8192 limit are refused.
+"""
+import glob
+import json
+import os
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "distributed-video-filter_amd", "csrc")
+SRC = os.path.join(ROOT, "tests", "fuzz", "jpeg_parse_fuzz.cc")
+CORPUS = sorted(glob.glob(os.path.join(ROOT, "tests", "golden", "jpeg", "*.jpg")))
+
+
+@pytest.fixture(scope="module")
+def fuzzer(tmp_path_factory):
+    gxx = shutil.which("g++")
+    if gxx is None:
+        pytest.skip("g++ not available")
+    exe = str(tmp_path_factory.mktemp("fuzz") / "jpeg_parse_fuzz")
+    cmd = [gxx, "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
+           "-fno-omit-frame-pointer", "-Wall", "-Werror", "-I", CSRC, SRC, "-o", exe]
+    subprocess.run(cmd, check=True, capture_output=True, text=True, timeout=300)
+    return exe
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("seed", [1, 2])
+def test_parse_survives_mutations_under_asan_ubsan(fuzzer, seed):
+    assert len(CORPUS) >= 10
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1", UBSAN_OPTIONS="print_stacktrace=1")
+    p = subprocess.run([fuzzer, str(seed), "30000"] + CORPUS, capture_output=True, text=True, timeout=240, env=env)
+    assert p.returncode == 0, (p.returncode, p.stdout[-2000:], p.stderr[-4000:])
+    lines = [json.loads(x) for x in p.stdout.splitlines() if x.startswith("{")]
+    limits, summary = lines[0], lines[-1]
+    assert limits["limit_at"] == 1 and "limit" in limits["limit_below"]
+    assert "65500" in limits["dim_65535"] and "limit" in limits["dim_65500"]
+    assert summary["cases"] == 30000 and summary["corpus_ok"] == summary["corpus"] == len(CORPUS)
+    # the mutations reach both outcomes and the size checks; tables both build and get refused
+    assert summary["accepted"] > 1000 and summary["rejected"] > 1000 and summary["too_big"] > 100
+    assert summary["tables_ok"] > 100 and summary["tables_bad"] > 100
