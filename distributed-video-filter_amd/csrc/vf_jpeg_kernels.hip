@@ -1101,14 +1101,32 @@ __global__ __launch_bounds__(256) void k_write4(const DecSeg *__restrict__ sg, c
 #define FIX_3_072711026 25172
 #define DESCALE(x, n) (((x) + ((int32_t)1 << ((n)-1))) >> (n))
 
-// jidctint.c jpeg_idct_islow, one 8-point line; `shift` 11 (pass 1) or 18 (pass 2)
+// jidctint.c jpeg_idct_islow, one 8-point line; `shift` 11 (pass 1) or 18 (pass 2).  M24: the
+// constant multiplies as v_mul_i32_i24 / v_mad_i32_i24 (full VALU rate) instead of 32-bit
+// v_mul_lo_u32 / v_mad_u64_u32 (a quarter of it).  Exact when every input is under 2^21 in
+// magnitude (idct_fits_m24): each multiplicand is a sum of at most four inputs (z3 + z4), so
+// it fits the 24-bit signed operand, and the 32-bit result is the C code's.  Decoded data is
+// far inside that (dequantised coefficients of 8-bit samples are ~2^11); a corrupt or extreme
+// stream takes the 32-bit form, wave by wave, so the output stays bit-exact either way.
+template <bool M24>
+__device__ __forceinline__ int32_t imul(int32_t a, int32_t b) {
+  if constexpr (M24) return __mul24(a, b);
+  else return a * b;
+}
+__device__ __forceinline__ bool idct_fits_m24(const int32_t in[8]) {
+  uint32_t o = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) o |= (uint32_t)(in[i] + (1 << 21));
+  return o < (1u << 22);
+}
+template <bool M24>
 __device__ __forceinline__ void idct_line(const int32_t in[8], int32_t out[8], int shift) {
   int32_t tmp0, tmp1, tmp2, tmp3, tmp10, tmp11, tmp12, tmp13, z1, z2, z3, z4, z5;
   z2 = in[2];
   z3 = in[6];
-  z1 = (z2 + z3) * FIX_0_541196100;
-  tmp2 = z1 + z3 * -FIX_1_847759065;
-  tmp3 = z1 + z2 * FIX_0_765366865;
+  z1 = imul<M24>(z2 + z3, FIX_0_541196100);
+  tmp2 = z1 + imul<M24>(z3, -FIX_1_847759065);
+  tmp3 = z1 + imul<M24>(z2, FIX_0_765366865);
   tmp0 = (in[0] + in[4]) * (1 << 13);
   tmp1 = (in[0] - in[4]) * (1 << 13);
   tmp10 = tmp0 + tmp3;
@@ -1123,15 +1141,15 @@ __device__ __forceinline__ void idct_line(const int32_t in[8], int32_t out[8], i
   z2 = tmp1 + tmp2;
   z3 = tmp0 + tmp2;
   z4 = tmp1 + tmp3;
-  z5 = (z3 + z4) * FIX_1_175875602;
-  tmp0 *= FIX_0_298631336;
-  tmp1 *= FIX_2_053119869;
-  tmp2 *= FIX_3_072711026;
-  tmp3 *= FIX_1_501321110;
-  z1 *= -FIX_0_899976223;
-  z2 *= -FIX_2_562915447;
-  z3 *= -FIX_1_961570560;
-  z4 *= -FIX_0_390180644;
+  z5 = imul<M24>(z3 + z4, FIX_1_175875602);
+  tmp0 = imul<M24>(tmp0, FIX_0_298631336);
+  tmp1 = imul<M24>(tmp1, FIX_2_053119869);
+  tmp2 = imul<M24>(tmp2, FIX_3_072711026);
+  tmp3 = imul<M24>(tmp3, FIX_1_501321110);
+  z1 = imul<M24>(z1, -FIX_0_899976223);
+  z2 = imul<M24>(z2, -FIX_2_562915447);
+  z3 = imul<M24>(z3, -FIX_1_961570560);
+  z4 = imul<M24>(z4, -FIX_0_390180644);
   z3 += z5;
   z4 += z5;
   tmp0 += z1 + z3;
@@ -1147,6 +1165,11 @@ __device__ __forceinline__ void idct_line(const int32_t in[8], int32_t out[8], i
   out[5] = (tmp12 - tmp1 + r) >> shift;
   out[3] = (tmp13 + tmp0 + r) >> shift;
   out[4] = (tmp13 - tmp0 + r) >> shift;
+}
+// the 24-bit form when the whole wave's inputs fit it (wave-uniform branch)
+__device__ __forceinline__ void idct_line_any(const int32_t in[8], int32_t out[8], int shift, bool active) {
+  if (__all(!active || idct_fits_m24(in))) idct_line<true>(in, out, shift);
+  else idct_line<false>(in, out, shift);
 }
 
 // jdmaster.c prepare_range_limit_table, post-IDCT part (RANGE_MASK 1023)
@@ -1255,8 +1278,8 @@ __global__ __launch_bounds__(256) void k_idct(const DecFrame *__restrict__ fr, c
     int32_t in[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i)
-      in[i] = blkv[h * 32 + slot][i * 8 + ((colg >> (4 * i)) & 7)] * s_q[k][i * 8 + r];
-    idct_line(in, col[h], 11);
+      in[i] = __mul24(blkv[h * 32 + slot][i * 8 + ((colg >> (4 * i)) & 7)], s_q[k][i * 8 + r]);  // int16 x u16: exact
+    idct_line_any(in, col[h], 11, true);
   }
   __syncthreads();
 #pragma unroll
@@ -1272,7 +1295,7 @@ __global__ __launch_bounds__(256) void k_idct(const DecFrame *__restrict__ fr, c
     int32_t in[8], out[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) in[i] = blkv[h * 32 + slot][r * 9 + i];
-    idct_line(in, out, 18);
+    idct_line_any(in, out, 18, true);
     uint32_t lo = 0, hi = 0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -1579,6 +1602,14 @@ __device__ __forceinline__ int enc_sample(const Geom &g, const uint8_t *img, int
   return (sum + he * ve / 2) / (he * ve);
 }
 
+// 24-bit multiplies for the forward DCT.  A 32-bit v_mul_lo_u32 / v_mad_u64_u32 (what `*` on
+// int32 compiles to) issues at a quarter of the VALU rate; v_mul_i32_i24 / v_mad_i32_i24 at the
+// full rate, and they are exact here: the encoder's samples are 8-bit, so pass 1's multiplicands
+// are sums of at most four differences of level-shifted samples (|x| < 2^10) and pass 2's of at
+// most four pass-1 outputs (|x| < 2^15), every constant is under 2^15, and each product fits
+// the 32-bit result the C code computes.
+__device__ __forceinline__ int32_t m24(int32_t a, int32_t b) { return __mul24(a, b); }
+
 // jfdctint.c jpeg_fdct_islow, one line; pass 0 = rows, 1 = columns
 __device__ __forceinline__ void fdct_islow_line(int32_t p[8], int pass) {
   int32_t tmp0 = p[0] + p[7], tmp7 = p[0] - p[7];
@@ -1588,6 +1619,7 @@ __device__ __forceinline__ void fdct_islow_line(int32_t p[8], int pass) {
   const int32_t tmp10 = tmp0 + tmp3, tmp13 = tmp0 - tmp3;
   const int32_t tmp11 = tmp1 + tmp2, tmp12 = tmp1 - tmp2;
   const int sh = pass ? 15 : 11;
+  const int32_t rnd = 1 << (sh - 1);  // DESCALE's rounding, folded into the products' sums
   if (!pass) {
     p[0] = (tmp10 + tmp11) * 4;
     p[4] = (tmp10 - tmp11) * 4;
@@ -1595,26 +1627,16 @@ __device__ __forceinline__ void fdct_islow_line(int32_t p[8], int pass) {
     p[0] = DESCALE(tmp10 + tmp11, 2);
     p[4] = DESCALE(tmp10 - tmp11, 2);
   }
-  int32_t z1 = (tmp12 + tmp13) * FIX_0_541196100;
-  p[2] = DESCALE(z1 + tmp13 * FIX_0_765366865, sh);
-  p[6] = DESCALE(z1 + tmp12 * -FIX_1_847759065, sh);
-  z1 = tmp4 + tmp7;
-  int32_t z2 = tmp5 + tmp6, z3 = tmp4 + tmp6, z4 = tmp5 + tmp7;
-  const int32_t z5 = (z3 + z4) * FIX_1_175875602;
-  tmp4 *= FIX_0_298631336;
-  tmp5 *= FIX_2_053119869;
-  tmp6 *= FIX_3_072711026;
-  tmp7 *= FIX_1_501321110;
-  z1 *= -FIX_0_899976223;
-  z2 *= -FIX_2_562915447;
-  z3 *= -FIX_1_961570560;
-  z4 *= -FIX_0_390180644;
-  z3 += z5;
-  z4 += z5;
-  p[7] = DESCALE(tmp4 + z1 + z3, sh);
-  p[5] = DESCALE(tmp5 + z2 + z4, sh);
-  p[3] = DESCALE(tmp6 + z2 + z3, sh);
-  p[1] = DESCALE(tmp7 + z1 + z4, sh);
+  const int32_t z1 = m24(tmp12 + tmp13, FIX_0_541196100) + rnd;
+  p[2] = (z1 + m24(tmp13, FIX_0_765366865)) >> sh;
+  p[6] = (z1 + m24(tmp12, -FIX_1_847759065)) >> sh;
+  const int32_t z5 = m24(tmp4 + tmp6 + tmp5 + tmp7, FIX_1_175875602) + rnd;
+  const int32_t z1o = m24(tmp4 + tmp7, -FIX_0_899976223), z2 = m24(tmp5 + tmp6, -FIX_2_562915447);
+  const int32_t z3 = m24(tmp4 + tmp6, -FIX_1_961570560) + z5, z4 = m24(tmp5 + tmp7, -FIX_0_390180644) + z5;
+  p[7] = (m24(tmp4, FIX_0_298631336) + z1o + z3) >> sh;
+  p[5] = (m24(tmp5, FIX_2_053119869) + z2 + z4) >> sh;
+  p[3] = (m24(tmp6, FIX_3_072711026) + z2 + z3) >> sh;
+  p[1] = (m24(tmp7, FIX_1_501321110) + z1o + z4) >> sh;
 }
 
 // jfdctfst.c jpeg_fdct_ifast, one line (both passes identical)
@@ -1627,16 +1649,16 @@ __device__ __forceinline__ void fdct_ifast_line(int32_t p[8]) {
   int32_t tmp11 = tmp1 + tmp2, tmp12 = tmp1 - tmp2;
   p[0] = tmp10 + tmp11;
   p[4] = tmp10 - tmp11;
-  const int32_t z1 = ((tmp12 + tmp13) * 181) >> 8;
+  const int32_t z1 = m24(tmp12 + tmp13, 181) >> 8;
   p[2] = tmp13 + z1;
   p[6] = tmp13 - z1;
   tmp10 = tmp4 + tmp5;
   tmp11 = tmp5 + tmp6;
   tmp12 = tmp6 + tmp7;
-  const int32_t z5 = ((tmp10 - tmp12) * 98) >> 8;
-  const int32_t z2 = ((tmp10 * 139) >> 8) + z5;
-  const int32_t z4 = ((tmp12 * 334) >> 8) + z5;
-  const int32_t z3 = (tmp11 * 181) >> 8;
+  const int32_t z5 = m24(tmp10 - tmp12, 98) >> 8;
+  const int32_t z2 = (m24(tmp10, 139) >> 8) + z5;
+  const int32_t z4 = (m24(tmp12, 334) >> 8) + z5;
+  const int32_t z3 = m24(tmp11, 181) >> 8;
   const int32_t z11 = tmp7 + z3, z13 = tmp7 - z3;
   p[5] = z13 + z2;
   p[3] = z13 - z2;
