@@ -50,7 +50,7 @@ bool fired(hipEvent_t e, hipError_t *err) {
 }  // namespace
 
 // ---- host copy pool -----------------------------------------------------------------------
-CopyPool::CopyPool(int nthreads) : n_(std::max(1, nthreads)) {
+CopyPool::CopyPool(int nthreads, size_t split_min) : split_min_(split_min), n_(std::max(1, nthreads)) {
   for (int i = 1; i < n_; ++i) threads_.emplace_back([this, i] { run(i); });
 }
 
@@ -65,7 +65,7 @@ CopyPool::~CopyPool() {
 }
 
 void CopyPool::copy(uint8_t *dst, const uint8_t *src, size_t len) {
-  if (len < kSplitMin || n_ == 1) {
+  if (len < split_min_ || n_ == 1) {
     std::memcpy(dst, src, len);
     return;
   }
@@ -129,6 +129,11 @@ Engine::~Engine() {
     if (s.d_out) (void)hipFree(s.d_out);
   }
   for (hipEvent_t e : free_events_) (void)hipEventDestroy(e);
+  for (auto &g : stg_) {
+    if (g.ev) (void)hipEventDestroy(g.ev);
+    (void)numa_pinned_free(g.in);
+    (void)numa_pinned_free(g.out);
+  }
   if (s_in_) (void)hipStreamDestroy(s_in_);
   if (s_out_) (void)hipStreamDestroy(s_out_);
   if (s_map_) (void)hipStreamDestroy(s_map_);
@@ -281,17 +286,20 @@ bool Engine::run_now(const std::vector<Seg> &segs, JobResult *out) {
   }
   std::vector<Seg> dsegs;
   size_t total = 0;
+  bool all_mapped = true;
   for (const Seg &s : segs) {
     if (!s.len) continue;
     uint8_t *ds = mapped(s.src, s.len), *dd = mapped(s.dst, s.len);
-    if (!ds || !dd) return false;
+    all_mapped = all_mapped && ds && dd;
     dsegs.push_back(Seg{ds, dd, s.len});
     total += s.len;
   }
-  if (dsegs.empty() || hipSetDevice(device_) != hipSuccess || ensure_streams() != hipSuccess) {
+  if (dsegs.empty() || (!all_mapped && total > kStagedMax)) return false;
+  if (hipSetDevice(device_) != hipSuccess || ensure_streams() != hipSuccess) {
     (void)hipGetLastError();
     return false;
   }
+  if (!all_mapped) return run_staged(segs, total, out);
   hipEvent_t a = take_event(), b = take_event();
   if (!a || !b) {
     give_event(a);
@@ -320,6 +328,111 @@ bool Engine::run_now(const std::vector<Seg> &segs, JobResult *out) {
     out->status = kStatusHip;
     out->hip = e;
     out->msg = std::string("zero-copy launch failed: ") + hipGetErrorString(e);
+  } else {
+    float ms = -1.f;
+    if (hipEventElapsedTime(&ms, a, b) != hipSuccess) ms = -1.f;
+    out->kernel_ms = out->gpu_ms = ms;
+    out->zero_copy = true;
+    out->timeline.push_back(ChunkTime{total, 0.f, 0.f, ms, ms});
+  }
+  give_event(a);
+  give_event(b);
+  return true;
+}
+
+hipError_t Engine::ensure_staging() {
+  if (stg_ready_) return hipSuccess;
+  const int node = device_numa_node(device_);
+  for (auto &g : stg_) {
+    hipError_t e;
+    if ((!g.in && (e = numa_pinned_alloc((void **)&g.in, kStgBytes, node)) != hipSuccess) ||
+        (!g.out && (e = numa_pinned_alloc((void **)&g.out, kStgBytes, node)) != hipSuccess) ||
+        (!g.ev && (e = hipEventCreateWithFlags(&g.ev, hipEventDisableTiming)) != hipSuccess))
+      return e;
+    void *di = nullptr, *dout = nullptr;
+    if ((e = hipHostGetDevicePointer(&di, g.in, 0)) != hipSuccess ||
+        (e = hipHostGetDevicePointer(&dout, g.out, 0)) != hipSuccess)
+      return e;
+    g.din = static_cast<uint8_t *>(di);
+    g.dout = static_cast<uint8_t *>(dout);
+  }
+  if (!cpool_) cpool_.reset(new CopyPool((int)env_or("VF_HOST_THREADS", 8), (size_t)256 << 10));
+  stg_ready_ = true;
+  return hipSuccess;
+}
+
+// A small synchronous job with a side outside the mapped ranges (a pageable frame: the
+// drop-in's own shape, vfilter.bitwise_not(frame) for cv2.bitwise_not(frame), inverter.py:41)
+// on the calling thread: the job is cut into pieces of up to kStgBytes; an unmapped source
+// piece is copied into a mapped staging piece, an unmapped destination piece is written by the
+// kernel into one and copied out afterwards, and a mapped side is read or written in place.
+// One invert_mapped_kernel launch per piece on the zero-copy stream, so piece i's launch runs
+// over PCIe while the CPU copies piece i + 1 in (and piece i - 1 out): no slot-ring DMA, no
+// hand-off to the engine thread.  1080p pageable -> pinned was 0.44-0.49 ms per call through
+// the slot ring (profiles/r02_per_frame.jsonl).
+bool Engine::run_staged(const std::vector<Seg> &segs, size_t total, JobResult *out) {
+  std::unique_lock<std::mutex> lk(stg_mu_, std::try_to_lock);
+  if (!lk.owns_lock()) return false;  // another thread is staging: the engine path takes it
+  if (ensure_staging() != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  // piece size: about six pieces per job, 256 KiB .. kStgBytes, 64-KiB multiples
+  size_t piece = std::min(kStgBytes, std::max<size_t>((size_t)256 << 10, (total / 6 + 65535) & ~(size_t)65535));
+  hipEvent_t a = take_event(), b = take_event();
+  if (!a || !b) {
+    give_event(a);
+    give_event(b);
+    return false;
+  }
+  hipError_t e = hipEventRecord(a, s_map_);
+  int k = 0;  // ring position
+  auto drain = [&](StgSlot &g) {  // wait for the slot's launch and copy its output out
+    if (!g.busy) return hipSuccess;
+    hipError_t r = hipEventSynchronize(g.ev);
+    if (r == hipSuccess && g.copy_len) cpool_->copy(g.copy_to, g.out, g.copy_len);
+    g.busy = false;
+    g.copy_len = 0;
+    return r;
+  };
+  MappedBatch mb;
+  for (const Seg &sg : segs) {
+    for (size_t off = 0; off < sg.len && e == hipSuccess; off += piece) {
+      const size_t n = std::min(piece, sg.len - off);
+      StgSlot &g = stg_[k];
+      k = (k + 1) % kStg;
+      if ((e = drain(g)) != hipSuccess) break;
+      const uint8_t *ds = mapped(sg.src + off, n);
+      uint8_t *dd = mapped(sg.dst + off, n);
+      if (!ds) {
+        cpool_->copy(g.in, sg.src + off, n);
+        ds = g.din;
+      }
+      if (!dd) {
+        dd = g.dout;
+        g.copy_to = sg.dst + off;
+        g.copy_len = n;
+      }
+      mb.src[0] = ds;
+      mb.dst[0] = dd;
+      mb.n[0] = n;
+      if ((e = launch_invert_mapped(mb, 1, n, s_map_)) == hipSuccess) e = hipEventRecord(g.ev, s_map_);
+      g.busy = e == hipSuccess;
+      // the piece launched two steps ago is likely done: copy it out while this one runs
+      if (e == hipSuccess) e = drain(stg_[(k + kStg - 3) % kStg]);
+    }
+  }
+  for (int i = 0; i < kStg && e == hipSuccess; ++i) e = drain(stg_[(k + i) % kStg]);
+  if (e == hipSuccess) e = hipEventRecord(b, s_map_);
+  if (e == hipSuccess) e = hipEventSynchronize(b);
+  *out = JobResult();
+  if (e != hipSuccess) {
+    (void)hipStreamSynchronize(s_map_);  // nothing may land in the caller's buffers later
+    (void)hipGetLastError();
+    for (auto &g : stg_) g.busy = false, g.copy_len = 0;
+    out->status = kStatusHip;
+    out->hip = e;
+    out->msg = std::string("staged zero-copy launch failed: ") + hipGetErrorString(e);
   } else {
     float ms = -1.f;
     if (hipEventElapsedTime(&ms, a, b) != hipSuccess) ms = -1.f;

@@ -49,12 +49,12 @@ hipError_t launch_invert_mapped(const MappedBatch &b, int n, size_t total_bytes,
 // with 4 threads, 40.5 with 8; pinned, i.e. no staging: 42.9).
 class CopyPool {
  public:
-  explicit CopyPool(int nthreads);
+  explicit CopyPool(int nthreads, size_t split_min = (size_t)1 << 20);
   ~CopyPool();
   void copy(uint8_t *dst, const uint8_t *src, size_t len);
 
  private:
-  static constexpr size_t kSplitMin = 1 << 20;
+  const size_t split_min_;  // shorter copies run on the calling thread alone
   void part(int i);
   void run(int i);
   int n_;
@@ -101,6 +101,8 @@ class Engine {
   uint64_t submit(std::vector<Seg> &&segs);  // returns the job id (> 0); never blocks on the GPU
   // Synchronous zero-copy on the calling thread (no hand-off to the engine thread and back):
   // false, with nothing done, unless every byte lies in noted device-mapped ranges.
+  // Otherwise, for a job of at most kStagedMax bytes, the same launches on the calling thread
+  // with the unmapped side staged through a small mapped ring (run_staged).
   bool run_now(const std::vector<Seg> &segs, JobResult *out);
   bool wait(uint64_t id, JobResult *out);    // false: unknown id
   bool query(uint64_t id, bool *done);       // false: unknown id
@@ -154,6 +156,8 @@ class Engine {
   bool step_d2h();
   bool step_retire();
   bool launch_mapped(Job *job);
+  bool run_staged(const std::vector<Seg> &segs, size_t total, JobResult *out);
+  hipError_t ensure_staging();
   bool step_mapped_retire();
   void fail_all(hipError_t e, const char *what);
   int busy_slots() const;
@@ -172,6 +176,23 @@ class Engine {
   std::vector<Slot> slots_;
   size_t fill_ = 0, d2h_ = 0, retire_ = 0;
   std::unique_ptr<CopyPool> pool_;
+  // run_staged: a ring of page-locked, device-mapped staging pieces (input and output halves)
+  // and a copy pool of its own (the engine thread's pool_ is not reentrant)
+  static constexpr int kStg = 4;
+  static constexpr size_t kStgBytes = (size_t)2 << 20;
+  static constexpr size_t kStagedMax = (size_t)32 << 20;
+  struct StgSlot {
+    uint8_t *in = nullptr, *out = nullptr;      // host addresses
+    uint8_t *din = nullptr, *dout = nullptr;    // their device addresses
+    hipEvent_t ev = nullptr;                    // the launch that reads in / writes out
+    uint8_t *copy_to = nullptr;                 // pending copy-out of `out` (unmapped destination)
+    size_t copy_len = 0;
+    bool busy = false;
+  };
+  StgSlot stg_[kStg];
+  bool stg_ready_ = false;
+  std::mutex stg_mu_;                           // one staged job at a time
+  std::unique_ptr<CopyPool> cpool_;
   std::mutex ev_mu_;             // free_events_: the engine thread and run_now's caller both take and give
   std::vector<hipEvent_t> free_events_;
 

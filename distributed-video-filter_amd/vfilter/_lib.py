@@ -154,6 +154,86 @@ def _addr(a) -> int:
     raise TypeError(f"cannot take the address of {type(a).__name__}")
 
 
+class _PinnedBlock:
+    """A block of a context's pinned arena seen as an array (``np.asarray(block)``): the array
+    keeps the block alive, and the block goes back to the arena when the last view of it dies."""
+
+    def __init__(self, arena: "_PinnedArena", ptr: int, cap: int, shape, dtype):
+        self._arena, self.ptr, self.cap = arena, ptr, cap
+        self.__array_interface__ = {"shape": tuple(shape), "typestr": np.dtype(dtype).str,
+                                    "data": (ptr, False), "version": 3}
+
+    def __del__(self):
+        try:
+            self._arena.release(self.ptr, self.cap)
+        except Exception:
+            pass
+
+
+class _PinnedArena:
+    """Page-locked, device-mapped result buffers of one context (vf_alloc_host: on the GPU's NUMA
+    node, noted as mapped), recycled by size.  An array from here is a destination the invert
+    kernel writes directly over PCIe (no staging, no copy-out) -- the drop-in's result of
+    ``bitwise_not(frame)`` (inverter.py:41) and the worker's receive buffers.  Free blocks beyond
+    ``keep_bytes`` are returned to the library; blocks still referenced by arrays keep the context
+    alive past ``close`` (its memory must outlive them)."""
+
+    def __init__(self, ctx: "Context", keep_bytes: int = 256 << 20):
+        self._ctx = ctx
+        self._lock = threading.Lock()
+        self._free: dict = {}
+        self._free_bytes = 0
+        self._keep = keep_bytes
+        self.outstanding = 0
+
+    @staticmethod
+    def _cap(nbytes: int) -> int:
+        return max(4096, (int(nbytes) + 4095) & ~4095)
+
+    def empty(self, shape, dtype=np.uint8) -> np.ndarray:
+        dtype = np.dtype(dtype)
+        nbytes = int(np.prod(shape, dtype=np.int64)) * dtype.itemsize
+        cap = self._cap(nbytes)
+        with self._lock:
+            lst = self._free.get(cap)
+            ptr = lst.pop() if lst else 0
+            if ptr:
+                self._free_bytes -= cap
+            self.outstanding += 1
+        if not ptr:
+            try:
+                ptr = self._ctx.alloc_host(cap)
+            except Exception:
+                with self._lock:
+                    self.outstanding -= 1
+                raise
+        return np.asarray(_PinnedBlock(self, ptr, cap, shape, dtype))
+
+    def release(self, ptr: int, cap: int) -> None:
+        drop = []
+        with self._lock:
+            self.outstanding -= 1
+            self._free.setdefault(cap, []).append(ptr)
+            self._free_bytes += cap
+            while self._free_bytes > self._keep:
+                k = max(self._free, key=lambda c: c if self._free[c] else -1)
+                drop.append(self._free[k].pop())
+                self._free_bytes -= k
+            last = self.outstanding == 0
+        ctx = self._ctx
+        for p in drop:
+            ctx._free_host_raw(p)
+        if last and ctx._closing:
+            ctx.close()
+
+    def drain(self) -> list:
+        with self._lock:
+            ptrs = [p for lst in self._free.values() for p in lst]
+            self._free.clear()
+            self._free_bytes = 0
+            return ptrs
+
+
 class Context:
     """One ``vf_ctx``: a device, its HIP streams and the pinned staging ring.
 
@@ -168,6 +248,8 @@ class Context:
         if st != VF_OK:
             raise VFilterError(self._lib.vf_last_error(None).decode(), st, self._lib.vf_last_hip_error(None))
         self.device = int(device)
+        self._closing = False
+        self._arena = _PinnedArena(self)
 
     # -- plumbing -----------------------------------------------------------------------
     def _check(self, st: int) -> None:
@@ -181,9 +263,33 @@ class Context:
         return self._ctx.value or 0
 
     def close(self) -> None:
+        """Destroy the context -- once no array of its pinned arena is alive (their memory must
+        outlive them; the last one to go finishes the close)."""
+        if not self._ctx:
+            return
+        self._closing = True
+        arena = self.__dict__.get("_arena")
+        if arena is not None:
+            for p in arena.drain():
+                self._free_host_raw(p)
+            if arena.outstanding:
+                return
+        self._lib.vf_destroy(self._ctx)
+        self._ctx = _vp()
+
+    def _free_host_raw(self, p: int) -> None:
         if self._ctx:
-            self._lib.vf_destroy(self._ctx)
-            self._ctx = _vp()
+            self._lib.vf_free_host(self._ctx, p)
+
+    # -- pinned result arrays ------------------------------------------------------------------
+    def pinned_empty(self, shape, dtype=np.uint8) -> np.ndarray:
+        """An uninitialised array in page-locked, device-mapped memory from the context's arena
+        (recycled when the array and its views are gone): the invert kernel writes such a
+        destination directly over PCIe, and reads such a source directly."""
+        return self._arena.empty(shape, dtype)
+
+    def pinned_empty_like(self, a: np.ndarray) -> np.ndarray:
+        return self._arena.empty(a.shape, a.dtype)
 
     def __enter__(self) -> "Context":
         return self

@@ -27,11 +27,14 @@ def bitwise_not(src: np.ndarray, dst: Optional[np.ndarray] = None, mask=None,
     if mask is not None:
         raise NotImplementedError("bitwise_not: mask is not supported (inverter.py:41 passes none)")
     src = np.ascontiguousarray(src)
+    ctx = ctx or get_context()
     if dst is None:
-        dst = np.empty_like(src)
+        # a result in the context's pinned arena: the kernel writes it directly over PCIe
+        # (no staging copy out); it goes back to the arena when the array is dropped
+        dst = ctx.pinned_empty_like(src)
     elif dst.shape != src.shape or dst.dtype != src.dtype or not dst.flags.c_contiguous:
         raise ValueError("bitwise_not: dst must be C-contiguous with src's shape and dtype")
-    (ctx or get_context()).invert_host(src, dst, src.nbytes)
+    ctx.invert_host(src, dst, src.nbytes)
     return dst
 
 

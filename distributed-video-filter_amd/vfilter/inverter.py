@@ -54,6 +54,8 @@ class InverterWorker(Worker):
         # re-encoded JPEGs written straight into their ring slots (VF_JPEG_SCATTER=0: copied by the loop)
         self.sized_results = self.jpeg is not None and os.environ.get("VF_JPEG_SCATTER", "1") != "0"
         self._registered: List[int] = []
+        if self.jpeg is None:  # raw frames off the socket land in the pinned arena: read in place
+            self.dealer_socket.recv_alloc = lambda n: self.ctx.pinned_empty((n,))
         if install_signal_handlers:                                  # inverter.py:16-18
             signal.signal(signal.SIGINT, self._signal_handler)
             signal.signal(signal.SIGTERM, self._signal_handler)
@@ -77,7 +79,7 @@ class InverterWorker(Worker):
             frame = np.frombuffer(frame_bytes, dtype=np.uint8)      # inverter.py:34, any size
         if self.delay > 0:                                          # inverter.py:37-38
             time.sleep(self.delay)
-        out = np.empty_like(frame)
+        out = self.ctx.pinned_empty_like(frame)  # written directly over PCIe, recycled after the send
         if frame.nbytes:
             self.ctx.invert_host(frame, out, frame.nbytes)          # inverter.py:41
         if self.jpeg:

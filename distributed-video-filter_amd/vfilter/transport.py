@@ -52,9 +52,11 @@ def resolve(kind: str) -> str:
 # stdlib TCP implementation
 # ---------------------------------------------------------------------------------------
 
-def _recv_exact(sock: socket.socket, n: int) -> bytearray:
-    buf = bytearray(n)
-    view = memoryview(buf)
+def _recv_exact(sock: socket.socket, n: int, alloc=None):
+    """n bytes from ``sock``: into a new bytearray, or into ``alloc(n)`` (a writable buffer the
+    caller provides, e.g. a pinned arena array the GPU reads directly)."""
+    buf = alloc(n) if alloc is not None else bytearray(n)
+    view = memoryview(buf).cast("B")
     got = 0
     while got < n:
         k = sock.recv_into(view[got:], n - got)
@@ -64,12 +66,12 @@ def _recv_exact(sock: socket.socket, n: int) -> bytearray:
     return buf
 
 
-def _recv_msg(sock: socket.socket) -> List[bytes]:
+def _recv_msg(sock: socket.socket, alloc=None) -> List[bytes]:
     (nparts,) = _HDR.unpack(_recv_exact(sock, _HDR.size))
     parts = []
     for _ in range(nparts):
         (n,) = _LEN.unpack(_recv_exact(sock, _LEN.size))
-        parts.append(bytes(_recv_exact(sock, n)) if n < (1 << 16) else _recv_exact(sock, n))
+        parts.append(bytes(_recv_exact(sock, n)) if n < (1 << 16) else _recv_exact(sock, n, alloc))
     return parts
 
 
@@ -218,9 +220,9 @@ class _Connection:
         r, _, _ = select.select([self.sock], [], [], timeout_ms / 1000.0)
         return bool(r)
 
-    def recv(self) -> List[bytes]:
+    def recv(self, alloc=None) -> List[bytes]:
         self._ensure()
-        return _recv_msg(self.sock)
+        return _recv_msg(self.sock, alloc)
 
     def close(self):
         if self.sock is not None:
@@ -316,6 +318,9 @@ class DealerEnd:
             self.sock.connect(f"tcp://{host}:{port}")
         else:
             self.sock = _Connection(host, port)
+        # "tcp": parts of 64 KiB or more are received into recv_alloc(n) when it is set (a GPU
+        # worker gives its pinned arena, so a received frame is a source the kernel reads in place)
+        self.recv_alloc = None
 
     def send(self, parts: Sequence) -> None:
         if self.kind == "zmq":
@@ -329,7 +334,7 @@ class DealerEnd:
     def recv(self) -> List[bytes]:
         if self.kind == "zmq":
             return self.sock.recv_multipart(self._zmq.NOBLOCK)
-        return self.sock.recv()
+        return self.sock.recv(self.recv_alloc)
 
     def close(self):
         self.sock.close(0) if self.kind == "zmq" else self.sock.close()

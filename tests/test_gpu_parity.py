@@ -445,6 +445,36 @@ def test_sync_zero_copy_while_async_in_flight(vf_ctx):
             vf_ctx.free_host(p)
 
 
+@pytest.mark.parametrize("n", [1, 17, 300_001, FB_1080, 3 * FB_1080 + 5])
+def test_staged_small_jobs_every_side(vf_ctx, n):
+    """Synchronous jobs up to 32 MiB with an unmapped side run on the caller's thread
+    (Engine::run_staged): pageable source -> pinned arena destination (the drop-in's
+    bitwise_not(frame)), pinned source -> pageable destination, pageable -> pageable, and in
+    place; every byte exact, nothing outside the destination touched, one launch record."""
+    rng = np.random.default_rng(n)
+    x = rng.integers(0, 256, n + 32, dtype=np.uint8)
+    want = ~x[7:7 + n]
+    d = vf_ctx.pinned_empty((n + 32,))
+    d[:] = 0x5A
+    vf_ctx.invert_host(x[7:7 + n], d[3:3 + n], n)          # pageable -> mapped
+    assert _zero_copy(vf_ctx.last_timeline())
+    assert np.array_equal(d[3:3 + n], want) and (d[:3] == 0x5A).all() and (d[3 + n:] == 0x5A).all()
+    p = vf_ctx.pinned_empty((n,))
+    p[:] = x[7:7 + n]
+    y = np.full(n + 32, 0x5A, np.uint8)
+    vf_ctx.invert_host(p, y[5:5 + n], n)                    # mapped -> pageable
+    assert _zero_copy(vf_ctx.last_timeline())
+    assert np.array_equal(y[5:5 + n], want) and (y[:5] == 0x5A).all() and (y[5 + n:] == 0x5A).all()
+    z = np.full(n + 32, 0x5A, np.uint8)
+    vf_ctx.invert_host(x[7:7 + n], z[1:1 + n], n)          # pageable -> pageable
+    assert np.array_equal(z[1:1 + n], want) and z[0] == 0x5A and (z[1 + n:] == 0x5A).all()
+    w = x.copy()
+    vf_ctx.invert_host(w, w, w.nbytes)                      # in place, pageable
+    assert np.array_equal(w, ~x)
+    r = vfilter.bitwise_not(x[7:7 + n], ctx=vf_ctx)         # the drop-in: result in the arena
+    assert np.array_equal(r, want)
+
+
 def _zero_copy(tl):
     """A zero-copy call reports one record whose H2D start = kernel start = 0 and kernel end =
     D2H end (one launch read the source and wrote the destination over PCIe)."""

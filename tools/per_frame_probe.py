@@ -2,7 +2,10 @@
 """One frame per call, the drop-in's own shape (``vfilter.bitwise_not(frame)`` in place of
 ``cv2.bitwise_not(frame)``, inverter.py:41): per-call latency at 480p / 1080p / 4K for
   cpu        numpy's bitwise_not on one core (the reference arithmetic)
-  pageable   vfilter.bitwise_not on an ordinary numpy frame (staged through the slot ring)
+  dropin     vfilter.bitwise_not(frame): an ordinary numpy frame in, the result in the context's
+             pinned arena (the drop-in's own call: the source staged through the mapped ring
+             piece by piece beside the launches, the result written in place over PCIe)
+  pageable   vfilter.bitwise_not(frame, out) with an ordinary numpy destination as well
   pinned     vfilter.bitwise_not with src and dst in vf_alloc_host memory (zero-copy launch)
 Prints one JSON line per size.
   python tools/per_frame_probe.py"""
@@ -45,10 +48,12 @@ def main():
             reps = 200 if h < 2000 else 60
             r = {"size": name, "frame_bytes": n}
             r["cpu_ms"] = timed(lambda: np.bitwise_not(frame), reps) * 1e3
+            r["dropin_ms"] = timed(lambda: vfilter.bitwise_not(frame, ctx=ctx), reps) * 1e3
             r["pageable_ms"] = timed(lambda: vfilter.bitwise_not(frame, out, ctx=ctx), reps) * 1e3
             r["pinned_ms"] = timed(lambda: vfilter.bitwise_not(fs, fd, ctx=ctx), reps) * 1e3
+            assert np.array_equal(vfilter.bitwise_not(frame, ctx=ctx), ~frame)
             assert np.array_equal(out, ~frame) and np.array_equal(fd, ~frame)
-            for k in ("cpu", "pageable", "pinned"):
+            for k in ("cpu", "dropin", "pageable", "pinned"):
                 r[f"{k}_fps"] = round(1e3 / r[f"{k}_ms"], 1)
                 r[f"{k}_ms"] = round(r[f"{k}_ms"], 4)
             print(json.dumps(r), flush=True)
