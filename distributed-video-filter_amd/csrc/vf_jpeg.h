@@ -49,7 +49,7 @@ struct SpecBufs {
   uint64_t *wBX;
   uint8_t *rE;     // resolved walk column
   uint32_t *rK;    // resolved: prefix covers subsequences 0..rK
-  uint32_t *stats;  // diagnostics (VF_SYNC_STATS builds): [1] walker decodes [2] traced workgroups
+  uint32_t *stats;  // diagnostics (builds with tools/sync_stats.patch applied): [1] walker decodes [2] traced workgroups
                     // [3] traced subsequences [4] link misses
 };
 constexpr int kSpecLanesMax = 16;

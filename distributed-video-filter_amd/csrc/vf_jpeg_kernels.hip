@@ -418,9 +418,6 @@ __device__ __forceinline__ void load_sync_tables(const DecFrame &F, HuffSync *ta
 // trajectory (marks a decode did not reach from its entry are invalidated).
 
 constexpr uint64_t kNoCk = ~0ull;
-#ifndef VF_SYNC_STATS
-#define VF_SYNC_STATS 0
-#endif
 
 // One sync pass.  Every thread decodes its subsequence from its entry state; then, inside
 // the workgroup, a thread whose entry differs from its predecessor's current exit takes that
@@ -469,9 +466,7 @@ __global__ __launch_bounds__(256) void k_sync(const DecSeg *__restrict__ sg, con
       need = true;
     }
   }
-  uint32_t rounds = 0;
   for (;;) {
-    ++rounds;
     if (need) {
       decoded = true;
       BitReader br;
@@ -528,10 +523,6 @@ __global__ __launch_bounds__(256) void k_sync(const DecSeg *__restrict__ sg, con
         }
       }
       if (pass == 0 || ex != exit_in[gi]) atomicOr(changed, 1u);
-      if (VF_SYNC_STATS && t == 0) {  // debug: rounds histogram in the pass-flag tail
-        atomicMax(changed + (kMaxPasses - 1 - pass), rounds);
-        atomicAdd(changed + (kMaxPasses - 3 - pass), rounds);
-      }
     }
   }
 }
@@ -615,7 +606,6 @@ __global__ __launch_bounds__(256) void k_spec(const DecSeg *__restrict__ sg, con
   const DecSeg S = sg[blockIdx.y];  // by value: held in scalar registers
   const DecFrame &F = fr[S.frame];
   if (blockIdx.x >= S.nwg) return;
-  const long long c_start = VF_SYNC_STATS ? clock64() : 0;
   const HuffGeom hg(F.g);
   const uint32_t L = spec_lanes(hg.bpm), NS = 256 / L;
   const uint32_t t = threadIdx.x, sl = t / L, c0 = t % L;
@@ -657,7 +647,6 @@ __global__ __launch_bounds__(256) void k_spec(const DecSeg *__restrict__ sg, con
   }
   s_E[t] = E;
   __syncthreads();
-  if (VF_SYNC_STATS && t == 0) atomicAdd(B.stats + 8, (uint32_t)((clock64() - c_start) >> 10));
   if (live) {
     B.tE[ti] = E;
     if (sl == 0) {  // checkpoints of the first subsequence, for k_wglink
@@ -677,13 +666,11 @@ __global__ __launch_bounds__(256) void k_spec(const DecSeg *__restrict__ sg, con
     M = spec_link(s_w, woff, s_E[(sl - 1) * L + c0], base, end, s + 1 == nsub, hg, tabs,
                   [&](uint32_t c2, int m) { return s_ck[m][row + c2]; },
                   [&](uint32_t c2, int m) { return s_rem[m][row + c2]; }, &C, &X);
-    if (VF_SYNC_STATS && M == kLinkNone) atomicAdd(B.stats + 4, 1u);
   }
   s_M[t] = (uint8_t)M;
   s_C[t] = C;
   s_X[t] = X;
   __syncthreads();
-  if (VF_SYNC_STATS && t == 0) atomicAdd(B.stats + 9, (uint32_t)((clock64() - c_start) >> 10));
   // C: the walks.  Walk e is trajectory e of the first subsequence followed through the links:
   // j_k = f_k(j_{k-1}), f_k(j) = s_M[k * L + j].  While every step is a link (no explicit
   // state), j_k = (f_k o ... o f_1)(e), and map composition is associative, so one lane per
@@ -770,7 +757,6 @@ __global__ __launch_bounds__(256) void k_spec(const DecSeg *__restrict__ sg, con
         cnt = s_C[k * L + j];
         xe = s_X[k * L + j];
       } else {  // explicit state: link it into subsequence k here
-        if (VF_SYNC_STATS) atomicAdd(B.stats + 1, 1u);
         const uint32_t bk = sk * kSubBits, ek = (sk + 1 >= nsub) ? nbits : (sk + 1) * kSubBits;
         const uint32_t row = k * L;
         M2 = spec_link(s_w, woff, st, bk, ek, sk + 1 == nsub, hg, tabs,
@@ -790,7 +776,6 @@ __global__ __launch_bounds__(256) void k_spec(const DecSeg *__restrict__ sg, con
       if (j == kLinkLast) break;
     }
     B.wF[(uint64_t)(S.wg0 + blockIdx.x) * kSpecLanesMax + e] = (uint8_t)(j < hg.bpm ? j : kLinkNone);
-    if (VF_SYNC_STATS) atomicAdd(B.stats + 10, (uint32_t)((clock64() - c_start) >> 10));
   }
 }
 
@@ -884,7 +869,6 @@ __global__ __launch_bounds__(256) void k_resolve(const DecSeg *__restrict__ sg, 
   const uint32_t *gw = reinterpret_cast<const uint32_t *>(us + S.us_off);
   const uint8_t kTraced = 0xFF;  // sJ: the prefix was written by the tracer
   if (threadIdx.x == 0) {
-    long long c_loop = VF_SYNC_STATS ? clock64() : 0, c_trace = 0;
     sE[0] = 0;
     sK[0] = 0;
     sJ[0] = kTraced;  // workgroup 0: frame start = trajectory 0 (records written below)
@@ -907,8 +891,6 @@ __global__ __launch_bounds__(256) void k_resolve(const DecSeg *__restrict__ sg, 
         }
       }
       // trace from the explicit state at the end of w-1 (or after w's first subsequence)
-      if (VF_SYNC_STATS) atomicAdd(B.stats + 2, 1u);
-      const long long c_t0 = VF_SYNC_STATS ? clock64() : 0;
       uint64_t X;
       uint32_t k = 0;
       if (jl < bpm) {  // the boundary link decoded subsequence 0 without rejoining
@@ -925,7 +907,6 @@ __global__ __launch_bounds__(256) void k_resolve(const DecSeg *__restrict__ sg, 
         const uint32_t sk = w * NS + k;
         const uint32_t ek = (sk + 1 >= nsub) ? nbits : (sk + 1) * kSubBits;
         // the subsequence's words, fetched together (independent loads), then decoded from LDS
-        if (VF_SYNC_STATS) atomicAdd(B.stats + 3, 1u);
         const uint32_t w0 = (uint32_t)(X >> 16) >> 5;
         for (uint32_t q = 0; q < kTraceWords; ++q) s_tw[q] = w0 + q < fwords ? gw[w0 + q] : 0u;
         BitReader br;
@@ -949,11 +930,6 @@ __global__ __launch_bounds__(256) void k_resolve(const DecSeg *__restrict__ sg, 
       sK[w] = (uint8_t)(found ? k : NS - 1);
       sJ[w] = kTraced;
       kj = found ? k : NS - 1;
-      if (VF_SYNC_STATS) c_trace += clock64() - c_t0;
-    }
-    if (VF_SYNC_STATS) {  // shader-clock kcycles: the trace path, the whole walk
-      atomicAdd(B.stats + 5, (uint32_t)(c_trace >> 10));
-      atomicAdd(B.stats + 6, (uint32_t)((clock64() - c_loop) >> 10));
     }
   }
   __syncthreads();

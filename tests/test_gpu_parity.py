@@ -58,7 +58,7 @@ def test_dst_argument_and_in_place(vf_ctx):
     assert np.array_equal(out, x)
 
 
-def test_batch_config2_1080p_x32(vf_ctx):
+def test_batch_configs1_1080p_x32(vf_ctx):
     frames = np.stack([oracle.synthetic_frame(s, 1080, 1920) for s in range(32)])
     out = vfilter.invert_batch(frames, ctx=vf_ctx)
     assert np.array_equal(out, oracle.c_invert(frames))

@@ -83,12 +83,12 @@ def _sharded_4k(nworkers, nframes, ring_slots):
 
 
 @pytest.mark.timeout(180)
-def test_config3_4k_batch16_sharded_in_order_ring():
+def test_configs2_4k_batch16_sharded_in_order_ring():
     _sharded_4k(2, 64, 24)
 
 
 @pytest.mark.timeout(240)
-def test_config2_4k_batch16_eight_way_shard_one_card():
+def test_configs2_4k_batch16_eight_way_shard_one_card():
     """BASELINE configs[2]'s fan-out width: 8 worker processes (on the box's one GPU), 8
     frame-index shards, 160 frames (10 chunks of 16) through 8 per-worker ring slices."""
     st = _sharded_4k(8, 160, 16)
@@ -96,7 +96,7 @@ def test_config2_4k_batch16_eight_way_shard_one_card():
 
 
 @pytest.mark.timeout(180)
-def test_config4_mixed_resolution_pull_tcp_payloads():
+def test_configs3_mixed_resolution_pull_tcp_payloads():
     shapes = [(480, 640), (1080, 1920), (2160, 3840)]
     frames = [oracle.synthetic_frame(i, *shapes[i % 3]) for i in range(24)]
     d = Distributor(0, 0, 5, True, policy="pull", reassembly="ordered", queue_size=16, transport="tcp",

@@ -164,7 +164,7 @@ def _drain_ordered(d, frames, timeout=30.0):
 
 
 @pytest.mark.timeout(120)
-def test_config1_latest_policy_two_v0_workers():
+def test_configs0_latest_policy_two_v0_workers():
     """configs[0]: 640x480 frames through the distributor + 2 CPU workers speaking the
     reference protocol (v0); reference policy: latest-wins dispatch, lossy display."""
     d = _dist(policy="latest", reassembly="display", frame_delay=2)

@@ -1,4 +1,4 @@
-# k_spec / k_resolve phase counters (tools/libv_stats.so: -DVF_SYNC_STATS=1 build) at 480p and
+# k_spec / k_resolve phase counters (tools/libv_stats.so: tools/build_stats_lib.sh, the sync_stats.patch build) at 480p and
 # 1080p, plus the custom-table JPEG GPU test on the in-tree library
 set -o pipefail
 mkdir -p gpurun_out
