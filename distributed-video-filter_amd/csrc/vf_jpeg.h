@@ -49,6 +49,14 @@ struct SpecBufs {
   uint64_t *wBX;
   uint8_t *rE;     // resolved walk column
   uint32_t *rK;    // resolved: prefix covers subsequences 0..rK
+  // traces k_wglink runs where the path may meet an explicit state (per workgroup, by lane):
+  uint8_t *wTE;    //   boundary link j missed: the walk column its trace joins (kLinkNone: none
+  uint8_t *wTK;    //   in the workgroup, kLinkLast: frame end) and at which subsequence; records in pX
+  uint8_t *wQE;    //   walk column e of the workgroup before ended explicit: the same, records in qX
+  uint8_t *wQK;
+  uint64_t *qX;    // prefix records of those traces (lane = e), like pX / pC
+  uint32_t *qC;
+  uint8_t *rL;     // resolved: where the prefix records are (0x80 | lane: pX, 0xC0 | lane: qX)
   uint32_t *stats;  // diagnostics (builds with tools/sync_stats.patch applied): [1] walker decodes [2] traced workgroups
                     // [3] traced subsequences [4] link misses
 };

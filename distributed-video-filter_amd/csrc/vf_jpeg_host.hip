@@ -420,6 +420,13 @@ int Codec::prepare_decode(const uint8_t *const *jpegs, const size_t *sizes, int 
     CK(d_wBX_.ensure(sizeof(uint64_t) * wl));
     CK(d_rE_.ensure(wgs));
     CK(d_rK_.ensure(sizeof(uint32_t) * wgs));
+    CK(d_wTE_.ensure(wl));
+    CK(d_wTK_.ensure(wl));
+    CK(d_wQE_.ensure(wl));
+    CK(d_wQK_.ensure(wl));
+    CK(d_qX_.ensure(sizeof(uint64_t) * sl));
+    CK(d_qC_.ensure(sizeof(uint32_t) * sl));
+    CK(d_rL_.ensure(wgs));
     CK(d_unres_.ensure(sizeof(uint32_t) * 16));
   }
   CK(d_changed_.ensure(sizeof(uint32_t) * kMaxPasses));
@@ -478,7 +485,9 @@ int Codec::run_decode(int bgr, bool invert, std::string *err) {
     SpecBufs sb{d_tE_.as<uint64_t>(), d_tG_.as<uint8_t>(), d_tX_.as<uint64_t>(), d_tXc_.as<uint32_t>(),
                 d_pX_.as<uint64_t>(), d_pC_.as<uint32_t>(), d_wF_.as<uint8_t>(), d_wck_.as<uint64_t>(),
                 d_wrem_.as<uint32_t>(), d_wB_.as<uint8_t>(), d_wBC_.as<uint32_t>(), d_wBX_.as<uint64_t>(),
-                d_rE_.as<uint8_t>(), d_rK_.as<uint32_t>(), d_unres_.as<uint32_t>()};
+                d_rE_.as<uint8_t>(), d_rK_.as<uint32_t>(), d_wTE_.as<uint8_t>(), d_wTK_.as<uint8_t>(),
+                d_wQE_.as<uint8_t>(), d_wQK_.as<uint8_t>(), d_qX_.as<uint64_t>(), d_qC_.as<uint32_t>(),
+                d_rL_.as<uint8_t>(), d_unres_.as<uint32_t>()};
     CK(hipMemsetAsync(d_unres_.p, 0, sizeof(uint32_t) * 16, s_));
     CK(dec_sync_spec(sg, fr, ns, dmax_wg_, d_us_.as<uint8_t>(), us_len, sb, d_exit_[0].as<uint64_t>(),
                      d_cnt_[0].as<uint32_t>(), d_unres_.as<uint32_t>(), s_));

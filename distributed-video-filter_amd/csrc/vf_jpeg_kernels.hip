@@ -779,8 +779,58 @@ __global__ __launch_bounds__(256) void k_spec(const DecSeg *__restrict__ sg, con
   }
 }
 
+// Where the speculative path misses, it must be traced: decoded on from an explicit state
+// until its exit equals the exit of some walk column (tX) at a subsequence, after which it IS
+// that column.  Which explicit states the true path can meet at workgroup w is known before
+// the path is: the exit of boundary link j when it rejoined nothing (wBX), or the end state of
+// a walk column of w-1 that ended explicit (tX at w-1's last subsequence).  So those traces
+// run in parallel in k_wglink, one lane each, and k_resolve's serial walk across a frame's
+// workgroups only picks the precomputed result of the one it meets (round 2: ~2 serial traces
+// per 1080p frame were half of k_resolve's 68 us per batch).
+constexpr uint32_t kResolveLds = 4096;  // workgroups per frame resolved here (else fallback)
+constexpr uint32_t kTraceWords = kSubBits / 32 + 6;  // one subsequence + overshoot + lookahead
+constexpr uint8_t kNotTraced = 0xFD;   // wTE / wQE: no precomputed trace for this lane
+constexpr uint8_t kRecP = 0x80, kRecQ = 0xC0;  // rL: prefix records in pX / qX, lane = low 4 bits
+
+// Decode from explicit state X through subsequences k0.. of workgroup w (words staged per
+// subsequence into the caller's `tw` row) until the exit equals walk column q's exit tX there
+// (returns q, *kend = k), the frame ends (kLinkLast) or the workgroup does (kLinkNone, *kend =
+// its last subsequence).  Every subsequence's exit and block count go to rX / rC at lane `lane`.
+__device__ __forceinline__ uint32_t trace_on(const uint32_t *gw, uint32_t fwords, uint32_t *tw, uint64_t X,
+                                             uint32_t w, uint32_t k0, uint32_t NS, uint32_t L, uint32_t nsub,
+                                             uint32_t nbits, uint64_t tr0, const HuffGeom &hg,
+                                             const HuffSync *tabs, const uint64_t *tX, uint64_t *rX, uint32_t *rC,
+                                             uint32_t lane, uint32_t *kend) {
+  uint32_t k = k0;
+  for (; k < NS && w * NS + k < nsub; ++k) {
+    const uint32_t sk = w * NS + k;
+    const uint32_t ek = (sk + 1 >= nsub) ? nbits : (sk + 1) * kSubBits;
+    // the subsequence's words, fetched together (independent loads), then decoded from LDS
+    const uint32_t w0 = (uint32_t)(X >> 16) >> 5;
+    for (uint32_t q = 0; q < kTraceWords; ++q) tw[q] = w0 + q < fwords ? gw[w0 + q] : 0u;
+    BitReader br;
+    br.init_words(tw, (uint32_t)(X >> 16), w0);
+    uint32_t z = (X >> 8) & 0xFF, c = X & 0xFF, n = 0;
+    const uint32_t lim = min(ek, (w0 + kTraceWords - 4) * 32u);  // stays inside tw (binds only on corrupt data)
+    while (br.pos < lim) sync_step(br, z, c, n, hg, tabs, tabs + 3);
+    X = pack_state(br.pos, z, c);
+    const uint64_t at = tr0 + (uint64_t)w * 256 + k * L;
+    rX[at + lane] = X;
+    rC[at + lane] = n;
+    *kend = k;
+    if (sk + 1 == nsub) return kLinkLast;
+    for (uint32_t c2 = 0; c2 < hg.bpm; ++c2)
+      if (tX[at + c2] == X) return c2;  // the path is walk column c2 from here on
+  }
+  *kend = k ? k - 1 : 0;
+  return kLinkNone;
+}
+
 // Links across workgroup boundaries: trajectory j of the last subsequence of workgroup w-1
-// into the first subsequence of w.  16 boundaries per workgroup, one lane per j.
+// into the first subsequence of w.  16 boundaries per workgroup, one lane per j.  Lanes
+// j < bpm: the link, and where it rejoined nothing, its trace on through w (records in pX lane
+// j, result in wTE / wTK).  Lanes 8 + e (bpm <= 8): walk column e of w-1 ended explicit: its
+// trace through w from subsequence 0 (records in qX lane e, result in wQE / wQK).
 __global__ __launch_bounds__(256) void k_wglink(const DecSeg *__restrict__ sg, const DecFrame *__restrict__ fr, const uint8_t *us, const uint32_t *us_len,
                                                 SpecBufs B) {
   constexpr uint32_t kLinkWords = kSubBits / 32 + kSpecPadWords;  // as k_spec's window for one subsequence
@@ -788,6 +838,7 @@ __global__ __launch_bounds__(256) void k_wglink(const DecSeg *__restrict__ sg, c
   __shared__ uint32_t s_lw[16][kLinkWords];
   __shared__ uint64_t s_ck[16][kSpecLanesMax * kCk];
   __shared__ uint32_t s_rem[16][kSpecLanesMax * kCk];
+  __shared__ uint32_t s_tw[256][kTraceWords];  // each tracing lane's staged words
   const DecSeg S = sg[blockIdx.y];  // by value: held in scalar registers
   const DecFrame &F = fr[S.frame];
   if (blockIdx.x * 16 >= S.nwg) return;
@@ -797,12 +848,13 @@ __global__ __launch_bounds__(256) void k_wglink(const DecSeg *__restrict__ sg, c
   const uint32_t nbits = us_len[blockIdx.y] * 8u, nsub = (nbits + kSubBits - 1) / kSubBits;
   const uint32_t s = w * NS;
   const bool live = w > 0 && w < S.nwg && s < nsub;
+  const uint32_t fwords = (((S.in_len + 64) + 15) & ~15u) / 4;
+  const uint32_t *gw = reinterpret_cast<const uint32_t *>(us + S.us_off);
   // Stage each boundary's stream words and the checkpoints it compares against (all loads
   // issued before the decode, instead of one dependent global load per refill and per mark)
   const uint64_t wc = (uint64_t)(S.wg0 + w) * kSpecLanesMax;
   if (live) {
-    const uint32_t fwords = (((S.in_len + 64) + 15) & ~15u) / 4, woff = s * (kSubBits / 32);
-    const uint32_t *gw = reinterpret_cast<const uint32_t *>(us + S.us_off);
+    const uint32_t woff = s * (kSubBits / 32);
     for (uint32_t i = j; i < kLinkWords; i += 16) s_lw[wl][i] = woff + i < fwords ? gw[woff + i] : 0u;
     if (j < hg.bpm) {
 #pragma unroll
@@ -813,29 +865,52 @@ __global__ __launch_bounds__(256) void k_wglink(const DecSeg *__restrict__ sg, c
     }
   }
   load_sync_tables(F, tabs);  // its barrier also publishes the staged words and checkpoints
-  if (!live || j >= hg.bpm) return;
+  if (!live) return;
   const uint32_t base = s * kSubBits, end = (s + 1 >= nsub) ? nbits : (s + 1) * kSubBits;
-  const uint64_t X = B.tE[S.tr0 + (uint64_t)(w - 1) * 256 + (NS - 1) * L + j];
-  uint32_t C = 0;
-  uint64_t xe = 0;
-  const uint32_t M = spec_link(s_lw[wl], s * (kSubBits / 32), X, base, end, s + 1 == nsub, hg, tabs,
-                               [&](uint32_t c2, int m) { return s_ck[wl][c2 * kCk + m]; },
-                               [&](uint32_t c2, int m) { return s_rem[wl][c2 * kCk + m]; }, &C, &xe);
-  const uint64_t wb = wc + j;
-  B.wB[wb] = (uint8_t)M;
-  B.wBC[wb] = C;
-  B.wBX[wb] = xe;
+  uint32_t *tw = s_tw[threadIdx.x];
+  if (j < hg.bpm) {
+    const uint64_t X = B.tE[S.tr0 + (uint64_t)(w - 1) * 256 + (NS - 1) * L + j];
+    uint32_t C = 0;
+    uint64_t xe = 0;
+    const uint32_t M = spec_link(s_lw[wl], s * (kSubBits / 32), X, base, end, s + 1 == nsub, hg, tabs,
+                                 [&](uint32_t c2, int m) { return s_ck[wl][c2 * kCk + m]; },
+                                 [&](uint32_t c2, int m) { return s_rem[wl][c2 * kCk + m]; }, &C, &xe);
+    const uint64_t wb = wc + j;
+    B.wB[wb] = (uint8_t)M;
+    B.wBC[wb] = C;
+    B.wBX[wb] = xe;
+    uint32_t te = kNotTraced, tk = 0;
+    if (M == kLinkNone) {  // subsequence 0 decoded without rejoining: trace on from its end
+      const uint64_t at = S.tr0 + (uint64_t)w * 256;
+      B.pX[at + j] = xe;
+      B.pC[at + j] = C;
+      te = 1 < NS && s + 1 < nsub ? trace_on(gw, fwords, tw, xe, w, 1, NS, L, nsub, nbits, S.tr0, hg, tabs, B.tX,
+                                             B.pX, B.pC, j, &tk)
+                                  : kLinkNone;
+    }
+    B.wTE[wb] = (uint8_t)te;
+    B.wTK[wb] = (uint8_t)tk;
+  } else if (hg.bpm <= 8 && j >= 8 && j - 8 < hg.bpm) {
+    const uint32_t e = j - 8;
+    const uint64_t wb = wc + e;
+    uint32_t te = kNotTraced, tk = 0;
+    if (B.wF[(uint64_t)(S.wg0 + w - 1) * kSpecLanesMax + e] == kLinkNone) {  // walk e ended explicit
+      const uint64_t X = B.tX[S.tr0 + (uint64_t)(w - 1) * 256 + (NS - 1) * L + e];
+      te = trace_on(gw, fwords, tw, X, w, 0, NS, L, nsub, nbits, S.tr0, hg, tabs, B.tX, B.qX, B.qC, e, &tk);
+    }
+    B.wQE[wb] = (uint8_t)te;
+    B.wQK[wb] = (uint8_t)tk;
+  }
 }
 
 // The true path across the workgroups of a frame (one workgroup per frame).  Per workgroup w
 // it finds the walk column e* that is the path from subsequence kj + 1 on; subsequences
-// 0..kj get prefix records (exit state, count) in pX / pC.  The common case is two nibble
-// lookups in LDS (the boundary link from the trajectory ending w-1 rejoined trajectory e* of
-// w's first subsequence); where it did not, or the column ending w-1 was in an explicit
-// state, lane 0 decodes on until its exit state equals some column's exit (tX) there.
-constexpr uint32_t kResolveLds = 4096;  // workgroups per frame resolved here (else fallback)
-constexpr uint32_t kTraceWords = kSubBits / 32 + 6;  // one subsequence + overshoot + lookahead
-
+// 0..kj take prefix records (exit state, count) from pX or qX at lane rL & 15.  The common
+// case is two nibble lookups in LDS (the boundary link from the trajectory ending w-1 rejoined
+// trajectory e* of w's first subsequence); where it did not, or the column ending w-1 was in
+// an explicit state, the trace k_wglink ran for that state is taken.  Lane 0 decodes only
+// where none was run (the continuation of a trace that crossed a whole workgroup, or an
+// explicit walk with bpm > 8), into pX lane 0.
 __global__ __launch_bounds__(256) void k_resolve(const DecSeg *__restrict__ sg, const DecFrame *__restrict__ fr, const uint8_t *us, const uint32_t *us_len,
                                                  SpecBufs B, uint32_t *unresolved) {
   __shared__ uint64_t sF[kResolveLds], sB[kResolveLds];
@@ -867,17 +942,19 @@ __global__ __launch_bounds__(256) void k_resolve(const DecSeg *__restrict__ sg, 
   auto slot = [&](uint32_t w, uint32_t k, uint32_t lane) { return S.tr0 + (uint64_t)w * 256 + k * L + lane; };
   const uint32_t fwords = (((S.in_len + 64) + 15) & ~15u) / 4;
   const uint32_t *gw = reinterpret_cast<const uint32_t *>(us + S.us_off);
-  const uint8_t kTraced = 0xFF;  // sJ: the prefix was written by the tracer
   if (threadIdx.x == 0) {
     sE[0] = 0;
     sK[0] = 0;
-    sJ[0] = kTraced;  // workgroup 0: frame start = trajectory 0 (records written below)
+    sJ[0] = kRecP;  // workgroup 0: frame start = trajectory 0 (records written below)
     B.pX[slot(0, 0, 0)] = B.tX[slot(0, 0, 0)];
     B.pC[slot(0, 0, 0)] = B.tXc[slot(0, 0, 0)];
     uint32_t e = 0, kj = 0;
+    uint8_t rec = kRecP;  // where workgroup w-1's prefix records are
     for (uint32_t w = 1; w < nwg; ++w) {
       const uint32_t lastk = NS - 1;  // workgroup w-1 is full (only the frame's last one is not)
-      uint32_t jl = kLinkNone;
+      const uint64_t row = (uint64_t)(S.wg0 + w) * kSpecLanesMax;
+      uint32_t jl = kLinkNone, te = kNotTraced, tk = 0;
+      uint8_t code = kRecP;
       if (kj < lastk) jl = nib(sF[w - 1], e);
       if (jl < bpm) {
         const uint32_t jb = nib(sB[w], jl);
@@ -887,59 +964,66 @@ __global__ __launch_bounds__(256) void k_resolve(const DecSeg *__restrict__ sg, 
           sJ[w] = (uint8_t)jl;
           e = jb < bpm ? jb : 0;
           kj = 0;
+          rec = kRecP;
           continue;
         }
+        te = B.wTE[row + jl];  // the boundary link missed: its trace
+        tk = B.wTK[row + jl];
+        code = (uint8_t)(kRecP | jl);
+      } else if (kj < lastk) {
+        te = B.wQE[row + e];  // walk column e ended explicit in w-1: its trace (bpm <= 8)
+        tk = B.wQK[row + e];
+        code = (uint8_t)(kRecQ | e);
+        if (bpm > 8) te = kNotTraced;
       }
-      // trace from the explicit state at the end of w-1 (or after w's first subsequence)
+      if (te != kNotTraced) {
+        const bool found = te < bpm;
+        sE[w] = (uint8_t)(found ? te : 0);
+        sK[w] = (uint8_t)(found ? tk : NS - 1);
+        sJ[w] = code;
+        e = found ? te : 0;
+        kj = found ? tk : NS - 1;
+        rec = code;
+        continue;
+      }
+      // no precomputed trace: decode on serially (records into pX lane 0)
       uint64_t X;
       uint32_t k = 0;
-      if (jl < bpm) {  // the boundary link decoded subsequence 0 without rejoining
-        const uint64_t wb = (uint64_t)(S.wg0 + w) * kSpecLanesMax + jl;
-        X = B.wBX[wb];
+      if (jl < bpm) {  // cannot happen (k_wglink traces every missed link); kept for safety
+        X = B.wBX[row + jl];
         B.pX[slot(w, 0, 0)] = X;
-        B.pC[slot(w, 0, 0)] = B.wBC[wb];
+        B.pC[slot(w, 0, 0)] = B.wBC[row + jl];
         k = 1;
-      } else {
-        X = kj < lastk ? B.tX[slot(w - 1, lastk, e)] : B.pX[slot(w - 1, lastk, 0)];
+      } else if (kj < lastk) {
+        X = B.tX[slot(w - 1, lastk, e)];
+      } else {  // the previous workgroup's trace ran through it: continue from its last record
+        X = ((rec & 0x40) ? B.qX : B.pX)[slot(w - 1, lastk, rec & 15)];
       }
-      bool found = false;
-      for (; k < NS && w * NS + k < nsub; ++k) {
-        const uint32_t sk = w * NS + k;
-        const uint32_t ek = (sk + 1 >= nsub) ? nbits : (sk + 1) * kSubBits;
-        // the subsequence's words, fetched together (independent loads), then decoded from LDS
-        const uint32_t w0 = (uint32_t)(X >> 16) >> 5;
-        for (uint32_t q = 0; q < kTraceWords; ++q) s_tw[q] = w0 + q < fwords ? gw[w0 + q] : 0u;
-        BitReader br;
-        br.init_words(s_tw, (uint32_t)(X >> 16), w0);
-        uint32_t z = (X >> 8) & 0xFF, c = X & 0xFF, n = 0;
-        const uint32_t lim = min(ek, (w0 + kTraceWords - 4) * 32u);  // stays inside s_tw (binds only on corrupt data)
-        while (br.pos < lim) sync_step(br, z, c, n, hg, tabs, tabs + 3);
-        X = pack_state(br.pos, z, c);
-        B.pX[slot(w, k, 0)] = X;
-        B.pC[slot(w, k, 0)] = n;
-        if (sk + 1 == nsub) break;
-        for (uint32_t c2 = 0; c2 < bpm; ++c2)
-          if (B.tX[slot(w, k, c2)] == X) {  // the path is column c2 from here on
-            e = c2;
-            found = true;
-            break;
-          }
-        if (found) break;
-      }
-      sE[w] = (uint8_t)(found ? e : 0);
-      sK[w] = (uint8_t)(found ? k : NS - 1);
-      sJ[w] = kTraced;
-      kj = found ? k : NS - 1;
+      uint32_t kf = 0;
+      te = k < NS && w * NS + k < nsub
+               ? trace_on(gw, fwords, s_tw, X, w, k, NS, L, nsub, nbits, S.tr0, hg, tabs, B.tX, B.pX, B.pC, 0, &kf)
+               : kLinkNone;
+      const bool found = te < bpm;
+      sE[w] = (uint8_t)(found ? te : 0);
+      sK[w] = (uint8_t)(found ? kf : NS - 1);
+      sJ[w] = kRecP;
+      e = found ? te : 0;
+      kj = found ? kf : NS - 1;
+      rec = kRecP;
     }
   }
   __syncthreads();
   for (uint32_t w = threadIdx.x; w < nwg; w += 256) {
     B.rE[S.wg0 + w] = sE[w];
     B.rK[S.wg0 + w] = sK[w];
-    if (sJ[w] != kTraced) {  // rejoined at the boundary: prefix record of subsequence 0
-      const uint64_t wb = (uint64_t)(S.wg0 + w) * kSpecLanesMax + sJ[w];
-      B.pX[slot(w, 0, 0)] = sK[w] == 0 && nib(sB[w], sJ[w]) < bpm ? B.tE[slot(w, 0, sE[w])] : B.wBX[wb];
+    const uint8_t code = sJ[w];
+    if (code < kRecP) {  // rejoined at the boundary: prefix record of subsequence 0, into pX lane 0
+      const uint64_t wb = (uint64_t)(S.wg0 + w) * kSpecLanesMax + code;
+      B.pX[slot(w, 0, 0)] = sK[w] == 0 && nib(sB[w], code) < bpm ? B.tE[slot(w, 0, sE[w])] : B.wBX[wb];
       B.pC[slot(w, 0, 0)] = B.wBC[wb];
+      B.rL[S.wg0 + w] = kRecP;
+    } else {
+      B.rL[S.wg0 + w] = code;
     }
   }
 }
@@ -966,8 +1050,10 @@ __global__ __launch_bounds__(256) void k_finalize(const DecSeg *__restrict__ sg,
   const uint64_t g0 = S.tr0 + (uint64_t)blockIdx.x * 256;
   const uint32_t kj = B.rK[S.wg0 + blockIdx.x], e = B.rE[S.wg0 + blockIdx.x];
   if (sl <= kj) {
-    exit_out[gi] = B.pX[g0 + sl * L];
-    cnt_out[gi] = B.pC[g0 + sl * L];
+    const uint8_t rl = B.rL[S.wg0 + blockIdx.x];
+    const uint64_t at = g0 + sl * L + (rl & 15);
+    exit_out[gi] = (rl & 0x40) ? B.qX[at] : B.pX[at];
+    cnt_out[gi] = (rl & 0x40) ? B.qC[at] : B.pC[at];
   } else {
     exit_out[gi] = B.tX[g0 + sl * L + e];
     cnt_out[gi] = B.tXc[g0 + sl * L + e];
