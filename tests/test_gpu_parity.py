@@ -438,7 +438,7 @@ def test_sync_zero_copy_while_async_in_flight(vf_ctx):
             assert np.array_equal(hd[4], ~hs[4]), r
             for t in ts:
                 vf_ctx.wait(t)
-        for k in range(5):
+        for k in (0, 1, 2, 4):
             assert np.array_equal(hd[k], ~hs[k]), k
     finally:
         for p in ps + pd:
