@@ -75,6 +75,7 @@ def parse():
                     help="processes of the multi-process CPU baseline (capped by the CPU affinity; 0 = skip)")
     ap.add_argument("--probe", action="store_true", help=argparse.SUPPRESS)  # child under rocprofv3
     ap.add_argument("--cpu-worker", type=float, default=0.0, help=argparse.SUPPRESS)  # cpu_baseline_multi child
+    ap.add_argument("--host-copy-child", type=float, default=0.0, help=argparse.SUPPRESS)  # host_copy_ceiling child
     ap.add_argument("--jpeg-child", type=int, default=-1, help=argparse.SUPPRESS)  # jpeg leg on device N
     return ap.parse_args()
 
@@ -222,6 +223,80 @@ def cpu_baseline_multi(seconds, procs):
             "GBps_r_plus_w": round(rate * 2 * FRAME_BYTES / 1e9, 1),
             "sample": f"{procs} processes x {seconds:.0f} s of np.bitwise_not(x, out=y) over a 32-frame "
                       f"1080p batch each (oracle arithmetic of inverter.py:41)"}
+
+
+def cgroup_cpus():
+    """CPUs this process may use by its cgroup's CPU quota (cpu.max), None when unlimited: on
+    the GPU box the lease's share (16 per GPU) is far below the machine's CPU count."""
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            with open(path) as f:
+                q, per = f.read().split()[:2]
+            return None if q == "max" else max(1, int(int(q) / int(per)))
+        except (OSError, ValueError):
+            pass
+    return None
+
+
+def host_copy_child(seconds):
+    """Child of host_copy_ceiling: on each NUMA node, threads pinned to the node's CPUs copy
+    between two node-local 64 MiB buffers (np.copyto, no GIL) for `seconds`, all nodes at once;
+    prints read + write GB/s per node.  Threads per node: the node's CPUs, capped by the
+    process's CPU quota shared evenly over the nodes."""
+    import threading
+    import numpy as np
+    from vfilter import numa
+    nodes = [n for n in range(numa.node_count()) if numa.node_cpus(n)] or [None]
+    quota = cgroup_cpus() or len(os.sched_getaffinity(0))
+    per = {n: max(1, min(len(numa.node_cpus(n)) if n is not None else quota, quota // len(nodes))) for n in nodes}
+    moved = {n: [0] * per[n] for n in nodes}
+    ready = threading.Barrier(sum(per.values()) + 1)
+    stop = threading.Event()
+
+    def run(n, i):
+        numa.pin_thread_to_node(n)
+        a = np.ones(64 << 20, np.uint8)  # first touch after the pin: node-local pages
+        b = np.zeros_like(a)
+        ready.wait()
+        k = 0
+        while not stop.is_set():
+            np.copyto(b, a)
+            k += 1
+        moved[n][i] = 2 * k * a.nbytes
+    ths = [threading.Thread(target=run, args=(n, i)) for n in nodes for i in range(per[n])]
+    for t in ths:
+        t.start()
+    ready.wait()
+    t0 = time.perf_counter()
+    time.sleep(seconds)
+    stop.set()
+    for t in ths:
+        t.join()
+    dt = time.perf_counter() - t0
+    out = {str(n): round(sum(moved[n]) / dt / 1e9, 1) for n in nodes}
+    print(json.dumps({"GBps_r_plus_w_per_node": out, "threads_per_node": {str(n): per[n] for n in nodes},
+                      "cpu_quota": cgroup_cpus(), "affinity_cpus": len(os.sched_getaffinity(0))}), flush=True)
+
+
+def host_copy_ceiling(seconds=3.0):
+    """The host side's own bound for the distributor legs: node-local copy bandwidth (read +
+    write) summed over the NUMA nodes, measured in a fresh child with threads pinned per node
+    (host_copy_child).  It replaces round 2's figure from 16 numpy processes, which was bound
+    by the lease's CPU share, not by DRAM; when the share still binds it (threads < CPUs), the
+    line says so."""
+    cmd = [sys.executable, os.path.abspath(__file__), "--host-copy-child", str(seconds)]
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=seconds + 120)
+        d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    except Exception as e:  # reported, never raised
+        return {"error": repr(e)[:300]}
+    tot = round(sum(d["GBps_r_plus_w_per_node"].values()), 1)
+    threads = sum(d["threads_per_node"].values())
+    d["GBps_r_plus_w"] = tot
+    d["bound"] = ("CPU share (threads < the nodes' CPUs): a lower bound on host DRAM bandwidth"
+                  if d.get("cpu_quota") and threads < d["affinity_cpus"] else "host DRAM (all CPUs copying)")
+    d["what"] = f"np.copyto between node-local 64 MiB buffers, {threads} pinned threads over all nodes at once"
+    return d
 
 
 def resolution_leg(ctx, np, rank, world, steps, barrier_sync, reduce_max):
@@ -406,6 +481,24 @@ def jpeg_mode(ctx, batch, iters=20):
     h2h_async2x = worker_form(jpgs + jpgs, reps=11)  # the worker CLI's batch of 64 frames
     outs = tj.invert_batch(jpgs)
     passes = stages.pop("sync_passes", 0.0)
+    # hard content: 32 distinct noisy scenes at q95 (long blocks, dense entropy streams)
+    from vfilter.synthetic import synthetic_noisy_scene
+    hard = tj.encode_batch([synthetic_noisy_scene(s, H, W) for s in range(batch)], quality=95)
+    ctx.jpeg_bench_invert(hard, 85, 1, 0, iters=2)
+    hms, hst = ctx.jpeg_bench_invert(hard, 85, 1, 0, iters=iters)
+    hpasses = hst.pop("sync_passes", 0.0)
+    h_async = worker_form(hard, reps=11)
+    hard_out = tj.invert_batch(hard)
+    hard_content = {
+        "workload": f"1080p noisy scenes (vfilter.synthetic.synthetic_noisy_scene, +-40 noise) encoded at q95 "
+                    f"4:2:2, {batch} distinct frames, re-encoded at q85",
+        "gpu_resident_fps": round(batch / (hms / 1e3), 1), "gpu_resident_ms_per_batch": round(hms, 3),
+        "stages_ms": {k: round(v, 4) for k, v in hst.items()},
+        "huffman_sync_mode": "speculative (one pass)" if hpasses == 0 else f"pass-based, {hpasses:.1f} passes",
+        "host_to_host_worker_fps": round(batch / h_async, 1),
+        "jpeg_bytes_mean": round(sum(len(j) for j in hard) / batch),
+        "jpeg_bytes_out_mean": round(sum(len(o) for o in hard_out) / batch),
+        "roofline": jpeg_roofline(hst, H, W, batch, sum(len(j) for j in hard), sum(len(o) for o in hard_out))}
     return {"workload": f"1080p JPEG (q85 4:2:2) decode -> bitwise_not -> encode, batch {batch}",
             "gpu_resident_fps": round(batch / (ms / 1e3), 1), "gpu_resident_ms_per_batch": round(ms, 3),
             "stages_ms": {k: round(v, 4) for k, v in stages.items()},
@@ -417,7 +510,8 @@ def jpeg_mode(ctx, batch, iters=20):
             f"host_to_host_worker_batch{2 * batch}_fps": round(2 * batch / h2h_async2x, 1),
             "host_to_host_note": "1 call at a time | 2 host threads | the worker's form: 1 thread, 3 batches "
                                  "in flight (vf_jpeg_invert_submit / _wait / _fetch)",
-            "jpeg_bytes_mean": round(sum(len(j) for j in jpgs) / batch)}, jpgs
+            "jpeg_bytes_mean": round(sum(len(j) for j in jpgs) / batch),
+            "hard_content": hard_content}, jpgs
 
 
 def jpeg_roofline(stages, h, w, batch, j_in, j_out):
@@ -512,7 +606,10 @@ def distributor_leg(nworkers, ngpu, host_gbps=None, pcie_gbps=None, frames_scale
                            (640 * 480 + 1920 * 1080 + 3840 * 2160) * 3 // 3, 4.25),
             # the reference's default deployment: JPEG frames, workers in JPEG mode
             "jpeg_1080p": (["--jpeg", "--size", "1080p", "--batch", "32", "--policy", "pull",
-                            "--frames", str(int(4096 * nworkers * frames_scale))], 181876, None)}
+                            "--frames", str(int(4096 * nworkers * frames_scale))], 181876, None),
+            # the same deployment on hard content: 32 distinct noisy scenes at q95
+            "jpeg_1080p_hard": (["--jpeg", "--content", "hard", "--size", "1080p", "--batch", "32", "--policy",
+                                 "pull", "--frames", str(int(1536 * nworkers * frames_scale))], None, None)}
     out = {}
     for name, (extra, fbytes, host_x) in legs.items():
         cmd = [sys.executable, tool, "--workers", str(nworkers), "--gpus", str(ngpu)] + extra
@@ -531,7 +628,8 @@ def distributor_leg(nworkers, ngpu, host_gbps=None, pcie_gbps=None, frames_scale
             out[name] = {"error": f"rc={p.returncode}: {se[-300:]}"}
             continue
         r = json.loads(lines[-1])
-        keep = ("kind", "size", "workers", "gpus", "policy", "producer", "producers", "batch", "inflight_per_worker",
+        keep = ("kind", "size", "content", "workers", "gpus", "policy", "producer", "producers", "batch",
+                "inflight_per_worker", "host_work_placement",
                 "ring_slots_per_worker", "frames", "fps", "GBps_each_way",
                 "latency_ms_mean", "latency_ms_p99", "reorder_wait_mean_ms", "reorder_wait_max_ms",
                 "max_buffer_depth", "out_of_order_arrivals", "n_errors", "verify_full_every",
@@ -551,8 +649,9 @@ def distributor_leg(nworkers, ngpu, host_gbps=None, pcie_gbps=None, frames_scale
         out[name] = leg
     out["note"] = ("host->host through distributor + per-worker shared-memory ring slices + one worker process "
                    "per GPU; bound by host memory and PCIe, not HBM; never the headline value. ceilings: pcie = "
-                   "GPUs x end_to_end.pinned_pipelined GB/s each way / frame bytes; host_dram = the multi-process "
-                   "CPU baseline's r+w GB/s / host bytes per frame")
+                   "GPUs x end_to_end.pinned_pipelined GB/s each way / frame bytes; host_dram = "
+                   "cpu_baseline.host_copy_ceiling's node-local r+w GB/s (pinned threads on every node; its "
+                   "'bound' says whether the lease's CPU share limited it) / host bytes per frame")
     return out
 
 
@@ -589,6 +688,8 @@ def main():
         return jpeg_child(args)
     if args.cpu_worker:
         return cpu_worker(args.cpu_worker)
+    if args.host_copy_child:
+        return host_copy_child(args.host_copy_child)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -699,6 +800,7 @@ def main():
                 cpu["process_scaling_fps"] = series
         if full:
             cpu["sizes"] = cpu_baseline_sizes(min(3.0, args.cpu_seconds), np)
+        cpu["host_copy_ceiling"] = host_copy_ceiling(3.0 if full else 1.5)
         log(f"cpu baseline: {cpu}")
 
     ctx.close()
@@ -707,7 +809,7 @@ def main():
     if not args.no_distributor:
         if rank == 0:
             # one worker per rank; workers share GPUs only when rehearsing N ranks on fewer cards
-            host_gbps = (cpu or {}).get("multi_process", {}).get("GBps_r_plus_w")
+            host_gbps = (cpu or {}).get("host_copy_ceiling", {}).get("GBps_r_plus_w")
             pcie_gbps = (e2e or {}).get("pinned_pipelined_GBps_each_way")
             fanout = distributor_leg(world, max(1, min(world, torch.cuda.device_count())), host_gbps, pcie_gbps)
             log(f"distributor leg: {fanout}")

@@ -1160,7 +1160,7 @@ class Distributor:
                                                 "shards": sorted(k for k, o in self._shard_owner.items()
                                                                  if o == p.pid),
                                                 "in_flight": len(p.inflight), "evictions": p.evictions,
-                                                "slice": self._slice_info(p.slice)}
+                                                "slice": self._slice_info(p.slice), "slice_id": p.slice}
                                   for p in self._peers.values()}})
             return s
 

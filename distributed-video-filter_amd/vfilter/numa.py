@@ -98,3 +98,41 @@ def page_nodes(addr: int, nbytes: int, max_pages: int = 4096) -> List[int]:
     if rc != 0:
         return []
     return list(status)
+
+
+def node_cpus(node: Optional[int]) -> List[int]:
+    """CPUs of NUMA node ``node`` that this process may run on (sysfs cpulist intersected with
+    the affinity mask); empty when unknown."""
+    if node is None or node < 0:
+        return []
+    try:
+        with open(f"/sys/devices/system/node/node{node}/cpulist") as f:
+            spec = f.read().strip()
+    except OSError:
+        return []
+    cpus = set()
+    for part in spec.split(","):
+        if not part:
+            continue
+        a, _, b = part.partition("-")
+        cpus.update(range(int(a), int(b or a) + 1))
+    try:
+        cpus &= os.sched_getaffinity(0)
+    except (AttributeError, OSError):
+        pass
+    return sorted(cpus)
+
+
+def pin_thread_to_node(node: Optional[int]) -> bool:
+    """Restrict the calling thread to the CPUs of ``node`` (Linux: sched_setaffinity(0) is per
+    thread), so the pages it first touches and the memory it streams stay on that socket.
+    False (nothing changed) when the node's CPUs are unknown."""
+    cpus = node_cpus(node)
+    if not cpus:
+        return False
+    try:
+        os.sched_setaffinity(0, cpus)
+        return True
+    except (AttributeError, OSError):
+        return False
+

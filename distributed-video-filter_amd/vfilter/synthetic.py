@@ -43,3 +43,14 @@ def synthetic_scene(seed: int, h: int, w: int) -> np.ndarray:
         img[y0:y1, x0:x1, :] = rng.uniform(0, 255, 3)
     img += rng.normal(0.0, 3.0, img.shape)
     return np.clip(np.rint(img), 0, 255).astype(np.uint8)
+
+
+def synthetic_noisy_scene(seed: int, h: int, w: int, amp: int = 40) -> np.ndarray:
+    """A camera-like scene with strong sensor-like noise (uniform +-amp per sample): the hard
+    content of tests/test_gpu_jpeg.py's sync tests at full size.  Encoded at q95 its blocks are
+    long (~1 MB per 1080p frame vs ~0.18 MB for the smooth scenes), the Huffman-table cache and
+    the speculative sync's links see dense, varied streams, and the encoder codes many more
+    AC coefficients."""
+    rng = np.random.default_rng(10_000 + seed)
+    img = synthetic_scene(seed, h, w).astype(np.int16) + rng.integers(-amp, amp + 1, (h, w, 3), dtype=np.int16)
+    return np.clip(img, 0, 255).astype(np.uint8)

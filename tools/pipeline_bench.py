@@ -68,6 +68,13 @@ def main():
     ap.add_argument("--producers", type=int, default=0,
                     help="producer threads (0: one per worker, at most 8); each reserves, fills and "
                          "commits its own frames, so copies into the slices run in parallel")
+    ap.add_argument("--content", default="scene", choices=("scene", "hard"),
+                    help="--jpeg frames: camera-like scenes at q85 (8 distinct per shape), or 'hard': noisy "
+                         "scenes at q95 (32 distinct per shape, vfilter.synthetic.synthetic_noisy_scene)")
+    ap.add_argument("--numa-local", type=int, default=1,
+                    help="1: frame copies and full checks run on threads pinned to the NUMA node of the "
+                         "slot's ring slice (per-node pools; each node gets its own copy of the source "
+                         "frames); 0: on the producer / one verification pool")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
 
@@ -77,10 +84,12 @@ def main():
     if args.jpeg:  # 8 distinct JPEGs per shape and their inverted JPEGs, from the product
         from vfilter import Context
         from vfilter.jpeg import TurboJPEG
-        from vfilter.synthetic import synthetic_scene
+        from vfilter.synthetic import synthetic_noisy_scene, synthetic_scene
+        hard = args.content == "hard"
+        gen, nd, q = (synthetic_noisy_scene, 32, 95) if hard else (synthetic_scene, 8, 85)
         with Context(int(os.environ.get("VF_DEVICE", "0"))) as cctx:
             tj = TurboJPEG(ctx=cctx)
-            jpgs = [bytes(j) for h, w in shapes for j in tj.encode_batch([synthetic_scene(s, h, w) for s in range(8)])]
+            jpgs = [bytes(j) for h, w in shapes for j in tj.encode_batch([gen(s, h, w) for s in range(nd)], quality=q)]
             want = [bytes(o) for o in tj.invert_batch(jpgs)]
         want_np = [np.frombuffer(w_, np.uint8) for w_ in want]
         fbytes = [len(j) for j in jpgs]
@@ -127,6 +136,26 @@ def main():
                                    " | ".join((p.stderr.read() or b"").decode()[-300:] for p in procs if p.poll() is not None))
             time.sleep(0.05)
 
+        # NUMA-local host work: one pool of threads pinned to each slice's node; a frame's copy
+        # into its slot and its full check run on the pool of the slot's node, from that node's
+        # own copy of the source frames, so neither crosses the socket link
+        from concurrent.futures import ThreadPoolExecutor
+        from vfilter import numa as vnuma
+        wk = d.ordering_stats()["workers"]
+        sid_node = {}
+        for w_ in wk.values():
+            sl = w_.get("slice")
+            if sl and w_.get("slice_id") is not None:
+                sid_node[w_["slice_id"]] = sl["numa"]
+        nodes = sorted({n_ for n_ in sid_node.values() if n_ is not None}) if args.numa_local else []
+        per_node = max(2, min(8, (len(os.sched_getaffinity(0)) // max(1, len(nodes))))) if nodes else 0
+        node_pool = {n_: ThreadPoolExecutor(max_workers=per_node, thread_name_prefix=f"node{n_}",
+                                            initializer=vnuma.pin_thread_to_node, initargs=(n_,)) for n_ in nodes}
+        pinned_ok = {n_: bool(node_pool[n_].submit(vnuma.pin_thread_to_node, n_).result()) for n_ in nodes}
+
+        def slot_node(slot):
+            return sid_node.get(slot // d.ring_slots) if nodes else None
+
         rng = np.random.default_rng(0)
         # resident content: each slot's input half holds random bytes once
         if args.producer == "resident":
@@ -134,6 +163,8 @@ def main():
                 d.in_view(s, slot_bytes)[:] = rng.integers(0, 256, slot_bytes, dtype=np.uint8)
         pregen = ([np.frombuffer(j, np.uint8) for j in jpgs] if args.jpeg else
                   [rng.integers(0, 256, fb, dtype=np.uint8) for fb in fbytes])
+        # each node's own copy of the sources, first touched by a thread of that node
+        pregen_on = {n_: node_pool[n_].submit(lambda: [p_.copy() for p_ in pregen]).result() for n_ in nodes}
         # warmup: every worker maps and page-locks its slice on its first batch (hipHostRegister,
         # ~0.15 s per GB) -- a one-off start-up cost kept out of the timing
         warm = 2 * args.batch * args.workers * len(shapes)
@@ -169,17 +200,25 @@ def main():
                 done_ = 0
                 while done_ < g:
                     slots = d.reserve_frames(max_nb, g - done_)
-                    nbs, shs = [], []
+                    nbs, shs, futs, idxs = [], [], [], []
                     for j, slot in enumerate(slots):
                         idx = d.reserved_index(slot)
                         idx = i0 + done_ + j if idx is None else idx
+                        idxs.append(idx)
                         k = idx % len(shapes)
                         nb = fbytes[k]
                         if args.producer == "copy":
-                            copy_into(d.frame_view(slot, nb), pregen[k], threads=1 if nprod > 1 else 4)
-                        commit_t[idx] = time.perf_counter()
+                            nd_ = slot_node(slot)
+                            if nd_ in node_pool:  # on the slice's own node
+                                futs.append(node_pool[nd_].submit(copy_into, d.frame_view(slot, nb), pregen_on[nd_][k],
+                                                                  1))
+                            else:
+                                copy_into(d.frame_view(slot, nb), pregen[k], threads=1 if nprod > 1 else 4)
                         nbs.append(nb)
                         shs.append(None if args.jpeg else [shapes[k][0], shapes[k][1], 3])
+                    for f_ in futs:
+                        f_.result()
+                    commit_t[idxs] = time.perf_counter()
                     d.commit_frames(slots, nbs, shs)
                     done_ += len(slots)
 
@@ -236,7 +275,8 @@ def main():
                 continue
             src = d.in_view(info["slot"], view.nbytes)
             if i % args.verify_every == 0:
-                pending.append(vpool.submit(full_check, i, idx, view, src))
+                nd_ = slot_node(info["slot"])
+                pending.append((node_pool.get(nd_) or vpool).submit(full_check, i, idx, view, src))
             else:
                 if not (np.array_equal(view[:4096], np.bitwise_not(src[:4096])) and
                         np.array_equal(view[-4096:], np.bitwise_not(src[-4096:]))):
@@ -254,6 +294,8 @@ def main():
         vpool.shutdown()
         for th in ths:
             th.join()
+        for p_ in node_pool.values():
+            p_.shutdown()
         el = t_end - t_start
         lat = (release_t[warm:] - commit_t[warm:]) * 1e3
         st = d.ordering_stats()
@@ -266,6 +308,11 @@ def main():
                   "ring_slots_per_worker": slots, "verify_full_every": args.verify_every,
                   "slice_bytes_per_worker": slices[0]["bytes"] if slices else None,
                   "slice_numa": [sl["numa"] for sl in slices], "slice_numa_bound": [sl["numa_bound"] for sl in slices],
+                  "host_work_placement": ({"per_node_threads": per_node, "nodes": nodes,
+                                           "pinned": {str(k_): v_ for k_, v_ in pinned_ok.items()},
+                                           "node_cpus": {str(n_): len(vnuma.node_cpus(n_)) for n_ in nodes}}
+                                          if nodes else "unpinned (one pool)"),
+                  "content": args.content if args.jpeg else "random",
                   "evictions": st["evictions"], "frames_lost": st["frames_lost"], "fps": round(n / el, 1), "GBps_each_way": round(total_bytes / el / 1e9, 2),
                   "latency_ms_mean": round(float(lat.mean()), 3), "latency_ms_p99": round(float(np.percentile(lat, 99)), 3),
                   "reorder_wait_mean_ms": round(st["reorder_wait_mean_ms"], 3),

@@ -37,3 +37,7 @@ timeout -s KILL 90 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INST
 ls gpurun_out/pmc_a/*/
 timeout -k 10 120 python -u tools/per_frame_probe.py > gpurun_out/r3_per_frame.jsonl 2> gpurun_out/r3_per_frame.log || { echo PERFRAME_FAILED; tail -20 gpurun_out/r3_per_frame.log; exit 1; }
 cat gpurun_out/r3_per_frame.jsonl
+timeout -k 10 200 python -u tools/pipeline_bench.py --workers 1 --size 4k --batch 16 --frames 256 --policy shard --producer copy > gpurun_out/r3_pipe_4k.jsonl 2> gpurun_out/r3_pipe_4k.log || { echo PIPE4K_FAILED; tail -20 gpurun_out/r3_pipe_4k.log; exit 1; }
+cut -c1-700 gpurun_out/r3_pipe_4k.jsonl
+timeout -k 10 200 python -u tools/pipeline_bench.py --workers 1 --jpeg --content hard --size 1080p --batch 32 --frames 1024 --policy pull > gpurun_out/r3_pipe_jpeg_hard.jsonl 2> gpurun_out/r3_pipe_jpeg_hard.log || { echo PIPEJH_FAILED; tail -20 gpurun_out/r3_pipe_jpeg_hard.log; exit 1; }
+cut -c1-700 gpurun_out/r3_pipe_jpeg_hard.jsonl
