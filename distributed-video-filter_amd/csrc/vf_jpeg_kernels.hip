@@ -1163,32 +1163,18 @@ __global__ __launch_bounds__(256) void k_write4(const DecSeg *__restrict__ sg, c
 #define FIX_3_072711026 25172
 #define DESCALE(x, n) (((x) + ((int32_t)1 << ((n)-1))) >> (n))
 
-// jidctint.c jpeg_idct_islow, one 8-point line; `shift` 11 (pass 1) or 18 (pass 2).  M24: the
-// constant multiplies as v_mul_i32_i24 / v_mad_i32_i24 (full VALU rate) instead of 32-bit
-// v_mul_lo_u32 / v_mad_u64_u32 (a quarter of it).  Exact when every input is under 2^21 in
-// magnitude (idct_fits_m24): each multiplicand is a sum of at most four inputs (z3 + z4), so
-// it fits the 24-bit signed operand, and the 32-bit result is the C code's.  Decoded data is
-// far inside that (dequantised coefficients of 8-bit samples are ~2^11); a corrupt or extreme
-// stream takes the 32-bit form, wave by wave, so the output stays bit-exact either way.
-template <bool M24>
-__device__ __forceinline__ int32_t imul(int32_t a, int32_t b) {
-  if constexpr (M24) return __mul24(a, b);
-  else return a * b;
-}
-__device__ __forceinline__ bool idct_fits_m24(const int32_t in[8]) {
-  uint32_t o = 0;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) o |= (uint32_t)(in[i] + (1 << 21));
-  return o < (1u << 22);
-}
-template <bool M24>
+// jidctint.c jpeg_idct_islow, one 8-point line; `shift` 11 (pass 1) or 18 (pass 2).  32-bit
+// products, as the C code: a decoded stream's dequantised coefficients are only bounded by
+// int16 x the quantiser, so a 24-bit multiply is not exact on every legal input; guarding it
+// per wave (a range check and a ballot per line, round 3) made k_idct slower, 129.8 -> 142.5 us
+// at 1080p x 32.
 __device__ __forceinline__ void idct_line(const int32_t in[8], int32_t out[8], int shift) {
   int32_t tmp0, tmp1, tmp2, tmp3, tmp10, tmp11, tmp12, tmp13, z1, z2, z3, z4, z5;
   z2 = in[2];
   z3 = in[6];
-  z1 = imul<M24>(z2 + z3, FIX_0_541196100);
-  tmp2 = z1 + imul<M24>(z3, -FIX_1_847759065);
-  tmp3 = z1 + imul<M24>(z2, FIX_0_765366865);
+  z1 = (z2 + z3) * FIX_0_541196100;
+  tmp2 = z1 + z3 * -FIX_1_847759065;
+  tmp3 = z1 + z2 * FIX_0_765366865;
   tmp0 = (in[0] + in[4]) * (1 << 13);
   tmp1 = (in[0] - in[4]) * (1 << 13);
   tmp10 = tmp0 + tmp3;
@@ -1203,15 +1189,15 @@ __device__ __forceinline__ void idct_line(const int32_t in[8], int32_t out[8], i
   z2 = tmp1 + tmp2;
   z3 = tmp0 + tmp2;
   z4 = tmp1 + tmp3;
-  z5 = imul<M24>(z3 + z4, FIX_1_175875602);
-  tmp0 = imul<M24>(tmp0, FIX_0_298631336);
-  tmp1 = imul<M24>(tmp1, FIX_2_053119869);
-  tmp2 = imul<M24>(tmp2, FIX_3_072711026);
-  tmp3 = imul<M24>(tmp3, FIX_1_501321110);
-  z1 = imul<M24>(z1, -FIX_0_899976223);
-  z2 = imul<M24>(z2, -FIX_2_562915447);
-  z3 = imul<M24>(z3, -FIX_1_961570560);
-  z4 = imul<M24>(z4, -FIX_0_390180644);
+  z5 = (z3 + z4) * FIX_1_175875602;
+  tmp0 *= FIX_0_298631336;
+  tmp1 *= FIX_2_053119869;
+  tmp2 *= FIX_3_072711026;
+  tmp3 *= FIX_1_501321110;
+  z1 *= -FIX_0_899976223;
+  z2 *= -FIX_2_562915447;
+  z3 *= -FIX_1_961570560;
+  z4 *= -FIX_0_390180644;
   z3 += z5;
   z4 += z5;
   tmp0 += z1 + z3;
@@ -1227,11 +1213,6 @@ __device__ __forceinline__ void idct_line(const int32_t in[8], int32_t out[8], i
   out[5] = (tmp12 - tmp1 + r) >> shift;
   out[3] = (tmp13 + tmp0 + r) >> shift;
   out[4] = (tmp13 - tmp0 + r) >> shift;
-}
-// the 24-bit form when the whole wave's inputs fit it (wave-uniform branch)
-__device__ __forceinline__ void idct_line_any(const int32_t in[8], int32_t out[8], int shift, bool active) {
-  if (__all(!active || idct_fits_m24(in))) idct_line<true>(in, out, shift);
-  else idct_line<false>(in, out, shift);
 }
 
 // jdmaster.c prepare_range_limit_table, post-IDCT part (RANGE_MASK 1023)
@@ -1341,7 +1322,7 @@ __global__ __launch_bounds__(256) void k_idct(const DecFrame *__restrict__ fr, c
 #pragma unroll
     for (int i = 0; i < 8; ++i)
       in[i] = __mul24(blkv[h * 32 + slot][i * 8 + ((colg >> (4 * i)) & 7)], s_q[k][i * 8 + r]);  // int16 x u16: exact
-    idct_line_any(in, col[h], 11, true);
+    idct_line(in, col[h], 11);
   }
   __syncthreads();
 #pragma unroll
@@ -1357,7 +1338,7 @@ __global__ __launch_bounds__(256) void k_idct(const DecFrame *__restrict__ fr, c
     int32_t in[8], out[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) in[i] = blkv[h * 32 + slot][r * 9 + i];
-    idct_line_any(in, out, 18, true);
+    idct_line(in, out, 18);
     uint32_t lo = 0, hi = 0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -1885,10 +1866,11 @@ __device__ __forceinline__ uint32_t qo_at(uint32_t slot, uint32_t zz) {
 // After quantisation the 8 lanes Huffman-code the block's AC coefficients (jchuff.c
 // encode_one_block, AC part): the quantised block sits in LDS in zigzag order, so lane r
 // reads zigzag positions 8r..8r+7 with one 16-B load.  Each lane finds the run before each of
-// its coefficients from a running "previous nonzero" position (seeded from the block's 64-bit
-// nonzero mask; ZRL for each 16), looks each code up once and keeps it in registers, takes
-// its offset from an 8-lane scan of the lanes' bit counts, and writes its bits through a
-// register accumulator into an LDS image of the block's AC stream that is then copied out.
+// its nonzero coefficients from a running "previous nonzero" position (seeded from the block's
+// 64-bit nonzero mask), lists them by rank, and the 8 lanes code the list 8 nonzeros per round
+// (ZRL for each 16 zeros of a run): one code lookup per lane and round, offsets from an 8-lane
+// scan of the round's bit counts, bits ORed into an LDS image of the block's AC stream that is
+// then copied out.
 // Outputs per block: quantised DC, AC bit count, AC bits (MSB-first words).
 constexpr uint32_t kFdctGroup = 8;  // MCUs per wave
 __global__ __launch_bounds__(256) void k_fdct(const EncFrame *__restrict__ fr, const EncTables *tab, const uint8_t *pix,
@@ -1991,60 +1973,56 @@ __global__ __launch_bounds__(256) void k_fdct(const EncFrame *__restrict__ fr, c
   const bool eob = mask == 0 || (63 - __clzll(mask)) < 63;
   // the last nonzero position before this lane's first (the DC position starts the first run)
   int prev = r ? 63 - __clzll((mask | 1ull) & ((1ull << (8 * r)) - 1)) : 0;
-  uint32_t code[8], clen[8], nzr[8];
-  uint32_t nbits = 0;
+  // The block's nonzero AC coefficients in zigzag order, as (run << 16) | (uint16) value, in
+  // the slot's pass-1 workspace (free since pass 2): lane r writes its own at their ranks.
+  // Then rounds of 8: in round i lane r codes nonzero 8i + r, so a block costs ceil(nnz / 8)
+  // rounds of one code per lane instead of eight coefficient slots per lane (a 1080p q85 frame
+  // averages ~4 nonzero AC coefficients per block).
+  const uint32_t cnt = __popc(m8);
+  const uint32_t rinc = scan8(cnt, r);
+  const uint32_t nnz = last8(rinc);
+  uint32_t *const lst = reinterpret_cast<uint32_t *>(&ws[slot][0][0]);
+  {
+    uint32_t at = rinc - cnt;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const bool nz = (m8 >> j) & 1;
-    const int kk = 8 * (int)r + j;
-    const int run = kk - prev - 1;
-    const int v = vz[j];
+    for (int j = 0; j < 8; ++j) {
+      const int kk = 8 * (int)r + j;
+      if ((m8 >> j) & 1) {
+        lst[at++] = ((uint32_t)(kk - prev - 1) << 16) | (uint32_t)(uint16_t)vz[j];
+        prev = kk;
+      }
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // the group's list, read across its lanes
+  uint32_t off = 0;  // the block's AC bits so far (the same in its 8 lanes)
+  for (uint32_t q0 = 0; __ballot(q0 < nnz) != 0; q0 += 8) {
+    const uint32_t q = q0 + r;
+    const bool act = q < nnz;
+    const uint32_t ent = act ? lst[q] : 0u;
+    const uint32_t run = ent >> 16;
+    const int v = (int)(int16_t)(ent & 0xFFFF);
     const uint32_t av = (uint32_t)(v < 0 ? -v : v);
     const uint32_t nb = 32 - __clz(av);
-    // zero coefficients all read entry 0 (one broadcast address): with their own (run, 0)
-    // entries they land on 2 banks, up to 8 distinct addresses each
-    const uint32_t e = s_ac[t][nz ? ((run & 15) << 4) + (nb & 15) : 0u];
-    code[j] = nz ? ((e >> 8) << nb) | ((uint32_t)(v < 0 ? v - 1 : v) & ((1u << nb) - 1)) : 0u;  // put() ORs it
-    clen[j] = nz ? (e & 0xFF) + nb : 0u;
-    nzr[j] = nz ? (uint32_t)(run >> 4) : 0u;
-    nbits += __umul24(nzr[j], zlen) + clen[j];
-    prev = nz ? kk : prev;
-  }
-  if (r == 7 && eob) nbits += eobc & 0xFF;
-  const uint32_t incl = scan8(nbits, r);
-  const uint32_t total = last8(incl);
-  if (real && nbits) {
-    LdsBits out(acw[slot], incl - nbits);
-    const bool e = r == 7 && eob;
-    // A lane whose bits (no ZRL) fit 64 concatenates its codes (and the EOB) in a register and
-    // writes them with two puts; the other lanes write codes in pairs (one put for codes j and
-    // j + 1 when no ZRL comes between them and they fit 32 bits), the second put of a pair
-    // skipped wave-wide when every lane merged it.  Zero coefficients have clen 0, and a
-    // zero-length put is an idempotent OR.
-    const bool fast = nbits <= 64 && (nzr[0] | nzr[1] | nzr[2] | nzr[3] | nzr[4] | nzr[5] | nzr[6] | nzr[7]) == 0;
-    uint64_t v = 0;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v = (v << clen[j]) | code[j];
-    if (e) v = (v << (eobc & 0xFF)) | (eobc >> 8);
-    const bool two = fast && nbits > 32;
-    out.put(fast ? (uint32_t)(two ? v >> 32 : v) : 0u, fast ? (two ? nbits - 32 : nbits) : 0u);
-    out.put(two ? (uint32_t)v : 0u, two ? 32u : 0u);
-    if (__ballot(!fast)) {
-#pragma unroll
-      for (int j = 0; j < 8; j += 2) {
-        for (uint32_t z = fast ? 0u : nzr[j]; z; --z) out.put(zrl >> 8, zlen);
-        const uint32_t l2 = clen[j] + clen[j + 1];
-        const bool m = nzr[j + 1] == 0 && l2 <= 32;
-        out.put(fast ? 0u : m ? (code[j] << clen[j + 1]) | code[j + 1] : code[j], fast ? 0u : m ? l2 : clen[j]);
-        if (__ballot(!fast && !m)) {
-          for (uint32_t z = fast ? 0u : nzr[j + 1]; z; --z) out.put(zrl >> 8, zlen);
-          out.put(fast || m ? 0u : code[j + 1], fast || m ? 0u : clen[j + 1]);
-        }
-      }
-      out.put(!fast && e ? eobc >> 8 : 0u, !fast && e ? eobc & 0xFF : 0u);
+    const uint32_t e = s_ac[t][((run & 15) << 4) + (nb & 15)];
+    const uint32_t code = ((e >> 8) << nb) | ((uint32_t)(v < 0 ? v - 1 : v) & ((1u << nb) - 1));
+    const uint32_t clen = (e & 0xFF) + nb;
+    const uint32_t nzr = run >> 4;  // ZRL codes before it
+    const uint32_t nbits = act ? __umul24(nzr, zlen) + clen : 0u;
+    const uint32_t incl = scan8(nbits, r);
+    if (act) {
+      LdsBits out(acw[slot], off + incl - nbits);
+      for (uint32_t z = nzr; z; --z) out.put(zrl >> 8, zlen);
+      out.put(code, clen);
+      out.finish();
     }
+    off += last8(incl);
+  }
+  if (real && eob && r == 0) {  // jchuff.c: EOB unless the last coefficient is nonzero
+    LdsBits out(acw[slot], off);
+    out.put(eobc >> 8, eobc & 0xFF);
     out.finish();
   }
+  const uint32_t total = off + (eob ? (eobc & 0xFF) : 0u);
   __syncthreads();
   if (real) {
     const uint64_t gb = F.blk0 + b;

@@ -1,0 +1,76 @@
+#!/usr/bin/env python3
+"""Issue fractions of the JPEG kernels from a per-dispatch rocprofv3 PMC pass.
+
+  rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS ... GRBM_GUI_ACTIVE GRBM_COUNT \\
+      -d DIR -o pmc -- python3 tools/jpeg_bench.py --sizes 1080p --batch 32 --iters 3
+  python tools/pmc_issue.py DIR/pmc_counter_collection.csv [--durations KERNEL_STATS.csv]
+
+Per kernel, the LAST dispatch of the run (a bench iteration, not the input encode) gives:
+  waves, VALU / LDS / SALU instructions per wave,
+  clock_GHz       GRBM_GUI_ACTIVE / the dispatch's duration (the counter ticks the GPU clock
+                  while the GUI is busy; rocprofv3 sums it over the XCDs, so it is divided by 8),
+  valu_issue_frac SQ_INSTS_VALU x 2 cycles (a wave64 VALU instruction holds a SIMD-32 for two
+                  cycles, MI355X_MICROARCH.md "Wave scheduling") / (1024 SIMDs x kernel cycles),
+  lds_issue_frac  SQ_INSTS_LDS / (256 CUs x kernel cycles) (one LDS instruction per CU per cycle
+                  at best; b64 / b128 accesses take 2-4 cycles each, so this is a lower bound).
+Kernel cycles = duration x clock.  With --durations (a rocprofv3 --stats kernel_stats.csv of the
+same workload run WITHOUT counters) the durations come from there: counter collection
+serialises dispatches and can stretch them.  Prints one JSON object keyed by kernel name.
+"""
+import argparse
+import csv
+import json
+import re
+from collections import defaultdict
+
+SIMDS, CUS, XCDS = 1024, 256, 8
+
+
+def short(name):
+    return re.sub(r"\(.*", "", name.replace("(anonymous namespace)::", "")).split("::")[-1]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("counters")
+    ap.add_argument("--durations", default="")
+    ap.add_argument("--min-waves", type=int, default=1000)
+    a = ap.parse_args()
+    disp = defaultdict(dict)  # dispatch id -> {counter: value, _name, _dur}
+    for r in csv.DictReader(open(a.counters)):
+        d = disp[int(r["Dispatch_Id"])]
+        d["_name"] = short(r["Kernel_Name"])
+        d["_dur_ns"] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+        d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    last = {}
+    for i in sorted(disp):
+        last[disp[i]["_name"]] = disp[i]
+    stats = {}
+    if a.durations:
+        for r in csv.DictReader(open(a.durations)):
+            stats[short(r["Name"])] = float(r["AverageNs"])
+    out = {}
+    for name, d in last.items():
+        waves = d.get("SQ_WAVES", 0.0)
+        if waves < a.min_waves:
+            continue
+        dur = stats.get(name, d["_dur_ns"])
+        clk = d.get("GRBM_GUI_ACTIVE", 0.0) / XCDS / d["_dur_ns"] if d["_dur_ns"] else 0.0
+        cyc = dur * clk
+        r = {"waves": int(waves), "duration_us": round(dur / 1e3, 2), "clock_GHz": round(clk, 3),
+             "valu_per_wave": round(d.get("SQ_INSTS_VALU", 0) / waves, 1),
+             "lds_per_wave": round(d.get("SQ_INSTS_LDS", 0) / waves, 1),
+             "salu_per_wave": round(d.get("SQ_INSTS_SALU", 0) / waves, 1),
+             "vmem_rd_per_wave": round(d.get("SQ_INSTS_VMEM_RD", 0) / waves, 1),
+             "vmem_wr_per_wave": round(d.get("SQ_INSTS_VMEM_WR", 0) / waves, 1)}
+        if cyc > 0:
+            r["valu_issue_frac"] = round(2.0 * d.get("SQ_INSTS_VALU", 0) / (SIMDS * cyc), 3)
+            r["lds_issue_frac"] = round(d.get("SQ_INSTS_LDS", 0) / (CUS * cyc), 3)
+        if "SQ_BUSY_CYCLES" in d and cyc > 0:
+            r["sq_busy_frac"] = round(d["SQ_BUSY_CYCLES"] / (32 * cyc), 3)  # 32 shader engines
+        out[name] = r
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
