@@ -83,6 +83,22 @@ void CopyPool::copy(uint8_t *dst, const uint8_t *src, size_t len) {
   done_cv_.wait(lk, [this] { return pending_ == 0; });
 }
 
+void CopyPool::start(std::function<void(int, int)> fn) {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    fn_ = std::move(fn);
+    pending_ = n_ - 1;
+    ++gen_;
+  }
+  cv_.notify_all();
+}
+
+void CopyPool::join() {
+  std::unique_lock<std::mutex> lk(mu_);
+  done_cv_.wait(lk, [this] { return pending_ == 0; });
+  fn_ = nullptr;
+}
+
 void CopyPool::part(int i) {
   size_t per = (len_ / n_ + 63) & ~size_t(63);
   size_t b = std::min(len_, per * (size_t)i);
@@ -99,7 +115,8 @@ void CopyPool::run(int i) {
       seen = gen_;
       if (stop_) return;
     }
-    part(i);
+    if (fn_) fn_(i - 1, n_ - 1);
+    else part(i);
     {
       std::lock_guard<std::mutex> lk(mu_);
       if (--pending_ == 0) done_cv_.notify_one();
@@ -129,11 +146,8 @@ Engine::~Engine() {
     if (s.d_out) (void)hipFree(s.d_out);
   }
   for (hipEvent_t e : free_events_) (void)hipEventDestroy(e);
-  for (auto &g : stg_) {
-    if (g.ev) (void)hipEventDestroy(g.ev);
-    (void)numa_pinned_free(g.in);
-    (void)numa_pinned_free(g.out);
-  }
+  (void)numa_pinned_free(stg_in_);
+  (void)numa_pinned_free(stg_out_);
   if (s_in_) (void)hipStreamDestroy(s_in_);
   if (s_out_) (void)hipStreamDestroy(s_out_);
   if (s_map_) (void)hipStreamDestroy(s_map_);
@@ -343,33 +357,31 @@ bool Engine::run_now(const std::vector<Seg> &segs, JobResult *out) {
 hipError_t Engine::ensure_staging() {
   if (stg_ready_) return hipSuccess;
   const int node = device_numa_node(device_);
-  for (auto &g : stg_) {
-    hipError_t e;
-    if ((!g.in && (e = numa_pinned_alloc((void **)&g.in, kStgBytes, node)) != hipSuccess) ||
-        (!g.out && (e = numa_pinned_alloc((void **)&g.out, kStgBytes, node)) != hipSuccess) ||
-        (!g.ev && (e = hipEventCreateWithFlags(&g.ev, hipEventDisableTiming)) != hipSuccess))
-      return e;
-    void *di = nullptr, *dout = nullptr;
-    if ((e = hipHostGetDevicePointer(&di, g.in, 0)) != hipSuccess ||
-        (e = hipHostGetDevicePointer(&dout, g.out, 0)) != hipSuccess)
-      return e;
-    g.din = static_cast<uint8_t *>(di);
-    g.dout = static_cast<uint8_t *>(dout);
-  }
-  if (!cpool_) cpool_.reset(new CopyPool((int)env_or("VF_HOST_THREADS", 8), (size_t)256 << 10));
+  hipError_t e;
+  if ((!stg_in_ && (e = numa_pinned_alloc((void **)&stg_in_, kStagedMax, node)) != hipSuccess) ||
+      (!stg_out_ && (e = numa_pinned_alloc((void **)&stg_out_, kStagedMax, node)) != hipSuccess))
+    return e;
+  void *di = nullptr, *dout = nullptr;
+  if ((e = hipHostGetDevicePointer(&di, stg_in_, 0)) != hipSuccess ||
+      (e = hipHostGetDevicePointer(&dout, stg_out_, 0)) != hipSuccess)
+    return e;
+  stg_din_ = static_cast<uint8_t *>(di);
+  stg_dout_ = static_cast<uint8_t *>(dout);
+  if (!cpool_) cpool_.reset(new CopyPool((int)env_or("VF_HOST_THREADS", 8) + 1, (size_t)256 << 10));
   stg_ready_ = true;
   return hipSuccess;
 }
 
 // A small synchronous job with a side outside the mapped ranges (a pageable frame: the
 // drop-in's own shape, vfilter.bitwise_not(frame) for cv2.bitwise_not(frame), inverter.py:41)
-// on the calling thread: the job is cut into pieces of up to kStgBytes; an unmapped source
-// piece is copied into a mapped staging piece, an unmapped destination piece is written by the
-// kernel into one and copied out afterwards, and a mapped side is read or written in place.
-// One invert_mapped_kernel launch per piece on the zero-copy stream, so piece i's launch runs
-// over PCIe while the CPU copies piece i + 1 in (and piece i - 1 out): no slot-ring DMA, no
-// hand-off to the engine thread.  1080p pageable -> pinned was 0.44-0.49 ms per call through
-// the slot ring (profiles/r02_per_frame.jsonl).
+// on the calling thread.  The job is cut into ~6 pieces; an unmapped source is copied into the
+// mapped staging input by the copy pool's workers -- woken once, they copy the pieces in order,
+// each worker a 1/n share of each piece, and count every piece as it lands -- while this
+// thread launches invert_mapped_kernel on each piece as soon as it is complete, so the copy of
+// piece i + 1 overlaps piece i's launch over PCIe.  A mapped side is read or written in place;
+// an unmapped destination is written into the staging output and copied out by the pool at
+// the end.  1080p pageable -> pinned: 0.44-0.49 ms per call through the slot ring
+// (profiles/r02_per_frame.jsonl).
 bool Engine::run_staged(const std::vector<Seg> &segs, size_t total, JobResult *out) {
   std::unique_lock<std::mutex> lk(stg_mu_, std::try_to_lock);
   if (!lk.owns_lock()) return false;  // another thread is staging: the engine path takes it
@@ -377,59 +389,65 @@ bool Engine::run_staged(const std::vector<Seg> &segs, size_t total, JobResult *o
     (void)hipGetLastError();
     return false;
   }
-  // piece size: about six pieces per job, 256 KiB .. kStgBytes, 64-KiB multiples
-  size_t piece = std::min(kStgBytes, std::max<size_t>((size_t)256 << 10, (total / 6 + 65535) & ~(size_t)65535));
-  hipEvent_t a = take_event(), b = take_event();
-  if (!a || !b) {
-    give_event(a);
-    give_event(b);
-    return false;
-  }
-  hipError_t e = hipEventRecord(a, s_map_);
-  int k = 0;  // ring position
-  auto drain = [&](StgSlot &g) {  // wait for the slot's launch and copy its output out
-    if (!g.busy) return hipSuccess;
-    hipError_t r = hipEventSynchronize(g.ev);
-    if (r == hipSuccess && g.copy_len) cpool_->copy(g.copy_to, g.out, g.copy_len);
-    g.busy = false;
-    g.copy_len = 0;
-    return r;
+  struct P {
+    const uint8_t *src;   // caller's source
+    uint8_t *dst;         // caller's destination
+    size_t off, len;      // position in the staging buffers
+    const uint8_t *ds;    // device address of the source (mapped, or the staging input)
+    uint8_t *dd;          // device address of the destination (mapped, or the staging output)
+    bool stage_in, stage_out;
   };
-  MappedBatch mb;
-  for (const Seg &sg : segs) {
-    for (size_t off = 0; off < sg.len && e == hipSuccess; off += piece) {
-      const size_t n = std::min(piece, sg.len - off);
-      StgSlot &g = stg_[k];
-      k = (k + 1) % kStg;
-      if ((e = drain(g)) != hipSuccess) break;
-      const uint8_t *ds = mapped(sg.src + off, n);
-      uint8_t *dd = mapped(sg.dst + off, n);
-      if (!ds) {
-        cpool_->copy(g.in, sg.src + off, n);
-        ds = g.din;
-      }
-      if (!dd) {
-        dd = g.dout;
-        g.copy_to = sg.dst + off;
-        g.copy_len = n;
-      }
-      mb.src[0] = ds;
-      mb.dst[0] = dd;
-      mb.n[0] = n;
-      if ((e = launch_invert_mapped(mb, 1, n, s_map_)) == hipSuccess) e = hipEventRecord(g.ev, s_map_);
-      g.busy = e == hipSuccess;
-      // the piece launched two steps ago is likely done: copy it out while this one runs
-      if (e == hipSuccess) e = drain(stg_[(k + kStg - 3) % kStg]);
+  const size_t piece = std::max<size_t>((size_t)256 << 10, (total / 6 + 65535) & ~(size_t)65535);
+  std::vector<P> ps;
+  size_t at = 0;
+  bool any_in = false, any_out = false;
+  for (const Seg &sg : segs)
+    for (size_t o = 0; o < sg.len; o += piece) {
+      const size_t n = std::min(piece, sg.len - o);
+      P p{sg.src + o, sg.dst + o, at, n, mapped(sg.src + o, n), mapped(sg.dst + o, n), false, false};
+      if (!p.ds) p.ds = stg_din_ + at, p.stage_in = any_in = true;
+      if (!p.dd) p.dd = stg_dout_ + at, p.stage_out = any_out = true;
+      ps.push_back(p);
+      at += n;
     }
+  const size_t np = ps.size();
+  std::unique_ptr<std::atomic<int>[]> landed(new std::atomic<int>[np]);
+  for (size_t i = 0; i < np; ++i) landed[i].store(0, std::memory_order_relaxed);
+  if (any_in)
+    cpool_->start([&](int w, int nw) {
+      for (size_t i = 0; i < np; ++i) {
+        const P &p = ps[i];
+        if (p.stage_in) {
+          const size_t per = (p.len / nw + 63) & ~(size_t)63;
+          const size_t b = std::min(p.len, per * (size_t)w), e = w == nw - 1 ? p.len : std::min(p.len, b + per);
+          if (e > b) std::memcpy(stg_in_ + p.off + b, p.src + b, e - b);
+        }
+        landed[i].fetch_add(1, std::memory_order_release);
+      }
+    });
+  const int nw = cpool_->workers();
+  hipEvent_t a = take_event(), b = take_event();
+  hipError_t e = (a && b) ? hipEventRecord(a, s_map_) : hipErrorOutOfMemory;
+  MappedBatch mb;
+  for (size_t i = 0; i < np && e == hipSuccess; ++i) {
+    const P &p = ps[i];
+    if (p.stage_in)
+      while (landed[i].load(std::memory_order_acquire) < nw) std::this_thread::yield();
+    mb.src[0] = p.ds;
+    mb.dst[0] = p.dd;
+    mb.n[0] = p.len;
+    e = launch_invert_mapped(mb, 1, p.len, s_map_);
   }
-  for (int i = 0; i < kStg && e == hipSuccess; ++i) e = drain(stg_[(k + i) % kStg]);
+  if (any_in) cpool_->join();  // also on a failed launch: the workers read the caller's buffers
   if (e == hipSuccess) e = hipEventRecord(b, s_map_);
   if (e == hipSuccess) e = hipEventSynchronize(b);
+  if (e == hipSuccess && any_out)
+    for (const P &p : ps)
+      if (p.stage_out) cpool_->copy(p.dst, stg_out_ + p.off, p.len);
   *out = JobResult();
   if (e != hipSuccess) {
     (void)hipStreamSynchronize(s_map_);  // nothing may land in the caller's buffers later
     (void)hipGetLastError();
-    for (auto &g : stg_) g.busy = false, g.copy_len = 0;
     out->status = kStatusHip;
     out->hip = e;
     out->msg = std::string("staged zero-copy launch failed: ") + hipGetErrorString(e);

@@ -7,6 +7,7 @@
 #include <atomic>
 #include <condition_variable>
 #include <deque>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -52,9 +53,15 @@ class CopyPool {
   explicit CopyPool(int nthreads, size_t split_min = (size_t)1 << 20);
   ~CopyPool();
   void copy(uint8_t *dst, const uint8_t *src, size_t len);
+  // fn(i, n) on each of the pool's n = threads() - 1 worker threads (i = 0 .. n-1), without
+  // the caller: start() returns at once, join() waits for every fn to return
+  int workers() const { return n_ - 1; }
+  void start(std::function<void(int, int)> fn);
+  void join();
 
  private:
   const size_t split_min_;  // shorter copies run on the calling thread alone
+  std::function<void(int, int)> fn_;  // start(): the workers' task
   void part(int i);
   void run(int i);
   int n_;
@@ -176,20 +183,12 @@ class Engine {
   std::vector<Slot> slots_;
   size_t fill_ = 0, d2h_ = 0, retire_ = 0;
   std::unique_ptr<CopyPool> pool_;
-  // run_staged: a ring of page-locked, device-mapped staging pieces (input and output halves)
-  // and a copy pool of its own (the engine thread's pool_ is not reentrant)
-  static constexpr int kStg = 4;
-  static constexpr size_t kStgBytes = (size_t)2 << 20;
+  // run_staged: page-locked, device-mapped staging for the unmapped side of a job (one input
+  // and one output buffer of kStagedMax) and a copy pool of its own (the engine thread's pool_
+  // is not reentrant)
   static constexpr size_t kStagedMax = (size_t)32 << 20;
-  struct StgSlot {
-    uint8_t *in = nullptr, *out = nullptr;      // host addresses
-    uint8_t *din = nullptr, *dout = nullptr;    // their device addresses
-    hipEvent_t ev = nullptr;                    // the launch that reads in / writes out
-    uint8_t *copy_to = nullptr;                 // pending copy-out of `out` (unmapped destination)
-    size_t copy_len = 0;
-    bool busy = false;
-  };
-  StgSlot stg_[kStg];
+  uint8_t *stg_in_ = nullptr, *stg_out_ = nullptr;    // host addresses
+  uint8_t *stg_din_ = nullptr, *stg_dout_ = nullptr;  // their device addresses
   bool stg_ready_ = false;
   std::mutex stg_mu_;                           // one staged job at a time
   std::unique_ptr<CopyPool> cpool_;

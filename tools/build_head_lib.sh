@@ -2,7 +2,7 @@
 set -e
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 T=$(mktemp -d)
-git -C "$ROOT" archive HEAD distributed-video-filter_amd/csrc include | tar -x -C "$T"
+git -C "$ROOT" archive ${HEAD_REF:-HEAD} distributed-video-filter_amd/csrc include | tar -x -C "$T"
 cd "$T"
 C=distributed-video-filter_amd/csrc
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -fvisibility=hidden -Wall -Iinclude -shared \

@@ -37,6 +37,9 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--cpu-seconds", type=float, default=5.0)
     ap.add_argument("--subsamp", type=int, default=J.TJSAMP_422)
+    ap.add_argument("--content", default="scene", choices=("scene", "hard"),
+                    help="scene: 8 camera-like scenes at q85; hard: 32 distinct noisy scenes at q95 "
+                         "(vfilter.synthetic.synthetic_noisy_scene)")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
     from vfilter import Context
@@ -45,8 +48,13 @@ def main():
     tj = TurboJPEG(ctx=ctx)
     for name in args.sizes.split(","):
         h, w = SIZES[name]
-        frames = [J.synthetic_scene(s, h, w) for s in range(min(args.batch, 8))]
-        jpgs = [J.encode(frames[i % len(frames)], 85, J.TJPF_BGR, args.subsamp) for i in range(args.batch)]
+        if args.content == "hard":
+            from vfilter.synthetic import synthetic_noisy_scene
+            frames = [synthetic_noisy_scene(s, h, w) for s in range(min(args.batch, 32))]
+            jpgs = [J.encode(frames[i % len(frames)], 95, J.TJPF_BGR, args.subsamp) for i in range(args.batch)]
+        else:
+            frames = [J.synthetic_scene(s, h, w) for s in range(min(args.batch, 8))]
+            jpgs = [J.encode(frames[i % len(frames)], 85, J.TJPF_BGR, args.subsamp) for i in range(args.batch)]
         in_bytes = sum(len(j) for j in jpgs)
         ms, stages = ctx.jpeg_bench_invert(jpgs, 85, args.subsamp, 0, iters=2)  # warm
         ms, stages = ctx.jpeg_bench_invert(jpgs, 85, args.subsamp, 0, iters=args.iters)
@@ -78,7 +86,7 @@ def main():
                 n += 1
             dt = time.perf_counter() - t0
             cpu = {"fps": round(n / dt, 2), "cores": 1, "frames": n, "kind": "reference codec (libjpeg-turbo 2.1.2)"}
-        rec = {"kind": "jpeg_invert", "size": name, "frame": [h, w, 3], "batch": args.batch,
+        rec = {"kind": "jpeg_invert", "size": name, "content": args.content, "frame": [h, w, 3], "batch": args.batch,
                "subsamp": args.subsamp, "quality": 85, "jpeg_bytes_in_mean": round(in_bytes / args.batch),
                "jpeg_bytes_out_mean": round(sum(len(o) for o in outs) / len(outs)),
                "gpu_resident_ms_per_batch": round(ms, 3), "gpu_resident_fps": round(args.batch / (ms / 1e3), 1),
