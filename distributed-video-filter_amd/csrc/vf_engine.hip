@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -397,7 +398,9 @@ bool Engine::run_staged(const std::vector<Seg> &segs, size_t total, JobResult *o
     uint8_t *dd;          // device address of the destination (mapped, or the staging output)
     bool stage_in, stage_out;
   };
-  const size_t piece = std::max<size_t>((size_t)256 << 10, (total / 6 + 65535) & ~(size_t)65535);
+  static const size_t kPieces = std::max<size_t>(1, env_or("VF_STAGE_PIECES", 6));
+  static const size_t kMinPiece = env_or("VF_STAGE_MIN_PIECE", (size_t)256 << 10);
+  const size_t piece = std::max<size_t>(kMinPiece, (total / kPieces + 65535) & ~(size_t)65535);
   std::vector<P> ps;
   size_t at = 0;
   bool any_in = false, any_out = false;
@@ -426,6 +429,10 @@ bool Engine::run_staged(const std::vector<Seg> &segs, size_t total, JobResult *o
       }
     });
   const int nw = cpool_->workers();
+  static const bool trace = env_or("VF_STAGE_TRACE", 0) != 0;  // per-call host timeline on stderr
+  const auto t0 = std::chrono::steady_clock::now();
+  auto us = [&] { return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count(); };
+  std::vector<double> tl;
   hipEvent_t a = take_event(), b = take_event();
   hipError_t e = (a && b) ? hipEventRecord(a, s_map_) : hipErrorOutOfMemory;
   MappedBatch mb;
@@ -433,14 +440,23 @@ bool Engine::run_staged(const std::vector<Seg> &segs, size_t total, JobResult *o
     const P &p = ps[i];
     if (p.stage_in)
       while (landed[i].load(std::memory_order_acquire) < nw) std::this_thread::yield();
+    if (trace) tl.push_back(us());
     mb.src[0] = p.ds;
     mb.dst[0] = p.dd;
     mb.n[0] = p.len;
     e = launch_invert_mapped(mb, 1, p.len, s_map_);
   }
   if (any_in) cpool_->join();  // also on a failed launch: the workers read the caller's buffers
+  if (trace) tl.push_back(us());
   if (e == hipSuccess) e = hipEventRecord(b, s_map_);
   if (e == hipSuccess) e = hipEventSynchronize(b);
+  if (trace) {
+    tl.push_back(us());
+    std::string line = "vf_stage: " + std::to_string(total) + " B, " + std::to_string(np) + " pieces; launch at";
+    for (size_t i = 0; i + 2 < tl.size(); ++i) line += " " + std::to_string((int)tl[i]);
+    line += " us; copy-in joined " + std::to_string((int)tl[tl.size() - 2]) + ", GPU done " + std::to_string((int)tl.back()) + " us";
+    std::fprintf(stderr, "%s\n", line.c_str());
+  }
   if (e == hipSuccess && any_out)
     for (const P &p : ps)
       if (p.stage_out) cpool_->copy(p.dst, stg_out_ + p.off, p.len);

@@ -1709,15 +1709,16 @@ __device__ __forceinline__ void fdct_ifast_line(int32_t p[8]) {
   p[7] = z11 - z4;
 }
 
-// jcdctmgr.c quantize (16-bit DCTELEM reciprocal form)
+// jcdctmgr.c quantize (16-bit DCTELEM reciprocal form), branch-free: the sign is taken off,
+// the magnitude scaled by the reciprocal and the sign put back (two's complement), instead of
+// a divergent if / else that ran both sides in every wave.  |t| + corr <= 2^16 and recip <
+// 2^16, so the unsigned product fits 32 bits as in the C code's UDCTELEM2.
 __device__ __forceinline__ int16_t quantize(int32_t x, uint32_t recip, uint32_t corr, int32_t shift) {
   const int32_t t = (int16_t)x;
-  if (t < 0) {
-    const uint32_t p = ((uint32_t)(-t + (int32_t)corr) * recip) >> (shift + 16);
-    return (int16_t)(-(int16_t)p);
-  }
-  const uint32_t p = ((uint32_t)(t + (int32_t)corr) * recip) >> (shift + 16);
-  return (int16_t)p;
+  const int32_t sg = t >> 31;
+  const uint32_t a = (uint32_t)((t ^ sg) - sg);
+  const uint32_t p = ((a + corr) * recip) >> (shift + 16);
+  return (int16_t)(((int32_t)p ^ sg) - sg);
 }
 
 // jccolor.c rgb_ycc_convert for one component over a pixel's bytes in memory order:
@@ -1856,7 +1857,7 @@ __constant__ uint8_t kZig[64] = {0,  1,  5,  6,  14, 15, 27, 28, 2,  4,  7,  13,
 // reads conflict-free; SQ_LDS_BANK_CONFLICT 3.45e8 per 1080p batch before,
 // profiles/r01_jpeg_pmc_sq.txt).
 __device__ __forceinline__ uint32_t qo_at(uint32_t slot, uint32_t zz) {
-  return (((zz >> 3) ^ ((0x7250u >> (4 * (slot & 3))) & 7)) << 3) | (zz & 7);
+  return zz ^ (((0x7250u >> (4 * (slot & 3))) & 7) << 3);  // the octet index's XOR, in place
 }
 
 // 8 lanes per block.  A wave codes block-in-MCU c of 8 consecutive MCUs (an MCU group); a
@@ -1917,24 +1918,24 @@ __global__ __launch_bounds__(256) void k_fdct(const EncFrame *__restrict__ fr, c
     const int sy = min((int)(by * 8 + r), real_rows - 1);
     int32_t v[8];
     const Ycc q = ycc_coefs((int)k, bgr != 0);
+    // The level shift (jcdctmgr.c: sample - CENTERJSAMPLE) is folded into each path's last
+    // add, exactly: (s + c - 128 * 2^n) >> n == ((s + c) >> n) - 128 for an arithmetic shift.
     if (ve == 1 && he <= 2) {  // he == 1: full-resolution line; he == 2: h2v1_downsample
-      if (he == 1) rows_acc<1, 1>(img, g.w, g.h, (int)bx * 8, sy, q, v);
+      if (he == 1) rows_acc<1, 1>(img, g.w, g.h, (int)bx * 8, sy, Ycc{q.a0, q.a1, q.a2, q.bias - (128 << 16)}, v);
       else rows_acc<2, 1>(img, g.w, g.h, (int)bx * 16, sy, q, v);
       if (he == 2) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = (v[j] + (j & 1)) >> 1;
+        for (int j = 0; j < 8; ++j) v[j] = (v[j] + (j & 1) - 256) >> 1;
       }
     } else if (he == 2 && ve == 2) {  // h2v2_downsample
       rows_acc<2, 2>(img, g.w, g.h, (int)bx * 16, 2 * sy, q, v);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = (v[j] + 1 + (j & 1)) >> 2;
+      for (int j = 0; j < 8; ++j) v[j] = (v[j] + 1 + (j & 1) - 512) >> 2;
     } else {
       const int ro = bgr ? 2 : 0, bo = 2 - ro;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = enc_sample(g, img, (int)k, (int)(bx * 8 + j), sy, ro, bo);
+      for (int j = 0; j < 8; ++j) v[j] = enc_sample(g, img, (int)k, (int)(bx * 8 + j), sy, ro, bo) - 128;
     }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] -= 128;
     if (fastdct) fdct_ifast_line(v);
     else fdct_islow_line(v, 0);
 #pragma unroll
