@@ -156,6 +156,81 @@ def pmc_traffic(args, device=0):
                            "correction": "bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024"}
 
 
+# kernels of each stage of the fused JPEG pass (vf_jpeg_host.hip run_decode / run_encode; the
+# speculative sync at 1080p), for the per-stage issue fractions
+JPEG_STAGE_KERNELS = {
+    "unstuff": ("k_unstuff_count", "k_unstuff_write"),
+    "huffman_sync": ("k_spec", "k_wglink", "k_resolve", "k_finalize", "k_sync"),
+    "huffman_write": ("k_write", "k_write4"),
+    "dc_idct": ("k_idct",),
+    "color_invert": ("k_color",),
+    "fdct_huffman": ("k_fdct", "k_len", "k_zero_stream", "k_pack"),
+    "stuffing": ("k_ff_count", "k_ff_write", "k_compact"),
+}
+
+
+def pmc_jpeg(device=0):
+    """One per-dispatch rocprofv3 PMC pass over the 1080p JPEG batch (tools/jpeg_bench.py, the
+    jpeg_mode workload: 32 frames of the 8 camera-like scenes, q85 4:2:2), run as a child
+    before anything in this process touches the GPU.  Per kernel, from its last dispatch:
+    VALU / LDS / SALU instructions and waves, and the shader clock (tools/pmc_issue.py).
+    Returns {kernel: {...}} or {"error": why}."""
+    rp = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(rp):
+        return {"error": "rocprofv3 not found"}
+    out = tempfile.mkdtemp(prefix="vf_pmcj_", dir=os.environ.get("TMPDIR", "/tmp"))
+    cmd = ["timeout", "-s", "KILL", "120", rp, "--kernel-trace", "--pmc", "SQ_WAVES", "SQ_INSTS_VALU",
+           "SQ_INSTS_LDS", "SQ_INSTS_SALU", "SQ_BUSY_CYCLES", "GRBM_GUI_ACTIVE", "GRBM_COUNT",
+           "--output-format", "csv", "-d", out, "-o", "pmc", "--", sys.executable,
+           os.path.join(ROOT, "tools", "jpeg_bench.py"), "--sizes", "1080p", "--batch", "32", "--iters", "3",
+           "--cpu-seconds", "0"]
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, env=dict(os.environ, VF_DEVICE=str(device)),
+                           timeout=240)
+        files = glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True)
+        if r.returncode != 0 or not files:
+            return {"error": f"rocprofv3 --pmc failed (rc={r.returncode}): {r.stderr[-300:]}"}
+        import importlib.util
+        spec = importlib.util.spec_from_file_location("pmc_issue", os.path.join(ROOT, "tools", "pmc_issue.py"))
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        return mod.per_kernel(files[0], min_waves=1)
+    except Exception as e:  # reported in the line, never raised
+        return {"error": repr(e)[:300]}
+    finally:
+        shutil.rmtree(out, ignore_errors=True)
+
+
+def jpeg_issue_fractions(roofline, per_kernel):
+    """Per stage of jpeg_mode.roofline: the VALU and LDS issue fractions -- the compute-side
+    bound beside the HBM fraction.  valu_issue_frac = the stage's VALU instructions x 2 cycles
+    (a wave64 instruction holds a SIMD-32 for two) / (1,024 SIMDs x the stage's hipEvent time
+    x the shader clock); lds_issue_frac = its LDS instructions / (256 CUs x the same cycles),
+    one LDS instruction per CU and cycle at best (b64 / b128 accesses take more, so a lower
+    bound).  Instruction counts: pmc_jpeg's pass over the same workload."""
+    if not per_kernel or "error" in per_kernel:
+        return
+    clocks = sorted(v["clock_GHz"] for v in per_kernel.values() if v.get("duration_us", 0) > 50)
+    clk = clocks[len(clocks) // 2] if clocks else 2.4
+    for stage, kernels in JPEG_STAGE_KERNELS.items():
+        st = roofline.get(stage)
+        if not st:
+            continue
+        valu = sum(per_kernel[k]["valu_total"] for k in kernels if k in per_kernel)
+        lds = sum(per_kernel[k]["lds_total"] for k in kernels if k in per_kernel)
+        cyc = st["ms"] * 1e-3 * clk * 1e9
+        st["valu_issue_frac"] = round(2.0 * valu / (1024 * cyc), 3)
+        st["lds_issue_frac"] = round(lds / (256 * cyc), 3)
+        st["kernels"] = {k: {x: per_kernel[k][x] for x in ("duration_us", "valu_per_wave", "lds_per_wave",
+                                                             "valu_issue_frac", "lds_issue_frac") if x in per_kernel[k]}
+                         for k in kernels if k in per_kernel}
+    roofline["issue_fraction_note"] = (
+        f"valu_issue_frac = VALU instructions x 2 / (1024 SIMDs x stage cycles), lds_issue_frac = LDS "
+        f"instructions / (256 CUs x stage cycles); instruction counts per kernel from a rocprofv3 PMC pass "
+        f"(SQ_INSTS_VALU / SQ_INSTS_LDS, last dispatch) over the same 1080p batch, shader clock "
+        f"{clk:.2f} GHz (GRBM_GUI_ACTIVE / duration, median of the kernels above 50 us)")
+
+
 # ---------------------------------------------------------------------------------------
 # CPU baseline: the oracle's restatement of inverter.py:41 on the host
 # ---------------------------------------------------------------------------------------
@@ -714,10 +789,15 @@ def main():
     # PMC passes run before ANY rank touches a GPU: rank 0's profiler child owns rank 0's GPU
     # (the others wait on a host-only barrier, so nothing else runs on the card being counted)
     traffic, traffic_detail = None, "skipped"
+    jpeg_pmc = None
     if rank == 0 and not args.no_traffic:
         t0 = time.time()
         traffic, traffic_detail = pmc_traffic(args, device)
         log(f"pmc traffic: {traffic} ({traffic_detail}) in {time.time() - t0:.1f}s")
+        if not args.no_jpeg:
+            t0 = time.time()
+            jpeg_pmc = pmc_jpeg(device)
+            log(f"pmc jpeg: {len(jpeg_pmc)} kernels in {time.time() - t0:.1f}s")
     if world > 1:
         dist.barrier(group=cpu_group)
     have_gpu = torch.cuda.is_available()
@@ -781,6 +861,8 @@ def main():
     jpeg = None
     if rank == 0 and not args.no_jpeg:
         jpeg = run_jpeg_child(device, args.batch, args.cpu_seconds)
+        if isinstance(jpeg.get("roofline"), dict):
+            jpeg_issue_fractions(jpeg["roofline"], jpeg_pmc)
         log(f"jpeg mode: {jpeg}")
     if rank == 0 and args.cpu_seconds > 0:
         # after every timed region (the other ranks wait at the distributor leg's barrier); at

@@ -30,14 +30,13 @@ def short(name):
     return re.sub(r"\(.*", "", name.replace("(anonymous namespace)::", "")).split("::")[-1]
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("counters")
-    ap.add_argument("--durations", default="")
-    ap.add_argument("--min-waves", type=int, default=1000)
-    a = ap.parse_args()
-    disp = defaultdict(dict)  # dispatch id -> {counter: value, _name, _dur}
-    for r in csv.DictReader(open(a.counters)):
+def per_kernel(counters_csv, durations_csv="", min_waves=1000):
+    """{kernel: counts and fractions} from a counter_collection.csv (see the module docstring);
+    bench.py's jpeg leg uses it.  Short kernels' clock estimates are unreliable (the GRBM
+    window is wider than the dispatch), so their fractions use the median clock of the kernels
+    above 50 us."""
+    disp = defaultdict(dict)
+    for r in csv.DictReader(open(counters_csv)):
         d = disp[int(r["Dispatch_Id"])]
         d["_name"] = short(r["Kernel_Name"])
         d["_dur_ns"] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
@@ -46,29 +45,39 @@ def main():
     for i in sorted(disp):
         last[disp[i]["_name"]] = disp[i]
     stats = {}
-    if a.durations:
-        for r in csv.DictReader(open(a.durations)):
+    if durations_csv:
+        for r in csv.DictReader(open(durations_csv)):
             stats[short(r["Name"])] = float(r["AverageNs"])
+    clk_of = {n: (d.get("GRBM_GUI_ACTIVE", 0.0) / XCDS / d["_dur_ns"] if d["_dur_ns"] else 0.0) for n, d in last.items()}
+    longs = sorted(c for n, c in clk_of.items() if last[n]["_dur_ns"] > 50_000 and c > 0)
+    clk_med = longs[len(longs) // 2] if longs else 2.4
     out = {}
     for name, d in last.items():
         waves = d.get("SQ_WAVES", 0.0)
-        if waves < a.min_waves:
+        if waves < min_waves:
             continue
         dur = stats.get(name, d["_dur_ns"])
-        clk = d.get("GRBM_GUI_ACTIVE", 0.0) / XCDS / d["_dur_ns"] if d["_dur_ns"] else 0.0
+        clk = clk_of[name] if d["_dur_ns"] > 50_000 else clk_med
         cyc = dur * clk
         r = {"waves": int(waves), "duration_us": round(dur / 1e3, 2), "clock_GHz": round(clk, 3),
+             "valu_total": d.get("SQ_INSTS_VALU", 0.0), "lds_total": d.get("SQ_INSTS_LDS", 0.0),
              "valu_per_wave": round(d.get("SQ_INSTS_VALU", 0) / waves, 1),
              "lds_per_wave": round(d.get("SQ_INSTS_LDS", 0) / waves, 1),
-             "salu_per_wave": round(d.get("SQ_INSTS_SALU", 0) / waves, 1),
-             "vmem_rd_per_wave": round(d.get("SQ_INSTS_VMEM_RD", 0) / waves, 1),
-             "vmem_wr_per_wave": round(d.get("SQ_INSTS_VMEM_WR", 0) / waves, 1)}
+             "salu_per_wave": round(d.get("SQ_INSTS_SALU", 0) / waves, 1)}
         if cyc > 0:
             r["valu_issue_frac"] = round(2.0 * d.get("SQ_INSTS_VALU", 0) / (SIMDS * cyc), 3)
             r["lds_issue_frac"] = round(d.get("SQ_INSTS_LDS", 0) / (CUS * cyc), 3)
-        if "SQ_BUSY_CYCLES" in d and cyc > 0:
-            r["sq_busy_frac"] = round(d["SQ_BUSY_CYCLES"] / (32 * cyc), 3)  # 32 shader engines
         out[name] = r
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("counters")
+    ap.add_argument("--durations", default="")
+    ap.add_argument("--min-waves", type=int, default=1000)
+    a = ap.parse_args()
+    out = per_kernel(a.counters, a.durations, a.min_waves)
     print(json.dumps(out, indent=1))
 
 
