@@ -335,7 +335,8 @@ int Codec::prepare_decode(const uint8_t *const *jpegs, const size_t *sizes, int 
         wgs += S.nwg;
         trs += (uint64_t)S.nwg * 256;
         dmax_wg_ = std::max(dmax_wg_, S.nwg);
-        if (S.nwg > 4096) spec_ok_ = false;  // k_resolve stages at most 4096 workgroups per segment
+        // k_resolve stages at most 4096 workgroups and 16384 (workgroup, entry) transitions per segment
+        if (S.nwg > 4096 || (uint64_t)S.nwg * (uint64_t)F.g.bpm > 16384) spec_ok_ = false;
       }
       S.us_off = us_off;
       in_off += align_up(len, 16);

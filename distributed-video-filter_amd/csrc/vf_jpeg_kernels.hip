@@ -905,15 +905,19 @@ __global__ __launch_bounds__(256) void k_wglink(const DecSeg *__restrict__ sg, c
 
 // The true path across the workgroups of a frame (one workgroup per frame).  Per workgroup w
 // it finds the walk column e* that is the path from subsequence kj + 1 on; subsequences
-// 0..kj take prefix records (exit state, count) from pX or qX at lane rL & 15.  The common
-// case is two nibble lookups in LDS (the boundary link from the trajectory ending w-1 rejoined
-// trajectory e* of w's first subsequence); where it did not, or the column ending w-1 was in
-// an explicit state, the trace k_wglink ran for that state is taken.  Lane 0 decodes only
-// where none was run (the continuation of a trace that crossed a whole workgroup, or an
-// explicit walk with bpm > 8), into pX lane 0.
+// 0..kj take prefix records (exit state, count) from pX or qX at lane rL & 15.  Where the
+// path enters w depends only on the walk column e it followed through w - 1: the boundary link
+// from that column's last trajectory rejoined trajectory e* of w's first subsequence, or it
+// missed, or the column ended explicit -- and for both misses k_wglink has already traced the
+// state on.  So every workgroup's transition e -> (e*, kj, where the records are) is made in
+// parallel first (one thread per workgroup, into LDS), and the serial walk across the frame
+// is one LDS read per workgroup.  Lane 0 decodes only where no trace was run (the path
+// crossed a whole workgroup in a trace, or an explicit walk with bpm > 8), into pX lane 0.
+constexpr uint32_t kResolveT = 16384;  // transitions staged per frame (workgroups x bpm)
+constexpr uint32_t kTrSerial = 1u << 20;
 __global__ __launch_bounds__(256) void k_resolve(const DecSeg *__restrict__ sg, const DecFrame *__restrict__ fr, const uint8_t *us, const uint32_t *us_len,
                                                  SpecBufs B, uint32_t *unresolved) {
-  __shared__ uint64_t sF[kResolveLds], sB[kResolveLds];
+  __shared__ uint32_t sT[kResolveT];  // [w * bpm + e]: e* | kj << 4 | code << 12 | kTrSerial
   __shared__ uint8_t sE[kResolveLds], sK[kResolveLds], sJ[kResolveLds];
   __shared__ HuffSync tabs[6];
   __shared__ uint32_t s_tw[kTraceWords];
@@ -923,20 +927,41 @@ __global__ __launch_bounds__(256) void k_resolve(const DecSeg *__restrict__ sg, 
   const uint32_t bpm = hg.bpm, L = spec_lanes(bpm), NS = 256 / L;
   const uint32_t nbits = us_len[blockIdx.x] * 8u, nsub = (nbits + kSubBits - 1) / kSubBits;
   const uint32_t nwg = min(S.nwg, (nsub + NS - 1) / NS);
-  if (nwg > kResolveLds) {
+  if (nwg > kResolveLds || nwg * bpm > kResolveT) {
     if (threadIdx.x == 0) atomicOr(unresolved, 1u);
     return;
   }
-  load_sync_tables(F, tabs);
-  for (uint32_t i = threadIdx.x; i < nwg; i += 256) {
-    uint64_t fr_ = 0, br_ = 0;
-    const uint64_t row = (uint64_t)(S.wg0 + i) * kSpecLanesMax;
+  const uint32_t lastk = NS - 1;  // every workgroup but the frame's last is full
+  // the sync tables' copy is issued with the transition loads; one barrier publishes both
+  {
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(&F.sdc[0]);
+    uint32_t *dst = reinterpret_cast<uint32_t *>(tabs);
+    for (uint32_t j = threadIdx.x; j < 6 * sizeof(HuffSync) / 4; j += 256) dst[j] = src[j];
+  }
+  for (uint32_t w = threadIdx.x + 1; w < nwg; w += 256) {
+    const uint64_t rowp = (uint64_t)(S.wg0 + w - 1) * kSpecLanesMax, row = rowp + kSpecLanesMax;
+    const uint4 f4 = *reinterpret_cast<const uint4 *>(B.wF + rowp);
+    const uint4 b4 = *reinterpret_cast<const uint4 *>(B.wB + row);
+    const uint32_t fw[4] = {f4.x, f4.y, f4.z, f4.w}, bw[4] = {b4.x, b4.y, b4.z, b4.w};
     for (uint32_t e = 0; e < bpm; ++e) {
-      fr_ |= (uint64_t)(B.wF[row + e] & 0xF) << (4 * e);
-      if (i > 0) br_ |= (uint64_t)(B.wB[row + e] & 0xF) << (4 * e);
+      const uint32_t jl = (fw[e >> 2] >> (8 * (e & 3))) & 0xF;
+      uint32_t tr = kTrSerial;
+      if (jl < bpm) {
+        const uint32_t jb = (bw[jl >> 2] >> (8 * (jl & 3))) & 0xF;
+        if (jb < bpm || jb == kLinkLast) {  // rejoined (or the frame's last subsequence)
+          tr = (jb < bpm ? jb : 0u) | ((jl | (jb < bpm ? 0u : 0x20u)) << 12);
+        } else {  // the link missed: its trace
+          const uint32_t te = B.wTE[row + jl], tk = B.wTK[row + jl];
+          if (te != kNotTraced)
+            tr = te < bpm ? te | (tk << 4) | ((kRecP | jl) << 12) : (lastk << 4) | ((kRecP | jl) << 12);
+        }
+      } else if (bpm <= 8) {  // walk column e ended explicit in w - 1: its trace
+        const uint32_t te = B.wQE[row + e], tk = B.wQK[row + e];
+        if (te != kNotTraced)
+          tr = te < bpm ? te | (tk << 4) | ((kRecQ | e) << 12) : (lastk << 4) | ((kRecQ | e) << 12);
+      }
+      sT[w * bpm + e] = tr;
     }
-    sF[i] = fr_;
-    sB[i] = br_;
   }
   __syncthreads();
   auto slot = [&](uint32_t w, uint32_t k, uint32_t lane) { return S.tr0 + (uint64_t)w * 256 + k * L + lane; };
@@ -951,45 +976,25 @@ __global__ __launch_bounds__(256) void k_resolve(const DecSeg *__restrict__ sg, 
     uint32_t e = 0, kj = 0;
     uint8_t rec = kRecP;  // where workgroup w-1's prefix records are
     for (uint32_t w = 1; w < nwg; ++w) {
-      const uint32_t lastk = NS - 1;  // workgroup w-1 is full (only the frame's last one is not)
-      const uint64_t row = (uint64_t)(S.wg0 + w) * kSpecLanesMax;
-      uint32_t jl = kLinkNone, te = kNotTraced, tk = 0;
-      uint8_t code = kRecP;
-      if (kj < lastk) jl = nib(sF[w - 1], e);
-      if (jl < bpm) {
-        const uint32_t jb = nib(sB[w], jl);
-        if (jb < bpm || jb == kLinkLast) {  // rejoined (or the frame's last subsequence)
-          sE[w] = (uint8_t)(jb < bpm ? jb : 0);
-          sK[w] = 0;
-          sJ[w] = (uint8_t)jl;
-          e = jb < bpm ? jb : 0;
-          kj = 0;
-          rec = kRecP;
+      if (kj < lastk) {
+        const uint32_t tr = sT[w * bpm + e];
+        if (!(tr & kTrSerial)) {
+          const uint8_t code = (uint8_t)(tr >> 12);
+          e = tr & 0xF;
+          kj = (tr >> 4) & 0xFF;
+          sE[w] = (uint8_t)e;
+          sK[w] = (uint8_t)kj;
+          sJ[w] = code;
+          rec = code < kRecP ? kRecP : code;
           continue;
         }
-        te = B.wTE[row + jl];  // the boundary link missed: its trace
-        tk = B.wTK[row + jl];
-        code = (uint8_t)(kRecP | jl);
-      } else if (kj < lastk) {
-        te = B.wQE[row + e];  // walk column e ended explicit in w-1: its trace (bpm <= 8)
-        tk = B.wQK[row + e];
-        code = (uint8_t)(kRecQ | e);
-        if (bpm > 8) te = kNotTraced;
       }
-      if (te != kNotTraced) {
-        const bool found = te < bpm;
-        sE[w] = (uint8_t)(found ? te : 0);
-        sK[w] = (uint8_t)(found ? tk : NS - 1);
-        sJ[w] = code;
-        e = found ? te : 0;
-        kj = found ? tk : NS - 1;
-        rec = code;
-        continue;
-      }
-      // no precomputed trace: decode on serially (records into pX lane 0)
+      // no precomputed transition: decode on serially (records into pX lane 0)
+      const uint64_t row = (uint64_t)(S.wg0 + w) * kSpecLanesMax;
+      const uint32_t jl = kj < lastk ? B.wF[row - kSpecLanesMax + e] & 0xF : kLinkNone;
       uint64_t X;
       uint32_t k = 0;
-      if (jl < bpm) {  // cannot happen (k_wglink traces every missed link); kept for safety
+      if (jl < bpm) {  // cannot happen (every missed link is traced in k_wglink); kept for safety
         X = B.wBX[row + jl];
         B.pX[slot(w, 0, 0)] = X;
         B.pC[slot(w, 0, 0)] = B.wBC[row + jl];
@@ -1000,15 +1005,16 @@ __global__ __launch_bounds__(256) void k_resolve(const DecSeg *__restrict__ sg, 
         X = ((rec & 0x40) ? B.qX : B.pX)[slot(w - 1, lastk, rec & 15)];
       }
       uint32_t kf = 0;
-      te = k < NS && w * NS + k < nsub
-               ? trace_on(gw, fwords, s_tw, X, w, k, NS, L, nsub, nbits, S.tr0, hg, tabs, B.tX, B.pX, B.pC, 0, &kf)
-               : kLinkNone;
+      const uint32_t te = k < NS && w * NS + k < nsub
+                              ? trace_on(gw, fwords, s_tw, X, w, k, NS, L, nsub, nbits, S.tr0, hg, tabs, B.tX, B.pX,
+                                         B.pC, 0, &kf)
+                              : kLinkNone;
       const bool found = te < bpm;
       sE[w] = (uint8_t)(found ? te : 0);
-      sK[w] = (uint8_t)(found ? kf : NS - 1);
+      sK[w] = (uint8_t)(found ? kf : lastk);
       sJ[w] = kRecP;
       e = found ? te : 0;
-      kj = found ? kf : NS - 1;
+      kj = found ? kf : lastk;
       rec = kRecP;
     }
   }
@@ -1018,8 +1024,8 @@ __global__ __launch_bounds__(256) void k_resolve(const DecSeg *__restrict__ sg, 
     B.rK[S.wg0 + w] = sK[w];
     const uint8_t code = sJ[w];
     if (code < kRecP) {  // rejoined at the boundary: prefix record of subsequence 0, into pX lane 0
-      const uint64_t wb = (uint64_t)(S.wg0 + w) * kSpecLanesMax + code;
-      B.pX[slot(w, 0, 0)] = sK[w] == 0 && nib(sB[w], code) < bpm ? B.tE[slot(w, 0, sE[w])] : B.wBX[wb];
+      const uint64_t wb = (uint64_t)(S.wg0 + w) * kSpecLanesMax + (code & 15);
+      B.pX[slot(w, 0, 0)] = (code & 0x20) ? B.wBX[wb] : B.tE[slot(w, 0, sE[w])];
       B.pC[slot(w, 0, 0)] = B.wBC[wb];
       B.rL[S.wg0 + w] = kRecP;
     } else {
