@@ -1901,8 +1901,8 @@ __global__ __launch_bounds__(256) void k_fdct(const EncFrame *__restrict__ fr, c
                            (uint32_t)(uint16_t)tab->shift[t][i] | ((uint32_t)kZig[i] << 16));
   }
   for (int i = threadIdx.x; i < 512; i += 256) s_ac[i >> 8][i & 255] = tab->ac[i >> 8][i & 255];
-  for (int i = threadIdx.x; i < 32 * (int)kAcWords; i += 256) (&acw[0][0])[i] = 0;
   const uint32_t slot = threadIdx.x >> 3, r = threadIdx.x & 7, lm = slot & (kFdctGroup - 1);
+  for (uint32_t i = r; i < kAcWords; i += 8) acw[slot][i] = 0;  // the block's own lanes: wave-local
   const uint32_t unit = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t grp = unit / bpm, c = unit - grp * bpm;  // scalar
   const uint32_t mcu = grp * kFdctGroup + lm;
@@ -1961,7 +1961,12 @@ __global__ __launch_bounds__(256) void k_fdct(const EncFrame *__restrict__ fr, c
       qo[slot][qo_at(slot, q.y >> 16)] = quantize(v[i], q.x & 0xFFFF, q.x >> 16, (int32_t)(int16_t)(q.y & 0xFFFF));
     }
   }
-  __syncthreads();
+  // From here on a block's 8 lanes read only their own slot's LDS (qo, ws, acw), written by
+  // lanes of the same wave: LDS operations of a wave complete in order, so a wavefront fence
+  // (ordering for the compiler) replaces the workgroup barriers -- the 4 waves of a workgroup
+  // code different components (luma waves finish pass 1 sooner than chroma waves) and no
+  // longer wait for one another.
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   // AC Huffman coding; every lane of the wave takes part in the 8-lane shuffles
   int vz[8];
   {
@@ -2030,7 +2035,7 @@ __global__ __launch_bounds__(256) void k_fdct(const EncFrame *__restrict__ fr, c
     out.finish();
   }
   const uint32_t total = off + (eob ? (eobc & 0xFF) : 0u);
-  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // the block's AC words, from its own lanes
   if (real) {
     const uint64_t gb = F.blk0 + b;
     const uint32_t nw = (total + 31) >> 5;

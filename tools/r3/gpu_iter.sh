@@ -26,11 +26,11 @@ for n in ("k_fdct", "k_idct", "k_color", "k_spec", "k_wglink", "k_resolve"):
     d = st.get(n, {})
     print(f"{n:12s} head {d.get('head', 0):8.1f}  new {d.get('new', 0):8.1f} us")
 PY
-for mode in auto spec; do
+for mode in auto; do
   VF_JPEG_SYNC=$mode timeout -k 10 200 python3 -u tools/jpeg_bench.py --sizes 1080p --batch 32 --iters 5 --cpu-seconds 0 --content hard > gpurun_out/it_hard_$mode.jsonl 2> gpurun_out/it_hard_$mode.log || { echo HARD_FAILED $mode; tail -20 gpurun_out/it_hard_$mode.log; exit 1; }
   python3 -c "import json; d=json.loads(open('gpurun_out/it_hard_$mode.jsonl').read().splitlines()[-1]); print('hard', '$mode', d['gpu_resident_fps'], d['parity_vs_oracle'], d['stages_ms'])"
 done
-for np_ in 3 6 12; do
+for np_ in 1 2 3; do
   VF_STAGE_PIECES=$np_ timeout -k 10 120 python -u tools/per_frame_probe.py > gpurun_out/it_pf_$np_.jsonl 2> gpurun_out/it_pf_$np_.log || { echo PF_FAILED; tail -20 gpurun_out/it_pf_$np_.log; exit 1; }
   python3 -c "
 import json
