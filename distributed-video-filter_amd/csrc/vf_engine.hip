@@ -375,7 +375,7 @@ hipError_t Engine::ensure_staging() {
 
 // A small synchronous job with a side outside the mapped ranges (a pageable frame: the
 // drop-in's own shape, vfilter.bitwise_not(frame) for cv2.bitwise_not(frame), inverter.py:41)
-// on the calling thread.  The job is cut into ~6 pieces; an unmapped source is copied into the
+// on the calling thread.  The job is cut into pieces (below); an unmapped source is copied into the
 // mapped staging input by the copy pool's workers -- woken once, they copy the pieces in order,
 // each worker a 1/n share of each piece, and count every piece as it lands -- while this
 // thread launches invert_mapped_kernel on each piece as soon as it is complete, so the copy of
@@ -398,9 +398,13 @@ bool Engine::run_staged(const std::vector<Seg> &segs, size_t total, JobResult *o
     uint8_t *dd;          // device address of the destination (mapped, or the staging output)
     bool stage_in, stage_out;
   };
-  static const size_t kPieces = std::max<size_t>(1, env_or("VF_STAGE_PIECES", 6));
-  static const size_t kMinPiece = env_or("VF_STAGE_MIN_PIECE", (size_t)256 << 10);
-  const size_t piece = std::max<size_t>(kMinPiece, (total / kPieces + 65535) & ~(size_t)65535);
+  // Pieces: a hot frame's copy runs at ~250 GB/s on the pool (6.2 MB in ~25 us) while each
+  // extra launch over PCIe costs more than the overlap gains, so a frame up to 8 MiB is one
+  // piece (1080p: 0.223 ms per call at 1 piece, 0.235 at 2, 0.240 at 3, 0.267 at 6;
+  // profiles/r03_per_frame_pieces.txt); larger jobs take 3.  VF_STAGE_PIECES overrides.
+  static const size_t kPieces = env_or("VF_STAGE_PIECES", 0);
+  const size_t npieces = kPieces ? kPieces : total <= ((size_t)8 << 20) ? 1 : 3;
+  const size_t piece = std::max<size_t>((size_t)256 << 10, (total / npieces + 65535) & ~(size_t)65535);
   std::vector<P> ps;
   size_t at = 0;
   bool any_in = false, any_out = false;
