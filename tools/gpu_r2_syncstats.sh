@@ -1,4 +1,4 @@
-# k_spec / k_resolve phase counters (tools/libv_stats.so: tools/build_stats_lib.sh, the sync_stats.patch build) at 480p and
+# k_spec phase counters (tools/libv_stats.so: tools/build_stats_lib.sh, the sync_stats.patch build; round 3 dropped the k_resolve ones: its serial walk is one LDS read per workgroup now) at 480p and
 # 1080p, plus the custom-table JPEG GPU test on the in-tree library
 set -o pipefail
 mkdir -p gpurun_out
