@@ -1919,55 +1919,6 @@ __global__ __launch_bounds__(256) void k_fdct(const EncFrame *__restrict__ fr, c
     real = mcu < nmcu && bx < (uint32_t)g.wb[k] && by < (uint32_t)g.hb[k];  // dummy blocks: k_len / k_pack
   }
   const uint8_t *img = pix + F.img_off;
-  // 4:2:2 with full-size luma (TJSAMP_422, the PyTurboJPEG default and the bench's workload):
-  // a workgroup is one MCU group with all four blocks of each MCU (Y0, Y1, Cb, Cr), so each
-  // pixel is loaded ONCE: lane t converts 4 pixels of one MCU row (all three components, the
-  // chroma pairs downsampled) and stages the samples in ws; after the barrier each block's
-  // lanes run the row pass in place.  The per-component path below loads every pixel three
-  // times (once per component's wave): ~80 of 270 us of k_fdct at 1080p x 32 were pixel loads
-  // and colour (round 3, timing ablation).
-  const bool joint = bpm == 4 && g.he[0] == 1 && g.ve[0] == 1 && g.he[1] == 2 && g.ve[1] == 1 && g.he[2] == 2 &&
-                     g.ve[2] == 1 && g.bcomp[2] == 1 && g.bcomp[3] == 2;
-  if (joint) {
-    const uint32_t tj = threadIdx.x, jl = tj >> 5, rr = (tj >> 2) & 7, qd = tj & 3;
-    const uint32_t jm = grp * kFdctGroup + jl, mcux = (uint32_t)g.mcux;
-    uint32_t mx = (grp * kFdctGroup) % mcux + jl, my = (grp * kFdctGroup) / mcux;
-    while (mx >= mcux) mx -= mcux, ++my;
-    if (grp < ngroups && jm < nmcu) {
-      const int w = g.w, py = min((int)(my * 8 + rr), g.h - 1), px = (int)mx * 16 + 4 * (int)qd;
-      const uint8_t *row = img + (size_t)py * w * 3;
-      uint32_t c[4][3];  // the 4 pixels' bytes in memory order
-      if (px + 4 <= w && ((reinterpret_cast<uintptr_t>(row) + (uintptr_t)px * 3) & 3) == 0) {
-        const uint32_t *s32 = reinterpret_cast<const uint32_t *>(row + (size_t)px * 3);
-        const uint32_t d0 = s32[0], d1 = s32[1], d2 = s32[2];
-        const uint32_t wd[3] = {d0, d1, d2};
-#pragma unroll
-        for (int x = 0; x < 4; ++x)
-#pragma unroll
-          for (int ch = 0; ch < 3; ++ch) c[x][ch] = (wd[(3 * x + ch) / 4] >> (8 * ((3 * x + ch) % 4))) & 0xFF;
-      } else {
-#pragma unroll
-        for (int x = 0; x < 4; ++x) {
-          const uint8_t *pp = row + (size_t)min(px + x, w - 1) * 3;
-          c[x][0] = pp[0], c[x][1] = pp[1], c[x][2] = pp[2];
-        }
-      }
-      const Ycc qy = ycc_coefs(0, bgr != 0), qb = ycc_coefs(1, bgr != 0), qr = ycc_coefs(2, bgr != 0);
-      const Ycc qy0{qy.a0, qy.a1, qy.a2, qy.bias - (128 << 16)};  // level shift folded in
-      const uint32_t ys = (qd < 2 ? 0u : 8u) + jl, yc = (4 * qd) & 7;
-#pragma unroll
-      for (int x = 0; x < 4; ++x) ws[ys][rr][yc + x] = ycc_apply(qy0, (int)c[x][0], (int)c[x][1], (int)c[x][2]);
-#pragma unroll
-      for (int m = 0; m < 2; ++m) {  // h2v1_downsample: (a + b + bias) >> 1, bias 0, 1, 0, 1, ...
-        const int cb = ycc_apply(qb, (int)c[2 * m][0], (int)c[2 * m][1], (int)c[2 * m][2]) +
-                       ycc_apply(qb, (int)c[2 * m + 1][0], (int)c[2 * m + 1][1], (int)c[2 * m + 1][2]);
-        const int cr = ycc_apply(qr, (int)c[2 * m][0], (int)c[2 * m][1], (int)c[2 * m][2]) +
-                       ycc_apply(qr, (int)c[2 * m + 1][0], (int)c[2 * m + 1][1], (int)c[2 * m + 1][2]);
-        ws[16 + jl][rr][2 * qd + m] = (cb + m - 256) >> 1;
-        ws[24 + jl][rr][2 * qd + m] = (cr + m - 256) >> 1;
-      }
-    }
-  } else
   if (real) {  // pass 1: row r of the block's samples
     const int he = g.he[k], ve = g.ve[k], real_rows = g.rrows[k];
     const int sy = min((int)(by * 8 + r), real_rows - 1);
@@ -1997,16 +1948,6 @@ __global__ __launch_bounds__(256) void k_fdct(const EncFrame *__restrict__ fr, c
     for (int j = 0; j < 8; ++j) ws[slot][r][j] = v[j];
   }
   __syncthreads();
-  if (joint && real) {  // the row pass over the staged samples, in place (the block's own lanes)
-    int32_t v[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = ws[slot][r][j];
-    if (fastdct) fdct_ifast_line(v);
-    else fdct_islow_line(v, 0);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) ws[slot][r][j] = v[j];
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // pass 2 reads the block's columns
-  }
   const int t = k > 0;
   if (real) {  // pass 2: column r, quantised
     int32_t v[8];
