@@ -78,7 +78,8 @@ hipError_t dec_color(const DecFrame *fr, int n, int max_w, int max_h, const uint
                      int bgr, int invert, hipStream_t s);
 
 hipError_t enc_fdct(const EncFrame *fr, int n, uint32_t max_blocks, const EncTables *tab, const uint8_t *pix,
-                    int16_t *dcq, uint32_t *acbits, uint32_t *acscr, int bgr, int fastdct, hipStream_t s);
+                    int16_t *dcq, uint32_t *acbits, uint32_t *acscr, int bgr, int fastdct, int ch, int cv,
+                    hipStream_t s);  // (ch, cv): chroma downsampling factors
 hipError_t enc_len(const EncFrame *fr, int n, uint32_t max_blocks, const EncTables *tab, const int16_t *dcq,
                    uint32_t *acbits, uint32_t *bits, uint32_t *pre, hipStream_t s);
 hipError_t enc_pack(const EncFrame *fr, int n, uint32_t max_blocks, const uint32_t *pre, const uint32_t *acbits,

@@ -125,10 +125,18 @@ void build_enc_tables(int quality, bool fastdct, EncTables *t) {
       t->shift[tb][i] = (int16_t)(r - 16);
     }
   }
+  for (int tb = 0; tb < 2; ++tb)
+    for (int i = 0; i < 64; ++i) {
+      uint32_t y = (uint32_t)(t->shift[tb][i] + 16);
+      for (uint32_t j = 0; j < 4; ++j) y |= qo_pos(j, kZigOf[i]) << (8 + 6 * j);
+      t->fdct_lds[2 * (64 * tb + i)] = (uint32_t)t->recip[tb][i] | ((uint32_t)t->corr[tb][i] << 16);
+      t->fdct_lds[2 * (64 * tb + i) + 1] = y;
+    }
   code_table(kDcLBits, kDcVals, t->dc[0], 16);
   code_table(kDcCBits, kDcVals, t->dc[1], 16);
   code_table(kAcLBits, kAcLVals, t->ac[0], 256);
   code_table(kAcCBits, kAcCVals, t->ac[1], 256);
+  std::memcpy(t->fdct_lds + 256, t->ac, sizeof t->ac);
 }
 
 // worst case per block: DC 16 + 11 bits, 63 AC codes of 16 + 10 bits
@@ -643,6 +651,7 @@ int Codec::prepare_encode(const int *ws, const int *hs, const uint64_t *img_offs
     emax_tiles_ = std::max(emax_tiles_, F.ntiles_max);
   }
   en_ = n;
+  esub_ = subsamp;
   eblocks_ = blk;
   ebits_bytes_ = bits;
   std::vector<ScanSeg> segs;
@@ -697,7 +706,7 @@ int Codec::run_encode(int bgr, bool fastdct, std::string *err) {
   const int n = en_;
   CK(hipEventRecord(ev_[6], s_));
   CK(enc_fdct(fr, n, emax_blocks_, tab, d_pix_.as<uint8_t>(), d_dcq_.as<int16_t>(), d_acbits_.as<uint32_t>(),
-              d_acscr_.as<uint32_t>(), bgr, fastdct ? 1 : 0, s_));
+              d_acscr_.as<uint32_t>(), bgr, fastdct ? 1 : 0, kSampH[esub_], kSampV[esub_], s_));
   CK(enc_len(fr, n, emax_blocks_, tab, d_dcq_.as<int16_t>(), d_acbits_.as<uint32_t>(), d_bits_.as<uint32_t>(),
              d_pre_.as<uint32_t>(), s_));
   uint32_t *total_bits = d_etotals_.as<uint32_t>();

@@ -1621,36 +1621,6 @@ __global__ __launch_bounds__(256) void k_color(const DecFrame *__restrict__ fr, 
 
 // ---- encoder: colour + downsampling + FDCT + quantisation -----------------------------------
 
-// component k (0 = Y, 1 = Cb, 2 = Cr) of the pixel at (px, py), edges replicated (jccolor.c)
-__device__ __forceinline__ int comp_at(const uint8_t *img, int w, int h, int px, int py, int k, int ro, int bo) {
-  px = px < w ? px : w - 1;
-  py = py < h ? py : h - 1;
-  const uint8_t *p = img + ((size_t)py * w + px) * 3;
-  const int r = p[ro], g = p[1], b = p[bo];
-  if (k == 0) return (19595 * r + 38470 * g + 7471 * b + 32768) >> 16;
-  if (k == 1) return (-11059 * r - 21709 * g + 32768 * b + (128 << 16) + 32767) >> 16;
-  return (32768 * r - 27439 * g - 5329 * b + (128 << 16) + 32767) >> 16;
-}
-
-// sample (sx, sy) of component k's downsampled plane (jcsample.c + jcprepct.c edges)
-__device__ __forceinline__ int enc_sample(const Geom &g, const uint8_t *img, int k, int sx, int sy, int ro,
-                                          int bo) {
-  const int he = g.he[k], ve = g.ve[k], real_rows = g.rrows[k];
-  if (sy > real_rows - 1) sy = real_rows - 1;
-  if (he == 1 && ve == 1) return comp_at(img, g.w, g.h, sx, sy, k, ro, bo);
-  if (he == 2 && ve == 1)
-    return (comp_at(img, g.w, g.h, 2 * sx, sy, k, ro, bo) + comp_at(img, g.w, g.h, 2 * sx + 1, sy, k, ro, bo) +
-            (sx & 1)) >> 1;
-  if (he == 2 && ve == 2)
-    return (comp_at(img, g.w, g.h, 2 * sx, 2 * sy, k, ro, bo) + comp_at(img, g.w, g.h, 2 * sx + 1, 2 * sy, k, ro, bo) +
-            comp_at(img, g.w, g.h, 2 * sx, 2 * sy + 1, k, ro, bo) +
-            comp_at(img, g.w, g.h, 2 * sx + 1, 2 * sy + 1, k, ro, bo) + 1 + (sx & 1)) >> 2;
-  int sum = 0;  // int_downsample
-  for (int a = 0; a < ve; ++a)
-    for (int c = 0; c < he; ++c) sum += comp_at(img, g.w, g.h, sx * he + c, sy * ve + a, k, ro, bo);
-  return (sum + he * ve / 2) / (he * ve);
-}
-
 // 24-bit multiplies for the forward DCT.  A 32-bit v_mul_lo_u32 / v_mad_u64_u32 (what `*` on
 // int32 compiles to) issues at a quarter of the VALU rate; v_mul_i32_i24 / v_mad_i32_i24 at the
 // full rate, and they are exact here: the encoder's samples are 8-bit, so pass 1's multiplicands
@@ -1719,11 +1689,13 @@ __device__ __forceinline__ void fdct_ifast_line(int32_t p[8]) {
 // the magnitude scaled by the reciprocal and the sign put back (two's complement), instead of
 // a divergent if / else that ran both sides in every wave.  |t| + corr <= 2^16 and recip <
 // 2^16, so the unsigned product fits 32 bits as in the C code's UDCTELEM2.
-__device__ __forceinline__ int16_t quantize(int32_t x, uint32_t recip, uint32_t corr, int32_t shift) {
+// `sh` carries shift + 16 (0..31) in its low 5 bits; its upper bits are ignored, as the
+// hardware's shift does, so the table word that holds it serves other fields too.
+__device__ __forceinline__ int16_t quantize(int32_t x, uint32_t recip, uint32_t corr, uint32_t sh) {
   const int32_t t = (int16_t)x;
   const int32_t sg = t >> 31;
   const uint32_t a = (uint32_t)((t ^ sg) - sg);
-  const uint32_t p = ((a + corr) * recip) >> (shift + 16);
+  const uint32_t p = ((a + corr) * recip) >> (sh & 31);
   return (int16_t)(((int32_t)p ^ sg) - sg);
 }
 
@@ -1750,37 +1722,50 @@ __device__ __forceinline__ int ycc_apply(const Ycc &q, int c0, int c1, int c2) {
   return (q.a0 * c0 + q.a1 * c1 + q.a2 * c2 + q.bias) >> 16;
 }
 
-// One component of the 8 * H pixels of rows py .. py + R - 1 from px, summed over groups of H
-// pixels and over the R rows into v[0..7] (R = 2: h2v2).  Edges replicated (jccolor.c on
-// expand_right_edge / expand_bottom_edge input).  Inside the image every row's words are
-// loaded before any is converted, so a lane waits for memory once, not once per 4 pixels.
+// The 8 * H pixels of rows py .. py + R - 1 from px that one lane converts, edges replicated
+// (jccolor.c on expand_right_edge / expand_bottom_edge input).  Loading and converting are
+// split, so a wave issues its pixel loads before it waits on anything else: inside the image
+// every row's words are in flight at once; a lane at the right edge (or on an unaligned row)
+// reads its pixels one by one while converting.
 template <int H, int R>
-__device__ __forceinline__ void rows_acc(const uint8_t *img, int w, int h, int px, int py, const Ycc &q,
-                                         int32_t v[8]) {
+struct RowPix {
+  uint32_t wd[R][6 * H];
   const uint8_t *row[R];
-  bool fast = px + 8 * H <= w;
+  bool fast;
+};
+// The loads are unconditional (a lane with no block, or on the slow path, reads `dummy`, any
+// 16-B aligned 24 * H readable bytes): with no branch around them the wait for the table load
+// issued before them does not have to wait for them too.
+template <int H, int R>
+__device__ __forceinline__ void rows_load(const uint8_t *img, int w, int h, int px, int py, bool real,
+                                          const uint8_t *dummy, RowPix<H, R> &p) {
+  p.fast = real && px + 8 * H <= w;
 #pragma unroll
   for (int y = 0; y < R; ++y) {
-    row[y] = img + (size_t)min(py + y, h - 1) * w * 3;
-    fast = fast && ((reinterpret_cast<uintptr_t>(row[y]) + (uintptr_t)px * 3) & 3) == 0;
+    p.row[y] = img + (size_t)min(py + y, h - 1) * w * 3;
+    p.fast = p.fast && ((reinterpret_cast<uintptr_t>(p.row[y]) + (uintptr_t)px * 3) & 3) == 0;
   }
 #pragma unroll
+  for (int y = 0; y < R; ++y) {
+    const uint32_t *s32 = reinterpret_cast<const uint32_t *>(p.fast ? p.row[y] + (size_t)px * 3 : dummy);
+#pragma unroll
+    for (int i = 0; i < 6 * H; ++i) p.wd[y][i] = s32[i];
+  }
+}
+
+// One component of those pixels, summed over groups of H pixels and over the R rows into v[0..7]
+template <int H, int R>
+__device__ __forceinline__ void rows_conv(const RowPix<H, R> &p, int w, int px, const Ycc &q, int32_t v[8]) {
+#pragma unroll
   for (int j = 0; j < 8; ++j) v[j] = 0;
-  if (fast) {
-    uint32_t wd[R][6 * H];
-#pragma unroll
-    for (int y = 0; y < R; ++y) {
-      const uint32_t *s32 = reinterpret_cast<const uint32_t *>(row[y] + (size_t)px * 3);
-#pragma unroll
-      for (int i = 0; i < 6 * H; ++i) wd[y][i] = s32[i];
-    }
+  if (p.fast) {
 #pragma unroll
     for (int y = 0; y < R; ++y)
 #pragma unroll
       for (int x = 0; x < 8 * H; ++x) {
-        const int c0 = (int)((wd[y][(3 * x) / 4] >> (8 * ((3 * x) % 4))) & 0xFF);
-        const int c1 = (int)((wd[y][(3 * x + 1) / 4] >> (8 * ((3 * x + 1) % 4))) & 0xFF);
-        const int c2 = (int)((wd[y][(3 * x + 2) / 4] >> (8 * ((3 * x + 2) % 4))) & 0xFF);
+        const int c0 = (int)((p.wd[y][(3 * x) / 4] >> (8 * ((3 * x) % 4))) & 0xFF);
+        const int c1 = (int)((p.wd[y][(3 * x + 1) / 4] >> (8 * ((3 * x + 1) % 4))) & 0xFF);
+        const int c2 = (int)((p.wd[y][(3 * x + 2) / 4] >> (8 * ((3 * x + 2) % 4))) & 0xFF);
         v[x / H] += ycc_apply(q, c0, c1, c2);
       }
   } else {
@@ -1788,10 +1773,43 @@ __device__ __forceinline__ void rows_acc(const uint8_t *img, int w, int h, int p
     for (int y = 0; y < R; ++y)
 #pragma unroll
       for (int x = 0; x < 8 * H; ++x) {
-        const uint8_t *p = row[y] + (size_t)min(px + x, w - 1) * 3;
-        v[x / H] += ycc_apply(q, p[0], p[1], p[2]);
+        const uint8_t *b = p.row[y] + (size_t)min(px + x, w - 1) * 3;
+        v[x / H] += ycc_apply(q, b[0], b[1], b[2]);
       }
   }
+}
+
+// Pass 1 for one lane: component q of row sy of its block's samples, downsampled by (H, R)
+// (jcsample.c): (1, 1) fullsize, (2, 1) h2v1 (bias 0, 1 alternating), (2, 2) h2v2 (bias 1, 2),
+// (1, 2) int_downsample over two rows (TJSAMP_440: (sum + 1) / 2), with the level shift
+// (jcdctmgr.c: sample - CENTERJSAMPLE) folded into each path's last add, exactly:
+// (s + c - 128 * 2^n) >> n == ((s + c) >> n) - 128 for an arithmetic shift; then the FDCT's row
+// pass into the block's workspace row.  Between issuing the pixel loads and using them, the
+// lane stores its part of the workgroup's table image (tw, loaded before the pixels) and zeroes
+// its AC words, so the wave waits on the two memory round trips once, not one after the other.
+template <int H, int R, bool FAST>
+__device__ __forceinline__ void fdct_pass1(const uint8_t *img, const Geom &g, int bx, int sy, Ycc q, bool real,
+                                           const uint4 &tw, const uint8_t *dummy, uint4 *s_tab, uint32_t *acw_slot,
+                                           uint32_t r, int32_t *wsrow) {
+  RowPix<H, R> p;
+  const int px = bx * 8 * H;
+  rows_load<H, R>(img, g.w, g.h, px, sy * R, real, dummy, p);
+  if (threadIdx.x < 192) s_tab[threadIdx.x] = tw;
+  for (uint32_t i = r; i < (uint32_t)kAcScratchWords; i += 8) acw_slot[i] = 0;  // the block's own lanes
+  if (!real) return;
+  if (H == 1 && R == 1) q.bias -= 128 << 16;
+  int32_t v[8];
+  rows_conv<H, R>(p, g.w, px, q, v);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    if (H == 2 && R == 1) v[j] = (v[j] + (j & 1) - 256) >> 1;
+    if (H == 2 && R == 2) v[j] = (v[j] + 1 + (j & 1) - 512) >> 2;
+    if (H == 1 && R == 2) v[j] = (v[j] + 1 - 256) >> 1;
+  }
+  if (FAST) fdct_ifast_line(v);
+  else fdct_islow_line(v, 0);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) wsrow[j] = v[j];
 }
 
 constexpr uint32_t kAcWords = kAcScratchWords;
@@ -1849,11 +1867,6 @@ __device__ __forceinline__ uint32_t last8(uint32_t x) {  // swizzle: lane (i & 0
   return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0xF8);
 }
 
-// natural (row-major) index -> zigzag position (inverse of jutils.c jpeg_natural_order)
-__constant__ uint8_t kZig[64] = {0,  1,  5,  6,  14, 15, 27, 28, 2,  4,  7,  13, 16, 26, 29, 42,
-                                 3,  8,  12, 17, 25, 30, 41, 43, 9,  11, 18, 24, 31, 40, 44, 53,
-                                 10, 19, 23, 32, 39, 45, 52, 54, 20, 22, 33, 38, 46, 51, 55, 60,
-                                 21, 34, 37, 47, 50, 56, 59, 61, 35, 36, 48, 49, 57, 58, 62, 63};
 
 // Position of zigzag coefficient zz in a block's row of qo: its 16-B octet (zz / 8, the AC
 // coder's one ds_read_b128 per lane) is XOR-ed with (0, 5, 2, 7)[slot % 4].  The row is 32
@@ -1879,10 +1892,13 @@ __device__ __forceinline__ uint32_t qo_at(uint32_t slot, uint32_t zz) {
 // scan of the round's bit counts, bits ORed into an LDS image of the block's AC stream that is
 // then copied out.
 // Outputs per block: quantised DC, AC bit count, AC bits (MSB-first words).
+// Specialised per batch on the chroma downsampling (CH, CV) and the DCT (islow / ifast): luma
+// is full size in every TurboJPEG subsampling, so each wave's sample path and butterflies are
+// fixed at compile time.
 constexpr uint32_t kFdctGroup = 8;  // MCUs per wave
+template <int CH, int CV, bool FAST>
 __global__ __launch_bounds__(256) void k_fdct(const EncFrame *__restrict__ fr, const EncTables *tab, const uint8_t *pix,
-                                              int16_t *dcq, uint32_t *acbits, uint32_t *acscr, int bgr,
-                                              int fastdct) {
+                                              int16_t *dcq, uint32_t *acbits, uint32_t *acscr, int bgr) {
   const EncFrame &F = fr[blockIdx.y];
   const Geom &g = F.g;
   const uint32_t bpm = (uint32_t)g.bpm, nmcu = (uint32_t)g.nmcu;
@@ -1891,18 +1907,16 @@ __global__ __launch_bounds__(256) void k_fdct(const EncFrame *__restrict__ fr, c
   __shared__ int32_t ws[32][8][9];
   __shared__ int16_t qo[32][64];
   __shared__ uint32_t acw[32][kAcWords];
-  // quantiser entry of natural position n: {recip | corr << 16, shift | zigzag(n) << 16}, so
-  // pass 2's lane reads one 8-B entry per coefficient (8 lanes: 64 contiguous bytes)
-  __shared__ uint2 s_q[2][64];
-  __shared__ uint32_t s_ac[2][256];
-  if (threadIdx.x < 128) {
-    const int t = threadIdx.x >> 6, i = threadIdx.x & 63;
-    s_q[t][i] = make_uint2((uint32_t)tab->recip[t][i] | ((uint32_t)tab->corr[t][i] << 16),
-                           (uint32_t)(uint16_t)tab->shift[t][i] | ((uint32_t)kZig[i] << 16));
-  }
-  for (int i = threadIdx.x; i < 512; i += 256) s_ac[i >> 8][i & 255] = tab->ac[i >> 8][i & 255];
+  // The table image (EncTables::fdct_lds): s_q[t][n] = {recip | corr << 16, (shift + 16) | qo
+  // position of zigzag(n) for slot % 4 == j at bits 8 + 6j} (pass 2's lane reads one 8-B entry
+  // per coefficient, 8 lanes 64 contiguous bytes, and uses the second word as it is for the
+  // shift and through one bit-field extract for its store address), then s_ac[t][256].  Its
+  // load is issued first; fdct_pass1 stores it after issuing the pixel loads.
+  __shared__ uint4 s_tab[192];
+  const uint4 tw = threadIdx.x < 192 ? reinterpret_cast<const uint4 *>(tab->fdct_lds)[threadIdx.x] : make_uint4(0, 0, 0, 0);
+  const uint2 (*const s_q)[64] = reinterpret_cast<const uint2 (*)[64]>(s_tab);
+  const uint32_t (*const s_ac)[256] = reinterpret_cast<const uint32_t (*)[256]>(reinterpret_cast<const uint32_t *>(s_tab) + 256);
   const uint32_t slot = threadIdx.x >> 3, r = threadIdx.x & 7, lm = slot & (kFdctGroup - 1);
-  for (uint32_t i = r; i < kAcWords; i += 8) acw[slot][i] = 0;  // the block's own lanes: wave-local
   const uint32_t unit = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t grp = unit / bpm, c = unit - grp * bpm;  // scalar
   const uint32_t mcu = grp * kFdctGroup + lm;
@@ -1919,46 +1933,26 @@ __global__ __launch_bounds__(256) void k_fdct(const EncFrame *__restrict__ fr, c
     real = mcu < nmcu && bx < (uint32_t)g.wb[k] && by < (uint32_t)g.hb[k];  // dummy blocks: k_len / k_pack
   }
   const uint8_t *img = pix + F.img_off;
-  if (real) {  // pass 1: row r of the block's samples
-    const int he = g.he[k], ve = g.ve[k], real_rows = g.rrows[k];
-    const int sy = min((int)(by * 8 + r), real_rows - 1);
-    int32_t v[8];
+  const uint8_t *dummy = reinterpret_cast<const uint8_t *>(tab->fdct_lds);  // 3 KB, 16-B aligned
+  {  // pass 1: row r of the block's samples (the component is wave-uniform: luma is full size)
+    const int sy = min((int)(by * 8 + r), (int)g.rrows[k] - 1);
     const Ycc q = ycc_coefs((int)k, bgr != 0);
-    // The level shift (jcdctmgr.c: sample - CENTERJSAMPLE) is folded into each path's last
-    // add, exactly: (s + c - 128 * 2^n) >> n == ((s + c) >> n) - 128 for an arithmetic shift.
-    if (ve == 1 && he <= 2) {  // he == 1: full-resolution line; he == 2: h2v1_downsample
-      if (he == 1) rows_acc<1, 1>(img, g.w, g.h, (int)bx * 8, sy, Ycc{q.a0, q.a1, q.a2, q.bias - (128 << 16)}, v);
-      else rows_acc<2, 1>(img, g.w, g.h, (int)bx * 16, sy, q, v);
-      if (he == 2) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = (v[j] + (j & 1) - 256) >> 1;
-      }
-    } else if (he == 2 && ve == 2) {  // h2v2_downsample
-      rows_acc<2, 2>(img, g.w, g.h, (int)bx * 16, 2 * sy, q, v);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = (v[j] + 1 + (j & 1) - 512) >> 2;
-    } else {
-      const int ro = bgr ? 2 : 0, bo = 2 - ro;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = enc_sample(g, img, (int)k, (int)(bx * 8 + j), sy, ro, bo) - 128;
-    }
-    if (fastdct) fdct_ifast_line(v);
-    else fdct_islow_line(v, 0);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) ws[slot][r][j] = v[j];
+    if (k == 0) fdct_pass1<1, 1, FAST>(img, g, (int)bx, sy, q, real, tw, dummy, s_tab, acw[slot], r, ws[slot][r]);
+    else fdct_pass1<CH, CV, FAST>(img, g, (int)bx, sy, q, real, tw, dummy, s_tab, acw[slot], r, ws[slot][r]);
   }
-  __syncthreads();
+  __syncthreads();  // publishes the table image
   const int t = k > 0;
   if (real) {  // pass 2: column r, quantised
     int32_t v[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) v[i] = ws[slot][i][r];
-    if (fastdct) fdct_ifast_line(v);
+    if (FAST) fdct_ifast_line(v);
     else fdct_islow_line(v, 1);
+    const uint32_t qsel = 8 + 6 * (slot & 3);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const uint2 q = s_q[t][i * 8 + r];
-      qo[slot][qo_at(slot, q.y >> 16)] = quantize(v[i], q.x & 0xFFFF, q.x >> 16, (int32_t)(int16_t)(q.y & 0xFFFF));
+      qo[slot][(q.y >> qsel) & 63] = quantize(v[i], q.x & 0xFFFF, q.x >> 16, q.y);
     }
   }
   // From here on a block's 8 lanes read only their own slot's LDS (qo, ws, acw), written by
@@ -1989,20 +1983,22 @@ __global__ __launch_bounds__(256) void k_fdct(const EncFrame *__restrict__ fr, c
   // the slot's pass-1 workspace (free since pass 2): lane r writes its own at their ranks.
   // Then rounds of 8: in round i lane r codes nonzero 8i + r, so a block costs ceil(nnz / 8)
   // rounds of one code per lane instead of eight coefficient slots per lane (a 1080p q85 frame
-  // averages ~4 nonzero AC coefficients per block).
+  // averages ~4 nonzero AC coefficients per block).  The list is written without branches: a
+  // zero coefficient's entry goes to the lane's own spare word (64 + r; the list uses <= 63).
   const uint32_t cnt = __popc(m8);
   const uint32_t rinc = scan8(cnt, r);
   const uint32_t nnz = last8(rinc);
   uint32_t *const lst = reinterpret_cast<uint32_t *>(&ws[slot][0][0]);
   {
-    uint32_t at = rinc - cnt;
+    uint32_t *wp = lst + (rinc - cnt);
+    uint32_t *const spare = lst + 64 + r;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int kk = 8 * (int)r + j;
-      if ((m8 >> j) & 1) {
-        lst[at++] = ((uint32_t)(kk - prev - 1) << 16) | (uint32_t)(uint16_t)vz[j];
-        prev = kk;
-      }
+      const bool nz = (m8 >> j) & 1;
+      *(nz ? wp : spare) = ((uint32_t)(kk - prev - 1) << 16) | (uint32_t)(uint16_t)vz[j];
+      wp += nz ? 1 : 0;
+      prev = nz ? kk : prev;
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // the group's list, read across its lanes
@@ -2448,12 +2444,25 @@ hipError_t dec_color(const DecFrame *__restrict__ fr, int n, int max_w, int max_
 }
 
 hipError_t enc_fdct(const EncFrame *__restrict__ fr, int n, uint32_t max_blocks, const EncTables *tab, const uint8_t *pix,
-                    int16_t *dcq, uint32_t *acbits, uint32_t *acscr, int bgr, int fastdct, hipStream_t s) {
+                    int16_t *dcq, uint32_t *acbits, uint32_t *acscr, int bgr, int fastdct, int ch, int cv,
+                    hipStream_t s) {
   if (n <= 0 || !max_blocks) return hipSuccess;
   // a workgroup takes 4 units of 8 blocks; a frame has ceil(nmcu / 8) * bpm <= (nblocks + 70) / 8 units
-  hipLaunchKernelGGL(k_fdct, dim3((max_blocks + 70 + 31) / 32, (unsigned)n), dim3(256), 0, s, fr, tab, pix, dcq, acbits,
-                     acscr, bgr, fastdct);
-  return hipGetLastError();
+  const dim3 grid((max_blocks + 70 + 31) / 32, (unsigned)n);
+#define VF_FDCT(CH, CV)                                                                                              \
+  if (ch == CH && cv == CV) {                                                                                        \
+    if (fastdct)                                                                                                     \
+      hipLaunchKernelGGL((k_fdct<CH, CV, true>), grid, dim3(256), 0, s, fr, tab, pix, dcq, acbits, acscr, bgr);     \
+    else                                                                                                             \
+      hipLaunchKernelGGL((k_fdct<CH, CV, false>), grid, dim3(256), 0, s, fr, tab, pix, dcq, acbits, acscr, bgr);    \
+    return hipGetLastError();                                                                                        \
+  }
+  VF_FDCT(1, 1)
+  VF_FDCT(2, 1)
+  VF_FDCT(2, 2)
+  VF_FDCT(1, 2)
+#undef VF_FDCT
+  return hipErrorInvalidValue;  // no TurboJPEG subsampling downsamples chroma otherwise
 }
 
 hipError_t enc_len(const EncFrame *__restrict__ fr, int n, uint32_t max_blocks, const EncTables *tab, const int16_t *dcq,

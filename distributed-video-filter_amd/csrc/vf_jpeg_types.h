@@ -45,6 +45,18 @@ struct Geom {
 };
 
 
+// natural (row-major) index -> zigzag position (inverse of jutils.c jpeg_natural_order)
+inline constexpr uint8_t kZigOf[64] = {0,  1,  5,  6,  14, 15, 27, 28, 2,  4,  7,  13, 16, 26, 29, 42,
+                                       3,  8,  12, 17, 25, 30, 41, 43, 9,  11, 18, 24, 31, 40, 44, 53,
+                                       10, 19, 23, 32, 39, 45, 52, 54, 20, 22, 33, 38, 46, 51, 55, 60,
+                                       21, 34, 37, 47, 50, 56, 59, 61, 35, 36, 48, 49, 57, 58, 62, 63};
+
+// Position of zigzag coefficient zz in the row of k_fdct's quantised-block image for the
+// block in workgroup slot `slot`: its 16-B octet (zz / 8, the AC coder's one ds_read_b128 per
+// lane) XOR-ed with (0, 5, 2, 7)[slot % 4], which keeps the 4 blocks of a 32-lane half from
+// storing to the same LDS banks (searched exhaustively with the b128 reads kept conflict-free).
+constexpr uint32_t qo_pos(uint32_t slot, uint32_t zz) { return zz ^ (((0x7250u >> (4 * (slot & 3))) & 7) << 3); }
+
 // Encoder tables: jcdctmgr.c reciprocal divisors, jchuff.c derived code tables
 struct EncTables {
   uint16_t recip[2][64];  // natural order; [0] luma, [1] chroma
@@ -52,6 +64,10 @@ struct EncTables {
   int16_t shift[2][64];
   uint32_t dc[2][16];   // (code << 8) | size by magnitude category
   uint32_t ac[2][256];  // (code << 8) | size by run/size symbol
+  // k_fdct's LDS table image, copied in with one 16-B load per thread: per table t and natural
+  // position n the quantiser entry {recip | corr << 16, (shift + 16) | qo_pos(j, zigzag(n)) <<
+  // (8 + 6j) for j = 0..3} (words [0, 256)), then ac[2][256] (words [256, 768))
+  alignas(16) uint32_t fdct_lds[768];
 };
 
 // Codes longer than kLook bits: lim[i] = (maxcode[l] + 1) << (16 - l) for l = kLook + 1 + i,

@@ -1,0 +1,71 @@
+# Builds tools/variants/libv_phases.so: the working tree's library with k_fdct phase timers
+# (shader-clock reads at the phase boundaries of each wave, summed over waves by lane 0 of
+# each wave into a device array; enc_fdct prints and clears the sums after each launch when
+# VF_FDCT_STATS is set).  Diagnostics only, from a patched temp copy; the product source never
+# carries them.
+set -e
+ROOT=$(cd "$(dirname "$0")/.." && pwd)
+mkdir -p "$ROOT/tools/variants"
+T=$(mktemp -d)
+cp -r "$ROOT/distributed-video-filter_amd" "$ROOT/include" "$T/"
+python3 - "$T/distributed-video-filter_amd/csrc/vf_jpeg_kernels.hip" <<'PY'
+import sys
+p = sys.argv[1]
+s = open(p).read()
+def rep(a, b, cnt=1):
+    global s
+    assert s.count(a) >= 1, a[:70]
+    s = s.replace(a, b, cnt)
+k0 = s.index("__global__ __launch_bounds__(256) void k_fdct(")
+pre, body = s[:k0], s[k0:]
+k1 = body.index("\n}\n") + 3
+kern, post = body[:k1], body[k1:]
+def krep(a, b):
+    global kern
+    assert a in kern, a[:70]
+    kern = kern.replace(a, b, 1)
+pre = pre.replace("constexpr uint32_t kFdctGroup = 8;",
+    "__device__ unsigned long long g_fdct_ph[16];\n"
+    "#define PH(i) do { const long long _c = clock64(); if ((threadIdx.x & 63) == 0 && (blockIdx.x & 511) == 0) atomicAdd(&g_fdct_ph[i], (unsigned long long)(_c - _c0)); } while (0)\n"
+    "constexpr uint32_t kFdctGroup = 8;")
+krep("  if (blockIdx.x * 4 >= ngroups * bpm) return;\n", "  if (blockIdx.x * 4 >= ngroups * bpm) return;\n  const long long _c0 = clock64();\n")
+krep("  const uint8_t *img = pix + F.img_off;\n", "  PH(0);\n  const uint8_t *img = pix + F.img_off;\n")
+krep("    for (int j = 0; j < 8; ++j) ws[slot][r][j] = v[j];\n  }\n  __syncthreads();\n",
+     "    for (int j = 0; j < 8; ++j) ws[slot][r][j] = v[j];\n  }\n  PH(1);\n  __syncthreads();\n  PH(2);\n")
+krep("    if (FAST) fdct_ifast_line(v);\n    else fdct_islow_line(v, 0);\n", "    PH(7);\n    if (FAST) fdct_ifast_line(v);\n    else fdct_islow_line(v, 0);\n")
+krep("  // From here on a block's 8 lanes", "  PH(3);\n  // From here on a block's 8 lanes")
+krep("  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, \"wavefront\");  // the group's list",
+     "  PH(4);\n  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, \"wavefront\");  // the group's list")
+krep("  if (real && eob && r == 0) {", "  PH(5);\n  if (real && eob && r == 0) {")
+kern = kern[:-3] + "  PH(6);\n  if ((threadIdx.x & 63) == 0 && (blockIdx.x & 511) == 0) atomicAdd(&g_fdct_ph[15], 1ull);\n}\n"
+s = pre + kern + post
+rep("  VF_FDCT(1, 1)\n", "  VF_FDCT_STATS_HOOK\n  VF_FDCT(1, 1)\n")
+rep("#define VF_FDCT(CH, CV)", "#define VF_FDCT_STATS_HOOK\n#define VF_FDCT(CH, CV)")
+# print after the launch: wrap the dispatch so the print follows it
+rep("    return hipGetLastError();                                                                                        \\\n  }",
+    "    fdct_stats_print(s);                                                                                             \\\n    return hipGetLastError();                                                                                        \\\n  }")
+rep("hipError_t enc_fdct(", """static void fdct_stats_print(hipStream_t s) {
+  if (!std::getenv("VF_FDCT_STATS")) return;
+  unsigned long long h[16];
+  (void)hipStreamSynchronize(s);
+  (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_fdct_ph), sizeof h);
+  const double w = h[15] ? (double)h[15] : 1.0;
+  std::fprintf(stderr, "[fdct phases] waves %llu  avg cycles from start: tables %.0f pixels+colour %.0f pass1 %.0f barrier %.0f pass2 %.0f list %.0f rounds %.0f end %.0f\\n",
+               h[15], h[0] / w, h[7] / w, h[1] / w, h[2] / w, h[3] / w, h[4] / w, h[5] / w, h[6] / w);
+  unsigned long long z[16] = {0};
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_fdct_ph), z, sizeof z);
+}
+
+hipError_t enc_fdct(""")
+if "#include <cstdio>" not in s:
+    s = s.replace("#include <stdint.h>", "#include <stdint.h>\n#include <cstdio>\n#include <cstdlib>", 1)
+open(p, "w").write(s)
+PY
+cd "$T"
+C=distributed-video-filter_amd/csrc
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -fvisibility=hidden -Wall -Iinclude -shared \
+  -Wl,-rpath,/opt/rocm/lib -Wl,--no-undefined -pthread $C/vf_kernels.hip $C/vf_engine.hip $C/vf_api.hip \
+  $C/vf_jpeg_kernels.hip $C/vf_jpeg_host.hip -o "$ROOT/tools/variants/libv_phases.so"
+cd "$ROOT"
+rm -rf "$T"
+ls -la tools/variants/libv_phases.so
