@@ -1897,15 +1897,19 @@ __device__ __forceinline__ uint32_t qo_at(uint32_t slot, uint32_t zz) {
 // fixed at compile time.
 constexpr uint32_t kFdctGroup = 8;  // MCUs per wave
 template <int CH, int CV, bool FAST>
-__global__ __launch_bounds__(256) void k_fdct(const EncFrame *__restrict__ fr, const EncTables *tab, const uint8_t *pix,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_fdct(const EncFrame *__restrict__ fr, const EncTables *tab, const uint8_t *pix,
                                               int16_t *dcq, uint32_t *acbits, uint32_t *acscr, int bgr) {
   const EncFrame &F = fr[blockIdx.y];
   const Geom &g = F.g;
   const uint32_t bpm = (uint32_t)g.bpm, nmcu = (uint32_t)g.nmcu;
   const uint32_t ngroups = (nmcu + kFdctGroup - 1) / kFdctGroup;
   if (blockIdx.x * 4 >= ngroups * bpm) return;
+  // Per block slot: the pass-1 workspace ws (8 x 9 words); pass 2 reads its column and writes
+  // the quantised block qo over the slot's first 32 words (a wave's LDS reads complete before
+  // its later writes, and the slot's 8 lanes are in one wave); the AC coder reads qo into
+  // registers and then writes its coefficient list over the slot.  Shared this way, the
+  // workgroup's LDS is 18.5 KB: 8 workgroups per CU.
   __shared__ int32_t ws[32][8][9];
-  __shared__ int16_t qo[32][64];
   __shared__ uint32_t acw[32][kAcWords];
   // The table image (EncTables::fdct_lds): s_q[t][n] = {recip | corr << 16, (shift + 16) | qo
   // position of zigzag(n) for slot % 4 == j at bits 8 + 6j} (pass 2's lane reads one 8-B entry
@@ -1917,6 +1921,7 @@ __global__ __launch_bounds__(256) void k_fdct(const EncFrame *__restrict__ fr, c
   const uint2 (*const s_q)[64] = reinterpret_cast<const uint2 (*)[64]>(s_tab);
   const uint32_t (*const s_ac)[256] = reinterpret_cast<const uint32_t (*)[256]>(reinterpret_cast<const uint32_t *>(s_tab) + 256);
   const uint32_t slot = threadIdx.x >> 3, r = threadIdx.x & 7, lm = slot & (kFdctGroup - 1);
+  int16_t *const qo = reinterpret_cast<int16_t *>(&ws[slot][0][0]);
   const uint32_t unit = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t grp = unit / bpm, c = unit - grp * bpm;  // scalar
   const uint32_t mcu = grp * kFdctGroup + lm;
@@ -1952,7 +1957,7 @@ __global__ __launch_bounds__(256) void k_fdct(const EncFrame *__restrict__ fr, c
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const uint2 q = s_q[t][i * 8 + r];
-      qo[slot][(q.y >> qsel) & 63] = quantize(v[i], q.x & 0xFFFF, q.x >> 16, q.y);
+      qo[(q.y >> qsel) & 63] = quantize(v[i], q.x & 0xFFFF, q.x >> 16, q.y);
     }
   }
   // From here on a block's 8 lanes read only their own slot's LDS (qo, ws, acw), written by
@@ -1964,7 +1969,7 @@ __global__ __launch_bounds__(256) void k_fdct(const EncFrame *__restrict__ fr, c
   // AC Huffman coding; every lane of the wave takes part in the 8-lane shuffles
   int vz[8];
   {
-    const uint4 q4 = real ? *reinterpret_cast<const uint4 *>(&qo[slot][qo_at(slot, r * 8)]) : make_uint4(0, 0, 0, 0);
+    const uint4 q4 = real ? *reinterpret_cast<const uint4 *>(&qo[qo_at(slot, r * 8)]) : make_uint4(0, 0, 0, 0);
     const uint32_t qw[4] = {q4.x, q4.y, q4.z, q4.w};
 #pragma unroll
     for (int j = 0; j < 8; ++j) vz[j] = (int)(int16_t)(qw[j >> 1] >> (16 * (j & 1)));
@@ -2037,7 +2042,7 @@ __global__ __launch_bounds__(256) void k_fdct(const EncFrame *__restrict__ fr, c
     const uint32_t nw = (total + 31) >> 5;
     for (uint32_t i = r; i < nw; i += 8) acscr[acs_idx(gb, i)] = acw[slot][i];
     if (r == 0) {
-      dcq[gb] = qo[slot][qo_at(slot, 0)];
+      dcq[gb] = (int16_t)vz[0];  // lane 0 holds zigzag positions 0..7
       acbits[gb] = total;
     }
   }

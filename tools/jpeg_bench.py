@@ -41,6 +41,8 @@ def main():
                     help="scene: 8 camera-like scenes at q85; hard: 32 distinct noisy scenes at q95 "
                          "(vfilter.synthetic.synthetic_noisy_scene)")
     ap.add_argument("--out", default="")
+    ap.add_argument("--resident-only", action="store_true",
+                    help="only the GPU-resident batches (kernel profiles without the concurrent host forms)")
     args = ap.parse_args()
     from vfilter import Context
     from vfilter.jpeg import TurboJPEG
@@ -60,6 +62,15 @@ def main():
         ms, stages = ctx.jpeg_bench_invert(jpgs, 85, args.subsamp, 0, iters=args.iters)
         outs = tj.invert_batch(jpgs)
         parity = outs[0] == J.invert_jpeg(jpgs[0])
+        if args.resident_only:
+            rec = {"kind": "jpeg_invert", "size": name, "content": args.content, "batch": args.batch,
+                   "gpu_resident_ms_per_batch": round(ms, 3), "gpu_resident_fps": round(args.batch / (ms / 1e3), 1),
+                   "stages_ms": {k: round(v, 4) for k, v in stages.items()}, "parity_vs_oracle": parity}
+            print(json.dumps(rec), flush=True)
+            if args.out:
+                with open(args.out, "a") as f:
+                    f.write(json.dumps(rec) + "\n")
+            continue
         t0 = time.perf_counter()
         reps = max(1, args.iters // 4)
         for _ in range(reps):
