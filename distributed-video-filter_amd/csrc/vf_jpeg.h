@@ -25,6 +25,11 @@ hipError_t dec_unstuff_count(const DecSeg *sg, int nseg, uint32_t max_tiles, con
                              uint32_t *tile_cnt, hipStream_t s);
 hipError_t dec_unstuff_write(const DecSeg *sg, int nseg, uint32_t max_tiles, const uint8_t *in,
                              const uint32_t *tile_off, const uint32_t *us_len, uint8_t *us, hipStream_t s);
+// pass-based sync, G (1, 2, 4, 8) subsequences per thread, records updated in place; pass p
+// returns at once when changed[p - 1] == 0, so passes are queued without host round trips
+hipError_t dec_syncg(int G, const DecSeg *sg, const DecFrame *fr, int nseg, uint32_t max_sub, const uint8_t *us,
+                     const uint32_t *us_len, uint64_t *exits, uint32_t *cnts, uint64_t *used, uint64_t *ck,
+                     uint32_t *ckrem, uint32_t *changed, int pass, hipStream_t s);
 hipError_t dec_sync(const DecSeg *sg, const DecFrame *fr, int nseg, uint32_t max_sub, const uint8_t *us, const uint32_t *us_len,
                     const uint64_t *exit_in, uint64_t *exit_out, const uint32_t *cnt_in, uint32_t *cnt_out,
                     uint64_t *used, uint64_t *ck, uint32_t *ckrem, uint32_t *changed, int pass, hipStream_t s);

@@ -22,6 +22,7 @@ constexpr int kInvalid = -1;
 constexpr int kHip = -2;
 constexpr int kNoMem = -3;
 constexpr int kJpeg = -5;
+constexpr int kResync = -100;  // internal: check_decode found the queued sync passes unconverged
 
 // TurboJPEG flag bits honoured (turbojpeg.h)
 constexpr int kFlagFastUpsample = 256;
@@ -133,6 +134,8 @@ class Codec {
   int init(std::string *err);
   int prepare_decode(const uint8_t *const *jpegs, const size_t *sizes, int n, int flags, std::string *err);
   int run_decode(int bgr, bool invert, std::string *err);
+  int run_decode_post(int bgr, bool invert, std::string *err);  // write, DC, IDCT, colour
+  int finish_sync(std::string *err);  // host-looped span passes after the queued ones
   int queue_decode_check(std::string *err);
   int check_decode(std::string *err);
   int prepare_encode(const int *ws, const int *hs, const uint64_t *img_offs, int n, int quality, int subsamp,
@@ -182,6 +185,12 @@ class Codec {
   bool waited_ = false;
   std::vector<uint64_t> out_sizes_, out_offs_;
   bool spec_check_ = false;           // run_decode queued that flag's read; check_decode tests it
+  bool pass_check_ = false;           // the same for the last queued sync pass's change flag
+  int sync_g_ = 4;                    // span width of the queued passes (finish_sync continues them)
+  int queued_ = kQueuedPasses;        // span passes queued by run_decode
+  bool sync_spec_ = false;            // run_decode took the speculative sync (the write pass's form)
+  int sync_last_ = 0;                 // exit / count slot of the pass-based sync's result
+  bool enc_fast_ = false;             // submit_invert's DCT (wait_invert re-encodes after finish_sync)
   TaskPool pool_{4};
 };
 

@@ -464,7 +464,7 @@ int Codec::run_decode(int bgr, bool invert, std::string *err) {
   const DecFrame *fr = d_dfr_.as<DecFrame>();
   const DecSeg *sg = d_dsg_.as<DecSeg>();
   const ScanSeg *segs = d_segs_.as<ScanSeg>();
-  const int n = dn_, ns = dnseg_;
+  const int ns = dnseg_;
   CK(hipEventRecord(ev_[0], s_));
   // 1. unstuff
   CK(dec_unstuff_count(sg, ns, dmax_tiles_, d_in_.as<uint8_t>(), d_tile_.as<uint32_t>(), s_));
@@ -519,6 +519,32 @@ int Codec::run_decode(int bgr, bool invert, std::string *err) {
                    dmax_wg_ * (uint32_t)ns, dmax_sub_ * (uint32_t)ns, st[5], st[6]);
     }
   }
+  // pass-based: spans of G subsequences per thread (VF_JPEG_SYNC_G = 1, 2, 4, 8; 0 = the
+  // host-looped one-subsequence k_sync), kQueuedPasses passes queued without a host round trip
+  // (a pass after convergence returns at once); the last pass's flag is read at check_decode
+  const int sync_g = [] {  // read per call: tests switch it inside one process
+    const char *v = std::getenv("VF_JPEG_SYNC_G");
+    const int g = v ? std::atoi(v) : 4;
+    return g == 0 || g == 1 || g == 2 || g == 4 || g == 8 ? g : 4;
+  }();
+  if (flag && sync_g > 0) {
+    // VF_JPEG_SYNC_QUEUED = 1..kQueuedPasses (tests): fewer queued passes, so check_decode
+    // reports them unconverged and finish_sync runs the rest
+    const char *qv = std::getenv("VF_JPEG_SYNC_QUEUED");
+    queued_ = qv ? std::min(std::max(std::atoi(qv), 1), kQueuedPasses) : kQueuedPasses;
+    CK(hipMemsetAsync(d_changed_.p, 0, sizeof(uint32_t) * kMaxPasses, s_));
+    for (int p = 0; p < queued_; ++p)
+      CK(dec_syncg(sync_g, sg, fr, ns, dmax_sub_, d_us_.as<uint8_t>(), us_len, d_exit_[0].as<uint64_t>(),
+                   d_cnt_[0].as<uint32_t>(), d_used_.as<uint64_t>(), d_ck_.as<uint64_t>(), d_ckrem_.as<uint32_t>(),
+                   d_changed_.as<uint32_t>(), p, s_));
+    CK(h_flag_.ensure(64));
+    CK(hipMemcpyAsync(h_flag_.p, d_changed_.as<uint32_t>() + queued_ - 1, sizeof(uint32_t),
+                      hipMemcpyDeviceToHost, s_));
+    pass_check_ = true;
+    flag = 0;
+    last = 0;
+    pass = queued_;
+  }
   if (flag) CK(hipMemsetAsync(d_changed_.p, 0, sizeof(uint32_t) * kMaxPasses, s_));
   for (; flag;) {
     const int a = pass & 1;
@@ -550,6 +576,45 @@ int Codec::run_decode(int bgr, bool invert, std::string *err) {
                  (dmax_sub_ + 255) / 256 * (uint32_t)ns);
   }
   CK(hipEventRecord(ev_[2], s_));
+  sync_spec_ = use_spec;
+  sync_last_ = last;
+  sync_g_ = sync_g;
+  return run_decode_post(bgr, invert, err);
+}
+
+// The queued span passes left a workgroup's last exit changing (a stream that takes more than
+// kQueuedPasses - 1 workgroups of 1024 subsequences to resynchronise: corrupt or adversarial
+// data in practice): more passes, each followed by a flag read, until none changes.  The caller
+// then queues the stages after the sync again.
+int Codec::finish_sync(std::string *err) {
+  const DecFrame *fr = d_dfr_.as<DecFrame>();
+  const DecSeg *sg = d_dsg_.as<DecSeg>();
+  const uint32_t *us_len = d_totals_.as<uint32_t>();
+  for (int p = queued_;; ++p) {
+    if (p >= kMaxPasses) {
+      *err = "Huffman synchronisation did not converge (corrupt stream?)";
+      return kJpeg;
+    }
+    CK(dec_syncg(sync_g_, sg, fr, dnseg_, dmax_sub_, d_us_.as<uint8_t>(), us_len, d_exit_[0].as<uint64_t>(),
+                 d_cnt_[0].as<uint32_t>(), d_used_.as<uint64_t>(), d_ck_.as<uint64_t>(), d_ckrem_.as<uint32_t>(),
+                 d_changed_.as<uint32_t>(), p, s_));
+    uint32_t flag = 0;
+    CK(hipMemcpyAsync(&flag, d_changed_.as<uint32_t>() + p, sizeof flag, hipMemcpyDeviceToHost, s_));
+    CK(hipStreamSynchronize(s_));
+    if (!flag) break;
+  }
+  return kOk;
+}
+
+// Decode stages after the sync: block offsets, write pass, DC prediction, IDCT, colour.
+int Codec::run_decode_post(int bgr, bool invert, std::string *err) {
+  const DecFrame *fr = d_dfr_.as<DecFrame>();
+  const DecSeg *sg = d_dsg_.as<DecSeg>();
+  const ScanSeg *segs = d_segs_.as<ScanSeg>();
+  const int n = dn_, ns = dnseg_;
+  const uint32_t *us_len = d_totals_.as<uint32_t>();
+  const bool use_spec = sync_spec_;
+  const int last = sync_last_;
   // 3. block offsets of the subsequences, then the write pass
   uint32_t *blocks_total = d_totals_.as<uint32_t>() + ns;
   CK(scan_u32(segs + ns, ns, (dmax_sub_ + kScanTile - 1) / kScanTile, d_cnt_[last].as<uint32_t>(),
@@ -591,6 +656,10 @@ int Codec::queue_decode_check(std::string *err) {
 // Check that every frame decoded all its blocks (after queue_decode_check and a synchronisation).
 int Codec::check_decode(std::string *err) {
   const uint32_t *tot = h_dtot_.as<uint32_t>();
+  if (pass_check_) {
+    pass_check_ = false;
+    if (*h_flag_.as<uint32_t>()) return kResync;  // the caller runs finish_sync and its stages again
+  }
   if (spec_check_) {
     spec_check_ = false;
     if (*h_flag_.as<uint32_t>()) {
@@ -845,11 +914,16 @@ int Codec::decode(const uint8_t *const *jpegs, const size_t *jsizes, int n, int 
     }
   }
   if ((rc = run_decode(pixel_format, false, err))) return rc;
-  if ((rc = queue_decode_check(err))) return rc;
-  CK(h_out_.ensure(dpix_bytes_));
-  CK(hipMemcpyAsync(h_out_.p, d_pix_.p, dpix_bytes_, hipMemcpyDeviceToHost, s_));
-  CK(hipStreamSynchronize(s_));
-  if ((rc = check_decode(err))) return rc;
+  for (bool again = false;; again = true) {
+    if (again && ((rc = finish_sync(err)) || (rc = run_decode_post(pixel_format, false, err)))) return rc;
+    if ((rc = queue_decode_check(err))) return rc;
+    CK(h_out_.ensure(dpix_bytes_));
+    CK(hipMemcpyAsync(h_out_.p, d_pix_.p, dpix_bytes_, hipMemcpyDeviceToHost, s_));
+    CK(hipStreamSynchronize(s_));
+    rc = check_decode(err);
+    if (rc != kResync) break;
+  }
+  if (rc) return rc;
   pool_.run(n, [&](int f) {
     std::memcpy(outs[f], h_out_.as<uint8_t>() + dfr_[(size_t)f].out_off,
                 (size_t)dfr_[(size_t)f].g.w * dfr_[(size_t)f].g.h * 3);
@@ -894,6 +968,7 @@ int Codec::submit_invert(const uint8_t *const *jpegs, const size_t *jsizes, int 
       if (gate_->last) CK(hipStreamWaitEvent(s_, gate_->last, 0));
     }
     // decode (BGR, inverted: cv2.bitwise_not, inverter.py:41) straight into the encoder's input
+    enc_fast_ = fast;
     if ((rc = run_decode(1, true, err))) return rc;
     if ((rc = run_encode(1, fast, err))) return rc;
     if (gate_) {
@@ -931,6 +1006,13 @@ int Codec::wait_invert(size_t *total, std::string *err) {
   const auto t0 = clk::now();
   CK(hipEventSynchronize(done_));
   int rc = check_decode(err);
+  while (rc == kResync) {  // more sync passes, then every stage after the sync again
+    if ((rc = finish_sync(err)) || (rc = run_decode_post(1, true, err)) || (rc = run_encode(1, enc_fast_, err)) ||
+        (rc = queue_decode_check(err)) || (rc = queue_fetch(guess_, err)))
+      return rc;
+    CK(hipEventSynchronize(done_));
+    rc = check_decode(err);
+  }
   if (rc) return rc;
   if ((rc = finish_fetch(err))) return rc;
   waited_ = true;
@@ -1028,7 +1110,15 @@ int Codec::bench_invert(const uint8_t *const *jpegs, const size_t *jsizes, int n
   }
   if ((rc = queue_decode_check(err))) return rc;
   CK(hipStreamSynchronize(s_));
-  if ((rc = check_decode(err))) return rc;
+  rc = check_decode(err);
+  while (rc == kResync) {
+    if ((rc = finish_sync(err)) || (rc = run_decode_post(1, true, err)) || (rc = run_encode(1, fast, err)) ||
+        (rc = queue_decode_check(err)))
+      return rc;
+    CK(hipStreamSynchronize(s_));
+    rc = check_decode(err);
+  }
+  if (rc) return rc;
   *ms = (float)(total_ms / iters);
   if (stage_ms) {
     for (int i = 0; i < 7; ++i) stage_ms[i] = acc[i] / iters;

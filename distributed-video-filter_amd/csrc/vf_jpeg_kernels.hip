@@ -365,7 +365,8 @@ __device__ __forceinline__ void load_tables(const DecFrame &F, HuffDec *tabs) {
 
 // (zigzag advance << 8) | bits of a symbol whose code is longer than kLook bits: jdhuff.c
 // jpeg_huff_decode's slow path (an unmatched code reads as symbol 0 after 16 bits)
-__device__ __forceinline__ uint32_t sync_slow(const BitReader &br, const HuffSync &t, bool dc) {
+template <typename BR>
+__device__ __forceinline__ uint32_t sync_slow(const BR &br, const HuffSync &t, bool dc) {
   const uint32_t c16 = br.peek(16);
   uint32_t len = long_code_len(c16, t.lim), sym = 0;
   if (len > 16) len = 16;  // corrupt code: symbol 0
@@ -383,7 +384,8 @@ __device__ __forceinline__ uint32_t sync_slow(const BitReader &br, const HuffSyn
 
 // One Huffman symbol of the sync decode: the same bits and zigzag / block progression as
 // decode_span, through one combined lookup (HuffSync) instead of symbol + extra-bits steps.
-__device__ __forceinline__ void sync_step(BitReader &br, uint32_t &z, uint32_t &c, uint32_t &blocks,
+template <typename BR>
+__device__ __forceinline__ void sync_step(BR &br, uint32_t &z, uint32_t &c, uint32_t &blocks,
                                           const HuffGeom &g, const HuffSync *dcT, const HuffSync *acT) {
   br.refill();
   const uint32_t k = g.comp(c);
@@ -399,11 +401,79 @@ __device__ __forceinline__ void sync_step(BitReader &br, uint32_t &z, uint32_t &
   }
 }
 
+// One lane's sync decoder with a short per-symbol chain, over stream words staged in LDS: the
+// bit buffer is refilled with selects (the next word re-read every symbol, off the critical
+// path), and the byte offset of c's component tables is kept in a register and recomputed with
+// selects, so a symbol is one table read and ~25 VALU with no branch but the rare long code.
+// sync_step's branchy form (refill, DC / AC, block end) measured ~530-700 shader cycles per
+// symbol for a lone lane on an idle GPU (tools/build_syncg_stats.sh).  Same bits, zigzag and
+// block progression as sync_step.
+struct SyncLane {
+  const uint32_t *w;  // staged words, minus woff
+  uint64_t buf;       // next bits, left-aligned
+  uint32_t nb, wi, nxt, pos;
+  uint32_t z, c, n;   // zigzag index, block-in-MCU, blocks completed
+  uint32_t toff;      // byte offset of the DC table of c's component (its AC table: 3 tables on)
+  uint32_t cpack, bpm;
+  __device__ __forceinline__ void init(const uint32_t *words, uint32_t woff, uint64_t X, const HuffGeom &hg) {
+    const uint32_t p = (uint32_t)(X >> 16);
+    w = words;
+    wi = (p >> 5) - woff;
+    buf = (((uint64_t)bswap32(w[wi]) << 32) | bswap32(w[wi + 1])) << (p & 31);
+    nb = 64 - (p & 31);
+    wi += 2;
+    nxt = w[wi];
+    pos = p;
+    z = (X >> 8) & 0xFF;
+    c = X & 0xFF;
+    n = 0;
+    cpack = hg.cpack;
+    bpm = hg.bpm;
+    toff = __umul24((cpack >> (2 * c)) & 3, (uint32_t)sizeof(HuffSync));
+  }
+  __device__ __forceinline__ void step(const HuffSync *tabs) {
+    const bool f = nb <= 32;
+    buf |= f ? (uint64_t)bswap32(nxt) << (32 - nb) : 0ull;
+    nb += f ? 32u : 0u;
+    wi += f ? 1u : 0u;
+    nxt = w[wi];
+    const HuffSync &T = *reinterpret_cast<const HuffSync *>(reinterpret_cast<const char *>(tabs) + toff +
+                                                             (z == 0 ? 0u : 3u * (uint32_t)sizeof(HuffSync)));
+    uint32_t e = T.sfast[(uint32_t)(buf >> (64 - kLook))];
+    if (!e) {  // a code longer than kLook bits: jdhuff.c's slow path (rare)
+      const uint32_t c16 = (uint32_t)(buf >> 48);
+      uint32_t len = long_code_len(c16, T.lim), sym = 0;
+      if (len > 16) len = 16;
+      else sym = T.vals[(uint32_t)((int32_t)(c16 >> (16 - len)) + T.valoff[len]) & 255];
+      uint32_t extra, adv;
+      if (z == 0) {
+        extra = sym > 16 ? 16 : sym;
+        adv = 1;
+      } else {
+        extra = sym & 15;
+        adv = extra ? (sym >> 4) + 1 : ((sym >> 4) == 15 ? 16 : 64);
+      }
+      e = (adv << 8) | (len + extra);
+    }
+    const uint32_t len = e & 0xFF;
+    buf <<= len;
+    nb -= len;
+    pos += len;
+    z += e >> 8;
+    const bool eob = z >= 64;
+    const uint32_t c1 = c + 1 == bpm ? 0u : c + 1;
+    c = eob ? c1 : c;
+    z = eob ? 0u : z;
+    n += eob ? 1u : 0u;
+    toff = __umul24((cpack >> (2 * c)) & 3, (uint32_t)sizeof(HuffSync));
+  }
+};
+
 __device__ __forceinline__ void load_sync_tables(const DecFrame &F, HuffSync *tabs) {
   const uint32_t *src = reinterpret_cast<const uint32_t *>(&F.sdc[0]);
   uint32_t *dst = reinterpret_cast<uint32_t *>(tabs);
   constexpr uint32_t nw = 6 * sizeof(HuffSync) / 4;
-  for (uint32_t j = threadIdx.x; j < nw; j += 256) dst[j] = src[j];
+  for (uint32_t j = threadIdx.x; j < nw; j += blockDim.x) dst[j] = src[j];
   __syncthreads();
 }
 
@@ -418,6 +488,7 @@ __device__ __forceinline__ void load_sync_tables(const DecFrame &F, HuffSync *ta
 // trajectory (marks a decode did not reach from its entry are invalidated).
 
 constexpr uint64_t kNoCk = ~0ull;
+constexpr uint32_t kSpecPadWords = 16;  // staged words past a workgroup's range: overshoot + lookahead
 
 // One sync pass.  Every thread decodes its subsequence from its entry state; then, inside
 // the workgroup, a thread whose entry differs from its predecessor's current exit takes that
@@ -527,6 +598,153 @@ __global__ __launch_bounds__(256) void k_sync(const DecSeg *__restrict__ sg, con
   }
 }
 
+// ---- decoder: pass-based sync over spans of G subsequences ---------------------------------
+//
+// k_sync's chains re-decode every thread whose entry changed, one subsequence per round: on
+// content whose codes resynchronise slowly (noise at q95: the state (pos, z, c) rejoins after
+// ~900 bits at the median, 5.5k at p99, tools/sync_distance.py), a workgroup needs ~25 rounds
+// and decodes its stream ~5 times per pass (tools/sync_sim.py).  Here a thread decodes G
+// consecutive subsequences as one trajectory (the records per subsequence -- checkpoints,
+// exit, block count -- are those k_sync writes, so the write pass is unchanged): with G = 4 a
+// guessed entry has 4x the bits to resynchronise in, and the simulation gives ~6 rounds and ~2.1
+// decodes of the stream per pass.  The records live in global memory and are updated in place;
+// a re-decode compares each mark's state with the recorded one (prefetched one mark ahead) and
+// stops where it rejoins.  Passes are queued without host round trips: a pass reads the
+// previous pass's flag and returns at once when no workgroup's last exit changed (then every
+// entry is consistent: within a workgroup by its rounds, across by the unchanged exits).
+
+// Re-decode (or first decode, check = false) of a thread's span from entry state X; returns the
+// span's last exit.  `last` is the previous decode's last exit (returned unchanged on a join).
+__device__ __forceinline__ uint64_t sync_span(const uint32_t *words, uint32_t woff, uint64_t X, uint32_t i0, uint32_t ng,
+                                              uint32_t nsub, uint32_t nbits, uint64_t gi0, bool check, uint64_t last,
+                                              uint64_t *exits, uint32_t *cnts, uint64_t *ck, uint32_t *ckrem,
+                                              const HuffGeom &hg, const HuffSync *tabs) {
+  SyncLane d;
+  d.init(words, woff, X, hg);
+  uint32_t j = 0, bj = i0 * kSubBits;
+  uint32_t ej = i0 + 1 >= nsub ? nbits : bj + kSubBits;  // end of subsequence j
+  // next mark of subsequence j: checkpoint m < kCk at bj + (m + 1) * kCkStep (if inside it), or
+  // m == kCk: its end.  An entry lies less than one symbol (<= 32 bits) past bj, before mark 0.
+  uint32_t m = bj + kCkStep < ej ? 0u : (uint32_t)kCk;
+  uint32_t mk = m < kCk ? bj + kCkStep : ej;
+  uint64_t old = check ? (m < kCk ? ck[gi0 * kCk] : exits[gi0]) : 0;
+  uint32_t n0 = 0, n1 = 0, n2 = 0;  // blocks at the checkpoints written in this decode
+  static_assert(kCk == 3, "n0..n2");
+  for (;;) {
+    while (d.pos < mk) d.step(tabs);
+    const uint64_t st = pack_state(d.pos, d.z, d.c);
+    const uint64_t gj = gi0 + j;
+    if (m < kCk) {
+      if (check && old == st) {  // rejoined: the rest of the span is the recorded trajectory
+        const uint32_t cj = d.n + ckrem[gj * kCk + m];
+        cnts[gj] = cj;
+        if (m > 0) ckrem[gj * kCk] = cj - n0;
+        if (m > 1) ckrem[gj * kCk + 1] = cj - n1;
+        return last;
+      }
+      ck[gj * kCk + m] = st;
+      n2 = m == 2 ? d.n : n2;
+      n1 = m == 1 ? d.n : n1;
+      n0 = m == 0 ? d.n : n0;
+      ++m;
+    } else {
+      const bool joined = check && old == st;
+      const uint32_t nw = bj + kCkStep < ej ? (bj + 2 * kCkStep < ej ? (bj + 3 * kCkStep < ej ? 3u : 2u) : 1u) : 0u;
+      cnts[gj] = d.n;
+      if (nw > 0) ckrem[gj * kCk] = d.n - n0;
+      if (nw > 1) ckrem[gj * kCk + 1] = d.n - n1;
+      if (nw > 2) ckrem[gj * kCk + 2] = d.n - n2;
+      if (joined) return last;  // the exit, and every later subsequence, unchanged
+      exits[gj] = st;
+      for (uint32_t q = nw; q < (uint32_t)kCk; ++q) ck[gj * kCk + q] = kNoCk;  // marks past the segment's end
+      if (j + 1 == ng) return st;
+      ++j;
+      d.n = 0;
+      bj += kSubBits;
+      ej = i0 + j + 1 >= nsub ? nbits : bj + kSubBits;
+      m = 0;
+      if (bj + kCkStep >= ej) m = kCk;
+    }
+    mk = m < kCk ? bj + (m + 1) * kCkStep : ej;
+    if (m < kCk && mk >= ej) {
+      m = kCk;
+      mk = ej;
+    }
+    if (check) old = m < kCk ? ck[(gi0 + j) * kCk + m] : exits[gi0 + j];  // one mark ahead of its use
+  }
+}
+
+// T threads per workgroup, T * G subsequences: the workgroup's stream words (32 KB at most) are
+// staged in LDS first, so a refill is an LDS read (global loads one word ahead exposed their
+// latency every few symbols: ~500-700 shader cycles per symbol on an idle GPU, counted with
+// tools/build_syncg_stats.sh).
+#ifndef VF_SYNCG_STAGE
+#define VF_SYNCG_STAGE 1
+#endif
+constexpr bool kSyncgStage = VF_SYNCG_STAGE;
+constexpr uint32_t syncg_threads(int G) { return !kSyncgStage || G <= 4 ? 256u : 1024u / (uint32_t)G; }
+template <int G>
+__global__ __launch_bounds__(256) void k_syncg(const DecSeg *__restrict__ sg, const DecFrame *__restrict__ fr, const uint8_t *us,
+                                               const uint32_t *us_len, uint64_t *exits, uint32_t *cnts, uint64_t *used,
+                                               uint64_t *ck, uint32_t *ckrem, uint32_t *changed, int pass) {
+  constexpr uint32_t T = syncg_threads(G), kWords = kSyncgStage ? T * G * (kSubBits / 32) + kSpecPadWords : 1;
+  __shared__ HuffSync tabs[6];
+  __shared__ uint64_t s_exit[T];
+  __shared__ uint32_t s_w[kWords];
+  const DecSeg S = sg[blockIdx.y];  // by value: held in scalar registers
+  const DecFrame &F = fr[S.frame];
+  if (blockIdx.x * T * G >= S.nsub_max) return;
+  if (pass > 0 && changed[pass - 1] == 0) return;  // converged (workgroup-uniform)
+  const uint32_t *gw = reinterpret_cast<const uint32_t *>(us + S.us_off);
+  const uint32_t woff = kSyncgStage ? blockIdx.x * T * G * (kSubBits / 32) : 0u;
+  if (kSyncgStage) {
+    const uint32_t fwords = (((S.in_len + 64) + 15) & ~15u) / 4;
+    for (uint32_t i = threadIdx.x; i < kWords; i += T) s_w[i] = woff + i < fwords ? gw[woff + i] : 0u;
+  }
+  const uint32_t *words = kSyncgStage ? s_w : gw;
+  load_sync_tables(F, tabs);  // its barrier also publishes s_w
+  const HuffGeom hg(F.g);
+  const uint32_t t = threadIdx.x;
+  const uint32_t nbits = us_len[blockIdx.y] * 8u, nsub = (nbits + kSubBits - 1) / kSubBits;
+  const uint32_t i0 = (blockIdx.x * T + t) * G;
+  const bool live = i0 < nsub;
+  const uint32_t ng = live ? min((uint32_t)G, nsub - i0) : 0u;
+  const uint64_t gi0 = S.sub0 + i0;
+  uint64_t entry = 0, last = 0, last_old = 0;
+  bool need = false;
+  if (live) {
+    if (pass == 0) {
+      entry = i0 == 0 ? 0 : pack_state(i0 * kSubBits, 0, 0);  // a guess, except at the segment's start
+      need = true;
+    } else {
+      entry = t == 0 ? (i0 == 0 ? 0 : exits[gi0 - 1]) : used[gi0];
+      last = exits[gi0 + ng - 1];
+      need = t == 0 && entry != used[gi0];
+    }
+  }
+  last_old = last;
+  bool check = pass > 0;  // records are valid from the first decode on
+  for (;;) {
+    if (need) {
+      last = sync_span(words, woff, entry, i0, ng, nsub, nbits, gi0, check, last, exits, cnts, ck, ckrem, hg, tabs);
+      used[gi0] = entry;
+    }
+    s_exit[t] = last;
+    __syncthreads();
+    need = false;
+    if (live && t > 0) {
+      const uint64_t e = s_exit[t - 1];
+      if (e != entry) {
+        entry = e;
+        need = true;
+      }
+    }
+    check = true;
+    if (!__syncthreads_or(need)) break;  // also orders the s_exit reads before the next writes
+  }
+  if (t == T - 1 && live && i0 + G < nsub && (pass == 0 || last != last_old)) atomicOr(changed + pass, 1u);
+}
+
 // ---- decoder: speculative Huffman synchronisation ------------------------------------------
 //
 // The pass-based k_sync above needs a re-decode chain whenever a guessed entry state has the
@@ -555,7 +773,6 @@ __device__ __forceinline__ uint32_t nib(uint64_t row, uint32_t i) { return (uint
 __device__ __forceinline__ uint32_t spec_lanes(uint32_t bpm) {
   return bpm <= 1 ? 1u : bpm <= 2 ? 2u : bpm <= 4 ? 4u : bpm <= 8 ? 8u : 16u;
 }
-constexpr uint32_t kSpecPadWords = 16;                                  // overshoot + lookahead
 constexpr uint32_t kSpecWords = 256 * (kSubBits / 32) + kSpecPadWords;  // NS <= 256 subsequences
 constexpr uint8_t kLinkNone = 0xF;  // rejoined no trajectory (explicit state follows)
 constexpr uint8_t kLinkLast = 0xE;  // the frame's last subsequence: decoded to the end
@@ -2400,6 +2617,25 @@ hipError_t dec_sync(const DecSeg *__restrict__ sg, const DecFrame *__restrict__ 
   hipLaunchKernelGGL(k_sync, dim3((max_sub + 255) / 256, (unsigned)nseg), dim3(256), 0, s, sg, fr, us, us_len,
                      exit_in, exit_out, cnt_in, cnt_out, used, ck, ckrem, changed, pass);
   return hipGetLastError();
+}
+
+hipError_t dec_syncg(int G, const DecSeg *__restrict__ sg, const DecFrame *__restrict__ fr, int nseg, uint32_t max_sub,
+                     const uint8_t *us, const uint32_t *us_len, uint64_t *exits, uint32_t *cnts, uint64_t *used,
+                     uint64_t *ck, uint32_t *ckrem, uint32_t *changed, int pass, hipStream_t s) {
+  if (nseg <= 0 || !max_sub) return hipSuccess;
+#define VF_SYNCG(GG)                                                                                              \
+  if (G == GG) {                                                                                                  \
+    const uint32_t span = syncg_threads(GG) * GG;                                                                 \
+    hipLaunchKernelGGL(k_syncg<GG>, dim3((max_sub + span - 1) / span, (unsigned)nseg), dim3(syncg_threads(GG)),   \
+                       0, s, sg, fr, us, us_len, exits, cnts, used, ck, ckrem, changed, pass);                    \
+    return hipGetLastError();                                                                                     \
+  }
+  VF_SYNCG(1)
+  VF_SYNCG(2)
+  VF_SYNCG(4)
+  VF_SYNCG(8)
+#undef VF_SYNCG
+  return hipErrorInvalidValue;
 }
 
 hipError_t dec_sync_spec(const DecSeg *__restrict__ sg, const DecFrame *__restrict__ fr, int nseg, uint32_t max_wg, const uint8_t *us,

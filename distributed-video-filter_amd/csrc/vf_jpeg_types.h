@@ -19,6 +19,7 @@ constexpr int kMaxBpm = 10;     // blocks per MCU (T.81 B.2.3)
 constexpr int kSubBits = 256;  // bits per Huffman-decoding subsequence
 constexpr int kTile = 4096;     // bytes per (un)stuffing tile
 constexpr int kMaxPasses = 64;  // sync-pass flags kept on the device
+constexpr int kQueuedPasses = 4;  // span sync passes queued per batch (k_syncg)
 #ifndef VF_KLOOK
 #define VF_KLOOK 9
 #endif

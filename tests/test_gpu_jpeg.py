@@ -222,6 +222,49 @@ def test_sync_modes_on_hard_content(tj, monkeypatch, mode, subsamp, quality):
         assert g == J.invert_jpeg(j)
 
 
+def _span_sync_batch(quality=95, subsamp=J.TJSAMP_422):
+    """Noise frames long enough for several span-sync workgroups per frame (a workgroup covers
+    256 x G subsequences of 256 bits), plus a scene and a small frame in the same batch."""
+    rng = np.random.default_rng(quality + 11)
+    imgs = [rng.integers(0, 256, (512, 640, 3), dtype=np.uint8),
+            np.clip(_img("scene", 5, 480, 640).astype(np.int16) + rng.integers(-60, 60, (480, 640, 3)), 0, 255)
+            .astype(np.uint8),
+            _img("scene", 6, 64, 48)]
+    return [J.encode(im, quality, J.TJPF_BGR, subsamp) for im in imgs]
+
+
+@pytest.mark.parametrize("g", ["0", "1", "2", "4", "8"])
+def test_span_sync_widths(tj, monkeypatch, g):
+    """The pass-based sync with G subsequences per thread (k_syncg: records updated in place,
+    passes queued and returning early once no workgroup's last exit changes; G = 0: the
+    host-looped one-subsequence k_sync), on frames spanning several workgroups, through the
+    fused invert and the plain decode, bit-exact with the oracle."""
+    monkeypatch.setenv("VF_JPEG_SYNC", "pass")
+    monkeypatch.setenv("VF_JPEG_SYNC_G", g)
+    jpgs = _span_sync_batch()
+    got = tj.invert_batch(jpgs)
+    for o, j in zip(got, jpgs):
+        assert o == J.invert_jpeg(j)
+    for j in jpgs[:2]:
+        assert np.array_equal(tj.decode(j), J.decode(j))
+
+
+@pytest.mark.parametrize("queued", ["1", "2"])
+def test_span_sync_unconverged_passes_resume(tj, monkeypatch, queued):
+    """When the queued span passes leave a workgroup's last exit changing (forced here with
+    VF_JPEG_SYNC_QUEUED: pass 0 always changes exits on a multi-workgroup frame), check_decode
+    reports it, finish_sync runs the remaining passes with a flag read each, and the stages after
+    the sync run again: decode, the synchronous invert and the submit / wait form all bit-exact."""
+    monkeypatch.setenv("VF_JPEG_SYNC", "pass")
+    monkeypatch.setenv("VF_JPEG_SYNC_G", "4")
+    monkeypatch.setenv("VF_JPEG_SYNC_QUEUED", queued)
+    jpgs = _span_sync_batch(90, J.TJSAMP_420)
+    assert np.array_equal(tj.decode(jpgs[0]), J.decode(jpgs[0]))
+    want = [J.invert_jpeg(j) for j in jpgs]
+    assert tj.invert_batch(jpgs) == want
+    assert [bytes(o) for o in tj.invert_batch_result(tj.invert_batch_submit(jpgs))] == want
+
+
 @pytest.mark.parametrize("mode", ["spec", "pass"])
 def test_custom_tables_long_codes(tj, monkeypatch, mode):
     """Frames whose Huffman tables are not Annex K (tests/jpeg_recode.py): many codes longer
