@@ -786,27 +786,26 @@ template <typename CK, typename REM>
 __device__ __forceinline__ uint32_t spec_link(const uint32_t *words, uint32_t woff, uint64_t X, uint32_t base,
                                               uint32_t end, bool last, const HuffGeom &hg, const HuffSync *tabs, CK ck,
                                               REM rem, uint32_t *count, uint64_t *endst) {
-  BitReader br;
-  br.init_words(words, (uint32_t)(X >> 16), woff);
-  uint32_t z = (X >> 8) & 0xFF, c = X & 0xFF, n = 0;
-  int m = 0;
-  while (m < kCk && base + (uint32_t)(m + 1) * kCkStep <= br.pos) ++m;
-  while (br.pos < end) {
-    sync_step(br, z, c, n, hg, tabs, tabs + 3);
-    if (last) continue;
-    const uint32_t mk = base + (uint32_t)(m + 1) * kCkStep;
-    if (m < kCk && mk < end && br.pos >= mk) {
-      const uint64_t st = pack_state(br.pos, z, c);
-      for (uint32_t c2 = 0; c2 < hg.bpm; ++c2)
-        if (ck(c2, m) == st) {
-          *count = n + rem(c2, m);
-          return c2;
-        }
-      ++m;
-    }
+  SyncLane d;
+  d.init(words, woff, X, hg);
+  uint32_t m = 0;
+  while (m < kCk && base + (m + 1) * kCkStep <= d.pos) ++m;
+  for (;;) {  // decode to the next mark (a checkpoint inside the subsequence) or to its end
+    const uint32_t mk = base + (m + 1) * kCkStep;
+    const bool cm = !last && m < kCk && mk < end;
+    const uint32_t stop = cm ? mk : end;
+    while (d.pos < stop) d.step(tabs);
+    if (!cm) break;
+    const uint64_t st = pack_state(d.pos, d.z, d.c);
+    for (uint32_t c2 = 0; c2 < hg.bpm; ++c2)
+      if (ck(c2, m) == st) {
+        *count = d.n + rem(c2, m);
+        return c2;
+      }
+    ++m;
   }
-  *count = n;
-  *endst = pack_state(br.pos, z, c);
+  *count = d.n;
+  *endst = pack_state(d.pos, d.z, d.c);
   return last ? kLinkLast : kLinkNone;
 }
 
@@ -845,22 +844,22 @@ __global__ __launch_bounds__(256) void k_spec(const DecSeg *__restrict__ sg, con
 #pragma unroll
   for (int m = 0; m < kCk; ++m) s_ck[m][t] = kNoCk;
   if (live) {
-    BitReader br;
-    br.init_words(s_w, base, woff);
-    uint32_t z = 0, c = c0, n = 0;
-    int m = 0;
-    while (br.pos < end) {
-      sync_step(br, z, c, n, hg, tabs, tabs + 3);
-      const uint32_t mk = base + (uint32_t)(m + 1) * kCkStep;
-      if (m < kCk && mk < end && br.pos >= mk) {
-        s_ck[m][t] = pack_state(br.pos, z, c);
-        s_rem[m][t] = n;
-        ++m;
-      }
+    SyncLane d;
+    d.init(s_w, woff, pack_state(base, 0, c0), hg);
+    uint32_t m = 0;
+    for (;;) {  // decode to the next checkpoint mark inside the subsequence, or to its end
+      const uint32_t mk = base + (m + 1) * kCkStep;
+      const bool cm = m < kCk && mk < end;
+      const uint32_t stop = cm ? mk : end;
+      while (d.pos < stop) d.step(tabs);
+      if (!cm) break;
+      s_ck[m][t] = pack_state(d.pos, d.z, d.c);
+      s_rem[m][t] = d.n;
+      ++m;
     }
-    for (int q = 0; q < m; ++q) s_rem[q][t] = n - s_rem[q][t];
-    E = pack_state(br.pos, z, c);
-    N = n;
+    for (uint32_t q = 0; q < m; ++q) s_rem[q][t] = d.n - s_rem[q][t];
+    E = pack_state(d.pos, d.z, d.c);
+    N = d.n;
   }
   s_E[t] = E;
   __syncthreads();
@@ -1025,12 +1024,12 @@ __device__ __forceinline__ uint32_t trace_on(const uint32_t *gw, uint32_t fwords
     // the subsequence's words, fetched together (independent loads), then decoded from LDS
     const uint32_t w0 = (uint32_t)(X >> 16) >> 5;
     for (uint32_t q = 0; q < kTraceWords; ++q) tw[q] = w0 + q < fwords ? gw[w0 + q] : 0u;
-    BitReader br;
-    br.init_words(tw, (uint32_t)(X >> 16), w0);
-    uint32_t z = (X >> 8) & 0xFF, c = X & 0xFF, n = 0;
+    SyncLane d;
+    d.init(tw, w0, X, hg);
     const uint32_t lim = min(ek, (w0 + kTraceWords - 4) * 32u);  // stays inside tw (binds only on corrupt data)
-    while (br.pos < lim) sync_step(br, z, c, n, hg, tabs, tabs + 3);
-    X = pack_state(br.pos, z, c);
+    while (d.pos < lim) d.step(tabs);
+    X = pack_state(d.pos, d.z, d.c);
+    const uint32_t n = d.n;
     const uint64_t at = tr0 + (uint64_t)w * 256 + k * L;
     rX[at + lane] = X;
     rC[at + lane] = n;
