@@ -257,24 +257,6 @@ __device__ __forceinline__ uint32_t long_code_len(uint32_t c16, const uint32_t *
          (c16 >= b.z);
 }
 
-// jdhuff.c jpeg_huff_decode with a kLook-bit first level
-__device__ __forceinline__ uint32_t huff_sym(BitReader &br, const HuffDec &t) {
-  const uint32_t e = t.fast[br.peek(kLook)];
-  uint32_t len = e >> 8, sym = e & 0xFF;
-  if (len == 0) {
-    const uint32_t c16 = br.peek(16);
-    len = long_code_len(c16, t.lim);
-    if (len > 16) {
-      len = 16;
-      sym = 0;  // corrupt code: jdhuff.c returns 0
-    } else {
-      sym = t.vals[(uint32_t)((int32_t)(c16 >> (16 - len)) + t.valoff[len]) & 255];
-    }
-  }
-  br.skip(len);
-  return sym;
-}
-
 __device__ __forceinline__ int extend(uint32_t v, uint32_t s) {  // jdhuff.h HUFF_EXTEND
   return v < (1u << (s - 1)) ? (int)v - (int)((1u << s) - 1) : (int)v;
 }
@@ -308,50 +290,67 @@ struct HuffGeom {
   __device__ __forceinline__ static T sel(const T *a, uint32_t k) { return k == 0 ? a[0] : k == 1 ? a[1] : a[2]; }
 };
 
-// Decode symbols from the reader's position until it reaches `end` (checked at symbol
-// boundaries).  State: z = next zigzag index of the current block (0 = DC next), c = its
-// block-in-MCU, blk = its block index (WRITE only), blocks = blocks completed.
-template <bool WRITE>
-__device__ __forceinline__ void decode_span(BitReader &br, uint32_t end, uint32_t &z, uint32_t &c,
-                                            uint32_t &blocks, const HuffGeom &g, const HuffDec *dcT,
-                                            const HuffDec *acT, uint32_t blk, int16_t *coef, int32_t *dcseq,
-                                            const uint64_t *dcbase) {
-  uint64_t dcb[3] = {0, 0, 0};
-  if (WRITE) {
-#pragma unroll
-    for (int k = 0; k < 3; ++k) dcb[k] = dcbase[k];
-  }
-  // One path for DC and AC symbols (a wave's lanes are at different places in their blocks;
-  // two paths meant both ran every step), and the MCU index kept as a counter instead of a
-  // division per DC symbol.
+// The write pass's decoder, on the short per-symbol step of SyncLane: the code and its extra bits are
+// consumed together, the bit buffer is refilled with selects, the block end and the table
+// switch are selects, so a symbol is one table read, its stores and no branch but the rare
+// long code.  Decodes from state X over staged LDS words until `end` (or the segment's last
+// block), storing coefficients (dense 64-entry rows, zigzag order) and DC differences
+// (jdhuff.c decode_mcu; an unmatched code reads as symbol 0 after 16 bits, a DC size over 16
+// as 16).
+__device__ __forceinline__ void write_span(const uint32_t *w, uint32_t woff, uint64_t X, uint32_t end,
+                                           const HuffGeom &g, const HuffDec *tabs, uint32_t blk, int16_t *coef,
+                                           int32_t *dcseq, const uint64_t *dcbase) {
+  const uint32_t p = (uint32_t)(X >> 16);
+  uint32_t wi = (p >> 5) - woff;
+  uint64_t buf = (((uint64_t)bswap32(w[wi]) << 32) | bswap32(w[wi + 1])) << (p & 31);
+  uint32_t nb = 64 - (p & 31), pos = p;
+  wi += 2;
+  uint32_t nxt = w[wi];
+  uint32_t z = (X >> 8) & 0xFF, c = X & 0xFF;
+  uint32_t k = g.comp(c);
   uint32_t mcu = blk / g.bpm;
-  while (br.pos < end) {
-    if (WRITE && blk >= g.nblocks) break;
-    br.refill();
-    const uint32_t k = g.comp(c);
+  uint64_t dcb[3];
+#pragma unroll
+  for (int q = 0; q < 3; ++q) dcb[q] = dcbase[q];
+  while (pos < end && blk < g.nblocks) {
+    const bool f = nb <= 32;
+    buf |= f ? (uint64_t)bswap32(nxt) << (32 - nb) : 0ull;
+    nb += f ? 32u : 0u;
+    wi += f ? 1u : 0u;
+    nxt = w[wi];
     const bool dc = z == 0;
-    const uint32_t sym = huff_sym(br, dc ? dcT[k] : acT[k]);
+    const HuffDec &T = tabs[dc ? k : 3 + k];
+    const uint32_t e = T.fast[(uint32_t)(buf >> (64 - kLook))];
+    uint32_t len = e >> 8, sym = e & 0xFF;
+    if (len == 0) {
+      const uint32_t c16 = (uint32_t)(buf >> 48);
+      len = long_code_len(c16, T.lim);
+      if (len > 16) {
+        len = 16;
+        sym = 0;
+      } else {
+        sym = T.vals[(uint32_t)((int32_t)(c16 >> (16 - len)) + T.valoff[len]) & 255];
+      }
+    }
     const uint32_t r = dc ? 0u : sym >> 4;
-    const uint32_t s = dc ? (sym > 16 ? 16u : sym) : (sym & 15);  // DC > 16: corrupt table
-    int v = 0;
-    if (s) {
-      v = extend(br.peek(s), s);
-      br.skip(s);
-    }
-    if (WRITE) {
-      if (dc)
-        dcseq[HuffGeom::sel(dcb, k) + (uint64_t)mcu * HuffGeom::sel(g.bpc, k) + (c - HuffGeom::sel(g.cfirst, k))] = v;
-      else if (s)
-        coef[(uint64_t)blk * 64 + (z + r < 63 ? z + r : 63)] = (int16_t)v;
-    }
-    z = dc ? 1u : s ? z + r + 1 : r == 15 ? z + 16 : 64u;
-    if (z >= 64) {
-      z = 0;
-      c = (c + 1 == g.bpm) ? 0 : c + 1;
-      mcu += c == 0 ? 1u : 0u;
-      ++blocks;
-      ++blk;
-    }
+    const uint32_t sz = dc ? (sym > 16 ? 16u : sym) : (sym & 15);
+    const uint64_t b2 = buf << len;
+    const int v = sz ? extend((uint32_t)(b2 >> (64 - sz)), sz) : 0;
+    buf = b2 << sz;
+    nb -= len + sz;
+    pos += len + sz;
+    if (dc)
+      dcseq[HuffGeom::sel(dcb, k) + (uint64_t)mcu * HuffGeom::sel(g.bpc, k) + (c - HuffGeom::sel(g.cfirst, k))] = v;
+    else if (sz)
+      coef[(uint64_t)blk * 64 + (z + r < 63 ? z + r : 63)] = (int16_t)v;
+    z = dc ? 1u : sz ? z + r + 1 : r == 15 ? z + 16 : 64u;
+    const bool eob = z >= 64;
+    const uint32_t c1 = c + 1 == g.bpm ? 0u : c + 1;
+    z = eob ? 0u : z;
+    mcu += eob && c1 == 0 ? 1u : 0u;
+    blk += eob ? 1u : 0u;
+    c = eob ? c1 : c;
+    k = g.comp(c);
   }
 }
 
@@ -383,7 +382,7 @@ __device__ __forceinline__ uint32_t sync_slow(const BR &br, const HuffSync &t, b
 }
 
 // One Huffman symbol of the sync decode: the same bits and zigzag / block progression as
-// decode_span, through one combined lookup (HuffSync) instead of symbol + extra-bits steps.
+// write_span, through one combined lookup (HuffSync) instead of symbol + extra-bits steps.
 template <typename BR>
 __device__ __forceinline__ void sync_step(BR &br, uint32_t &z, uint32_t &c, uint32_t &blocks,
                                           const HuffGeom &g, const HuffSync *dcT, const HuffSync *acT) {
@@ -1307,13 +1306,9 @@ __global__ __launch_bounds__(256) void k_write(const DecSeg *__restrict__ sg, co
   const uint32_t gi = S.sub0 + i;
   const uint64_t st = i == 0 ? 0 : exits[gi - 1];
   const uint32_t end = (i + 1 == nsub) ? nbits : (i + 1) * kSubBits;
-  BitReader br;
-  br.init_words(s_w, (uint32_t)(st >> 16), woff);
-  uint32_t z = (st >> 8) & 0xFF, c = st & 0xFF, blocks = 0;
   HuffGeom hg(F.g);
   hg.nblocks = S.nblocks;  // the segment's blocks (a restart interval: its whole MCUs)
-  decode_span<true>(br, end, z, c, blocks, hg, tabs, tabs + 3, bstart[gi], coef + S.blk0 * 64, dcseq,
-                    S.dcbase);
+  write_span(s_w, woff, st, end, hg, tabs, bstart[gi], coef + S.blk0 * 64, dcseq, S.dcbase);
 }
 
 // The write pass with 4 lanes per subsequence, for the pass-based sync (k_sync), whose
@@ -1360,13 +1355,9 @@ __global__ __launch_bounds__(256) void k_write4(const DecSeg *__restrict__ sg, c
       stop = (uint32_t)(cki[m] >> 16);
       break;
     }
-  BitReader br;
-  br.init_words(s_w, (uint32_t)(st >> 16), woff);
-  uint32_t z = (st >> 8) & 0xFF, c = st & 0xFF, blocks = 0;
   HuffGeom hg(F.g);
   hg.nblocks = S.nblocks;
-  decode_span<true>(br, stop, z, c, blocks, hg, tabs, tabs + 3, bstart[gi] + before, coef + S.blk0 * 64, dcseq,
-                    S.dcbase);
+  write_span(s_w, woff, st, stop, hg, tabs, bstart[gi] + before, coef + S.blk0 * 64, dcseq, S.dcbase);
 }
 
 // ---- decoder: IDCT -------------------------------------------------------------------------
