@@ -160,7 +160,7 @@ def pmc_traffic(args, device=0):
 # speculative sync at 1080p), for the per-stage issue fractions
 JPEG_STAGE_KERNELS = {
     "unstuff": ("k_unstuff_count", "k_unstuff_write"),
-    "huffman_sync": ("k_spec", "k_wglink", "k_resolve", "k_finalize", "k_sync"),
+    "huffman_sync": ("k_spec", "k_wglink", "k_resolve", "k_finalize", "k_sync", "k_syncg"),
     "huffman_write": ("k_write", "k_write4"),
     "dc_idct": ("k_idct",),
     "color_invert": ("k_color",),

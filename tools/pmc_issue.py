@@ -26,8 +26,8 @@ from collections import defaultdict
 SIMDS, CUS, XCDS = 1024, 256, 8
 
 
-def short(name):
-    return re.sub(r"\(.*", "", name.replace("(anonymous namespace)::", "")).split("::")[-1]
+def short(name):  # "k_fdct" for "void vf::jpeg::(anonymous namespace)::k_fdct<2, 1, false>(...)"
+    return re.sub(r"<.*", "", re.sub(r"\(.*", "", name.replace("(anonymous namespace)::", "")).split("::")[-1])
 
 
 def per_kernel(counters_csv, durations_csv="", min_waves=1000):
