@@ -286,7 +286,7 @@ int Codec::prepare_decode(const uint8_t *const *jpegs, const size_t *sizes, int 
     Parsed &P = parsed[(size_t)f];
     std::string &e = ferr[(size_t)f];
     DecFrame &F = dfr_[(size_t)f];
-    parse_frame(jpegs[f], sizes[f], max_pixels_, &P, &F.g, F.dc, F.ac, F.sdc, F.sac, &e);  // vf_jpeg_parse.h
+    parse_frame(jpegs[f], sizes[f], max_pixels_, &P, &F.g, F.dc, F.ac, F.sdc, F.sac, F.spair, &e);  // vf_jpeg_parse.h
     for (int c = 0; c < P.ncomp && e.empty(); ++c) std::memcpy(F.q[c], P.qt[P.tq[c]], sizeof F.q[c]);
   });
   for (int f = 0; f < n; ++f)

@@ -389,7 +389,7 @@ __device__ __forceinline__ void sync_step(BR &br, uint32_t &z, uint32_t &c, uint
   br.refill();
   const uint32_t k = g.comp(c);
   const HuffSync &T = z == 0 ? dcT[k] : acT[k];
-  uint32_t e = T.sfast[br.peek(kLook)];
+  uint32_t e = T.sfast[br.peek(kLook)] & 0xFFFF;  // one symbol (SyncLane also takes pairs)
   if (!e) e = sync_slow(br, T, z == 0);
   br.skip(e & 0xFF);
   z += e >> 8;
@@ -407,6 +407,43 @@ __device__ __forceinline__ void sync_step(BR &br, uint32_t &z, uint32_t &c, uint
 // sync_step's branchy form (refill, DC / AC, block end) measured ~530-700 shader cycles per
 // symbol for a lone lane on an idle GPU (tools/build_syncg_stats.sh).  Same bits, zigzag and
 // block progression as sync_step.
+// The span sync's LDS tables: DecFrame's HuffSync entries with, in the AC tables, the pair
+// entry (DecFrame::spair) in the upper 16 bits of each word.  The speculative kernels read
+// HuffSync itself (single-symbol entries only: with 32-bit entries k_spec's LDS cost it a
+// workgroup per CU, 200 -> 218 us at 1080p).
+struct SyncTab32 {
+  alignas(16) uint32_t lim[8];
+  uint32_t sfast[1 << kLook];
+  int32_t valoff[18];
+  uint8_t vals[256];
+};
+template <typename Tab>
+struct SyncPairs {
+  static constexpr bool v = false;
+};
+template <>
+struct SyncPairs<SyncTab32> {
+  static constexpr bool v = true;
+};
+
+// F's six sync tables (sdc[3], sac[3]) with the AC pairs into LDS, then a barrier (which also
+// publishes whatever the caller staged before the call)
+__device__ __forceinline__ void load_sync_tabs32(const DecFrame &F, SyncTab32 *tabs) {
+  for (uint32_t j = threadIdx.x; j < 6 * (8 + 18 + 64); j += blockDim.x) {
+    const uint32_t t = j / 90, i = j - t * 90;
+    const HuffSync &S = t < 3 ? F.sdc[t] : F.sac[t - 3];
+    if (i < 8) tabs[t].lim[i] = S.lim[i];
+    else if (i < 26) tabs[t].valoff[i - 8] = S.valoff[i - 8];
+    else reinterpret_cast<uint32_t *>(tabs[t].vals)[i - 26] = reinterpret_cast<const uint32_t *>(S.vals)[i - 26];
+  }
+  for (uint32_t j = threadIdx.x; j < 6 * (1 << kLook); j += blockDim.x) {
+    const uint32_t t = j >> kLook, i = j & ((1 << kLook) - 1);
+    tabs[t].sfast[i] = t < 3 ? (uint32_t)F.sdc[t].sfast[i] : F.sac[t - 3].sfast[i] | ((uint32_t)F.spair[t - 3][i] << 16);
+  }
+  __syncthreads();
+}
+
+template <typename Tab>
 struct SyncLane {
   const uint32_t *w;  // staged words, minus woff
   uint64_t buf;       // next bits, left-aligned
@@ -428,16 +465,19 @@ struct SyncLane {
     n = 0;
     cpack = hg.cpack;
     bpm = hg.bpm;
-    toff = __umul24((cpack >> (2 * c)) & 3, (uint32_t)sizeof(HuffSync));
+    toff = __umul24((cpack >> (2 * c)) & 3, (uint32_t)sizeof(Tab));
   }
-  __device__ __forceinline__ void step(const HuffSync *tabs) {
+  // one step: a symbol, or two (an AC table's pair entry) when the first leaves the block open
+  // and ends before `stop` -- so a mark's state is still taken at the first symbol boundary at
+  // or past it, whichever symbol a decoder's pairing started from
+  __device__ __forceinline__ void step(const Tab *tabs, uint32_t stop) {
     const bool f = nb <= 32;
     buf |= f ? (uint64_t)bswap32(nxt) << (32 - nb) : 0ull;
     nb += f ? 32u : 0u;
     wi += f ? 1u : 0u;
     nxt = w[wi];
-    const HuffSync &T = *reinterpret_cast<const HuffSync *>(reinterpret_cast<const char *>(tabs) + toff +
-                                                             (z == 0 ? 0u : 3u * (uint32_t)sizeof(HuffSync)));
+    const Tab &T = *reinterpret_cast<const Tab *>(reinterpret_cast<const char *>(tabs) + toff +
+                                                   (z == 0 ? 0u : 3u * (uint32_t)sizeof(Tab)));
     uint32_t e = T.sfast[(uint32_t)(buf >> (64 - kLook))];
     if (!e) {  // a code longer than kLook bits: jdhuff.c's slow path (rare)
       const uint32_t c16 = (uint32_t)(buf >> 48);
@@ -454,17 +494,19 @@ struct SyncLane {
       }
       e = (adv << 8) | (len + extra);
     }
-    const uint32_t len = e & 0xFF;
+    const uint32_t len1 = e & 0xFF, adv1 = (e >> 8) & 0xFF;
+    const bool two = SyncPairs<Tab>::v && (e >> 16) != 0 && z + adv1 < 64 && pos + len1 < stop;
+    const uint32_t len = two ? (e >> 16) & 0xFF : len1;  // pair word: (advance << 24) | (length << 16)
     buf <<= len;
     nb -= len;
     pos += len;
-    z += e >> 8;
+    z += two ? e >> 24 : adv1;
     const bool eob = z >= 64;
     const uint32_t c1 = c + 1 == bpm ? 0u : c + 1;
     c = eob ? c1 : c;
     z = eob ? 0u : z;
     n += eob ? 1u : 0u;
-    toff = __umul24((cpack >> (2 * c)) & 3, (uint32_t)sizeof(HuffSync));
+    toff = __umul24((cpack >> (2 * c)) & 3, (uint32_t)sizeof(Tab));
   }
 };
 
@@ -617,8 +659,8 @@ __global__ __launch_bounds__(256) void k_sync(const DecSeg *__restrict__ sg, con
 __device__ __forceinline__ uint64_t sync_span(const uint32_t *words, uint32_t woff, uint64_t X, uint32_t i0, uint32_t ng,
                                               uint32_t nsub, uint32_t nbits, uint64_t gi0, bool check, uint64_t last,
                                               uint64_t *exits, uint32_t *cnts, uint64_t *ck, uint32_t *ckrem,
-                                              const HuffGeom &hg, const HuffSync *tabs) {
-  SyncLane d;
+                                              const HuffGeom &hg, const SyncTab32 *tabs) {
+  SyncLane<SyncTab32> d;
   d.init(words, woff, X, hg);
   uint32_t j = 0, bj = i0 * kSubBits;
   uint32_t ej = i0 + 1 >= nsub ? nbits : bj + kSubBits;  // end of subsequence j
@@ -630,7 +672,7 @@ __device__ __forceinline__ uint64_t sync_span(const uint32_t *words, uint32_t wo
   uint32_t n0 = 0, n1 = 0, n2 = 0;  // blocks at the checkpoints written in this decode
   static_assert(kCk == 3, "n0..n2");
   for (;;) {
-    while (d.pos < mk) d.step(tabs);
+    while (d.pos < mk) d.step(tabs, mk);
     const uint64_t st = pack_state(d.pos, d.z, d.c);
     const uint64_t gj = gi0 + j;
     if (m < kCk) {
@@ -687,7 +729,7 @@ __global__ __launch_bounds__(256) void k_syncg(const DecSeg *__restrict__ sg, co
                                                const uint32_t *us_len, uint64_t *exits, uint32_t *cnts, uint64_t *used,
                                                uint64_t *ck, uint32_t *ckrem, uint32_t *changed, int pass) {
   constexpr uint32_t T = syncg_threads(G), kWords = kSyncgStage ? T * G * (kSubBits / 32) + kSpecPadWords : 1;
-  __shared__ HuffSync tabs[6];
+  __shared__ SyncTab32 tabs[6];
   __shared__ uint64_t s_exit[T];
   __shared__ uint32_t s_w[kWords];
   const DecSeg S = sg[blockIdx.y];  // by value: held in scalar registers
@@ -701,7 +743,7 @@ __global__ __launch_bounds__(256) void k_syncg(const DecSeg *__restrict__ sg, co
     for (uint32_t i = threadIdx.x; i < kWords; i += T) s_w[i] = woff + i < fwords ? gw[woff + i] : 0u;
   }
   const uint32_t *words = kSyncgStage ? s_w : gw;
-  load_sync_tables(F, tabs);  // its barrier also publishes s_w
+  load_sync_tabs32(F, tabs);  // its barrier also publishes s_w
   const HuffGeom hg(F.g);
   const uint32_t t = threadIdx.x;
   const uint32_t nbits = us_len[blockIdx.y] * 8u, nsub = (nbits + kSubBits - 1) / kSubBits;
@@ -785,7 +827,7 @@ template <typename CK, typename REM>
 __device__ __forceinline__ uint32_t spec_link(const uint32_t *words, uint32_t woff, uint64_t X, uint32_t base,
                                               uint32_t end, bool last, const HuffGeom &hg, const HuffSync *tabs, CK ck,
                                               REM rem, uint32_t *count, uint64_t *endst) {
-  SyncLane d;
+  SyncLane<HuffSync> d;
   d.init(words, woff, X, hg);
   uint32_t m = 0;
   while (m < kCk && base + (m + 1) * kCkStep <= d.pos) ++m;
@@ -793,7 +835,7 @@ __device__ __forceinline__ uint32_t spec_link(const uint32_t *words, uint32_t wo
     const uint32_t mk = base + (m + 1) * kCkStep;
     const bool cm = !last && m < kCk && mk < end;
     const uint32_t stop = cm ? mk : end;
-    while (d.pos < stop) d.step(tabs);
+    while (d.pos < stop) d.step(tabs, stop);
     if (!cm) break;
     const uint64_t st = pack_state(d.pos, d.z, d.c);
     for (uint32_t c2 = 0; c2 < hg.bpm; ++c2)
@@ -843,14 +885,14 @@ __global__ __launch_bounds__(256) void k_spec(const DecSeg *__restrict__ sg, con
 #pragma unroll
   for (int m = 0; m < kCk; ++m) s_ck[m][t] = kNoCk;
   if (live) {
-    SyncLane d;
+    SyncLane<HuffSync> d;
     d.init(s_w, woff, pack_state(base, 0, c0), hg);
     uint32_t m = 0;
     for (;;) {  // decode to the next checkpoint mark inside the subsequence, or to its end
       const uint32_t mk = base + (m + 1) * kCkStep;
       const bool cm = m < kCk && mk < end;
       const uint32_t stop = cm ? mk : end;
-      while (d.pos < stop) d.step(tabs);
+      while (d.pos < stop) d.step(tabs, stop);
       if (!cm) break;
       s_ck[m][t] = pack_state(d.pos, d.z, d.c);
       s_rem[m][t] = d.n;
@@ -1023,10 +1065,10 @@ __device__ __forceinline__ uint32_t trace_on(const uint32_t *gw, uint32_t fwords
     // the subsequence's words, fetched together (independent loads), then decoded from LDS
     const uint32_t w0 = (uint32_t)(X >> 16) >> 5;
     for (uint32_t q = 0; q < kTraceWords; ++q) tw[q] = w0 + q < fwords ? gw[w0 + q] : 0u;
-    SyncLane d;
+    SyncLane<HuffSync> d;
     d.init(tw, w0, X, hg);
     const uint32_t lim = min(ek, (w0 + kTraceWords - 4) * 32u);  // stays inside tw (binds only on corrupt data)
-    while (d.pos < lim) d.step(tabs);
+    while (d.pos < lim) d.step(tabs, lim);
     X = pack_state(d.pos, d.z, d.c);
     const uint32_t n = d.n;
     const uint64_t at = tr0 + (uint64_t)w * 256 + k * L;
@@ -1147,8 +1189,7 @@ __global__ __launch_bounds__(256) void k_resolve(const DecSeg *__restrict__ sg, 
     return;
   }
   const uint32_t lastk = NS - 1;  // every workgroup but the frame's last is full
-  // the sync tables' copy is issued with the transition loads; one barrier publishes both
-  {
+  {  // the sync tables' copy is issued with the transition loads; one barrier publishes both
     const uint32_t *src = reinterpret_cast<const uint32_t *>(&F.sdc[0]);
     uint32_t *dst = reinterpret_cast<uint32_t *>(tabs);
     for (uint32_t j = threadIdx.x; j < 6 * sizeof(HuffSync) / 4; j += 256) dst[j] = src[j];

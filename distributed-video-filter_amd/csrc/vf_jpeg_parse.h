@@ -141,6 +141,19 @@ inline bool decode_table(const uint8_t bits[17], const uint8_t *vals, bool dc, H
 }
 
 // jdhuff.c decode semantics folded into one lookup for the sync decoders (see HuffSync)
+inline void sync_entry(uint32_t f, bool dc, uint32_t *len, uint32_t *adv) {  // code + extra bits, zigzag advance
+  const uint32_t sym = f & 0xFF;
+  uint32_t extra;
+  if (dc) {
+    extra = sym > 16 ? 16 : sym;
+    *adv = 1;
+  } else {
+    extra = sym & 15;
+    *adv = extra ? (sym >> 4) + 1 : ((sym >> 4) == 15 ? 16 : 64);
+  }
+  *len = (f >> 8) + extra;
+}
+
 inline void sync_table(const HuffDec &t, bool dc, HuffSync *s) {
   std::memcpy(s->lim, t.lim, sizeof s->lim);
   std::memcpy(s->maxcode, t.maxcode, sizeof s->maxcode);
@@ -148,20 +161,27 @@ inline void sync_table(const HuffDec &t, bool dc, HuffSync *s) {
   std::memcpy(s->vals, t.vals, sizeof s->vals);
   for (int i = 0; i < (1 << kLook); ++i) {
     const uint32_t f = t.fast[i];
-    if (!f) {
-      s->sfast[i] = 0;
-      continue;
-    }
-    const uint32_t len = f >> 8, sym = f & 0xFF;
-    uint32_t extra, adv;
-    if (dc) {
-      extra = sym > 16 ? 16 : sym;
-      adv = 1;
-    } else {
-      extra = sym & 15;
-      adv = extra ? (sym >> 4) + 1 : ((sym >> 4) == 15 ? 16 : 64);
-    }
-    s->sfast[i] = (uint16_t)((adv << 8) | (len + extra));
+    uint32_t len = 0, adv = 0;
+    if (f) sync_entry(f, dc, &len, &adv);
+    s->sfast[i] = f ? (uint16_t)((adv << 8) | len) : 0;
+  }
+}
+
+// DecFrame::spair for one AC table: the next code must be whole inside the kLook - len bits
+// known after the first symbol, and its extra bits too
+inline void pair_table(const HuffDec &t, uint16_t *pair) {
+  for (int i = 0; i < (1 << kLook); ++i) {
+    pair[i] = 0;
+    const uint32_t f = t.fast[i];
+    if (!f) continue;
+    uint32_t len, adv;
+    sync_entry(f, false, &len, &adv);
+    if (len >= (uint32_t)kLook || adv >= 64) continue;
+    const uint32_t f2 = t.fast[((uint32_t)i << len) & ((1u << kLook) - 1)];
+    if (!f2 || (f2 >> 8) > (uint32_t)kLook - len) continue;
+    uint32_t len2, adv2;
+    sync_entry(f2, false, &len2, &adv2);
+    if (len + len2 <= (uint32_t)kLook) pair[i] = (uint16_t)(((adv + adv2) << 8) | (len + len2));
   }
 }
 
@@ -169,13 +189,15 @@ inline void sync_table(const HuffDec &t, bool dc, HuffSync *s) {
 // frames of a stream share their tables (one encoder, one set of settings), so a batch builds
 // each distinct table once per parsing thread instead of 6 times per frame (2 x 2^kLook
 // entries each; the table build was most of the host-side parse of a 480p batch).
-inline bool build_tables(const uint8_t bits[17], const uint8_t *vals, bool dc, HuffDec *t, HuffSync *s) {
+inline bool build_tables(const uint8_t bits[17], const uint8_t *vals, bool dc, HuffDec *t, HuffSync *s,
+                         uint16_t *pair = nullptr) {
   struct Entry {
     bool valid = false, dc = false;
     uint8_t bits[17];
     uint8_t vals[256];
     HuffDec t;
     HuffSync s;
+    uint16_t pair[1 << kLook];  // AC tables
   };
   static thread_local Entry cache[4];
   static thread_local int next = 0;
@@ -186,6 +208,7 @@ inline bool build_tables(const uint8_t bits[17], const uint8_t *vals, bool dc, H
     if (e.valid && e.dc == dc && std::memcmp(e.bits, bits, 17) == 0 && std::memcmp(e.vals, vals, (size_t)nvals) == 0) {
       std::memcpy(t, &e.t, sizeof *t);
       std::memcpy(s, &e.s, sizeof *s);
+      if (pair) std::memcpy(pair, e.pair, sizeof e.pair);
       return true;
     }
   if (!decode_table(bits, vals, dc, t)) return false;
@@ -199,6 +222,9 @@ inline bool build_tables(const uint8_t bits[17], const uint8_t *vals, bool dc, H
   std::memcpy(e.vals, vals, (size_t)nvals);
   std::memcpy(&e.t, t, sizeof *t);
   std::memcpy(&e.s, s, sizeof *s);
+  if (dc) std::memset(e.pair, 0, sizeof e.pair);
+  else pair_table(*t, e.pair);
+  if (pair) std::memcpy(pair, e.pair, sizeof e.pair);
   return true;
 }
 
@@ -449,7 +475,8 @@ inline bool check_segments(const uint8_t *jpeg, Parsed *P, const Geom &g, std::s
 // Everything the decoder's host side derives from one frame's bytes, in order: markers, the
 // size limits, geometry, restart layout, and the six Huffman tables (DecFrame's tables).
 inline bool parse_frame(const uint8_t *jpeg, size_t size, uint64_t max_pixels, Parsed *P, Geom *g,
-                        HuffDec dc[3], HuffDec ac[3], HuffSync sdc[3], HuffSync sac[3], std::string *err) {
+                        HuffDec dc[3], HuffDec ac[3], HuffSync sdc[3], HuffSync sac[3], uint16_t spair[3][1 << kLook],
+                        std::string *err) {
   if (!jpeg) {
     *err = "NULL JPEG buffer";
     return false;
@@ -463,7 +490,7 @@ inline bool parse_frame(const uint8_t *jpeg, size_t size, uint64_t max_pixels, P
   if (!check_segments(jpeg, P, *g, err)) return false;
   for (int c = 0; c < P->ncomp; ++c)
     if (!build_tables(P->dcbits[P->td[c]], P->dcvals[P->td[c]], true, &dc[c], &sdc[c]) ||
-        !build_tables(P->acbits[P->ta[c]], P->acvals[P->ta[c]], false, &ac[c], &sac[c])) {
+        !build_tables(P->acbits[P->ta[c]], P->acvals[P->ta[c]], false, &ac[c], &sac[c], spair[c])) {
       *err = "bad Huffman table";
       return false;
     }

@@ -103,6 +103,11 @@ struct DecFrame {
   uint16_t q[3][64];       // dequantisation per component, natural order
   HuffDec dc[3], ac[3];    // per component (kept adjacent: loaded into LDS as one block)
   HuffSync sdc[3], sac[3];  // the same, for the synchronisation decoders (adjacent too)
+  // AC pairs for the span sync: spair[k][next kLook bits] = (advance << 8) | length of an AC
+  // symbol of component k together with the one after it, when both codes and their extra bits
+  // lie inside the kLook bits (0: no pair); a step then moves over two symbols with one table
+  // read, unless the first ends the block or reaches a mark
+  uint16_t spair[3][1 << kLook];
   uint32_t flags;          // bit 0: fancy upsampling allowed; bits 1-2: k_color layout (0 other,
                            // 1 4:4:4, 2 chroma 2x1, 3 chroma 2x2; three components, full-size luma)
   uint64_t blk0;           // first block in the batch coefficient buffer

@@ -202,8 +202,9 @@ int main(int argc, char **argv) {
     Geom g;
     HuffDec dc[3], ac[3];
     HuffSync sdc[3], sac[3];
+    uint16_t spair[3][1 << kLook];
     std::string err;
-    if (parse_frame(c.data(), c.size(), kDefaultMaxPixels, &P, &g, dc, ac, sdc, sac, &err)) ++originals_ok;
+    if (parse_frame(c.data(), c.size(), kDefaultMaxPixels, &P, &g, dc, ac, sdc, sac, spair, &err)) ++originals_ok;
     else std::fprintf(stderr, "corpus file rejected: %s\n", err.c_str());
   }
   // the size limits on a known-good frame: its own pixel count passes, one less is refused,
@@ -222,7 +223,8 @@ int main(int argc, char **argv) {
       Geom g;
       HuffDec dc[3], ac[3];
       HuffSync sdc[3], sac[3];
-      return parse_frame(x.data(), x.size(), limit, &P, &g, dc, ac, sdc, sac, err);
+      uint16_t spair[3][1 << kLook];
+      return parse_frame(x.data(), x.size(), limit, &P, &g, dc, ac, sdc, sac, spair, err);
     };
     const uint64_t px = (uint64_t)((b[sof + 5] << 8) | b[sof + 6]) * (uint64_t)((b[sof + 7] << 8) | b[sof + 8]);
     std::string e1, e2, e3, e4;
@@ -248,9 +250,10 @@ int main(int argc, char **argv) {
     Geom g;
     HuffDec dc[3], ac[3];
     HuffSync sdc[3], sac[3];
+    uint16_t spair[3][1 << kLook];
     std::string err;
     const uint64_t limit = r.below(8) == 0 ? (uint64_t)r.below(1 << 20) + 1 : kDefaultMaxPixels;
-    if (parse_frame(buf, b.size(), limit, &P, &g, dc, ac, sdc, sac, &err)) {
+    if (parse_frame(buf, b.size(), limit, &P, &g, dc, ac, sdc, sac, spair, &err)) {
       ++accepted;
       if ((uint64_t)P.w * (uint64_t)P.h > limit || P.w > kMaxDimension || P.h > kMaxDimension) std::abort();
       sink += touch_layout(buf, b.size(), P, g);
@@ -279,7 +282,8 @@ int main(int argc, char **argv) {
     for (auto &v : vals) v = (uint8_t)r.next();
     HuffDec t;
     HuffSync s;
-    if (build_tables(bits, vals, r.below(2) == 0, &t, &s)) ++tables_ok;
+    uint16_t pr[1 << kLook];
+    if (build_tables(bits, vals, r.below(2) == 0, &t, &s, pr)) ++tables_ok;
     else ++tables_bad;
   }
   std::printf("{\"cases\": %ld, \"accepted\": %ld, \"rejected\": %ld, \"too_big\": %ld, \"header_ok\": %ld, "
