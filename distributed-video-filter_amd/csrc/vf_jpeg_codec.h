@@ -150,6 +150,8 @@ class Codec {
   uint64_t max_pixels_ = kDefaultMaxPixels;
   hipStream_t s_ = nullptr;
   hipEvent_t ev_[10] = {};
+  bool stage_events_ = false;  // record ev_[0..8] between the stages (bench_invert's breakdown only)
+  hipError_t stage_event(int i) { return stage_events_ ? hipEventRecord(ev_[i], s_) : hipSuccess; }
   hipEvent_t done_ = nullptr;  // the last call's downloads have landed
 
   // decode layout

@@ -465,7 +465,7 @@ int Codec::run_decode(int bgr, bool invert, std::string *err) {
   const DecSeg *sg = d_dsg_.as<DecSeg>();
   const ScanSeg *segs = d_segs_.as<ScanSeg>();
   const int ns = dnseg_;
-  CK(hipEventRecord(ev_[0], s_));
+  CK(stage_event(0));
   // 1. unstuff
   CK(dec_unstuff_count(sg, ns, dmax_tiles_, d_in_.as<uint8_t>(), d_tile_.as<uint32_t>(), s_));
   uint32_t *us_len = d_totals_.as<uint32_t>();  // totals of scan segments [0, ns)
@@ -473,7 +473,7 @@ int Codec::run_decode(int bgr, bool invert, std::string *err) {
               d_tsum_.as<uint32_t>(), us_len, false, s_));
   CK(dec_unstuff_write(sg, ns, dmax_tiles_, d_in_.as<uint8_t>(), d_tile_.as<uint32_t>(), us_len,
                        d_us_.as<uint8_t>(), s_));
-  CK(hipEventRecord(ev_[1], s_));
+  CK(stage_event(1));
   // 2. synchronise the subsequence entry states: speculative (one pass, one flag read), with
   // the pass-based sync as the fallback when a link did not rejoin (VF_JPEG_SYNC=pass forces it)
   // VF_JPEG_SYNC = spec | pass | auto (default).  auto: speculative for frames of up to
@@ -575,7 +575,7 @@ int Codec::run_decode(int bgr, bool invert, std::string *err) {
                  (unsigned long long)spec_calls_, (unsigned long long)spec_fallbacks_, pass, st[3], st[1], st[2], st[0],
                  (dmax_sub_ + 255) / 256 * (uint32_t)ns);
   }
-  CK(hipEventRecord(ev_[2], s_));
+  CK(stage_event(2));
   sync_spec_ = use_spec;
   sync_last_ = last;
   sync_g_ = sync_g;
@@ -633,15 +633,15 @@ int Codec::run_decode_post(int bgr, bool invert, std::string *err) {
   else
     CK(dec_write(sg, fr, ns, dmax_sub_, d_us_.as<uint8_t>(), us_len, d_exit_[last].as<uint64_t>(),
                  d_bstart_.as<uint32_t>(), d_coef_.as<int16_t>(), d_dcseq_.as<int32_t>(), s_));
-  CK(hipEventRecord(ev_[3], s_));
+  CK(stage_event(3));
   // 4. DC prediction (inclusive scan per component sequence)
   CK(scan_i32(segs + 2 * ns, ndcseg_, dc_max_tiles_, d_dcseq_.as<int32_t>(), d_dcseq_.as<int32_t>(),
               d_tsum_.as<int32_t>(), nullptr, true, s_));
   // 5. IDCT, 6. upsample + colour (+ invert)
   CK(dec_idct(fr, n, dmax_blocks_, d_coef_.as<int16_t>(), d_dcseq_.as<int32_t>(), d_planes_.as<uint8_t>(), s_));
-  CK(hipEventRecord(ev_[4], s_));
+  CK(stage_event(4));
   CK(dec_color(fr, n, dmax_w_, dmax_h_, d_planes_.as<uint8_t>(), d_pix_.as<uint8_t>(), bgr, invert ? 1 : 0, s_));
-  CK(hipEventRecord(ev_[5], s_));
+  CK(stage_event(5));
   return kOk;
 }
 
@@ -773,7 +773,7 @@ int Codec::run_encode(int bgr, bool fastdct, std::string *err) {
   const EncTables *tab = d_etab_.as<EncTables>();
   const ScanSeg *segs = d_esegs_.as<ScanSeg>();
   const int n = en_;
-  CK(hipEventRecord(ev_[6], s_));
+  CK(stage_event(6));
   CK(enc_fdct(fr, n, emax_blocks_, tab, d_pix_.as<uint8_t>(), d_dcq_.as<int16_t>(), d_acbits_.as<uint32_t>(),
               d_acscr_.as<uint32_t>(), bgr, fastdct ? 1 : 0, kSampH[esub_], kSampV[esub_], s_));
   CK(enc_len(fr, n, emax_blocks_, tab, d_dcq_.as<int16_t>(), d_acbits_.as<uint32_t>(), d_bits_.as<uint32_t>(),
@@ -783,7 +783,7 @@ int Codec::run_encode(int bgr, bool fastdct, std::string *err) {
               d_etsum_.as<uint32_t>(), total_bits, false, s_));
   CK(enc_pack(fr, n, emax_blocks_, d_pre_.as<uint32_t>(), d_acbits_.as<uint32_t>(), d_acscr_.as<uint32_t>(),
               d_bitoff_.as<uint32_t>(), total_bits, d_stream_.as<uint8_t>(), s_));
-  CK(hipEventRecord(ev_[7], s_));
+  CK(stage_event(7));
   CK(enc_ff_count(fr, n, emax_tiles_, total_bits, d_stream_.as<uint8_t>(), d_ffcnt_.as<uint32_t>(), s_));
   uint32_t *nff = d_etotals_.as<uint32_t>() + n;
   CK(scan_u32(segs + n, n, (emax_tiles_ + kScanTile - 1) / kScanTile, d_ffcnt_.as<uint32_t>(),
@@ -791,7 +791,7 @@ int Codec::run_encode(int bgr, bool fastdct, std::string *err) {
   CK(enc_ff_write(fr, n, emax_tiles_, total_bits, d_stream_.as<uint8_t>(), d_ffcnt_.as<uint32_t>(), nff,
                   d_hdr_.as<uint8_t>(), d_out_.as<uint8_t>(), d_outsize_.as<uint64_t>(), s_));
   CK(enc_compact(fr, n, d_outsize_.as<uint64_t>(), d_out_.as<uint8_t>(), d_pack_.as<uint8_t>(), s_));
-  CK(hipEventRecord(ev_[8], s_));
+  CK(stage_event(8));
   return kOk;
 }
 
@@ -1093,21 +1093,33 @@ int Codec::bench_invert(const uint8_t *const *jpegs, const size_t *jsizes, int n
   float acc[8] = {0};
   double total_ms = 0;
   int passes = 0;
-  for (int it = 0; it < iters; ++it) {
-    CK(hipStreamSynchronize(s_));
-    const auto t0 = std::chrono::steady_clock::now();
-    if ((rc = run_decode(1, true, err))) return rc;
-    if ((rc = run_encode(1, fast, err))) return rc;
-    CK(hipStreamSynchronize(s_));
-    total_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    passes += sync_passes_;
-    // stage times: unstuff, sync, write, dc+idct, colour, fdct+huff, stuff
-    const int pairs[7][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 4}, {4, 5}, {6, 7}, {7, 8}};
-    for (int i = 0; i < 7; ++i) {
-      float t = 0.f;
-      if (hipEventElapsedTime(&t, ev_[pairs[i][0]], ev_[pairs[i][1]]) == hipSuccess) acc[i] += t;
+  // the timed iterations run as the product does (no stage events: each costs ~5 us of GPU
+  // time between kernels, ~45 us per batch); then, for the stage breakdown, as many again with
+  // the events recorded
+  for (int pass = 0; pass < (stage_ms ? 2 : 1); ++pass) {
+    stage_events_ = pass == 1;
+    for (int it = 0; it < iters; ++it) {
+      CK(hipStreamSynchronize(s_));
+      const auto t0 = std::chrono::steady_clock::now();
+      if ((rc = run_decode(1, true, err)) || (rc = run_encode(1, fast, err))) {
+        stage_events_ = false;
+        return rc;
+      }
+      CK(hipStreamSynchronize(s_));
+      if (pass == 0) {
+        total_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        passes += sync_passes_;
+        continue;
+      }
+      // stage times: unstuff, sync, write, dc+idct, colour, fdct+huff, stuff
+      const int pairs[7][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 4}, {4, 5}, {6, 7}, {7, 8}};
+      for (int i = 0; i < 7; ++i) {
+        float t = 0.f;
+        if (hipEventElapsedTime(&t, ev_[pairs[i][0]], ev_[pairs[i][1]]) == hipSuccess) acc[i] += t;
+      }
     }
   }
+  stage_events_ = false;
   if ((rc = queue_decode_check(err))) return rc;
   CK(hipStreamSynchronize(s_));
   rc = check_decode(err);

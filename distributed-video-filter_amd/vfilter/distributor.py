@@ -634,8 +634,16 @@ class Distributor:
 
     # ---- dispatch (distributor.py:205-251) ------------------------------------------------
     def handle_distribute_requests(self):
-        poll_ms = 10 if self.policy == "latest" else 1
         while self.running:
+            # while a worker holds unserved credit, frames committed during the socket wait
+            # must not wait out a whole poll: 0.2 ms then (1 ms, or the reference's 10 ms under
+            # "latest", otherwise)
+            if self.policy == "latest":
+                poll_ms = 10
+            else:
+                with self._lock:
+                    hungry = any(p.alive and p.requests for p in self._peers.values())
+                poll_ms = 0.2 if hungry else 1
             try:
                 self.dispatch_step(poll_ms)
             except BlockingIOError:
@@ -644,7 +652,7 @@ class Distributor:
                 print(f"Error handling distribute request: {e}")
                 continue
 
-    def dispatch_step(self, poll_ms: int = 0) -> None:
+    def dispatch_step(self, poll_ms: float = 0) -> None:
         """One iteration of the dispatch loop (distributor.py:209-248): move at most one queued
         frame into the latest-wins slot, poll the dispatch socket for ``poll_ms`` and answer
         what arrived, evict workers past their deadline, serve outstanding requests."""

@@ -237,6 +237,12 @@ class _Connection:
 # role objects used by the distributor and the worker
 # ---------------------------------------------------------------------------------------
 
+def _zmq_ms(timeout_ms: float) -> int:
+    """zmq_poll takes whole milliseconds: a sub-millisecond wait (the runtime's short polls while
+    batches are in flight) becomes 1 ms there instead of 0, which would spin."""
+    return 0 if timeout_ms <= 0 else max(1, int(-(-timeout_ms // 1)))
+
+
 class RouterEnd:
     """Distributor dispatch socket (reference: ROUTER bind, distributor.py:30-31)."""
 
@@ -252,8 +258,8 @@ class RouterEnd:
             self.sock = _Listener(host, port)
             self.port = self.sock.port
 
-    def poll(self, timeout_ms: int) -> bool:
-        return bool(self.sock.poll(timeout_ms))
+    def poll(self, timeout_ms: float) -> bool:
+        return bool(self.sock.poll(_zmq_ms(timeout_ms) if self.kind == "zmq" else timeout_ms))
 
     def recv(self) -> Tuple[bytes, Optional[List[bytes]]]:
         """(peer, parts); parts is None when "tcp" saw the peer disconnect (the distributor
@@ -291,8 +297,8 @@ class PullEnd:
             self.sock = _Listener(host, port)
             self.port = self.sock.port
 
-    def poll(self, timeout_ms: int) -> bool:
-        return bool(self.sock.poll(timeout_ms))
+    def poll(self, timeout_ms: float) -> bool:
+        return bool(self.sock.poll(_zmq_ms(timeout_ms) if self.kind == "zmq" else timeout_ms))
 
     def recv(self) -> List[bytes]:
         if self.kind == "zmq":
@@ -328,8 +334,8 @@ class DealerEnd:
         else:
             self.sock.send(parts)
 
-    def poll(self, timeout_ms: int) -> bool:
-        return bool(self.sock.poll(timeout_ms))
+    def poll(self, timeout_ms: float) -> bool:
+        return bool(self.sock.poll(_zmq_ms(timeout_ms) if self.kind == "zmq" else timeout_ms))
 
     def recv(self) -> List[bytes]:
         if self.kind == "zmq":

@@ -321,7 +321,9 @@ class Worker:
                 self._collect_jobs(jobs, self.inflight)
                 if len(jobs) >= self.inflight:
                     continue
-                if not self.dealer_socket.poll(1 if jobs else 10):
+                # with batches in flight, wake every 0.2 ms to collect the one that finished
+                # (a 1 ms wait here delayed every result by up to a batch's GPU time)
+                if not self.dealer_socket.poll(0.2 if jobs else 10):
                     continue
                 parts = self.dealer_socket.recv()
                 start_time = time.time()
