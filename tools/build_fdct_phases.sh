@@ -30,9 +30,7 @@ pre = pre.replace("constexpr uint32_t kFdctGroup = 8;",
     "constexpr uint32_t kFdctGroup = 8;")
 krep("  if (blockIdx.x * 4 >= ngroups * bpm) return;\n", "  if (blockIdx.x * 4 >= ngroups * bpm) return;\n  const long long _c0 = clock64();\n")
 krep("  const uint8_t *img = pix + F.img_off;\n", "  PH(0);\n  const uint8_t *img = pix + F.img_off;\n")
-krep("    for (int j = 0; j < 8; ++j) ws[slot][r][j] = v[j];\n  }\n  __syncthreads();\n",
-     "    for (int j = 0; j < 8; ++j) ws[slot][r][j] = v[j];\n  }\n  PH(1);\n  __syncthreads();\n  PH(2);\n")
-krep("    if (FAST) fdct_ifast_line(v);\n    else fdct_islow_line(v, 0);\n", "    PH(7);\n    if (FAST) fdct_ifast_line(v);\n    else fdct_islow_line(v, 0);\n")
+krep("  __syncthreads();  // publishes the table image\n", "  PH(1);\n  __syncthreads();  // publishes the table image\n  PH(2);\n")
 krep("  // From here on a block's 8 lanes", "  PH(3);\n  // From here on a block's 8 lanes")
 krep("  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, \"wavefront\");  // the group's list",
      "  PH(4);\n  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, \"wavefront\");  // the group's list")
@@ -50,7 +48,7 @@ rep("hipError_t enc_fdct(", """static void fdct_stats_print(hipStream_t s) {
   (void)hipStreamSynchronize(s);
   (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_fdct_ph), sizeof h);
   const double w = h[15] ? (double)h[15] : 1.0;
-  std::fprintf(stderr, "[fdct phases] waves %llu  avg cycles from start: tables %.0f pixels+colour %.0f pass1 %.0f barrier %.0f pass2 %.0f list %.0f rounds %.0f end %.0f\\n",
+  std::fprintf(stderr, "[fdct phases] waves %llu  avg cycles from start: setup %.0f unused %.0f pass1 %.0f barrier %.0f pass2 %.0f list %.0f rounds %.0f end %.0f\\n",
                h[15], h[0] / w, h[7] / w, h[1] / w, h[2] / w, h[3] / w, h[4] / w, h[5] / w, h[6] / w);
   unsigned long long z[16] = {0};
   (void)hipMemcpyToSymbol(HIP_SYMBOL(g_fdct_ph), z, sizeof z);
