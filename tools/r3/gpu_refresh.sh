@@ -17,7 +17,7 @@ cp "$(find gpurun_out/prof_bench -name '*kernel_stats.csv' | head -1)" gpurun_ou
 rm -f gpurun_out/jpeg.jsonl
 timeout -k 10 300 python -u tools/jpeg_bench.py --sizes 480p,1080p,4k --batch 32 --iters 20 --cpu-seconds 5 --out gpurun_out/jpeg.jsonl > gpurun_out/jpeg.log 2>&1 || { echo JPEG_FAILED; tail -30 gpurun_out/jpeg.log; exit 1; }
 rm -rf gpurun_out/prof_js
-timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_js -o js -- python3 tools/jpeg_bench.py --sizes 1080p --batch 32 --iters 20 --cpu-seconds 0 > gpurun_out/js.log 2>&1 || { echo JPEG_PROF_FAILED; tail -30 gpurun_out/js.log; exit 1; }
+timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_js -o js -- python3 tools/jpeg_bench.py --sizes 1080p --batch 32 --iters 20 --cpu-seconds 0 --resident-only > gpurun_out/js.log 2>&1 || { echo JPEG_PROF_FAILED; tail -30 gpurun_out/js.log; exit 1; }
 cp "$(find gpurun_out/prof_js -name '*kernel_stats.csv' | head -1)" gpurun_out/jpeg_kernel_stats.csv
 
 timeout -k 10 120 python -u tools/per_frame_probe.py > gpurun_out/per_frame.jsonl 2> gpurun_out/per_frame.log || { echo PERFRAME_FAILED; tail -20 gpurun_out/per_frame.log; exit 1; }
