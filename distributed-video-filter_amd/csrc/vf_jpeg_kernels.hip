@@ -91,29 +91,20 @@ __global__ __launch_bounds__(256) void seg_tile_sum(const ScanSeg *segs, const T
   if (threadIdx.x == 0) tsum[sg.tile0 + blockIdx.x] = tot;
 }
 
-template <typename T>
-__global__ __launch_bounds__(256) void seg_tsum_scan(const ScanSeg *segs, T *tsum, T *totals) {
-  const ScanSeg sg = segs[blockIdx.x];
-  const uint32_t nt = (uint32_t)((sg.len + kScanTile - 1) / kScanTile);
-  __shared__ T sh[4];
-  T carry = 0;
-  for (uint32_t c = 0; c < nt; c += 256) {
-    const uint32_t i = c + threadIdx.x;
-    const T v = i < nt ? tsum[sg.tile0 + i] : T(0);
-    T tot;
-    const T ex = wg_excl_scan(v, sh, &tot);
-    if (i < nt) tsum[sg.tile0 + i] = carry + ex;
-    carry += tot;
-  }
-  if (threadIdx.x == 0 && totals) totals[blockIdx.x] = carry;
-}
-
+// Each tile's workgroup adds the sums of the tiles before it in its segment itself (a frame's
+// segment has a few hundred tiles at most at 8K, one or two loads per thread, from L2) instead
+// of a separate one-workgroup-per-segment kernel scanning them in between: one launch and one
+// dependent kernel boundary fewer per scan (five scans per batch).  The segment's last tile
+// writes the segment total; a segment with no tiles has its total written as 0 by tile 0.
 template <typename T, bool INCL>
-__global__ __launch_bounds__(256) void seg_apply(const ScanSeg *segs, const T *in, const T *tsum, T *out) {
+__global__ __launch_bounds__(256) void seg_apply(const ScanSeg *segs, const T *in, const T *tsum, T *out, T *totals) {
   const ScanSeg sg = segs[blockIdx.y];
   const uint64_t t0 = (uint64_t)blockIdx.x * kScanTile;
-  if (t0 >= sg.len) return;
-  __shared__ T sh[4];
+  if (t0 >= sg.len) {
+    if (blockIdx.x == 0 && threadIdx.x == 0 && totals) totals[blockIdx.y] = T(0);
+    return;
+  }
+  __shared__ T sh[8];
   const uint64_t b0 = t0 + (uint64_t)threadIdx.x * kScanPerThread;
   T v[kScanPerThread];
   T acc = 0;
@@ -122,14 +113,32 @@ __global__ __launch_bounds__(256) void seg_apply(const ScanSeg *segs, const T *i
     v[j] = b0 + j < sg.len ? in[sg.base + b0 + j] : T(0);
     acc += v[j];
   }
-  T tot;
-  T run = tsum[sg.tile0 + blockIdx.x] + wg_excl_scan(acc, sh, &tot);
+  T pre = 0;  // this thread's share of the preceding tiles' sums
+  for (uint32_t i = threadIdx.x; i < blockIdx.x; i += 256) pre += tsum[sg.tile0 + i];
+  // one barrier for both: the exclusive scan of acc and the sum of pre over the workgroup
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const T x = wave_incl_scan(acc);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) pre += __shfl_xor(pre, o, 64);
+  if (lane == 63) sh[wid] = x, sh[4 + wid] = pre;
+  __syncthreads();
+  T run = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const T t = sh[i];
+    if (i < wid) run += t;
+    tot += t;
+    run += sh[4 + i];  // every wave's preceding-tile share
+  }
+  const T before = sh[4] + sh[5] + sh[6] + sh[7];
+  run += x - acc;
 #pragma unroll
   for (int j = 0; j < kScanPerThread; ++j) {
     if (INCL) run += v[j];
     if (b0 + j < sg.len) out[sg.base + b0 + j] = run;
     if (!INCL) run += v[j];
   }
+  if (threadIdx.x == 0 && totals && t0 + kScanTile >= sg.len) totals[blockIdx.y] = before + tot;
 }
 
 template <typename T>
@@ -138,9 +147,8 @@ hipError_t seg_scan(const ScanSeg *segs, int nseg, uint32_t max_tiles, const T *
   if (nseg <= 0 || max_tiles == 0) return hipSuccess;
   const dim3 g(max_tiles, (unsigned)nseg);
   hipLaunchKernelGGL(seg_tile_sum<T>, g, dim3(256), 0, s, segs, in, tsum);
-  hipLaunchKernelGGL(seg_tsum_scan<T>, dim3((unsigned)nseg), dim3(256), 0, s, segs, tsum, totals);
-  if (inclusive) hipLaunchKernelGGL((seg_apply<T, true>), g, dim3(256), 0, s, segs, in, tsum, out);
-  else hipLaunchKernelGGL((seg_apply<T, false>), g, dim3(256), 0, s, segs, in, tsum, out);
+  if (inclusive) hipLaunchKernelGGL((seg_apply<T, true>), g, dim3(256), 0, s, segs, in, tsum, out, totals);
+  else hipLaunchKernelGGL((seg_apply<T, false>), g, dim3(256), 0, s, segs, in, tsum, out, totals);
   return hipGetLastError();
 }
 
