@@ -136,7 +136,6 @@ class Codec {
   int run_decode(int bgr, bool invert, std::string *err);
   int run_decode_post(int bgr, bool invert, std::string *err);  // write, DC, IDCT, colour
   int finish_sync(std::string *err);  // host-looped span passes after the queued ones
-  int queue_decode_check(std::string *err);
   int check_decode(std::string *err);
   int prepare_encode(const int *ws, const int *hs, const uint64_t *img_offs, int n, int quality, int subsamp,
                      bool fastdct, std::string *err);
@@ -181,6 +180,8 @@ class Codec {
   DevBuf d_efr_, d_etab_, d_hdr_, d_esegs_, d_etsum_, d_etotals_, d_dcq_, d_acbits_, d_acscr_, d_bits_, d_pre_, d_bitoff_, d_stream_, d_ffcnt_,
       d_out_, d_outsize_, d_pack_;
 
+  HostBuf h_unres_;            // k_resolve's per-segment unresolved flags (stored through the mapping)
+  void *unres_dev_ = nullptr, *dtot_dev_ = nullptr;  // device addresses of h_unres_ / h_dtot_
   HostBuf h_stage_, h_out_, h_flag_;  // h_flag_: the speculative sync's unresolved flag
   HostBuf h_ddesc_, h_edesc_, h_meta_, h_dtot_;  // pinned descriptor uploads; output sizes; block totals
   uint64_t guess_ = 0, out_total_ = 0, fetch_refills_ = 0;

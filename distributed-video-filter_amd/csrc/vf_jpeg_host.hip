@@ -404,6 +404,11 @@ int Codec::prepare_decode(const uint8_t *const *jpegs, const size_t *sizes, int 
   CK(d_tile_.ensure(sizeof(uint32_t) * tiles));
   CK(d_tsum_.ensure(sizeof(int32_t) * (t0 + 1)));
   CK(d_totals_.ensure(sizeof(int32_t) * segs.size()));
+  // page-locked per-segment results the kernels store through the mapping (check_decode)
+  CK(h_dtot_.ensure(sizeof(uint32_t) * (size_t)dnseg_ + 64));
+  CK(h_unres_.ensure(sizeof(uint32_t) * (size_t)dnseg_ + 64));
+  CK(hipHostGetDevicePointer(&dtot_dev_, h_dtot_.p, 0));
+  CK(hipHostGetDevicePointer(&unres_dev_, h_unres_.p, 0));
   CK(d_us_.ensure(us_off));
   CK(d_exit_[0].ensure(sizeof(uint64_t) * subs));
   CK(d_exit_[1].ensure(sizeof(uint64_t) * subs));
@@ -497,20 +502,23 @@ int Codec::run_decode(int bgr, bool invert, std::string *err) {
                 d_rE_.as<uint8_t>(), d_rK_.as<uint32_t>(), d_wTE_.as<uint8_t>(), d_wTK_.as<uint8_t>(),
                 d_wQE_.as<uint8_t>(), d_wQK_.as<uint8_t>(), d_qX_.as<uint64_t>(), d_qC_.as<uint32_t>(),
                 d_rL_.as<uint8_t>(), d_unres_.as<uint32_t>()};
-    CK(hipMemsetAsync(d_unres_.p, 0, sizeof(uint32_t) * 16, s_));
-    CK(dec_sync_spec(sg, fr, ns, dmax_wg_, d_us_.as<uint8_t>(), us_len, sb, d_exit_[0].as<uint64_t>(),
-                     d_cnt_[0].as<uint32_t>(), d_unres_.as<uint32_t>(), s_));
     // k_resolve reports a frame unresolved only when it has more workgroups than it stages,
     // which prepare_decode already excludes (spec_ok_), so the rest is queued without a host
-    // round trip; the flag is read at check_decode's synchronisation and turned into an error.
-    CK(h_flag_.ensure(64));
-    CK(hipMemcpyAsync(h_flag_.p, d_unres_.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s_));
+    // round trip; check_decode reads the flags after its synchronisation and turns one into an
+    // error.  Each segment's k_resolve workgroup stores its flag (0 or 1) straight into the
+    // codec's page-locked h_unres_ through the mapping: no fill and no download on the stream.
+    const bool stats = std::getenv("VF_JPEG_SYNC_STATS") != nullptr;
+    if (stats) CK(hipMemsetAsync(d_unres_.p, 0, sizeof(uint32_t) * 16, s_));  // SpecBufs::stats
+    CK(dec_sync_spec(sg, fr, ns, dmax_wg_, d_us_.as<uint8_t>(), us_len, sb, d_exit_[0].as<uint64_t>(),
+                     d_cnt_[0].as<uint32_t>(), static_cast<uint32_t *>(unres_dev_), s_));
     spec_check_ = true;
     flag = 0;  // exits / counts are in slot 0
     ++spec_calls_;
-    if (std::getenv("VF_JPEG_SYNC_STATS")) {
+    if (stats) {
       uint32_t st[16];
       CK(hipMemcpy(st, d_unres_.p, sizeof st, hipMemcpyDeviceToHost));
+      st[0] = 0;
+      for (int i = 0; i < ns; ++i) st[0] += h_unres_.as<uint32_t>()[i];
       std::fprintf(stderr, "[vf_jpeg] k_spec kcycles summed over workgroups, from start: part A %u, part B %u, "
                    "walkers end %u (x bpm)\n", st[8], st[9], st[10]);
       std::fprintf(stderr, "[vf_jpeg] spec: unresolved %u walker decodes %u traced workgroups %u traced subsequences "
@@ -616,7 +624,8 @@ int Codec::run_decode_post(int bgr, bool invert, std::string *err) {
   const bool use_spec = sync_spec_;
   const int last = sync_last_;
   // 3. block offsets of the subsequences, then the write pass
-  uint32_t *blocks_total = d_totals_.as<uint32_t>() + ns;
+  // the segments' decoded block counts go straight to the page-locked h_dtot_ (check_decode)
+  uint32_t *blocks_total = static_cast<uint32_t *>(dtot_dev_);
   CK(scan_u32(segs + ns, ns, (dmax_sub_ + kScanTile - 1) / kScanTile, d_cnt_[last].as<uint32_t>(),
               d_bstart_.as<uint32_t>(), d_tsum_.as<uint32_t>(), blocks_total, false, s_));
   CK(hipMemsetAsync(d_coef_.p, 0, dblocks_ * 128, s_));
@@ -645,15 +654,8 @@ int Codec::run_decode_post(int bgr, bool invert, std::string *err) {
   return kOk;
 }
 
-// Queue the D2H of every frame's decoded block count (written by run_decode) into pinned memory.
-int Codec::queue_decode_check(std::string *err) {
-  CK(h_dtot_.ensure(sizeof(uint32_t) * (size_t)dnseg_ + 64));
-  CK(hipMemcpyAsync(h_dtot_.p, d_totals_.as<uint32_t>() + dnseg_, sizeof(uint32_t) * (size_t)dnseg_,
-                    hipMemcpyDeviceToHost, s_));
-  return kOk;
-}
-
-// Check that every frame decoded all its blocks (after queue_decode_check and a synchronisation).
+// Check that every frame decoded all its blocks (after a synchronisation: run_decode_post's
+// block-offset scan stores each segment's count into h_dtot_ through the mapping).
 int Codec::check_decode(std::string *err) {
   const uint32_t *tot = h_dtot_.as<uint32_t>();
   if (pass_check_) {
@@ -662,7 +664,9 @@ int Codec::check_decode(std::string *err) {
   }
   if (spec_check_) {
     spec_check_ = false;
-    if (*h_flag_.as<uint32_t>()) {
+    bool unresolved = false;
+    for (int i = 0; i < dnseg_; ++i) unresolved = unresolved || h_unres_.as<uint32_t>()[i] != 0;
+    if (unresolved) {
       ++spec_fallbacks_;
       *err = "speculative Huffman synchronisation left a frame unresolved";
       return kJpeg;
@@ -916,7 +920,6 @@ int Codec::decode(const uint8_t *const *jpegs, const size_t *jsizes, int n, int 
   if ((rc = run_decode(pixel_format, false, err))) return rc;
   for (bool again = false;; again = true) {
     if (again && ((rc = finish_sync(err)) || (rc = run_decode_post(pixel_format, false, err)))) return rc;
-    if ((rc = queue_decode_check(err))) return rc;
     CK(h_out_.ensure(dpix_bytes_));
     CK(hipMemcpyAsync(h_out_.p, d_pix_.p, dpix_bytes_, hipMemcpyDeviceToHost, s_));
     CK(hipStreamSynchronize(s_));
@@ -976,7 +979,6 @@ int Codec::submit_invert(const uint8_t *const *jpegs, const size_t *jsizes, int 
       gate_->last = ev_[9];
     }
   }
-  if ((rc = queue_decode_check(err))) return rc;
   if ((rc = queue_fetch(guess, err))) return rc;
   if (trace) {
     auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
@@ -1008,7 +1010,7 @@ int Codec::wait_invert(size_t *total, std::string *err) {
   int rc = check_decode(err);
   while (rc == kResync) {  // more sync passes, then every stage after the sync again
     if ((rc = finish_sync(err)) || (rc = run_decode_post(1, true, err)) || (rc = run_encode(1, enc_fast_, err)) ||
-        (rc = queue_decode_check(err)) || (rc = queue_fetch(guess_, err)))
+        (rc = queue_fetch(guess_, err)))
       return rc;
     CK(hipEventSynchronize(done_));
     rc = check_decode(err);
@@ -1120,12 +1122,10 @@ int Codec::bench_invert(const uint8_t *const *jpegs, const size_t *jsizes, int n
     }
   }
   stage_events_ = false;
-  if ((rc = queue_decode_check(err))) return rc;
   CK(hipStreamSynchronize(s_));
   rc = check_decode(err);
   while (rc == kResync) {
-    if ((rc = finish_sync(err)) || (rc = run_decode_post(1, true, err)) || (rc = run_encode(1, fast, err)) ||
-        (rc = queue_decode_check(err)))
+    if ((rc = finish_sync(err)) || (rc = run_decode_post(1, true, err)) || (rc = run_encode(1, fast, err)))
       return rc;
     CK(hipStreamSynchronize(s_));
     rc = check_decode(err);

@@ -1192,10 +1192,10 @@ __global__ __launch_bounds__(256) void k_resolve(const DecSeg *__restrict__ sg, 
   const uint32_t bpm = hg.bpm, L = spec_lanes(bpm), NS = 256 / L;
   const uint32_t nbits = us_len[blockIdx.x] * 8u, nsub = (nbits + kSubBits - 1) / kSubBits;
   const uint32_t nwg = min(S.nwg, (nsub + NS - 1) / NS);
-  if (nwg > kResolveLds || nwg * bpm > kResolveT) {
-    if (threadIdx.x == 0) atomicOr(unresolved, 1u);
-    return;
-  }
+  const bool over = nwg > kResolveLds || nwg * bpm > kResolveT;
+  if (threadIdx.x == 0)  // every segment's flag, every decode (page-locked host memory)
+    __hip_atomic_store(unresolved + blockIdx.x, over ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (over) return;
   const uint32_t lastk = NS - 1;  // every workgroup but the frame's last is full
   {  // the sync tables' copy is issued with the transition loads; one barrier publishes both
     const uint32_t *src = reinterpret_cast<const uint32_t *>(&F.sdc[0]);
