@@ -607,8 +607,11 @@ def jpeg_roofline(stages, h, w, batch, j_in, j_out):
                           "dependent Huffman table lookups (LDS latency)"),
         "dc_idct": (coef + planes + 4 * blocks, "read coefficients + DC, write planes",
                     "load latency + VALU (LDS conflict-free)"),
-        "color_invert": (planes + pix, "read planes, write BGR pixels", "load latency per wave"),
-        "fdct_huffman": (pix + 3 * j_out + 10 * blocks, "read pixels, write + pack AC words",
+        # the invert path's fused colour pass: the encoder's 4:2:2 sample planes (as many samples
+        # as the decoder's) instead of BGR pixels, read back by k_fdct
+        "color_invert": (2 * planes, "read planes, write the encoder's sample planes (inverted)",
+                         "load latency per wave"),
+        "fdct_huffman": (planes + 3 * j_out + 10 * blocks, "read sample planes, write + pack AC words",
                          "VALU + issue latency"),
         "stuffing": (5 * j_out, "count + write FF00 stuffing, compact", "launch/latency (a few MB)"),
     }

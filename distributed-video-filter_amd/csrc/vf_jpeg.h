@@ -80,10 +80,10 @@ hipError_t dec_write4(const DecSeg *sg, const DecFrame *fr, int nseg, uint32_t m
 hipError_t dec_idct(const DecFrame *fr, int n, uint32_t max_blocks, const int16_t *coef, const int32_t *dcseq,
                     uint8_t *planes, hipStream_t s);
 hipError_t dec_color(const DecFrame *fr, int n, int max_w, int max_h, const uint8_t *planes, uint8_t *pix,
-                     int bgr, int invert, hipStream_t s);
+                     int bgr, int invert, const EncFrame *efr, int cm, hipStream_t s);
 
 hipError_t enc_fdct(const EncFrame *fr, int n, uint32_t max_blocks, const EncTables *tab, const uint8_t *pix,
-                    int16_t *dcq, uint32_t *acbits, uint32_t *acscr, int bgr, int fastdct, int ch, int cv,
+                    int16_t *dcq, uint32_t *acbits, uint32_t *acscr, int bgr, int fastdct, int ch, int cv, int planes,
                     hipStream_t s);  // (ch, cv): chroma downsampling factors
 hipError_t enc_len(const EncFrame *fr, int n, uint32_t max_blocks, const EncTables *tab, const int16_t *dcq,
                    uint32_t *acbits, uint32_t *bits, uint32_t *pre, hipStream_t s);

@@ -177,6 +177,9 @@ class Codec {
   int esub_ = 1;  // TJSAMP_* of the prepared encode
   uint32_t emax_blocks_ = 0, emax_tiles_ = 0;
   uint64_t eblocks_ = 0, ebits_bytes_ = 0;
+  DevBuf d_eplanes_;  // the invert path's encoder sample planes (fuse_)
+  bool fuse_ = false;
+  int dcm_ = -1;  // k_color layout shared by the batch's frames (1..3, 0 general), -1 mixed
   DevBuf d_efr_, d_etab_, d_hdr_, d_esegs_, d_etsum_, d_etotals_, d_dcq_, d_acbits_, d_acscr_, d_bits_, d_pre_, d_bitoff_, d_stream_, d_ffcnt_,
       d_out_, d_outsize_, d_pack_;
 

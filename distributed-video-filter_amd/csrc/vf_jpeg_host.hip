@@ -266,7 +266,15 @@ int Codec::init(std::string *err) {
 }
 
 // Host parse of every frame + batch layout + upload of inputs and descriptors.
+// The invert path's fused colour pass (k_color writes the encoder's sample planes, k_fdct reads
+// them); VF_JPEG_FUSE=0 keeps the pixel round trip (read per call: tests switch it).
+static bool fuse_enabled() {
+  const char *v = std::getenv("VF_JPEG_FUSE");
+  return !(v && std::strcmp(v, "0") == 0);
+}
+
 int Codec::prepare_decode(const uint8_t *const *jpegs, const size_t *sizes, int n, int flags, std::string *err) {
+  fuse_ = false;
   if (n <= 0) {
     *err = "empty batch";
     return kInvalid;
@@ -295,6 +303,7 @@ int Codec::prepare_decode(const uint8_t *const *jpegs, const size_t *sizes, int 
       return kJpeg;
     }
   dsg_.clear();
+  dcm_ = -2;  // the batch's common k_color layout, or -1 (mixed)
   for (int f = 0; f < n; ++f) {
     const Parsed &P = parsed[(size_t)f];
     DecFrame &F = dfr_[(size_t)f];
@@ -305,6 +314,7 @@ int Codec::prepare_decode(const uint8_t *const *jpegs, const size_t *sizes, int 
       if (g.ncomp == 3 && g.he[0] == 1 && g.ve[0] == 1 && g.he[1] == g.he[2] && g.ve[1] == g.ve[2])
         cm = g.he[1] == 1 && g.ve[1] == 1 ? 1u : g.he[1] == 2 && g.ve[1] == 1 ? 2u : g.he[1] == 2 && g.ve[1] == 2 ? 3u : 0u;
       F.flags |= cm << 1;
+      dcm_ = dcm_ == -2 || dcm_ == (int)cm ? (int)cm : -1;
     }
     F.blk0 = blk;
     for (int c = 0; c < P.ncomp; ++c) {
@@ -649,7 +659,9 @@ int Codec::run_decode_post(int bgr, bool invert, std::string *err) {
   // 5. IDCT, 6. upsample + colour (+ invert)
   CK(dec_idct(fr, n, dmax_blocks_, d_coef_.as<int16_t>(), d_dcseq_.as<int32_t>(), d_planes_.as<uint8_t>(), s_));
   CK(stage_event(4));
-  CK(dec_color(fr, n, dmax_w_, dmax_h_, d_planes_.as<uint8_t>(), d_pix_.as<uint8_t>(), bgr, invert ? 1 : 0, s_));
+  // the invert path (fuse_): the encoder's sample planes instead of pixels (enc_sample_rows)
+  CK(dec_color(fr, n, dmax_w_, dmax_h_, d_planes_.as<uint8_t>(), fuse_ ? d_eplanes_.as<uint8_t>() : d_pix_.as<uint8_t>(),
+               bgr, invert ? 1 : 0, fuse_ ? d_efr_.as<EncFrame>() : nullptr, dcm_, s_));
   CK(stage_event(5));
   return kOk;
 }
@@ -692,9 +704,10 @@ int Codec::prepare_encode(const int *ws, const int *hs, const uint64_t *img_offs
     *err = "unsupported subsampling (TJSAMP_444, 422, 420, GRAY, 440)";
     return kInvalid;
   }
+  fuse_ = false;  // the invert paths turn it on after both prepares
   efr_.assign((size_t)n, EncFrame());
   std::vector<uint8_t> hdr;
-  uint64_t blk = 0, bits = 0, out = 0;
+  uint64_t blk = 0, bits = 0, out = 0, epl = 0;
   uint32_t tiles = 0;
   emax_blocks_ = emax_tiles_ = 0;
   const int nc = subsamp == 3 ? 1 : 3;
@@ -706,6 +719,10 @@ int Codec::prepare_encode(const int *ws, const int *hs, const uint64_t *img_offs
       return kInvalid;
     }
     F.img_off = img_offs[f];
+    for (int k = 0; k < 3; ++k) {  // the invert path's sample planes: wb * 8 x rrows each
+      F.eplane_off[k] = epl;
+      if (k < nc) epl += align_up((size_t)F.g.wb[k] * 8 * (size_t)F.g.rrows[k], 256);
+    }
     F.blk0 = blk;
     F.bits_off = bits;
     const uint64_t bits_cap = align_up((size_t)F.g.nblocks * kMaxBlockBytes + 16, 256);
@@ -755,6 +772,7 @@ int Codec::prepare_encode(const int *ws, const int *hs, const uint64_t *img_offs
   CK(d_out_.ensure(out));
   CK(d_pack_.ensure(out));
   CK(d_outsize_.ensure(sizeof(uint64_t) * (size_t)n));
+  CK(d_eplanes_.ensure(epl));
   // frame descriptors, tables, headers and scan segments: one pinned blob, asynchronous uploads
   const size_t fsz = sizeof(EncFrame) * (size_t)n, ssz = sizeof(ScanSeg) * segs.size();
   const size_t o_tab = align_up(fsz, 256), o_hdr = o_tab + align_up(sizeof tab, 256),
@@ -778,8 +796,9 @@ int Codec::run_encode(int bgr, bool fastdct, std::string *err) {
   const ScanSeg *segs = d_esegs_.as<ScanSeg>();
   const int n = en_;
   CK(stage_event(6));
-  CK(enc_fdct(fr, n, emax_blocks_, tab, d_pix_.as<uint8_t>(), d_dcq_.as<int16_t>(), d_acbits_.as<uint32_t>(),
-              d_acscr_.as<uint32_t>(), bgr, fastdct ? 1 : 0, kSampH[esub_], kSampV[esub_], s_));
+  CK(enc_fdct(fr, n, emax_blocks_, tab, fuse_ ? d_eplanes_.as<uint8_t>() : d_pix_.as<uint8_t>(), d_dcq_.as<int16_t>(),
+              d_acbits_.as<uint32_t>(), d_acscr_.as<uint32_t>(), bgr, fastdct ? 1 : 0, kSampH[esub_], kSampV[esub_],
+              fuse_ ? 1 : 0, s_));
   CK(enc_len(fr, n, emax_blocks_, tab, d_dcq_.as<int16_t>(), d_acbits_.as<uint32_t>(), d_bits_.as<uint32_t>(),
              d_pre_.as<uint32_t>(), s_));
   uint32_t *total_bits = d_etotals_.as<uint32_t>();
@@ -963,6 +982,7 @@ int Codec::submit_invert(const uint8_t *const *jpegs, const size_t *jsizes, int 
   }
   const bool fast = (flags & kFlagFastDct) != 0;
   if ((rc = prepare_encode(ws.data(), hs.data(), offs.data(), n, quality, subsamp, fast, err))) return rc;
+  fuse_ = fuse_enabled();
   const auto t2 = clk::now();
   {
     std::unique_lock<std::mutex> gl;
@@ -1092,6 +1112,7 @@ int Codec::bench_invert(const uint8_t *const *jpegs, const size_t *jsizes, int n
   }
   const bool fast = (flags & kFlagFastDct) != 0;
   if ((rc = prepare_encode(ws.data(), hs.data(), offs.data(), n, quality, subsamp, fast, err))) return rc;
+  fuse_ = fuse_enabled();
   float acc[8] = {0};
   double total_ms = 0;
   int passes = 0;

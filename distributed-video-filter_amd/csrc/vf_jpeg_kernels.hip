@@ -1666,10 +1666,10 @@ __device__ __forceinline__ void ycc8(const int v[3][8], int ncomp, int bgr, int 
     if (ncomp == 1) {
       r = gg = b = (uint32_t)v[0][j];
     } else {
-      const int xcr = v[2][j] - 128, xcb = v[1][j] - 128;
-      r = clamp255(v[0][j] + ((91881 * xcr + 32768) >> 16));
-      gg = clamp255(v[0][j] + ((-22554 * xcb + 32768 - 46802 * xcr) >> 16));
-      b = clamp255(v[0][j] + ((116130 * xcb + 32768) >> 16));
+      const int xcr = v[2][j] - 128, xcb = v[1][j] - 128;  // 24-bit multiplies: |x| <= 128, constants < 2^17
+      r = clamp255(v[0][j] + ((__mul24(91881, xcr) + 32768) >> 16));
+      gg = clamp255(v[0][j] + ((__mul24(-22554, xcb) + 32768 - __mul24(46802, xcr)) >> 16));
+      b = clamp255(v[0][j] + ((__mul24(116130, xcb) + 32768) >> 16));
     }
     if (invert) {
       r ^= 0xFF;
@@ -1733,6 +1733,140 @@ __device__ __forceinline__ void color8(const DecFrame &F, const Geom &g, const u
   ycc8(v, g.ncomp, bgr, invert, o);
 }
 
+// jccolor.c rgb_ycc_convert for one component over a pixel's bytes in memory order:
+// (a0 * c0 + a1 * c1 + a2 * c2 + bias) >> 16.  The component and the channel order are
+// wave-uniform in k_fdct, so the coefficients sit in scalar registers and a pixel costs three
+// multiply-adds with no per-pixel select.  No sum is negative (Cb and Cr carry 128 << 16:
+// their smallest sums are 575535 and 65535), so the shift is jccolor.c's.
+struct Ycc {
+  int a0, a1, a2, bias;
+};
+__device__ __forceinline__ Ycc ycc_coefs(int k, bool bgr) {
+  int r, g, b, bias = (128 << 16) + 32767;
+  if (k == 0) {
+    r = 19595, g = 38470, b = 7471, bias = 32768;
+  } else if (k == 1) {
+    r = -11059, g = -21709, b = 32768;
+  } else {
+    r = 32768, g = -27439, b = -5329;
+  }
+  return bgr ? Ycc{b, g, r, bias} : Ycc{r, g, b, bias};
+}
+__device__ __forceinline__ int ycc_apply(const Ycc &q, int c0, int c1, int c2) {  // 8-bit samples, |a| <= 2^16
+  return (__mul24(q.a0, c0) + __mul24(q.a1, c1) + __mul24(q.a2, c2) + q.bias) >> 16;
+}
+
+// The invert path's encoder input, from the colour pass: the encoder's component samples
+// (jccolor.c rgb_ycc_convert of the inverted pixels, then jcsample.c downsampling) of the 8
+// pixels x0 .. x0 + 7 of rows y0 and y0 + 1, given as packed R | G << 8 | B << 16 (p1 = p0
+// when y0 is the last row: jcprepct.c's bottom expansion to whole row groups).  k_fdct then
+// reads one 8-byte sample row per lane instead of converting 8-48 pixels in each component's
+// wave, and the 3-byte pixels never reach memory.  Pixels past the right edge take the last
+// pixel's values (expand_right_edge); the thread holding it also fills the planes' columns past
+// the image, to the components' whole blocks.  Sample rows past rrows[k] are never read
+// (k_fdct clamps to the last).  One component at a time, from the packed pixels: the samples
+// of all three for both rows held at once cost the kernel two of its six waves per SIMD.
+__device__ __forceinline__ int ycc_of(uint32_t px, const Ycc &q) {  // q: R, G, B coefficients (scalar)
+  return (__mul24((int)(px & 0xFF), q.a0) + __mul24((int)((px >> 8) & 0xFF), q.a1) + __mul24((int)(px >> 16), q.a2) +
+          q.bias) >> 16;
+}
+
+__device__ __forceinline__ void enc_store_rows(const EncFrame &E, uint8_t *__restrict__ eplanes, uint32_t (&p0)[8],
+                                               uint32_t (&p1)[8], int y0, int x0, int w) {
+  const Geom &ge = E.g;
+  const bool edge = x0 + 8 >= w;  // holds pixel w - 1 (and fills past it, up to the whole blocks)
+  uint32_t l0 = 0, l1 = 0;        // the last pixel (edge thread)
+  if (edge) {
+    const int lp = w - 1 - x0;
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+      l0 = p == lp ? p0[p] : l0;
+      l1 = p == lp ? p1[p] : l1;
+    }
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+      p0[p] = p > lp ? l0 : p0[p];
+      p1[p] = p > lp ? l1 : p1[p];
+    }
+  }
+  // a rolled loop: one component's samples live at a time (unrolled, the three components'
+  // conversions interleaved and the kernel needed 131 VGPRs, 3 waves per SIMD)
+#pragma unroll 1
+  for (int k = 0; k < ge.ncomp; ++k) {
+    const int he = ge.he[k], ve = ge.ve[k], pitch = ge.wb[k] * 8, rr = ge.rrows[k];
+    uint8_t *const pl = eplanes + E.eplane_off[k];
+    const Ycc q = ycc_coefs(k, false);
+    int c0[8], c1[8];
+#pragma unroll
+    for (int p = 0; p < 8; ++p) c0[p] = ycc_of(p0[p], q), c1[p] = ycc_of(p1[p], q);
+    const int e0 = edge ? ycc_of(l0, q) : 0, e1 = edge ? ycc_of(l1, q) : 0;
+    if (ve == 1) {
+#pragma unroll
+      for (int rw = 0; rw < 2; ++rw) {
+        const int y = y0 + rw;
+        if (y >= rr) break;
+        uint8_t *row = pl + (size_t)y * pitch;
+        if (he == 1) {
+          uint32_t lo = 0, hi = 0;
+#pragma unroll
+          for (int p = 0; p < 4; ++p) {
+            lo |= (uint32_t)(rw ? c1[p] : c0[p]) << (8 * p);
+            hi |= (uint32_t)(rw ? c1[p + 4] : c0[p + 4]) << (8 * p);
+          }
+          *reinterpret_cast<uint2 *>(row + x0) = make_uint2(lo, hi);
+        } else {  // h2v1_downsample: bias 0, 1 alternating
+          uint32_t v = 0;
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            v |= (uint32_t)(((rw ? c1[2 * i] + c1[2 * i + 1] : c0[2 * i] + c0[2 * i + 1]) + (i & 1)) >> 1) << (8 * i);
+          *reinterpret_cast<uint32_t *>(row + (x0 >> 1)) = v;
+        }
+        if (edge) {
+          const int ev = rw ? e1 : e0;
+          for (int xs = (x0 + 8) / he; xs < pitch; ++xs) row[xs] = (uint8_t)ev;
+        }
+      }
+    } else {  // two rows into one: int_downsample (1x2: (a + b + 1) >> 1) or h2v2_downsample
+      const int y = y0 >> 1;
+      if (y < rr) {
+        uint8_t *row = pl + (size_t)y * pitch;
+        if (he == 1) {
+          uint32_t lo = 0, hi = 0;
+#pragma unroll
+          for (int p = 0; p < 4; ++p) {
+            lo |= (uint32_t)((c0[p] + c1[p] + 1) >> 1) << (8 * p);
+            hi |= (uint32_t)((c0[p + 4] + c1[p + 4] + 1) >> 1) << (8 * p);
+          }
+          *reinterpret_cast<uint2 *>(row + x0) = make_uint2(lo, hi);
+          if (edge)
+            for (int xs = x0 + 8; xs < pitch; ++xs) row[xs] = (uint8_t)((e0 + e1 + 1) >> 1);
+        } else {  // bias 1, 2 alternating
+          uint32_t v = 0;
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            v |= (uint32_t)((c0[2 * i] + c0[2 * i + 1] + c1[2 * i] + c1[2 * i + 1] + 1 + (i & 1)) >> 2) << (8 * i);
+          *reinterpret_cast<uint32_t *>(row + (x0 >> 1)) = v;
+          if (edge)
+            for (int xs = (x0 + 8) >> 1; xs < pitch; ++xs) row[xs] = (uint8_t)((2 * e0 + 2 * e1 + 1 + (xs & 1)) >> 2);
+        }
+      }
+    }
+  }
+}
+
+// The same from 8 interleaved output pixels per row (color8's general layouts)
+__device__ __forceinline__ void enc_sample_rows(const EncFrame &E, uint8_t *__restrict__ eplanes, const uint8_t o0[24],
+                                                const uint8_t o1[24], int y0, int x0, int w, int bgr) {
+  uint32_t p0[8], p1[8];
+  const int i0 = bgr ? 2 : 0, i2 = bgr ? 0 : 2;
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+    p0[p] = (uint32_t)o0[3 * p + i0] | (uint32_t)o0[3 * p + 1] << 8 | (uint32_t)o0[3 * p + i2] << 16;
+    p1[p] = (uint32_t)o1[3 * p + i0] | (uint32_t)o1[3 * p + 1] << 8 | (uint32_t)o1[3 * p + i2] << 16;
+  }
+  enc_store_rows(E, eplanes, p0, p1, y0, x0, w);
+}
+
 // 8 pixels (24 bytes of o) to dst, of which `left` are inside the row
 __device__ __forceinline__ void store24(uint8_t *dst, int left, const uint8_t o[24]) {
   if (left >= 8 && ((uintptr_t)dst & 7) == 0) {
@@ -1759,9 +1893,10 @@ __device__ __forceinline__ void store24(uint8_t *dst, int left, const uint8_t o[
 // with every plane load of both rows issued before any is used (color8's per-component
 // branches leave the compiler waiting on each component's loads in turn: six round trips per
 // thread at 4:2:0).  4:2:0 reads chroma rows iy - 1, iy, iy + 1 once for both output rows.
-template <int MODE>
+template <int MODE, bool ENC>
 __device__ __forceinline__ void color_rows(const DecFrame &F, const Geom &g, const uint8_t *__restrict__ planes,
-                                           uint8_t *__restrict__ pix, int y0, int x0, bool two, int bgr, int invert) {
+                                           uint8_t *__restrict__ pix, const EncFrame *__restrict__ efr, int y0, int x0,
+                                           bool two, int bgr, int invert) {
   const int y1 = two ? y0 + 1 : y0;
   int v0[3][8], v1[3][8];
   if constexpr (MODE == 0) {
@@ -1840,6 +1975,23 @@ __device__ __forceinline__ void color_rows(const DecFrame &F, const Geom &g, con
       up2(c1, i0, dw, fancy, MODE == 2 ? 2 : 1, v1[k + 1]);
     }
   }
+  if constexpr (ENC) {  // decoded YCbCr -> inverted RGB (packed) -> the encoder's samples
+    uint32_t p0[8], p1[8];
+#pragma unroll
+    for (int rw = 0; rw < 2; ++rw)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int yy = rw ? v1[0][j] : v0[0][j], cb = rw ? v1[1][j] : v0[1][j], cr = rw ? v1[2][j] : v0[2][j];
+        const int xcr = cr - 128, xcb = cb - 128;
+        const uint32_t r = clamp255(yy + ((__mul24(91881, xcr) + 32768) >> 16));
+        const uint32_t gg = clamp255(yy + ((__mul24(-22554, xcb) + 32768 - __mul24(46802, xcr)) >> 16));
+        const uint32_t b = clamp255(yy + ((__mul24(116130, xcb) + 32768) >> 16));
+        const uint32_t px = (r | gg << 8 | b << 16) ^ (invert ? 0xFFFFFFu : 0u);
+        if (rw) p1[j] = two ? px : p0[j];
+        else p0[j] = px;
+      }
+    return enc_store_rows(efr[blockIdx.z], pix, p0, p1, y0, x0, g.w);
+  }
   uint8_t o0[24], o1[24];
   ycc8(v0, 3, bgr, invert, o0);
   ycc8(v1, 3, bgr, invert, o1);
@@ -1852,8 +2004,16 @@ __device__ __forceinline__ void color_rows(const DecFrame &F, const Geom &g, con
 
 // Two rows per workgroup: both rows' plane loads are issued before either row is stored (the
 // kernel is bound by load latency per wave; one short row per workgroup left it exposed).
+// ENC: the invert path's fused form, pix = the encoder's sample planes (enc_sample_rows).
+// CM: the batch's layout when every frame has the same (1..3; 0 general), or -1 for a mixed
+// batch (dispatched per frame): a kernel holds only its own path, whose registers alone then
+// set its occupancy (with all paths in one kernel, the fused form needed 127 VGPRs).
+// (The fused 2x1 form: 96 VGPRs, 5 waves per SIMD; held to 80 for 6 waves it spilled two
+// registers and ran no faster, 102.5 vs 103 us at 1080p x 32.)
+template <bool ENC, int CM>
 __global__ __launch_bounds__(256) void k_color(const DecFrame *__restrict__ fr, const uint8_t *__restrict__ planes,
-                                               uint8_t *__restrict__ pix, int bgr, int invert) {
+                                               uint8_t *__restrict__ pix, const EncFrame *__restrict__ efr, int bgr,
+                                               int invert) {
   const DecFrame &F = fr[blockIdx.z];
   const Geom &g = F.g;
   const int y0 = blockIdx.y * 2, x0 = (blockIdx.x * 256 + threadIdx.x) * 8;
@@ -1862,13 +2022,14 @@ __global__ __launch_bounds__(256) void k_color(const DecFrame *__restrict__ fr, 
   // the common layouts (classified on the host: one scalar word, where the int8 sampling
   // fields would each be a vector load and a wait) take a path whose plane loads are all
   // issued up front
-  const uint32_t cm = (F.flags >> 1) & 3u;
-  if (cm == 1) return color_rows<0>(F, g, planes, pix, y0, x0, two, bgr, invert);
-  if (cm == 2) return color_rows<1>(F, g, planes, pix, y0, x0, two, bgr, invert);
-  if (cm == 3) return color_rows<2>(F, g, planes, pix, y0, x0, two, bgr, invert);
+  const uint32_t cm = CM >= 0 ? (uint32_t)CM : (F.flags >> 1) & 3u;
+  if (cm == 1) return color_rows<0, ENC>(F, g, planes, pix, efr, y0, x0, two, bgr, invert);
+  if (cm == 2) return color_rows<1, ENC>(F, g, planes, pix, efr, y0, x0, two, bgr, invert);
+  if (cm == 3) return color_rows<2, ENC>(F, g, planes, pix, efr, y0, x0, two, bgr, invert);
   uint8_t o0[24], o1[24];
   color8(F, g, planes, y0, x0, bgr, invert, o0);
   color8(F, g, planes, two ? y0 + 1 : y0, x0, bgr, invert, o1);
+  if constexpr (ENC) return enc_sample_rows(efr[blockIdx.z], pix, o0, o1, y0, x0, g.w, bgr);
   const int w = g.w;
   uint8_t *const d0 = pix + F.out_off + ((size_t)y0 * w + x0) * 3;
   store24(d0, w - x0, o0);
@@ -1953,29 +2114,6 @@ __device__ __forceinline__ int16_t quantize(int32_t x, uint32_t recip, uint32_t 
   const uint32_t a = (uint32_t)((t ^ sg) - sg);
   const uint32_t p = ((a + corr) * recip) >> (sh & 31);
   return (int16_t)(((int32_t)p ^ sg) - sg);
-}
-
-// jccolor.c rgb_ycc_convert for one component over a pixel's bytes in memory order:
-// (a0 * c0 + a1 * c1 + a2 * c2 + bias) >> 16.  The component and the channel order are
-// wave-uniform in k_fdct, so the coefficients sit in scalar registers and a pixel costs three
-// multiply-adds with no per-pixel select.  No sum is negative (Cb and Cr carry 128 << 16:
-// their smallest sums are 575535 and 65535), so the shift is jccolor.c's.
-struct Ycc {
-  int a0, a1, a2, bias;
-};
-__device__ __forceinline__ Ycc ycc_coefs(int k, bool bgr) {
-  int r, g, b, bias = (128 << 16) + 32767;
-  if (k == 0) {
-    r = 19595, g = 38470, b = 7471, bias = 32768;
-  } else if (k == 1) {
-    r = -11059, g = -21709, b = 32768;
-  } else {
-    r = 32768, g = -27439, b = -5329;
-  }
-  return bgr ? Ycc{b, g, r, bias} : Ycc{r, g, b, bias};
-}
-__device__ __forceinline__ int ycc_apply(const Ycc &q, int c0, int c1, int c2) {
-  return (q.a0 * c0 + q.a1 * c1 + q.a2 * c2 + q.bias) >> 16;
 }
 
 // The 8 * H pixels of rows py .. py + R - 1 from px that one lane converts, edges replicated
@@ -2068,6 +2206,26 @@ __device__ __forceinline__ void fdct_pass1(const uint8_t *img, const Geom &g, in
   for (int j = 0; j < 8; ++j) wsrow[j] = v[j];
 }
 
+// Pass 1 from the invert path's sample planes (enc_sample_rows): row sy of the block is one
+// 8-byte load; level shift and the FDCT's row pass.  The table image store and the AC-word
+// clearing sit between the load and its use, as in fdct_pass1.
+template <bool FAST>
+__device__ __forceinline__ void fdct_pass1_planes(const uint8_t *plane, int pitch, int bx, int sy, bool real,
+                                                  const uint4 &tw, const uint8_t *dummy, uint4 *s_tab,
+                                                  uint32_t *acw_slot, uint32_t r, int32_t *wsrow) {
+  const uint2 q = *reinterpret_cast<const uint2 *>(real ? plane + (size_t)sy * pitch + bx * 8 : dummy);
+  if (threadIdx.x < 192) s_tab[threadIdx.x] = tw;
+  for (uint32_t i = r; i < (uint32_t)kAcScratchWords; i += 8) acw_slot[i] = 0;  // the block's own lanes
+  if (!real) return;
+  int32_t v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = (int32_t)(((j < 4 ? q.x : q.y) >> (8 * (j & 3))) & 0xFF) - 128;
+  if (FAST) fdct_ifast_line(v);
+  else fdct_islow_line(v, 0);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) wsrow[j] = v[j];
+}
+
 constexpr uint32_t kAcWords = kAcScratchWords;
 
 // AC scratch layout: blocks in groups of 64, word i of the 64 blocks of a group contiguous,
@@ -2152,7 +2310,8 @@ __device__ __forceinline__ uint32_t qo_at(uint32_t slot, uint32_t zz) {
 // is full size in every TurboJPEG subsampling, so each wave's sample path and butterflies are
 // fixed at compile time.
 constexpr uint32_t kFdctGroup = 8;  // MCUs per wave
-template <int CH, int CV, bool FAST>
+// PL: pix holds the invert path's sample planes (EncFrame::eplane_off; CH, CV unused)
+template <int CH, int CV, bool FAST, bool PL>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_fdct(const EncFrame *__restrict__ fr, const EncTables *tab, const uint8_t *pix,
                                               int16_t *dcq, uint32_t *acbits, uint32_t *acscr, int bgr) {
   const EncFrame &F = fr[blockIdx.y];
@@ -2197,9 +2356,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
   const uint8_t *dummy = reinterpret_cast<const uint8_t *>(tab->fdct_lds);  // 3 KB, 16-B aligned
   {  // pass 1: row r of the block's samples (the component is wave-uniform: luma is full size)
     const int sy = min((int)(by * 8 + r), (int)g.rrows[k] - 1);
-    const Ycc q = ycc_coefs((int)k, bgr != 0);
-    if (k == 0) fdct_pass1<1, 1, FAST>(img, g, (int)bx, sy, q, real, tw, dummy, s_tab, acw[slot], r, ws[slot][r]);
-    else fdct_pass1<CH, CV, FAST>(img, g, (int)bx, sy, q, real, tw, dummy, s_tab, acw[slot], r, ws[slot][r]);
+    if constexpr (PL) {
+      fdct_pass1_planes<FAST>(pix + F.eplane_off[k], g.wb[k] * 8, (int)bx, sy, real, tw, dummy, s_tab, acw[slot], r,
+                              ws[slot][r]);
+    } else {
+      const Ycc q = ycc_coefs((int)k, bgr != 0);
+      if (k == 0) fdct_pass1<1, 1, FAST>(img, g, (int)bx, sy, q, real, tw, dummy, s_tab, acw[slot], r, ws[slot][r]);
+      else fdct_pass1<CH, CV, FAST>(img, g, (int)bx, sy, q, real, tw, dummy, s_tab, acw[slot], r, ws[slot][r]);
+    }
   }
   __syncthreads();  // publishes the table image
   const int t = k > 0;
@@ -2716,25 +2880,44 @@ hipError_t dec_idct(const DecFrame *__restrict__ fr, int n, uint32_t max_blocks,
 }
 
 hipError_t dec_color(const DecFrame *__restrict__ fr, int n, int max_w, int max_h, const uint8_t *planes, uint8_t *pix, int bgr,
-                     int invert, hipStream_t s) {
+                     int invert, const EncFrame *efr, int cm, hipStream_t s) {
   if (n <= 0 || max_w <= 0 || max_h <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_color, dim3((unsigned)((max_w + 2047) / 2048), (unsigned)((max_h + 1) / 2), (unsigned)n), dim3(256), 0, s,
-                     fr, planes, pix, bgr, invert);
+  const dim3 grid((unsigned)((max_w + 2047) / 2048), (unsigned)((max_h + 1) / 2), (unsigned)n);
+#define VF_COLOR(E, C) hipLaunchKernelGGL((k_color<E, C>), grid, dim3(256), 0, s, fr, planes, pix, efr, bgr, invert)
+  if (efr) {
+    if (cm == 0) VF_COLOR(true, 0);
+    else if (cm == 1) VF_COLOR(true, 1);
+    else if (cm == 2) VF_COLOR(true, 2);
+    else if (cm == 3) VF_COLOR(true, 3);
+    else VF_COLOR(true, -1);
+  } else {
+    if (cm == 0) VF_COLOR(false, 0);
+    else if (cm == 1) VF_COLOR(false, 1);
+    else if (cm == 2) VF_COLOR(false, 2);
+    else if (cm == 3) VF_COLOR(false, 3);
+    else VF_COLOR(false, -1);
+  }
+#undef VF_COLOR
   return hipGetLastError();
 }
 
 hipError_t enc_fdct(const EncFrame *__restrict__ fr, int n, uint32_t max_blocks, const EncTables *tab, const uint8_t *pix,
-                    int16_t *dcq, uint32_t *acbits, uint32_t *acscr, int bgr, int fastdct, int ch, int cv,
+                    int16_t *dcq, uint32_t *acbits, uint32_t *acscr, int bgr, int fastdct, int ch, int cv, int planes,
                     hipStream_t s) {
   if (n <= 0 || !max_blocks) return hipSuccess;
   // a workgroup takes 4 units of 8 blocks; a frame has ceil(nmcu / 8) * bpm <= (nblocks + 70) / 8 units
   const dim3 grid((max_blocks + 70 + 31) / 32, (unsigned)n);
+  if (planes) {  // pix: the invert path's sample planes
+    if (fastdct) hipLaunchKernelGGL((k_fdct<1, 1, true, true>), grid, dim3(256), 0, s, fr, tab, pix, dcq, acbits, acscr, bgr);
+    else hipLaunchKernelGGL((k_fdct<1, 1, false, true>), grid, dim3(256), 0, s, fr, tab, pix, dcq, acbits, acscr, bgr);
+    return hipGetLastError();
+  }
 #define VF_FDCT(CH, CV)                                                                                              \
   if (ch == CH && cv == CV) {                                                                                        \
     if (fastdct)                                                                                                     \
-      hipLaunchKernelGGL((k_fdct<CH, CV, true>), grid, dim3(256), 0, s, fr, tab, pix, dcq, acbits, acscr, bgr);     \
+      hipLaunchKernelGGL((k_fdct<CH, CV, true, false>), grid, dim3(256), 0, s, fr, tab, pix, dcq, acbits, acscr, bgr); \
     else                                                                                                             \
-      hipLaunchKernelGGL((k_fdct<CH, CV, false>), grid, dim3(256), 0, s, fr, tab, pix, dcq, acbits, acscr, bgr);    \
+      hipLaunchKernelGGL((k_fdct<CH, CV, false, false>), grid, dim3(256), 0, s, fr, tab, pix, dcq, acbits, acscr, bgr); \
     return hipGetLastError();                                                                                        \
   }
   VF_FDCT(1, 1)

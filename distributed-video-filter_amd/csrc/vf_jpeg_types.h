@@ -144,6 +144,9 @@ struct EncFrame {
   uint64_t out_off;     // finished JPEG in the output buffer
   uint32_t hdr_off, hdr_len;  // header bytes in the header buffer
   uint32_t tile0, ntiles_max;  // stuffing tiles
+  // invert path: the encoder's component samples, written by the decoder's colour pass
+  // (k_color<true>) in place of pixels; plane k is wb[k] * 8 samples wide, rrows[k] rows
+  uint64_t eplane_off[3];
 };
 
 // Segmented scans over per-frame arrays (Huffman bit offsets, block counts, DC prediction,

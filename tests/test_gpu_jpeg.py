@@ -84,11 +84,14 @@ def test_invert_is_decode_not_encode(tj):
     assert tj.invert(jpgs[0]) == got[0]
 
 
+@pytest.mark.parametrize("fuse", ["1", "0"])
 @pytest.mark.parametrize("out_ss", [0, 1, 2, 3, 4])
-def test_invert_samplings_and_edges(tj, out_ss):
+def test_invert_samplings_and_edges(tj, monkeypatch, out_ss, fuse):
     """invert_batch for every output sampling over a batch of every input sampling, sizes
     that are not whole MCUs (right / bottom edge replication), both upsamplings and both
-    forward DCTs."""
+    forward DCTs; with the colour pass writing the encoder's sample planes (VF_JPEG_FUSE,
+    the default) and with the pixel round trip."""
+    monkeypatch.setenv("VF_JPEG_FUSE", fuse)
     jpgs = [J.encode(_img("scene" if i % 2 else "noise", 200 + i, h, w), 80, J.TJPF_BGR, i % 5)
             for i, (h, w) in enumerate(SIZES + [(31, 45), (480, 641), (23, 100)])]
     for flags in (0, TJFLAG_FASTUPSAMPLE | TJFLAG_FASTDCT):
