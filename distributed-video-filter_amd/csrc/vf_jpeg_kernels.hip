@@ -1766,9 +1766,27 @@ __device__ __forceinline__ int ycc_apply(const Ycc &q, int c0, int c1, int c2) {
 // the image, to the components' whole blocks.  Sample rows past rrows[k] are never read
 // (k_fdct clamps to the last).  One component at a time, from the packed pixels: the samples
 // of all three for both rows held at once cost the kernel two of its six waves per SIMD.
-__device__ __forceinline__ int ycc_of(uint32_t px, const Ycc &q) {  // q: R, G, B coefficients (scalar)
-  return (__mul24((int)(px & 0xFF), q.a0) + __mul24((int)((px >> 8) & 0xFF), q.a1) + __mul24((int)(px >> 16), q.a2) +
-          q.bias) >> 16;
+// Two of each sum's three products by one signed v_dot2 over a byte-permuted pair of the
+// packed pixel, the third (the coefficient that does not fit int16: 38470 for Y's G, 2^15 for
+// Cb's B and Cr's R) a 24-bit multiply-add into the accumulator with the rounding bias:
+//   Y  = 19595 R + 7471 B       + (38470 G + ONE_HALF)
+//   Cb = -11059 R - 21709 G     + (32768 B + CBCR_OFFSET + ONE_HALF - 1)
+//   Cr = -27439 G - 5329 B      + (32768 R + CBCR_OFFSET + ONE_HALF - 1)
+// The component's selectors and constants are wave-uniform (scalar): one code path for all.
+typedef short vf_i16x2 __attribute__((ext_vector_type(2)));
+struct EncCoef {
+  uint32_t sel, sh;  // byte permutation of the pair; position of the third channel
+  vf_i16x2 c;
+  int m, bias;
+};
+__device__ __forceinline__ EncCoef enc_coef(int k) {
+  if (k == 0) return EncCoef{0x0C020C00u, 8u, vf_i16x2{19595, 7471}, 38470, 32768};
+  if (k == 1) return EncCoef{0x0C010C00u, 16u, vf_i16x2{-11059, -21709}, 32768, (128 << 16) + 32767};
+  return EncCoef{0x0C020C01u, 0u, vf_i16x2{-27439, -5329}, 32768, (128 << 16) + 32767};
+}
+__device__ __forceinline__ int enc_sample(uint32_t px, const EncCoef &q) {
+  const vf_i16x2 pr = __builtin_bit_cast(vf_i16x2, __builtin_amdgcn_perm(px, px, q.sel));
+  return __builtin_amdgcn_sdot2(pr, q.c, __mul24((int)((px >> q.sh) & 0xFF), q.m) + q.bias, false) >> 16;
 }
 
 __device__ __forceinline__ void enc_store_rows(const EncFrame &E, uint8_t *__restrict__ eplanes, uint32_t (&p0)[8],
@@ -1795,11 +1813,11 @@ __device__ __forceinline__ void enc_store_rows(const EncFrame &E, uint8_t *__res
   for (int k = 0; k < ge.ncomp; ++k) {
     const int he = ge.he[k], ve = ge.ve[k], pitch = ge.wb[k] * 8, rr = ge.rrows[k];
     uint8_t *const pl = eplanes + E.eplane_off[k];
-    const Ycc q = ycc_coefs(k, false);
+    const EncCoef q = enc_coef(k);
     int c0[8], c1[8];
 #pragma unroll
-    for (int p = 0; p < 8; ++p) c0[p] = ycc_of(p0[p], q), c1[p] = ycc_of(p1[p], q);
-    const int e0 = edge ? ycc_of(l0, q) : 0, e1 = edge ? ycc_of(l1, q) : 0;
+    for (int p = 0; p < 8; ++p) c0[p] = enc_sample(p0[p], q), c1[p] = enc_sample(p1[p], q);
+    const int e0 = edge ? enc_sample(l0, q) : 0, e1 = edge ? enc_sample(l1, q) : 0;
     if (ve == 1) {
 #pragma unroll
       for (int rw = 0; rw < 2; ++rw) {

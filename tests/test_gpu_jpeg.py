@@ -100,6 +100,17 @@ def test_invert_samplings_and_edges(tj, monkeypatch, out_ss, fuse):
             assert g == J.invert_jpeg(j, 85, out_ss, flags), (len(j), out_ss, flags)
 
 
+@pytest.mark.parametrize("in_ss", [0, 1, 2, 3, 4])
+def test_invert_uniform_batches(tj, in_ss):
+    """A batch whose frames share one input sampling takes k_color's kernel specialised on that
+    layout (mixed batches dispatch per frame): each, fused, into 4:2:2 and 4:2:0."""
+    jpgs = [J.encode(_img("scene" if i % 2 else "noise", 300 + i, h, w), 85, J.TJPF_BGR, in_ss)
+            for i, (h, w) in enumerate([(17, 13), (8, 8), (64, 48), (31, 45), (130, 66)])]
+    for out_ss in (J.TJSAMP_422, J.TJSAMP_420):
+        for g, j in zip(tj.invert_batch(jpgs, 85, out_ss, 0), jpgs):
+            assert g == J.invert_jpeg(j, 85, out_ss, 0), (len(j), in_ss, out_ss)
+
+
 def test_invert_1080p_batch(tj):
     jpgs = [J.encode(_img("scene", s, 1080, 1920)) for s in range(3)]
     for g, j in zip(tj.invert_batch(jpgs), jpgs):
