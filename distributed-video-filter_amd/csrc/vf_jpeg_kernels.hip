@@ -1792,6 +1792,9 @@ __device__ __forceinline__ int enc_sample(uint32_t px, const EncCoef &q) {
 __device__ __forceinline__ void enc_store_rows(const EncFrame &E, uint8_t *__restrict__ eplanes, uint32_t (&p0)[8],
                                                uint32_t (&p1)[8], int y0, int x0, int w) {
   const Geom &ge = E.g;
+  // The edge thread's fill loops stay one byte per trip: unrolled and vectorised by the
+  // compiler, that rare path needed 91 VGPRs and set the whole kernel's occupancy (5 waves per
+  // SIMD; 60 VGPRs and 8 waves without it).
   const bool edge = x0 + 8 >= w;  // holds pixel w - 1 (and fills past it, up to the whole blocks)
   uint32_t l0 = 0, l1 = 0;        // the last pixel (edge thread)
   if (edge) {
@@ -1841,6 +1844,7 @@ __device__ __forceinline__ void enc_store_rows(const EncFrame &E, uint8_t *__res
         }
         if (edge) {
           const int ev = rw ? e1 : e0;
+          #pragma clang loop unroll(disable) vectorize(disable)
           for (int xs = (x0 + 8) / he; xs < pitch; ++xs) row[xs] = (uint8_t)ev;
         }
       }
@@ -1857,6 +1861,7 @@ __device__ __forceinline__ void enc_store_rows(const EncFrame &E, uint8_t *__res
           }
           *reinterpret_cast<uint2 *>(row + x0) = make_uint2(lo, hi);
           if (edge)
+            #pragma clang loop unroll(disable) vectorize(disable)
             for (int xs = x0 + 8; xs < pitch; ++xs) row[xs] = (uint8_t)((e0 + e1 + 1) >> 1);
         } else {  // bias 1, 2 alternating
           uint32_t v = 0;
@@ -1865,6 +1870,7 @@ __device__ __forceinline__ void enc_store_rows(const EncFrame &E, uint8_t *__res
             v |= (uint32_t)((c0[2 * i] + c0[2 * i + 1] + c1[2 * i] + c1[2 * i + 1] + 1 + (i & 1)) >> 2) << (8 * i);
           *reinterpret_cast<uint32_t *>(row + (x0 >> 1)) = v;
           if (edge)
+            #pragma clang loop unroll(disable) vectorize(disable)
             for (int xs = (x0 + 8) >> 1; xs < pitch; ++xs) row[xs] = (uint8_t)((2 * e0 + 2 * e1 + 1 + (xs & 1)) >> 2);
         }
       }
