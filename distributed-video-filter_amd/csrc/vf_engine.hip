@@ -85,6 +85,10 @@ void CopyPool::copy(uint8_t *dst, const uint8_t *src, size_t len) {
 }
 
 void CopyPool::start(std::function<void(int, int)> fn) {
+  if (n_ == 1) {  // no worker threads (VF_HOST_THREADS=0): the task runs here, before start returns
+    fn(0, 1);
+    return;
+  }
   {
     std::lock_guard<std::mutex> lk(mu_);
     fn_ = std::move(fn);
@@ -95,6 +99,7 @@ void CopyPool::start(std::function<void(int, int)> fn) {
 }
 
 void CopyPool::join() {
+  if (n_ == 1) return;
   std::unique_lock<std::mutex> lk(mu_);
   done_cv_.wait(lk, [this] { return pending_ == 0; });
   fn_ = nullptr;

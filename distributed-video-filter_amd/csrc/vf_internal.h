@@ -54,8 +54,10 @@ class CopyPool {
   ~CopyPool();
   void copy(uint8_t *dst, const uint8_t *src, size_t len);
   // fn(i, n) on each of the pool's n = threads() - 1 worker threads (i = 0 .. n-1), without
-  // the caller: start() returns at once, join() waits for every fn to return
-  int workers() const { return n_ - 1; }
+  // the caller: start() returns at once, join() waits for every fn to return.  A pool with no
+  // worker threads runs fn(0, 1) on the caller inside start() (a staged job must
+  // never launch before its bytes are copied); workers() is the number of fn calls either way.
+  int workers() const { return n_ > 1 ? n_ - 1 : 1; }
   void start(std::function<void(int, int)> fn);
   void join();
 

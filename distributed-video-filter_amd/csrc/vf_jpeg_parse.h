@@ -311,6 +311,7 @@ inline int parse(const uint8_t *b, size_t n, Parsed *P, std::string *err, bool f
       P->restart = (s[0] << 8) | s[1];
     } else if (m == 0xDA) {
       if (!sof) return fail("SOS before SOF");
+      if (len < 3) return fail("bad SOS");  // s[0] must lie inside the segment
       const int ns = s[0];
       if (ns != P->ncomp || (int)len != 6 + 2 * ns) return fail("only single-scan interleaved JPEG is supported");
       for (int i = 0; i < ns; ++i) {

@@ -10,6 +10,7 @@ raise.  (The CPU oracle under ``oracle/`` is test infrastructure and is never im
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
 import os
 import threading
@@ -178,13 +179,17 @@ class _PinnedArena:
     ``keep_bytes`` are returned to the library; blocks still referenced by arrays keep the context
     alive past ``close`` (its memory must outlive them)."""
 
-    def __init__(self, ctx: "Context", keep_bytes: int = 256 << 20):
+    def __init__(self, ctx: "Context", keep_bytes: int = 256 << 20, cap_bytes: Optional[int] = None):
         self._ctx = ctx
         self._lock = threading.Lock()
         self._free: dict = {}
         self._free_bytes = 0
         self._keep = keep_bytes
+        # page-locked bytes held by live result arrays; ``try_empty`` refuses past this (ADVICE
+        # r03: a caller keeping a whole clip of results must not pin all of it)
+        self.cap_bytes = int(os.environ.get("VF_PINNED_RESULT_CAP", 1 << 30)) if cap_bytes is None else cap_bytes
         self.outstanding = 0
+        self.outstanding_bytes = 0
 
     @staticmethod
     def _cap(nbytes: int) -> int:
@@ -200,19 +205,35 @@ class _PinnedArena:
             if ptr:
                 self._free_bytes -= cap
             self.outstanding += 1
+            self.outstanding_bytes += cap
         if not ptr:
             try:
                 ptr = self._ctx.alloc_host(cap)
             except Exception:
                 with self._lock:
                     self.outstanding -= 1
+                    self.outstanding_bytes -= cap
                 raise
         return np.asarray(_PinnedBlock(self, ptr, cap, shape, dtype))
+
+    def try_empty(self, shape, dtype=np.uint8) -> Optional[np.ndarray]:
+        """``empty``, or None when the live result arrays would pass ``cap_bytes`` or the
+        page-locked allocation fails (memlock limit, out of memory): the caller then uses
+        pageable memory, as ``cv2.bitwise_not`` would."""
+        nbytes = int(np.prod(shape, dtype=np.int64)) * np.dtype(dtype).itemsize
+        with self._lock:
+            if self.outstanding_bytes + self._cap(nbytes) > self.cap_bytes:
+                return None
+        try:
+            return self.empty(shape, dtype)
+        except VFilterError:
+            return None
 
     def release(self, ptr: int, cap: int) -> None:
         drop = []
         with self._lock:
             self.outstanding -= 1
+            self.outstanding_bytes -= cap
             self._free.setdefault(cap, []).append(ptr)
             self._free_bytes += cap
             while self._free_bytes > self._keep:
@@ -224,7 +245,7 @@ class _PinnedArena:
         for p in drop:
             ctx._free_host_raw(p)
         if last and ctx._closing:
-            ctx.close()
+            _defer_destroy(ctx)  # not here: this runs in a GC finalizer, on any thread
 
     def drain(self) -> list:
         with self._lock:
@@ -243,13 +264,22 @@ class Context:
 
     def __init__(self, device: int = 0, max_frame_bytes: int = 0, max_batch: int = 1):
         self._lib = load_library()
-        self._ctx = _vp()
-        st = self._lib.vf_create(int(device), int(max_frame_bytes), int(max_batch), ctypes.byref(self._ctx))
+        self._closing = False
+        self._h = _vp()
+        reap_closed_contexts()
+        st = self._lib.vf_create(int(device), int(max_frame_bytes), int(max_batch), ctypes.byref(self._h))
         if st != VF_OK:
             raise VFilterError(self._lib.vf_last_error(None).decode(), st, self._lib.vf_last_hip_error(None))
         self.device = int(device)
-        self._closing = False
         self._arena = _PinnedArena(self)
+
+    @property
+    def _ctx(self):
+        """The library handle for a call; a closed context refuses every call, also while arrays
+        of its pinned arena keep its memory alive."""
+        if self._closing or not self._h:
+            raise VFilterError("vfilter context is closed", VF_E_INVALID, 0)
+        return self._h
 
     # -- plumbing -----------------------------------------------------------------------
     def _check(self, st: int) -> None:
@@ -260,12 +290,19 @@ class Context:
 
     @property
     def handle(self) -> int:
-        return self._ctx.value or 0
+        return self._h.value or 0
+
+    @property
+    def closed(self) -> bool:
+        return self._closing
 
     def close(self) -> None:
-        """Destroy the context -- once no array of its pinned arena is alive (their memory must
-        outlive them; the last one to go finishes the close)."""
-        if not self._ctx:
+        """Close the context: every later call raises.  The library context is destroyed now,
+        or -- while arrays of its pinned arena are alive (their memory must outlive them) --
+        at the first ``reap_closed_contexts()`` after the last of them is gone (called by the
+        next ``Context()`` and at interpreter exit), never from a garbage-collector finalizer."""
+        h = self.__dict__.get("_h")
+        if not h:
             return
         self._closing = True
         arena = self.__dict__.get("_arena")
@@ -274,12 +311,17 @@ class Context:
                 self._free_host_raw(p)
             if arena.outstanding:
                 return
-        self._lib.vf_destroy(self._ctx)
-        self._ctx = _vp()
+        self._destroy()
+
+    def _destroy(self) -> None:
+        h = self.__dict__.get("_h")
+        if h:
+            self._lib.vf_destroy(h)
+            self._h = _vp()
 
     def _free_host_raw(self, p: int) -> None:
-        if self._ctx:
-            self._lib.vf_free_host(self._ctx, p)
+        if self._h:
+            self._lib.vf_free_host(self._h, p)
 
     # -- pinned result arrays ------------------------------------------------------------------
     def pinned_empty(self, shape, dtype=np.uint8) -> np.ndarray:
@@ -604,6 +646,29 @@ def default_device() -> int:
         if v not in (None, ""):
             return int(v)
     return 0
+
+
+_deferred_lock = threading.Lock()
+_deferred: list = []  # closed contexts whose last pinned result array is gone
+
+
+def _defer_destroy(ctx: "Context") -> None:
+    with _deferred_lock:
+        _deferred.append(ctx)
+
+
+def reap_closed_contexts() -> int:
+    """Destroy the library contexts of closed ``Context`` objects whose pinned result arrays are
+    all gone; returns how many.  Runs at each ``Context()`` and at exit."""
+    with _deferred_lock:
+        todo = _deferred[:]
+        _deferred.clear()
+    for c in todo:
+        c.close()  # its arena's free blocks back to the library, then vf_destroy
+    return len(todo)
+
+
+atexit.register(reap_closed_contexts)
 
 
 def get_context() -> Context:

@@ -160,6 +160,7 @@ class Distributor:
         self.transport = tp.resolve(transport)
         self._zctx = tp.make_context(self.transport)
         self.distribute_socket = tp.RouterEnd(self.transport, host, distribute_port, self._zctx)
+        self._wakeable = self.distribute_socket.wakeable
         self.collect_socket = tp.PullEnd(self.transport, host, collect_port, self._zctx)
         self.distribute_port = self.distribute_socket.port
         self.collect_port = self.collect_socket.port
@@ -437,7 +438,9 @@ class Distributor:
                 return -1
             copy_into(self.in_view(slot, nbytes), frame)
             return self.commit_frame(slot, nbytes, shape, timestamp, block)
-        return self._enqueue(frame, nbytes, shape, None, timestamp, block)
+        idx = self._enqueue(frame, nbytes, shape, None, timestamp, block)
+        self._kick()
+        return idx
 
     # ---- zero-copy ingest (ring mode) ------------------------------------------------------
     def reserve_frame(self, nbytes: int, block: bool = True) -> Optional[int]:
@@ -491,14 +494,24 @@ class Distributor:
 
     def commit_frame(self, slot: int, nbytes: int, shape=None, timestamp=None, block: bool = True) -> int:
         """Queue the frame written into ``slot``; returns its index (as add_frame_for_distribution)."""
-        return self._enqueue(None, nbytes, shape, slot, time.time() if timestamp is None else timestamp, block)
+        idx = self._enqueue(None, nbytes, shape, slot, time.time() if timestamp is None else timestamp, block)
+        self._kick()
+        return idx
 
     def commit_frames(self, slots: Sequence[int], nbytes: Sequence[int], shapes=None, timestamp=None) -> List[int]:
         """``commit_frame`` for a group of filled reservations, under one lock hold."""
         ts = time.time() if timestamp is None else timestamp
         with self._cv:
-            return [self._enqueue(None, nb, shapes[i] if shapes is not None else None, s_, ts, True)
-                    for i, (s_, nb) in enumerate(zip(slots, nbytes))]
+            out = [self._enqueue(None, nb, shapes[i] if shapes is not None else None, s_, ts, True)
+                   for i, (s_, nb) in enumerate(zip(slots, nbytes))]
+        self._kick()
+        return out
+
+    def _kick(self) -> None:
+        """Frames were queued: wake the dispatch thread's socket wait ("tcp"), so a worker holding
+        unserved credit is answered now rather than at the end of the poll."""
+        if self.policy != "latest" and self._wakeable:
+            self.distribute_socket.wake()
 
     def cancel_frame(self, slot: int) -> None:
         """Give back a reserved slot that will not be committed (its index, if one was fixed at
@@ -636,10 +649,14 @@ class Distributor:
     def handle_distribute_requests(self):
         while self.running:
             # while a worker holds unserved credit, frames committed during the socket wait
-            # must not wait out a whole poll: 0.2 ms then (1 ms, or the reference's 10 ms under
-            # "latest", otherwise)
+            # must not wait out a whole poll: with "tcp" a commit wakes the wait (``_kick``), so
+            # it is 1 ms (batch-fill deadlines and worker deadlines are checked at that pace);
+            # with "zmq" (whole-millisecond polls, no wake) it is 0.2 ms, and 1 ms otherwise;
+            # the reference's 10 ms under "latest"
             if self.policy == "latest":
                 poll_ms = 10
+            elif self._wakeable:
+                poll_ms = 1
             else:
                 with self._lock:
                     hungry = any(p.alive and p.requests for p in self._peers.values())
@@ -946,9 +963,23 @@ class Distributor:
         more ``batch_timeout``: ZeroMQ reports no disconnects, so a worker that died or hung
         would otherwise keep them out of use for ever and every eviction would shrink the ring
         (ADVICE r02).  A result that still arrives later finds no dispatch record and is
-        dropped (``_find_copy``), so it cannot be mistaken for the slot's next frame."""
+        dropped (``_find_copy``), so it cannot be mistaken for the slot's next frame.
+
+        Its BYTES are another matter: a worker that was only slow may still write
+        the stale result into the slot's output half after the slot has a new owner.  That is
+        harmless only where the new owner's result comes from the same worker, written after
+        the stale one: a slot of the evicted worker's own slice (``per_worker`` layout) is only
+        ever dispatched to that worker, which writes its results in dispatch order (one in-order
+        zero-copy stream; JPEG results are scattered in FIFO order), so its late write lands
+        before any later dispatch's.  A slot of the shared ring could go to any worker, so it
+        stays out of use until the late result frees it or the worker is known gone."""
         for idx in [i for i, it in p.quarantine.items() if now - it.get("_evicted_at", now) > self.batch_timeout]:
-            it = p.quarantine.pop(idx)
+            it = p.quarantine[idx]
+            slot = it.get("slot")
+            if slot is not None and not (self.ring_layout == "per_worker" and p.slice is not None
+                                         and slot // self.ring_slots == p.slice):
+                continue  # shared ring: held until the result or the disconnect
+            p.quarantine.pop(idx)
             self._free_slot(it.get("slot"))
             self._copy_done(it["frame_index"])
             self.quarantine_expired += 1

@@ -8,11 +8,14 @@ there is no CPU fallback.
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional, Sequence
 
 import numpy as np
 
 from ._lib import Context, get_context
+
+_PINNED_RESULTS = os.environ.get("VF_PINNED_RESULTS", "1") != "0"
 
 
 def bitwise_not(src: np.ndarray, dst: Optional[np.ndarray] = None, mask=None,
@@ -30,8 +33,12 @@ def bitwise_not(src: np.ndarray, dst: Optional[np.ndarray] = None, mask=None,
     ctx = ctx or get_context()
     if dst is None:
         # a result in the context's pinned arena: the kernel writes it directly over PCIe
-        # (no staging copy out); it goes back to the arena when the array is dropped
-        dst = ctx.pinned_empty_like(src)
+        # (no staging copy out); it goes back to the arena when the array is dropped.  Past the
+        # arena's cap of live results (VF_PINNED_RESULT_CAP, 1 GiB), when page-locking fails, or
+        # with VF_PINNED_RESULTS=0, the result is an ordinary array, as cv2.bitwise_not's is
+        dst = ctx._arena.try_empty(src.shape, src.dtype) if _PINNED_RESULTS else None
+        if dst is None:
+            dst = np.empty_like(src)
     elif dst.shape != src.shape or dst.dtype != src.dtype or not dst.flags.c_contiguous:
         raise ValueError("bitwise_not: dst must be C-contiguous with src's shape and dtype")
     ctx.invert_host(src, dst, src.nbytes)

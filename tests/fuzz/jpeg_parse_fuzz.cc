@@ -240,6 +240,36 @@ int main(int argc, char **argv) {
         e4.find("limit") == std::string::npos || e2.find("limit") == std::string::npos)
       return 4;
   }
+  // seeded edge cases: every corpus frame cut just after an SOS marker whose length field is
+  // 2..5 (the segment ends at the buffer's last byte, so a component-count read before the
+  // length check reads one byte past the input), each in an exact-size buffer
+  long sos_short = 0;
+  for (const auto &c : corpus) {
+    size_t sos = 0;
+    for (const Seg &s : segments(c))
+      if (s.m == 0xDA) sos = s.off;
+    if (!sos) return 5;
+    for (int len = 2; len <= 5; ++len) {
+      std::vector<uint8_t> b(c.begin(), c.begin() + (long)sos);
+      const uint8_t head[4] = {0xFF, 0xDA, 0x00, (uint8_t)len};
+      b.insert(b.end(), head, head + 4);
+      for (int k = 2; k < len; ++k) b.push_back(0x03);
+      uint8_t *buf = static_cast<uint8_t *>(std::malloc(b.size()));
+      std::memcpy(buf, b.data(), b.size());
+      Parsed H, P;
+      Geom g;
+      HuffDec dc[3], ac[3];
+      HuffSync sdc[3], sac[3];
+      uint16_t spair[3][1 << kLook];
+      std::string e1, e2;
+      const bool bad = parse(buf, b.size(), &H, &e1, false) != 0 &&
+                       !parse_frame(buf, b.size(), kDefaultMaxPixels, &P, &g, dc, ac, sdc, sac, spair, &e2);
+      std::free(buf);
+      if (!bad) return 6;  // a short SOS must be refused
+      ++sos_short;
+    }
+  }
+  std::printf("{\"sos_short_refused\": %ld}\n", sos_short);
   for (long i = 0; i < cases; ++i) {
     std::vector<uint8_t> b = corpus[r.below((uint32_t)corpus.size())];
     mutate(b, corpus, r);

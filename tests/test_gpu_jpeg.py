@@ -405,3 +405,35 @@ def test_async_result_scattered_into_caller_buffers(tj):
     outs = [np.zeros(len(w) + 8, np.uint8) for w in want]
     got = tj.invert_batch_result_into(tj.invert_batch_submit(jpgs), outs)
     assert [bytes(g) for g in got] == want
+
+
+def _assert_auto_pass_sync(jpgs):
+    # the auto rule (vf_jpeg_host.hip run_decode): frames above kSpecAutoSubs = 12,288 256-bit
+    # subsequences (393,216 bytes of entropy-coded data) take the pass-based span sync
+    assert all(len(j) > 12288 * 32 + 4096 for j in jpgs), [len(j) for j in jpgs]
+
+
+@pytest.mark.parametrize("kind", ["4k_scene_q85", "1080p_hard_q95"])
+def test_bench_operating_points_on_the_auto_path(tj, monkeypatch, kind):
+    """VERDICT r03 missing #1: the JPEG bench's own operating points, with no VF_JPEG_SYNC
+    override -- 4K camera-like scenes at q85 4:2:2 (bench jpeg_mode 4K) and hard 1080p noisy
+    scenes at q95 (bench hard_content / distributor.jpeg_1080p_hard, vfilter.synthetic's
+    content), both above the auto rule's size limit, so the pass-based span sync runs as in the
+    bench.  Re-encoded at the reference's quality 85 (inverter.py:44), byte for byte against
+    the oracle, through the synchronous call and the worker's submit / fetch form."""
+    from vfilter.synthetic import synthetic_noisy_scene, synthetic_scene
+    for var in ("VF_JPEG_SYNC", "VF_JPEG_SYNC_G", "VF_JPEG_SYNC_QUEUED", "VF_JPEG_WRITE4", "VF_JPEG_FUSE"):
+        monkeypatch.delenv(var, raising=False)
+    if kind == "4k_scene_q85":
+        jpgs = [J.encode(synthetic_scene(s, 2160, 3840), 85) for s in range(2)]
+    else:
+        jpgs = [J.encode(synthetic_noisy_scene(s, 1080, 1920), 95) for s in range(2)]
+    _assert_auto_pass_sync(jpgs)
+    want = [J.invert_jpeg(j) for j in jpgs]
+    got = tj.invert_batch(jpgs)
+    for i, (g, w) in enumerate(zip(got, want)):
+        assert g == w, (kind, i, len(g), len(w))
+    t1 = tj.invert_batch_submit(jpgs)
+    t2 = tj.invert_batch_submit(jpgs[::-1])
+    assert [bytes(g) for g in tj.invert_batch_result(t1)] == want
+    assert [bytes(g) for g in tj.invert_batch_result(t2)] == want[::-1]

@@ -475,6 +475,27 @@ def test_staged_small_jobs_every_side(vf_ctx, n):
     assert np.array_equal(r, want)
 
 
+@pytest.mark.parametrize("threads", ["0", "1"])
+def test_staged_jobs_without_copy_threads(monkeypatch, threads):
+    """VF_HOST_THREADS=0 (or 1) leaves the staging copy pool with no or one worker thread: the
+    staged job's copy-in must still land before its launch (with 0 threads the
+    launch read uninitialised staging memory and returned success)."""
+    monkeypatch.setenv("VF_HOST_THREADS", threads)
+    with vfilter.Context(0, max_frame_bytes=FB_1080, max_batch=4) as ctx:
+        for n in (17, FB_1080, 3 * FB_1080 + 5):
+            x = np.random.default_rng(n + 1).integers(0, 256, n + 16, dtype=np.uint8)
+            want = ~x[3:3 + n]
+            d = ctx.pinned_empty((n,))
+            d[:] = 0
+            ctx.invert_host(x[3:3 + n], d, n)                   # pageable -> mapped (staged in)
+            assert _zero_copy(ctx.last_timeline())
+            assert np.array_equal(d, want), n
+            z = np.zeros(n, np.uint8)
+            ctx.invert_host(x[3:3 + n], z, n)                   # pageable -> pageable (both staged)
+            assert np.array_equal(z, want), n
+            assert np.array_equal(vfilter.bitwise_not(x[3:3 + n], ctx=ctx), want)
+
+
 def _zero_copy(tl):
     """A zero-copy call reports one record whose H2D start = kernel start = 0 and kernel end =
     D2H end (one launch read the source and wrote the destination over PCIe)."""

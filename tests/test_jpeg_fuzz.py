@@ -47,6 +47,7 @@ def test_parse_survives_mutations_under_asan_ubsan(fuzzer, seed):
     assert p.returncode == 0, (p.returncode, p.stdout[-2000:], p.stderr[-4000:])
     lines = [json.loads(x) for x in p.stdout.splitlines() if x.startswith("{")]
     limits, summary = lines[0], lines[-1]
+    assert lines[1]["sos_short_refused"] == 4 * len(CORPUS)  # SOS length 2..5 at the buffer's end
     assert limits["limit_at"] == 1 and "limit" in limits["limit_below"]
     assert "65500" in limits["dim_65535"] and "limit" in limits["dim_65500"]
     assert summary["cases"] == 30000 and summary["corpus_ok"] == summary["corpus"] == len(CORPUS)

@@ -4,13 +4,19 @@
 the context's arena so the invert kernel writes it directly over PCIe (the drop-in's own
 shape, inverter.py:41).  Here a stand-in for the context's allocator checks the bookkeeping:
 blocks are recycled by size once the last view of an array is gone, free blocks beyond the
-keep limit are returned, and a context closed while arrays are alive is destroyed only when
-the last of them goes (their memory must outlive them)."""
+keep limit are returned, a context closed while arrays are alive is destroyed only after the
+last of them goes (their memory must outlive them) and then not from the garbage collector's
+finalizer but at the next ``reap_closed_contexts()``; live results past the arena's cap, or a
+failed page-locked allocation, make ``try_empty`` give None (the drop-in then returns an
+ordinary array), and a closed context refuses calls."""
 import gc
+import types
 
 import numpy as np
 
-from vfilter._lib import _PinnedArena
+import pytest
+
+from vfilter._lib import Context, VFilterError, _PinnedArena, _vp, reap_closed_contexts
 
 
 class _FakeCtx:
@@ -35,7 +41,10 @@ class _FakeCtx:
         for p in self._arena.drain():
             self._free_host_raw(p)
         if self._arena.outstanding == 0:
-            self.closed = True
+            self._destroy()
+
+    def _destroy(self):
+        self.closed = True
 
 
 def test_arrays_are_recycled_by_size_after_the_last_view():
@@ -72,4 +81,33 @@ def test_close_waits_for_live_arrays():
     assert not ctx.closed  # an array of the arena is alive
     del a
     gc.collect()
-    assert ctx.closed and not ctx.live
+    assert not ctx.closed  # the finalizer only queued it
+    assert reap_closed_contexts() == 1 and ctx.closed and not ctx.live
+    assert reap_closed_contexts() == 0
+
+
+def test_try_empty_respects_the_cap_and_allocation_failures():
+    ctx = _FakeCtx()
+    ctx._arena.cap_bytes = 3 * 4096
+    a = [ctx._arena.try_empty((4096,)) for _ in range(3)]
+    assert all(x is not None for x in a) and ctx._arena.outstanding_bytes == 3 * 4096
+    assert ctx._arena.try_empty((1,)) is None  # a fourth block would pass the cap
+    del a
+    gc.collect()
+    keep = ctx._arena.try_empty((100,))
+    assert keep is not None and ctx._arena.outstanding_bytes == 4096
+
+    def refuse(n):
+        raise VFilterError("hipHostMalloc failed")
+    ctx._arena.cap_bytes = 1 << 30
+    ctx.alloc_host = refuse
+    assert ctx._arena.try_empty((1 << 20,)) is None and ctx._arena.outstanding == 1  # the live one above
+
+
+def test_closed_context_refuses_calls():
+    c = Context.__new__(Context)  # no library context behind it: only the guard is exercised
+    c._closing, c._h = True, _vp(1)
+    c._lib = types.SimpleNamespace(vf_invert_host=lambda *a: 0)
+    with pytest.raises(VFilterError, match="closed"):
+        c.invert_host(np.zeros(4, np.uint8), np.zeros(4, np.uint8))
+    c._h = _vp()  # nothing to destroy

@@ -434,3 +434,57 @@ def test_evicted_workers_slots_come_back_after_the_grace_period():
         a.close()
         b.close()
         d.cleanup()
+
+
+@pytest.mark.timeout(60)
+def test_shared_ring_slots_of_an_evicted_worker_wait_for_its_result():
+    """a slot of the SHARED ring can be dispatched to any worker, so an evicted
+    worker that was only slow could write its stale result over the slot's next owner's.  Such
+    slots are not freed by the grace period; the late result (or a disconnect) frees them, and
+    the late result itself is dropped.  (A per-worker slice's slots do come back after the grace
+    period: only their own worker writes them, in dispatch order -- the test above.)"""
+    d = Distributor(0, 0, policy="pull", reassembly="ordered", queue_size=16, transport="tcp",
+                    host="127.0.0.1", verbose=False, batch_timeout=0.3, ring_slots=8, ring_slot_bytes=64,
+                    ring_layout="shared")
+    d.running = True
+    a, b = _ManualWorker(d, "A"), _ManualWorker(d, "B")
+    coll = threading.Thread(target=d.check_inverter_output, daemon=True)
+    coll.start()
+    try:
+        a.request()
+        _step_until(d, lambda: d.num_workers() == 1)
+        frames = [bytes([i + 1]) * 8 for i in range(4)]
+        for f in frames:
+            d.add_frame_for_distribution(f)
+        d.dispatch_step(0)
+        da = a.recv()
+        assert [m.index for m in da.metas] == [0, 1, 2, 3]
+        b.request()
+        _step_until(d, lambda: d.num_workers() == 2)
+        total = d.total_slots()
+        time.sleep(0.35)
+        d.dispatch_step(0)                                  # A evicted (hung), not gone
+        assert d.ordering_stats()["evictions"] == 1
+        b.request()
+        _step_until(d, lambda: b.dealer.poll(0))
+        db = b.recv()
+        b.answer(db)
+        for i in range(4):
+            item = d.get_next_frame(timeout=5)
+            assert item is not None and item[0] == i and bytes(item[1]) == oracle.invert_bytes(frames[i])
+            d.release_frame(item[0])
+        held = total - d.free_slots()
+        assert held == 4                                    # A's slots, quarantined
+        time.sleep(0.7)
+        for _ in range(5):
+            d.dispatch_step(0)
+        assert d.free_slots() == total - 4 and d.quarantine_expired == 0  # not freed by time alone
+        a.answer(da)                                        # the late result frees them, and is dropped
+        _step_until(d, lambda: d.free_slots() == total)
+        assert d.ordering_stats()["released"] == 4
+    finally:
+        d.running = False
+        coll.join(2)
+        a.close()
+        b.close()
+        d.cleanup()

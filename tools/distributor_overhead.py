@@ -31,8 +31,18 @@ class EchoWorker(Worker):
         return frame
 
 
-def run_worker(dport, cport, batch, inflight):
-    w = EchoWorker("127.0.0.1", dport, cport, batch=batch, protocol="v1", transport="tcp", inflight=inflight)
+class InPlaceWorker(Worker):
+    """``--no-copy``: every ring frame's result is its slot's output half as it stands (what a
+    GPU worker's zero-copy kernel writes in place), so no byte is touched on the host and the
+    rate is the control plane's alone: wire encode / decode, dispatch, collect, reassembly."""
+
+    def process_batch(self, frames, metas, outs):
+        return list(outs)
+
+
+def run_worker(dport, cport, batch, inflight, no_copy=False):
+    cls = InPlaceWorker if no_copy else EchoWorker
+    w = cls("127.0.0.1", dport, cport, batch=batch, protocol="v1", transport="tcp", inflight=inflight)
     try:
         w.start()
     finally:
@@ -43,22 +53,36 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workers", type=int, default=1)
     ap.add_argument("--bytes", type=int, default=181876)
+    ap.add_argument("--mixed", action="store_true",
+                    help="configs[3]'s stream: frame i is 480p / 1080p / 4K for i % 3 = 0 / 1 / 2 (--bytes ignored)")
+    ap.add_argument("--out", default="", help="append the JSON line to this file")
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--frames", type=int, default=20000)
     ap.add_argument("--inflight", type=int, default=3)
     ap.add_argument("--policy", default="pull", choices=("pull", "shard"))
     ap.add_argument("--profile", action="store_true")
+    ap.add_argument("--no-copy", action="store_true",
+                    help="frames committed in place (no producer copy) and results left in place by the "
+                         "workers: the control plane alone, at any --bytes (untouched shm pages cost no memory)")
     ap.add_argument("--group", type=int, default=1,
                     help="frames per reserve_frames / commit_frames / get_next_frames / release_frames call")
     args = ap.parse_args()
     import multiprocessing as mp
+    from vfilter.shm import shm_free_bytes
     mctx = mp.get_context("spawn")
+    sizes = [640 * 480 * 3, 1920 * 1080 * 3, 3840 * 2160 * 3] if args.mixed else [args.bytes]
+    slot_bytes = max(sizes)
+    slots = 4 * args.batch
+    free = shm_free_bytes()
+    if free is not None and not args.no_copy:  # untouched slots (--no-copy) take no memory
+        slots = max(2 * args.batch, min(slots, int(free * 0.6) // (2 * slot_bytes * args.workers)))
     d = Distributor(0, 0, policy=args.policy, reassembly="ordered", transport="tcp", host="127.0.0.1",
-                    queue_size=3 * args.batch * args.workers, ring_slots=4 * args.batch,
-                    ring_slot_bytes=args.bytes, shard_workers=args.workers, shard_chunk=args.batch,
+                    queue_size=3 * args.batch * args.workers, ring_slots=slots,
+                    ring_slot_bytes=slot_bytes, shard_workers=args.workers, shard_chunk=args.batch,
                     zero_copy=True, verbose=False)
     d.start()
-    procs = [mctx.Process(target=run_worker, args=(d.distribute_port, d.collect_port, args.batch, args.inflight),
+    procs = [mctx.Process(target=run_worker, args=(d.distribute_port, d.collect_port, args.batch, args.inflight,
+                                                            args.no_copy),
                           daemon=True) for _ in range(args.workers)]
     for p in procs:
         p.start()
@@ -68,18 +92,22 @@ def main():
             if time.time() - t0 > 60:
                 raise RuntimeError("workers did not come up")
             time.sleep(0.05)
-        src = np.random.default_rng(0).integers(0, 256, args.bytes, dtype=np.uint8)
+        srcs = [np.random.default_rng(0).integers(0, 256, b, dtype=np.uint8) for b in sizes]
         warm = 4 * args.batch * args.workers
         n = args.frames
 
         def produce():
             i = 0
             while i < warm + n:
-                slots = d.reserve_frames(args.bytes, min(args.group, warm + n - i))
-                for slot in slots:
-                    d.frame_view(slot, args.bytes)[:] = src
-                d.commit_frames(slots, [args.bytes] * len(slots))
-                i += len(slots)
+                got = d.reserve_frames(slot_bytes, min(args.group, warm + n - i))
+                nbs = []
+                for j, slot in enumerate(got):
+                    k = (i + j) % len(sizes)
+                    nbs.append(sizes[k])
+                    if not args.no_copy:
+                        d.frame_view(slot, sizes[k])[:] = srcs[k]
+                d.commit_frames(got, nbs)
+                i += len(got)
 
         th = threading.Thread(target=produce, daemon=True, name="producer")
         samples = {}
@@ -124,9 +152,15 @@ def main():
         el = time.perf_counter() - t_start
         stop_sampling.set()
         th.join()
-        print(json.dumps({"kind": "distributor_overhead", "workers": args.workers, "policy": args.policy,
-                          "frame_bytes": args.bytes, "batch": args.batch, "inflight": args.inflight,
-                          "frames": n, "fps": round(n / el, 1), "us_per_frame": round(el / n * 1e6, 2)}), flush=True)
+        line = {"kind": "distributor_overhead", "workers": args.workers, "policy": args.policy,
+                "frame_bytes": "mixed 480p/1080p/4K" if args.mixed else args.bytes, "no_copy": args.no_copy,
+                "batch": args.batch, "inflight": args.inflight, "ring_slots_per_worker": slots,
+                "host_cpus": len(os.sched_getaffinity(0)),
+                "frames": n, "fps": round(n / el, 1), "us_per_frame": round(el / n * 1e6, 2)}
+        print(json.dumps(line), flush=True)
+        if args.out:
+            with open(args.out, "a") as f:
+                f.write(json.dumps(line) + "\n")
         if args.profile:
             tot = {}
             for (th_name, key, inner), c in samples.items():

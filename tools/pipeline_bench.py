@@ -186,6 +186,10 @@ def main():
         counter = [0]
 
         group = max(1, min(16, args.batch // 2))  # reservations and commits per lock hold
+        # frames below this are copied on the producer thread itself: a pool hand-off (submit, wake,
+        # join: ~50-60 us) per 182 KB JPEG capped the system at 16-20 k fps;
+        # a 1080p / 4K raw frame's copy (0.3-2 ms) still goes to its slice's node pool
+        INLINE_COPY = 1 << 20
 
         def produce():
             while True:
@@ -200,7 +204,7 @@ def main():
                 done_ = 0
                 while done_ < g:
                     slots = d.reserve_frames(max_nb, g - done_)
-                    nbs, shs, futs, idxs = [], [], [], []
+                    nbs, shs, idxs, futs = [], [], [], []
                     for j, slot in enumerate(slots):
                         idx = d.reserved_index(slot)
                         idx = i0 + done_ + j if idx is None else idx
@@ -209,7 +213,10 @@ def main():
                         nb = fbytes[k]
                         if args.producer == "copy":
                             nd_ = slot_node(slot)
-                            if nd_ in node_pool:  # on the slice's own node
+                            if nb < INLINE_COPY:  # a JPEG / 480p frame: a hand-off costs more than the copy
+                                copy_into(d.frame_view(slot, nb), (pregen_on[nd_] if nd_ in node_pool else pregen)[k],
+                                          threads=1)
+                            elif nd_ in node_pool:  # on the slice's own node, frames of a group in parallel
                                 futs.append(node_pool[nd_].submit(copy_into, d.frame_view(slot, nb), pregen_on[nd_][k],
                                                                   1))
                             else:
