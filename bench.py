@@ -676,15 +676,15 @@ def distributor_leg(nworkers, ngpu, host_gbps=None, pcie_gbps=None, frames_scale
     tool = os.path.join(ROOT, "tools", "pipeline_bench.py")
     k4 = 2160 * 3840 * 3
     legs = {"configs[2]": (["--size", "4k", "--batch", "16", "--policy", "shard", "--producer", "copy",
-                            "--frames", str(int(256 * nworkers * frames_scale))], k4, 4.25),
+                            "--frames", str(int(768 * nworkers * frames_scale))], k4, 4.25),
             "configs[2]_resident": (["--size", "4k", "--batch", "16", "--policy", "shard", "--producer",
-                                     "resident", "--frames", str(int(256 * nworkers * frames_scale))], k4, 2.25),
+                                     "resident", "--frames", str(int(768 * nworkers * frames_scale))], k4, 2.25),
             "configs[3]": (["--size", "mixed", "--batch", "16", "--policy", "pull", "--producer", "copy",
-                            "--frames", str(int(384 * nworkers * frames_scale))],
+                            "--frames", str(int(1152 * nworkers * frames_scale))],
                            (640 * 480 + 1920 * 1080 + 3840 * 2160) * 3 // 3, 4.25),
             # the reference's default deployment: JPEG frames, workers in JPEG mode
             "jpeg_1080p": (["--jpeg", "--size", "1080p", "--batch", "32", "--policy", "pull",
-                            "--frames", str(int(4096 * nworkers * frames_scale))], 181876, None),
+                            "--frames", str(int(12288 * nworkers * frames_scale))], 181876, None),
             # the same deployment on hard content: 32 distinct noisy scenes at q95
             "jpeg_1080p_hard": (["--jpeg", "--content", "hard", "--size", "1080p", "--batch", "32", "--policy",
                                  "pull", "--frames", str(int(1536 * nworkers * frames_scale))], None, None)}
