@@ -112,6 +112,9 @@ class _Listener:
         self.inbox: "collections.deque[Tuple[bytes, Optional[List[bytes]]]]" = collections.deque()
         self._cond = threading.Condition(threading.Lock())
         self._woken = False
+        # set_handler: messages are handled on the peer's reader thread as they arrive, instead
+        # of queued for a polling thread (one thread hand-off less per message)
+        self.handler = None
         self.peers = {}
         self._ids = itertools.count(1)
         self._lock = threading.Lock()
@@ -133,7 +136,12 @@ class _Listener:
     def _read_loop(self, pid, conn):
         try:
             while not self._closed:
-                self._put((pid, _recv_msg(conn)))
+                msg = _recv_msg(conn)
+                h = self.handler
+                if h is not None:
+                    h(pid, msg)
+                else:
+                    self._put((pid, msg))
         except (ConnectionError, OSError):
             pass
         finally:
@@ -144,7 +152,11 @@ class _Listener:
             except OSError:
                 pass
             if not self._closed:
-                self._put((pid, None))  # disconnect notice (ZeroMQ gives none; see RouterEnd.recv)
+                h = self.handler
+                if h is not None:
+                    h(pid, None)
+                else:
+                    self._put((pid, None))  # disconnect notice (ZeroMQ gives none; see RouterEnd.recv)
 
     def _put(self, item) -> None:
         with self._cond:
@@ -288,6 +300,14 @@ class RouterEnd:
     def wakeable(self) -> bool:
         return self.kind != "zmq"
 
+    def set_handler(self, fn) -> bool:
+        """"tcp": call fn(peer, parts) on the peer's reader thread for every message (parts None:
+        the peer disconnected) instead of queueing it for ``poll`` / ``recv``.  False for "zmq"."""
+        if self.kind == "zmq":
+            return False
+        self.sock.handler = fn
+        return True
+
     def recv(self) -> Tuple[bytes, Optional[List[bytes]]]:
         """(peer, parts); parts is None when "tcp" saw the peer disconnect (the distributor
         then re-queues that worker's frames at once instead of waiting for their deadline)."""
@@ -334,6 +354,13 @@ class PullEnd:
         if got is None or got[1] is None:  # nothing, or a PUSH peer's disconnect notice
             raise BlockingIOError
         return got[1]
+
+    def set_handler(self, fn) -> bool:
+        """"tcp": call fn(parts) on the peer's reader thread for every result message."""
+        if self.kind == "zmq":
+            return False
+        self.sock.handler = lambda pid, parts: None if parts is None else fn(parts)
+        return True
 
     def close(self):
         self.sock.close()

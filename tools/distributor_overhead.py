@@ -10,6 +10,7 @@ whether a system-level rate (tools/pipeline_bench.py) is bound by the Python plu
 import argparse
 import json
 import os
+import resource
 import sys
 import threading
 import time
@@ -38,6 +39,22 @@ class InPlaceWorker(Worker):
 
     def process_batch(self, frames, metas, outs):
         return list(outs)
+
+
+def thread_cpu() -> dict:
+    """CPU seconds (user + system) of every thread of this process, by thread name (Linux)."""
+    tick = os.sysconf("SC_CLK_TCK")
+    names = {t.native_id: t.name for t in threading.enumerate()}
+    out = {}
+    for tid in os.listdir("/proc/self/task"):
+        try:
+            f = open(f"/proc/self/task/{tid}/stat").read().rsplit(")", 1)[1].split()
+        except OSError:
+            continue
+        nm = names.get(int(tid), "other")
+        nm = "reader" if "_read_loop" in nm else nm
+        out[nm] = out.get(nm, 0.0) + (int(f[11]) + int(f[12])) / tick
+    return out
 
 
 def run_worker(dport, cport, batch, inflight, no_copy=False):
@@ -143,6 +160,8 @@ def main():
         while i < warm + n:
             if t_start is None and i >= warm:
                 t_start = time.perf_counter()
+                ru0 = resource.getrusage(resource.RUSAGE_SELF)
+                th0 = thread_cpu()
                 samples.clear()
             items = d.get_next_frames(min(args.group, warm + n - i), timeout=60)
             if not items:
@@ -150,13 +169,24 @@ def main():
             d.release_frames([it[0] for it in items])
             i += len(items)
         el = time.perf_counter() - t_start
+        ru1 = resource.getrusage(resource.RUSAGE_SELF)
+        th1 = thread_cpu()
+        per_thread = {k: round((th1[k] - th0.get(k, 0.0)) / n * 1e6, 2) for k in th1}
+        cpu_us = ((ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)) / n * 1e6
+        sys_us = (ru1.ru_stime - ru0.ru_stime) / n * 1e6
+        csw = (ru1.ru_nvcsw - ru0.ru_nvcsw + ru1.ru_nivcsw - ru0.ru_nivcsw) / n
         stop_sampling.set()
         th.join()
-        line = {"kind": "distributor_overhead", "workers": args.workers, "policy": args.policy,
+        wst = d.ordering_stats()["workers"].values()
+        fpb = sum(w_["sent"] for w_ in wst) / max(1, sum(w_["batches"] for w_ in wst))
+        line = {"kind": "distributor_overhead", "frames_per_batch": round(fpb, 1), "workers": args.workers, "policy": args.policy,
                 "frame_bytes": "mixed 480p/1080p/4K" if args.mixed else args.bytes, "no_copy": args.no_copy,
                 "batch": args.batch, "inflight": args.inflight, "ring_slots_per_worker": slots,
                 "host_cpus": len(os.sched_getaffinity(0)),
-                "frames": n, "fps": round(n / el, 1), "us_per_frame": round(el / n * 1e6, 2)}
+                "frames": n, "fps": round(n / el, 1), "us_per_frame": round(el / n * 1e6, 2),
+                "distributor_cpu_us_per_frame": round(cpu_us, 2), "of_which_sys_us": round(sys_us, 2),
+                "context_switches_per_frame": round(csw, 2),
+                "thread_cpu_us_per_frame": {k: v for k, v in sorted(per_thread.items(), key=lambda kv: -kv[1]) if v > 0.5}}
         print(json.dumps(line), flush=True)
         if args.out:
             with open(args.out, "a") as f:
