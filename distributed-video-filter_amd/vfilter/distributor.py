@@ -1117,6 +1117,47 @@ class Distributor:
                 return q, it
         return None, None
 
+    def _on_result_fast(self, res: wire.Result, pid_val) -> bool:
+        """The common result message -- every frame a zero-copy ring result of the sender's own
+        dispatch, in flight once, no error, ordered reassembly, no trace -- booked in one pass
+        under one lock hold: what ``_on_result``'s general path does for it, with the per-frame
+        helper calls inlined.  False (nothing done) for any other message."""
+        if not (self.zero_copy and self.reassembly == "ordered" and res.wid and not self.enable_trace_export):
+            return False
+        with self._cv:
+            sender = self._by_wid.get(res.wid)
+            if sender is None:
+                return False
+            inflight, copies, settled = sender.inflight, self._copies, self._settled
+            for m in res.metas:
+                if (m.error is not None or m.slot is None or m.index not in inflight or m.index in settled
+                        or copies.get(m.index) != 1 or inflight[m.index].get("slot") is None):
+                    return False
+            sender.last_seen = time.monotonic()
+            sid_of, rs = self.ring_slots, self._slices
+            held, push = self._held, self._ordered.push
+            pid = res.pid
+            for m in res.metas:
+                idx = m.index
+                it = inflight.pop(idx)
+                b = it.pop("_batch", None)
+                if b is not None:
+                    b[1].discard(idx)
+                copies.pop(idx, None)
+                slot = it["slot"]
+                sid, k = divmod(slot, sid_of)
+                held[idx] = slot
+                push(idx, rs[sid].ring.out_view(k, m.nbytes),
+                     {"process_id": pid, "start_time": m.start, "end_time": m.end, "shape": m.shape, "slot": slot})
+            bq = sender.batches
+            while bq and not bq[0][1]:
+                bq.popleft()
+            n = len(res.metas)
+            sender.results += n
+            self.results_received += n
+            self._release_ready()
+        return True
+
     def _on_result(self, res: wire.Result):
         """One result message (a batch): bookkeeping for all its frames under one lock hold,
         the result bytes read outside it (each copy and its slot are this thread's alone once
@@ -1125,6 +1166,8 @@ class Distributor:
         for sp in res.spans:
             self.log_gpu_span(sp.get("name", "?"), float(sp["begin"]), float(sp["end"]), pid_val,
                               int(sp.get("bytes", 0)))
+        if self._on_result_fast(res, pid_val):
+            return
         reads = []
         with self._cv:
             sender = self._by_wid.get(res.wid) if res.wid else None

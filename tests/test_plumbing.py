@@ -110,6 +110,37 @@ def test_wire_v1_roundtrip_with_ring_and_errors():
     assert wire.decode_request([b"HELLO"]) is None
 
 
+def test_wire_v1_columns_roundtrip_every_field():
+    """The columnar v1 metadata: every FrameMeta field survives dispatch and result encoding
+    for uniform and mixed shapes, slots present / absent / mixed, per-frame and uniform times,
+    sparse errors; the earlier per-frame form ({"frames": [...]}) still decodes."""
+    import json as _json
+    rng = random.Random(5)
+    for trial in range(40):
+        n = rng.randint(1, 40)
+        same_shape = trial % 3 == 0
+        ms = []
+        for i in range(n):
+            shape = [4, 6, 3] if same_shape else rng.choice([None, [480, 640, 3], [2, 3, 3]])
+            slot = None if trial % 4 == 1 else (rng.randrange(256) if trial % 4 else rng.choice([None, 7]))
+            st = 1.5 if trial % 2 else rng.random()
+            ms.append(wire.FrameMeta(1000 * trial + i, rng.randrange(1, 10 ** 7), shape, slot, st,
+                                     st + (0.25 if trial % 2 else rng.random()),
+                                     rng.choice([None, None, None, f"err {i}"])))
+        pay = [None if m.slot is not None else bytes([i % 256]) * 3 for i, m in enumerate(ms)]
+        d = wire.decode_dispatch(wire.encode_dispatch(ms, pay))
+        for a, b in zip(ms, d.metas):
+            assert (a.index, a.nbytes, a.shape, a.slot) == (b.index, b.nbytes, b.shape, b.slot)
+        assert d.payloads == pay
+        rpay = [p_ if m.error is None else None for p_, m in zip(pay, ms)]
+        r = wire.decode_result(wire.encode_result(7, ms, rpay, wid="w"))
+        assert r.metas == ms and r.wid == "w"
+        assert r.payloads == [p_ if (m.slot is None and m.error is None) else None for p_, m in zip(pay, ms)]
+    legacy = [wire.RESULT_V1, _json.dumps({"pid": "3", "frames": [m.to_json() for m in ms]}).encode()]
+    legacy += [p_ for p_, m in zip(rpay, ms) if m.slot is None and m.error is None]
+    assert wire.decode_result(legacy).metas == ms
+
+
 # ---- transport -------------------------------------------------------------------------------
 
 def test_tcp_transport_roles():
