@@ -616,7 +616,16 @@ class Distributor:
             if self.policy == "latest":
                 self._ingest_latest(item)
             else:
-                self._lane_for(item).append(item)  # the dispatch thread polls; nobody waits on this
+                # lanes stay in index order (_take serves lowest indices first from the left);
+                # several producers may commit out of order
+                ln = self._lane_for(item)
+                if ln and ln[-1]["frame_index"] > idx:
+                    at = len(ln)
+                    while at > 0 and ln[at - 1]["frame_index"] > idx:
+                        at -= 1
+                    ln.insert(at, item)
+                else:
+                    ln.append(item)
             self.log_frame_timing(idx, timestamp, "frame_captured")
         return idx
 
@@ -881,6 +890,22 @@ class Distributor:
         if not lanes:
             return []
         out: List[dict] = []
+        if len(lanes) == 1:  # one lane, kept in index order: take from the left
+            ln, settled, skipped, took = lanes[0], self._settled, [], False
+            while ln and len(out) < credit:
+                it = ln.popleft()
+                took = True
+                if it["frame_index"] in settled:  # delivered from another copy
+                    self._release_copy(it)
+                elif self._place(it, p):
+                    out.append(it)
+                else:  # no free slot in this worker's slice for the copy: not waited on
+                    skipped.append(it)
+            for it in reversed(skipped):
+                ln.appendleft(it)
+            if took:
+                self._cv.notify_all()  # ingest may be waiting for room
+            return out
         taken = set()
         # lowest indices first; a copy that must move into this worker's slice but finds no
         # free slot there is skipped, not waited on (the slots may be held by the frames
@@ -946,14 +971,21 @@ class Distributor:
             if use_ring:
                 sid = next(it["slot"] for it in items if it["slot"] is not None) // self.ring_slots
                 ring = {"name": self._slices[sid].ring.name, "slot_bytes": self._slices[sid].ring.slot_bytes}
-            metas, payloads = [], []
-            for it in items:
-                in_ring = use_ring and it["slot"] is not None
-                metas.append(wire.FrameMeta(index=it["frame_index"], nbytes=it["nbytes"], shape=it["shape"],
-                                            slot=it["slot"] % self.ring_slots if in_ring else None))
-                payloads.append(None if in_ring else (it["frame"] if it["slot"] is None else
-                                                      bytes(self.in_view(it["slot"], it["nbytes"]))))
-            ok = self.distribute_socket.send(p.pid, wire.encode_dispatch(metas, payloads, ring))
+            if use_ring and all(it["slot"] is not None for it in items):  # every frame in the ring
+                rs = self.ring_slots
+                parts = wire.encode_dispatch_columns([it["frame_index"] for it in items], [it["nbytes"] for it in items],
+                                                     [it["slot"] % rs for it in items], [it["shape"] for it in items],
+                                                     [], ring)
+            else:
+                metas, payloads = [], []
+                for it in items:
+                    in_ring = use_ring and it["slot"] is not None
+                    metas.append(wire.FrameMeta(index=it["frame_index"], nbytes=it["nbytes"], shape=it["shape"],
+                                                slot=it["slot"] % self.ring_slots if in_ring else None))
+                    payloads.append(None if in_ring else (it["frame"] if it["slot"] is None else
+                                                          bytes(self.in_view(it["slot"], it["nbytes"]))))
+                parts = wire.encode_dispatch(metas, payloads, ring)
+            ok = self.distribute_socket.send(p.pid, parts)
         if ok:
             p.frames_sent += len(items)
             p.batches_sent += 1

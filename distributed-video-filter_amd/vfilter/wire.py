@@ -188,6 +188,22 @@ def encode_dispatch(metas: Sequence[FrameMeta], payloads: Sequence, ring: Option
     return [FRAMES_V1, head] + [p for m, p in zip(metas, payloads) if m.slot is None]
 
 
+def encode_dispatch_columns(index: List[int], nbytes: List[int], slots: Optional[List[Optional[int]]],
+                            shapes: List, payloads: Sequence, ring: Optional[dict] = None) -> List:
+    """``encode_dispatch`` from columns the caller already holds (the distributor's hot path:
+    no FrameMeta per frame); ``payloads`` are the parts of the frames without a slot, in order."""
+    d = {"index": index, "nbytes": nbytes}
+    if slots is not None:
+        d["slot"] = slots
+    if all(x == shapes[0] for x in shapes):
+        d["shape1"] = shapes[0] if shapes else None
+    else:
+        d["shape"] = shapes
+    if ring is not None:
+        d["ring"] = ring
+    return [FRAMES_V1, json.dumps(d).encode()] + list(payloads)
+
+
 def decode_dispatch(parts: Sequence) -> Dispatch:
     tag = bytes(parts[0])
     if tag != FRAMES_V1:                     # v0: [index, frame]   (worker.py:50-51)
