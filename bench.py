@@ -163,18 +163,19 @@ JPEG_STAGE_KERNELS = {
     "huffman_sync": ("k_spec", "k_wglink", "k_resolve", "k_finalize", "k_sync", "k_syncg"),
     "huffman_write": ("k_write", "k_write4"),
     "dc_idct": ("k_idct",),
-    "color_invert": ("k_color",),
+    "color_invert": ("k_color", "k_idct_color422"),
     "fdct_huffman": ("k_fdct", "k_len", "k_zero_stream", "k_pack"),
     "stuffing": ("k_ff_count", "k_ff_write", "k_compact"),
 }
 
 
-def pmc_jpeg(device=0):
+def pmc_jpeg(device=0, content="scene"):
     """One per-dispatch rocprofv3 PMC pass over the 1080p JPEG batch (tools/jpeg_bench.py, the
-    jpeg_mode workload: 32 frames of the 8 camera-like scenes, q85 4:2:2), run as a child
-    before anything in this process touches the GPU.  Per kernel, from its last dispatch:
-    VALU / LDS / SALU instructions and waves, and the shader clock (tools/pmc_issue.py).
-    Returns {kernel: {...}} or {"error": why}."""
+    jpeg_mode workload: 32 frames of the 8 camera-like scenes, q85 4:2:2; content "hard": the
+    hard_content workload, 32 noisy scenes at q95), run as a child before anything in this
+    process touches the GPU.  Per kernel, from its last dispatch: VALU / LDS / SALU instructions
+    and waves, and the shader clock (tools/pmc_issue.py).  Returns {kernel: {...}} or
+    {"error": why}."""
     rp = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
     if not os.path.exists(rp):
         return {"error": "rocprofv3 not found"}
@@ -183,7 +184,7 @@ def pmc_jpeg(device=0):
            "SQ_INSTS_LDS", "SQ_INSTS_SALU", "SQ_BUSY_CYCLES", "GRBM_GUI_ACTIVE", "GRBM_COUNT",
            "--output-format", "csv", "-d", out, "-o", "pmc", "--", sys.executable,
            os.path.join(ROOT, "tools", "jpeg_bench.py"), "--sizes", "1080p", "--batch", "32", "--iters", "3",
-           "--cpu-seconds", "0"]
+           "--cpu-seconds", "0", "--resident-only", "--content", content]
     try:
         r = subprocess.run(cmd, capture_output=True, text=True, env=dict(os.environ, VF_DEVICE=str(device)),
                            timeout=240)
@@ -589,12 +590,14 @@ def jpeg_mode(ctx, batch, iters=20):
             "hard_content": hard_content}, jpgs
 
 
-def jpeg_roofline(stages, h, w, batch, j_in, j_out):
+def jpeg_roofline(stages, h, w, batch, j_in, j_out, fused=None):
     """Per-stage algorithmic bytes of the fused JPEG pass (1080p 4:2:2 in and out) against the
     stage's hipEvent time, as a fraction of the 8 TB/s HBM peak, with the resource that binds
     each stage (from the SQ counters in profiles/r02_jpeg_pmc_sq.txt: none of the entropy or
     pixel stages is HBM-bound).  Bytes: J = compressed bytes in / out of the batch; per 4:2:2
     MCU of 16x8 pixels, 4 blocks of 64 coefficients (int16: 128 B) and 64 plane samples."""
+    if fused is None:  # the invert path's one-pass IDCT + colour (4:2:2 input; VF_JPEG_FUSE_IDCT=0: two)
+        fused = os.environ.get("VF_JPEG_FUSE_IDCT", "1") != "0" and os.environ.get("VF_JPEG_FUSE", "1") != "0"
     mcus = -(-w // 16) * -(-h // 8)
     blocks = batch * mcus * 4
     pix = batch * h * w * 3
@@ -605,12 +608,17 @@ def jpeg_roofline(stages, h, w, batch, j_in, j_out):
                          "dependent Huffman table lookups (LDS latency)"),
         "huffman_write": (j_in + coef, "read J_in, write the coefficient blocks",
                           "dependent Huffman table lookups (LDS latency)"),
-        "dc_idct": (coef + planes + 4 * blocks, "read coefficients + DC, write planes",
-                    "load latency + VALU (LDS conflict-free)"),
-        # the invert path's fused colour pass: the encoder's 4:2:2 sample planes (as many samples
-        # as the decoder's) instead of BGR pixels, read back by k_fdct
-        "color_invert": (2 * planes, "read planes, write the encoder's sample planes (inverted)",
-                         "load latency per wave"),
+        "dc_idct": ((8 * blocks, "the DC scan: read + write one int32 per block", "launch/latency (a few MB)")
+                    if fused else (coef + planes + 4 * blocks, "read coefficients + DC, write planes",
+                                   "load latency + VALU (LDS conflict-free)")),
+        # the invert path's colour pass writes the encoder's 4:2:2 sample planes (as many samples
+        # as the decoder's) instead of BGR pixels, read back by k_fdct; fused with the IDCT, the
+        # decoder's planes stay in LDS
+        "color_invert": ((coef + 4 * blocks + planes, "k_idct_color422: read coefficients + DC, write the "
+                          "encoder's sample planes (inverted); decoder planes in LDS",
+                          "load latency + VALU (IDCT, then colour from LDS)")
+                         if fused else (2 * planes, "read planes, write the encoder's sample planes (inverted)",
+                                        "load latency per wave")),
         "fdct_huffman": (planes + 3 * j_out + 10 * blocks, "read sample planes, write + pack AC words",
                          "VALU + issue latency"),
         "stuffing": (5 * j_out, "count + write FF00 stuffing, compact", "launch/latency (a few MB)"),
@@ -792,7 +800,7 @@ def main():
     # PMC passes run before ANY rank touches a GPU: rank 0's profiler child owns rank 0's GPU
     # (the others wait on a host-only barrier, so nothing else runs on the card being counted)
     traffic, traffic_detail = None, "skipped"
-    jpeg_pmc = None
+    jpeg_pmc = jpeg_pmc_hard = None
     if rank == 0 and not args.no_traffic:
         t0 = time.time()
         traffic, traffic_detail = pmc_traffic(args, device)
@@ -800,7 +808,8 @@ def main():
         if not args.no_jpeg:
             t0 = time.time()
             jpeg_pmc = pmc_jpeg(device)
-            log(f"pmc jpeg: {len(jpeg_pmc)} kernels in {time.time() - t0:.1f}s")
+            jpeg_pmc_hard = pmc_jpeg(device, "hard")
+            log(f"pmc jpeg: {len(jpeg_pmc)} + {len(jpeg_pmc_hard)} (hard) kernels in {time.time() - t0:.1f}s")
     if world > 1:
         dist.barrier(group=cpu_group)
     have_gpu = torch.cuda.is_available()
@@ -866,6 +875,9 @@ def main():
         jpeg = run_jpeg_child(device, args.batch, args.cpu_seconds)
         if isinstance(jpeg.get("roofline"), dict):
             jpeg_issue_fractions(jpeg["roofline"], jpeg_pmc)
+        hc = jpeg.get("hard_content")
+        if isinstance(hc, dict) and isinstance(hc.get("roofline"), dict):
+            jpeg_issue_fractions(hc["roofline"], jpeg_pmc_hard)
         log(f"jpeg mode: {jpeg}")
     if rank == 0 and args.cpu_seconds > 0:
         # after every timed region (the other ranks wait at the distributor leg's barrier); at

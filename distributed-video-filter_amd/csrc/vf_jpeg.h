@@ -29,7 +29,7 @@ hipError_t dec_unstuff_write(const DecSeg *sg, int nseg, uint32_t max_tiles, con
 // returns at once when changed[p - 1] == 0, so passes are queued without host round trips
 hipError_t dec_syncg(int G, const DecSeg *sg, const DecFrame *fr, int nseg, uint32_t max_sub, const uint8_t *us,
                      const uint32_t *us_len, uint64_t *exits, uint32_t *cnts, uint64_t *used, uint64_t *ck,
-                     uint32_t *ckrem, uint32_t *changed, int pass, hipStream_t s);
+                     uint32_t *ckrem, uint32_t *changed, int pass, uint32_t warm, hipStream_t s);
 hipError_t dec_sync(const DecSeg *sg, const DecFrame *fr, int nseg, uint32_t max_sub, const uint8_t *us, const uint32_t *us_len,
                     const uint64_t *exit_in, uint64_t *exit_out, const uint32_t *cnt_in, uint32_t *cnt_out,
                     uint64_t *used, uint64_t *ck, uint32_t *ckrem, uint32_t *changed, int pass, hipStream_t s);
@@ -72,15 +72,23 @@ hipError_t dec_sync_spec(const DecSeg *sg, const DecFrame *fr, int nseg, uint32_
                          hipStream_t s);
 hipError_t dec_write(const DecSeg *sg, const DecFrame *fr, int nseg, uint32_t max_sub, const uint8_t *us, const uint32_t *us_len,
                      const uint64_t *exits, const uint32_t *bstart, int16_t *coef, int32_t *dcseq,
-                     hipStream_t s);
+                     uint8_t *nmask, hipStream_t s);  // nmask: chunked coefficient rows (else a cleared buffer)
 // the write pass with 4 lanes per subsequence from the pass-based sync's converged checkpoints
 hipError_t dec_write4(const DecSeg *sg, const DecFrame *fr, int nseg, uint32_t max_sub, const uint8_t *us,
                       const uint32_t *us_len, const uint64_t *exits, const uint32_t *cnt, const uint64_t *ck,
-                      const uint32_t *ckrem, const uint32_t *bstart, int16_t *coef, int32_t *dcseq, hipStream_t s);
+                      const uint32_t *ckrem, const uint32_t *bstart, int16_t *coef, int32_t *dcseq, uint8_t *nmask,
+                      hipStream_t s);
+// nmask: per-block stored-row masks from the write pass's chunked form (null: a cleared buffer)
 hipError_t dec_idct(const DecFrame *fr, int n, uint32_t max_blocks, const int16_t *coef, const int32_t *dcseq,
-                    uint8_t *planes, hipStream_t s);
+                    const uint8_t *nmask, uint8_t *planes, hipStream_t s);
 hipError_t dec_color(const DecFrame *fr, int n, int max_w, int max_h, const uint8_t *planes, uint8_t *pix,
                      int bgr, int invert, const EncFrame *efr, int cm, hipStream_t s);
+// the invert path's IDCT + colour in one pass for a batch of standard 4:2:2 frames (sampling 2x1,
+// 1x1, 1x1): the decoder planes stay in LDS, the encoder's sample planes come out
+hipError_t dec_idct_color422(const DecFrame *fr, int n, int max_w, int max_h, const int16_t *coef,
+                             const int32_t *dcseq, const uint8_t *nmask, uint8_t *eplanes, const EncFrame *efr,
+                             int invert, int one_row,
+                             hipStream_t s);  // one_row: the encoder's chroma is not vertically downsampled
 
 hipError_t enc_fdct(const EncFrame *fr, int n, uint32_t max_blocks, const EncTables *tab, const uint8_t *pix,
                     int16_t *dcq, uint32_t *acbits, uint32_t *acscr, int bgr, int fastdct, int ch, int cv, int planes,

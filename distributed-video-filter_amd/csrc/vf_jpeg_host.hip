@@ -268,6 +268,17 @@ int Codec::init(std::string *err) {
 // Host parse of every frame + batch layout + upload of inputs and descriptors.
 // The invert path's fused colour pass (k_color writes the encoder's sample planes, k_fdct reads
 // them); VF_JPEG_FUSE=0 keeps the pixel round trip (read per call: tests switch it).
+// Bits a span-sync thread decodes before its span in pass 0, so that its entry is (usually)
+// synchronised already: 8 blocks' worth of the batch's bits per block -- the full state (bit
+// position, zigzag index, block-in-MCU) resynchronises at block boundaries (hard 1080p: ~250
+// bits per block, 2,024 bits of warm-up; 4K scenes: ~20, 160).  VF_JPEG_SYNC_WARM=<bits>
+// overrides (0: guessed entries), read per call: tests and A/Bs switch it inside one process.
+uint32_t Codec::sync_warm() const {
+  const char *v = std::getenv("VF_JPEG_SYNC_WARM");
+  if (v && *v && std::strcmp(v, "auto") != 0) return (uint32_t)std::strtoul(v, nullptr, 10);
+  return (uint32_t)std::min<uint64_t>(4096, 8 * dbits_per_block_) & ~31u;
+}
+
 static bool fuse_enabled() {
   const char *v = std::getenv("VF_JPEG_FUSE");
   return !(v && std::strcmp(v, "0") == 0);
@@ -304,6 +315,7 @@ int Codec::prepare_decode(const uint8_t *const *jpegs, const size_t *sizes, int 
     }
   dsg_.clear();
   dcm_ = -2;  // the batch's common k_color layout, or -1 (mixed)
+  d422_ = true;  // every frame standard 4:2:2 (k_idct_color422)
   for (int f = 0; f < n; ++f) {
     const Parsed &P = parsed[(size_t)f];
     DecFrame &F = dfr_[(size_t)f];
@@ -315,6 +327,8 @@ int Codec::prepare_decode(const uint8_t *const *jpegs, const size_t *sizes, int 
         cm = g.he[1] == 1 && g.ve[1] == 1 ? 1u : g.he[1] == 2 && g.ve[1] == 1 ? 2u : g.he[1] == 2 && g.ve[1] == 2 ? 3u : 0u;
       F.flags |= cm << 1;
       dcm_ = dcm_ == -2 || dcm_ == (int)cm ? (int)cm : -1;
+      d422_ = d422_ && g.ncomp == 3 && g.hs[0] == 2 && g.vs[0] == 1 && g.hs[1] == 1 && g.vs[1] == 1 &&
+              g.hs[2] == 1 && g.vs[2] == 1 && g.bpm == 4;
     }
     F.blk0 = blk;
     for (int c = 0; c < P.ncomp; ++c) {
@@ -379,6 +393,11 @@ int Codec::prepare_decode(const uint8_t *const *jpegs, const size_t *sizes, int 
   }
   dblocks_ = blk;
   dpix_bytes_ = pix;
+  {
+    uint64_t bits = 0;
+    for (const DecSeg &S : dsg_) bits += (uint64_t)S.in_len * 8;
+    dbits_per_block_ = blk ? bits / blk : 0;
+  }
   // scan segments: [0, nseg) unstuff tiles, [nseg, 2 nseg) subsequence counts, then DC sequences
   // (per entropy-coded segment and component: restart intervals reset the DC prediction)
   std::vector<ScanSeg> segs;
@@ -455,6 +474,7 @@ int Codec::prepare_decode(const uint8_t *const *jpegs, const size_t *sizes, int 
   }
   CK(d_changed_.ensure(sizeof(uint32_t) * kMaxPasses));
   CK(d_coef_.ensure(blk * 128));
+  CK(d_nmask_.ensure(blk + 16));
   CK(d_dcseq_.ensure(sizeof(int32_t) * (dcoff + 1)));
   CK(d_planes_.ensure(plane));
   CK(d_pix_.ensure(pix));
@@ -554,7 +574,7 @@ int Codec::run_decode(int bgr, bool invert, std::string *err) {
     for (int p = 0; p < queued_; ++p)
       CK(dec_syncg(sync_g, sg, fr, ns, dmax_sub_, d_us_.as<uint8_t>(), us_len, d_exit_[0].as<uint64_t>(),
                    d_cnt_[0].as<uint32_t>(), d_used_.as<uint64_t>(), d_ck_.as<uint64_t>(), d_ckrem_.as<uint32_t>(),
-                   d_changed_.as<uint32_t>(), p, s_));
+                   d_changed_.as<uint32_t>(), p, sync_warm(), s_));
     CK(h_flag_.ensure(64));
     CK(hipMemcpyAsync(h_flag_.p, d_changed_.as<uint32_t>() + queued_ - 1, sizeof(uint32_t),
                       hipMemcpyDeviceToHost, s_));
@@ -615,7 +635,7 @@ int Codec::finish_sync(std::string *err) {
     }
     CK(dec_syncg(sync_g_, sg, fr, dnseg_, dmax_sub_, d_us_.as<uint8_t>(), us_len, d_exit_[0].as<uint64_t>(),
                  d_cnt_[0].as<uint32_t>(), d_used_.as<uint64_t>(), d_ck_.as<uint64_t>(), d_ckrem_.as<uint32_t>(),
-                 d_changed_.as<uint32_t>(), p, s_));
+                 d_changed_.as<uint32_t>(), p, sync_warm(), s_));
     uint32_t flag = 0;
     CK(hipMemcpyAsync(&flag, d_changed_.as<uint32_t>() + p, sizeof flag, hipMemcpyDeviceToHost, s_));
     CK(hipStreamSynchronize(s_));
@@ -638,7 +658,18 @@ int Codec::run_decode_post(int bgr, bool invert, std::string *err) {
   uint32_t *blocks_total = static_cast<uint32_t *>(dtot_dev_);
   CK(scan_u32(segs + ns, ns, (dmax_sub_ + kScanTile - 1) / kScanTile, d_cnt_[last].as<uint32_t>(),
               d_bstart_.as<uint32_t>(), d_tsum_.as<uint32_t>(), blocks_total, false, s_));
-  CK(hipMemsetAsync(d_coef_.p, 0, dblocks_ * 128, s_));
+  // After the speculative sync, the write pass stores whole 16-B coefficient rows with a
+  // per-block mask of the rows stored, which the IDCT reads: no 134 MB clear per 1080p batch
+  // (k_write + clear 118 -> 105 us).  Not after the pass-based sync: its write pass runs 4 lanes
+  // per subsequence, and with blocks of ~250 bits (hard content) nearly every lane would decode
+  // on to its last block's end and skip its first: k_write4 342 -> 1227 us
+  // (profiles/r04_jpeg_chunks_ab.txt).  VF_JPEG_CHUNKS=0 / 1 forces either form.
+  const bool chunks = [use_spec] {  // read per call: tests switch it inside one process
+    const char *v = std::getenv("VF_JPEG_CHUNKS");
+    return v && *v ? std::strcmp(v, "0") != 0 : use_spec;
+  }();
+  uint8_t *const nmask = chunks ? d_nmask_.as<uint8_t>() : nullptr;
+  if (!chunks) CK(hipMemsetAsync(d_coef_.p, 0, dblocks_ * 128, s_));
   // after the pass-based sync, every subsequence's checkpoints are states of the true path: the
   // write pass runs 4 lanes per subsequence from them (VF_JPEG_WRITE4=0: one lane)
   const bool write4 = [] {  // read per call: tests switch it inside one process
@@ -648,16 +679,29 @@ int Codec::run_decode_post(int bgr, bool invert, std::string *err) {
   if (!use_spec && write4)
     CK(dec_write4(sg, fr, ns, dmax_sub_, d_us_.as<uint8_t>(), us_len, d_exit_[last].as<uint64_t>(),
                   d_cnt_[last].as<uint32_t>(), d_ck_.as<uint64_t>(), d_ckrem_.as<uint32_t>(),
-                  d_bstart_.as<uint32_t>(), d_coef_.as<int16_t>(), d_dcseq_.as<int32_t>(), s_));
+                  d_bstart_.as<uint32_t>(), d_coef_.as<int16_t>(), d_dcseq_.as<int32_t>(), nmask, s_));
   else
     CK(dec_write(sg, fr, ns, dmax_sub_, d_us_.as<uint8_t>(), us_len, d_exit_[last].as<uint64_t>(),
-                 d_bstart_.as<uint32_t>(), d_coef_.as<int16_t>(), d_dcseq_.as<int32_t>(), s_));
+                 d_bstart_.as<uint32_t>(), d_coef_.as<int16_t>(), d_dcseq_.as<int32_t>(), nmask, s_));
   CK(stage_event(3));
   // 4. DC prediction (inclusive scan per component sequence)
   CK(scan_i32(segs + 2 * ns, ndcseg_, dc_max_tiles_, d_dcseq_.as<int32_t>(), d_dcseq_.as<int32_t>(),
               d_tsum_.as<int32_t>(), nullptr, true, s_));
-  // 5. IDCT, 6. upsample + colour (+ invert)
-  CK(dec_idct(fr, n, dmax_blocks_, d_coef_.as<int16_t>(), d_dcseq_.as<int32_t>(), d_planes_.as<uint8_t>(), s_));
+  // 5. IDCT, 6. upsample + colour (+ invert).  The invert path on standard 4:2:2 frames does both
+  // in one pass with the decoder planes in LDS (k_idct_color422; VF_JPEG_FUSE_IDCT=0: two passes)
+  const bool fuse_idct = fuse_ && d422_ && [] {  // read per call: tests switch it inside one process
+    const char *v = std::getenv("VF_JPEG_FUSE_IDCT");
+    return !(v && std::strcmp(v, "0") == 0);
+  }();
+  if (fuse_idct) {
+    CK(stage_event(4));  // the DC scan above is the dc_idct stage; the fused pass the colour stage
+    CK(dec_idct_color422(fr, n, dmax_w_, dmax_h_, d_coef_.as<int16_t>(), d_dcseq_.as<int32_t>(), nmask,
+                         d_eplanes_.as<uint8_t>(), d_efr_.as<EncFrame>(), invert ? 1 : 0, kSampV[esub_] == 1 ? 1 : 0,
+                         s_));
+    CK(stage_event(5));
+    return kOk;
+  }
+  CK(dec_idct(fr, n, dmax_blocks_, d_coef_.as<int16_t>(), d_dcseq_.as<int32_t>(), nmask, d_planes_.as<uint8_t>(), s_));
   CK(stage_event(4));
   // the invert path (fuse_): the encoder's sample planes instead of pixels (enc_sample_rows)
   CK(dec_color(fr, n, dmax_w_, dmax_h_, d_planes_.as<uint8_t>(), fuse_ ? d_eplanes_.as<uint8_t>() : d_pix_.as<uint8_t>(),

@@ -305,9 +305,18 @@ struct HuffGeom {
 // block), storing coefficients (dense 64-entry rows, zigzag order) and DC differences
 // (jdhuff.c decode_mcu; an unmatched code reads as symbol 0 after 16 bits, a DC size over 16
 // as 16).
+//
+// CHUNKS (the default): no cleared buffer.  A block's AC coefficients are collected in registers
+// as 16-B chunks of 8 zigzag positions; each chunk holding a nonzero coefficient is stored whole
+// (its zeros included) and the block's byte in nmask records which chunks were stored, so the
+// IDCT reads the others as zero.  A block is written by the thread that decoded its DC: past
+// `end` that thread decodes on to the block's end, and a thread whose entry state lies inside
+// a block skips to that block's end without storing (the block is its predecessor's).  Replaces
+// a 134 MB clear per 1080p batch and the 2-byte scatters.
+template <bool CHUNKS>
 __device__ __forceinline__ void write_span(const uint32_t *w, uint32_t woff, uint64_t X, uint32_t end,
                                            const HuffGeom &g, const HuffDec *tabs, uint32_t blk, int16_t *coef,
-                                           int32_t *dcseq, const uint64_t *dcbase) {
+                                           int32_t *dcseq, const uint64_t *dcbase, uint8_t *nmask) {
   const uint32_t p = (uint32_t)(X >> 16);
   uint32_t wi = (p >> 5) - woff;
   uint64_t buf = (((uint64_t)bswap32(w[wi]) << 32) | bswap32(w[wi + 1])) << (p & 31);
@@ -320,7 +329,10 @@ __device__ __forceinline__ void write_span(const uint32_t *w, uint32_t woff, uin
   uint64_t dcb[3];
 #pragma unroll
   for (int q = 0; q < 3; ++q) dcb[q] = dcbase[q];
-  while (pos < end && blk < g.nblocks) {
+  bool own = z == 0;            // CHUNKS: the block in progress is this thread's
+  uint32_t cq = 0, m8 = 0;      // CHUNKS: the chunk being collected, chunks stored so far
+  uint32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0;
+  while (blk < g.nblocks && (CHUNKS ? (pos < end ? true : own && z != 0) : pos < end)) {
     const bool f = nb <= 32;
     buf |= f ? (uint64_t)bswap32(nxt) << (32 - nb) : 0ull;
     nb += f ? 32u : 0u;
@@ -347,12 +359,46 @@ __device__ __forceinline__ void write_span(const uint32_t *w, uint32_t woff, uin
     buf = b2 << sz;
     nb -= len + sz;
     pos += len + sz;
-    if (dc)
+    if (dc) {
       dcseq[HuffGeom::sel(dcb, k) + (uint64_t)mcu * HuffGeom::sel(g.bpc, k) + (c - HuffGeom::sel(g.cfirst, k))] = v;
-    else if (sz)
-      coef[(uint64_t)blk * 64 + (z + r < 63 ? z + r : 63)] = (int16_t)v;
+    } else if (sz) {
+      const uint32_t zz = z + r < 63 ? z + r : 63;
+      if constexpr (CHUNKS) {
+        if (own) {
+          const uint32_t q = zz >> 3;
+          if (q != cq) {  // a new chunk: store the one collected (if any)
+            if (m8 >> cq & 1)
+              *reinterpret_cast<uint4 *>(coef + (uint64_t)blk * 64 + cq * 8) = make_uint4(q0, q1, q2, q3);
+            q0 = q1 = q2 = q3 = 0;
+            cq = q;
+          }
+          m8 |= 1u << q;
+          const uint32_t hv = ((uint32_t)v & 0xFFFFu) << (16 * (zz & 1)), wsel = (zz >> 1) & 3;
+          q0 |= wsel == 0 ? hv : 0u;
+          q1 |= wsel == 1 ? hv : 0u;
+          q2 |= wsel == 2 ? hv : 0u;
+          q3 |= wsel == 3 ? hv : 0u;
+        }
+      } else {
+        coef[(uint64_t)blk * 64 + zz] = (int16_t)v;
+      }
+    }
     z = dc ? 1u : sz ? z + r + 1 : r == 15 ? z + 16 : 64u;
     const bool eob = z >= 64;
+    if constexpr (CHUNKS) {
+      if (eob && own) {
+        if (m8 >> cq & 1)
+          *reinterpret_cast<uint4 *>(coef + (uint64_t)blk * 64 + cq * 8) = make_uint4(q0, q1, q2, q3);
+        nmask[blk] = (uint8_t)m8;
+      }
+      own = own || eob;  // the next block starts here: inside the span (or the loop ends)
+      cq = eob ? 0u : cq;
+      m8 = eob ? 0u : m8;
+      q0 = eob ? 0u : q0;
+      q1 = eob ? 0u : q1;
+      q2 = eob ? 0u : q2;
+      q3 = eob ? 0u : q3;
+    }
     const uint32_t c1 = c + 1 == g.bpm ? 0u : c + 1;
     z = eob ? 0u : z;
     mcu += eob && c1 == 0 ? 1u : 0u;
@@ -538,6 +584,9 @@ __device__ __forceinline__ void load_sync_tables(const DecFrame &F, HuffSync *ta
 
 constexpr uint64_t kNoCk = ~0ull;
 constexpr uint32_t kSpecPadWords = 16;  // staged words past a workgroup's range: overshoot + lookahead
+// the write pass's CHUNKS form decodes on to the end of a block begun in its span: one block
+// is at most 64 codes of 16 bits + 15 extra bits (and the DC's), 2,000 bits
+constexpr uint32_t kBlockPadWords = 64;
 
 // One sync pass.  Every thread decodes its subsequence from its entry state; then, inside
 // the workgroup, a thread whose entry differs from its predecessor's current exit takes that
@@ -732,11 +781,17 @@ __device__ __forceinline__ uint64_t sync_span(const uint32_t *words, uint32_t wo
 #endif
 constexpr bool kSyncgStage = VF_SYNCG_STAGE;
 constexpr uint32_t syncg_threads(int G) { return !kSyncgStage || G <= 4 ? 256u : 1024u / (uint32_t)G; }
+// Pass 0's guessed entries can be warmed: a thread first decodes the `warm` bits before its span
+// from a guessed state (nothing recorded), so its entry is the state at the first symbol boundary
+// at or past the span's start, usually the true one already (tools/sync_sim.py --warm).
+constexpr uint32_t kSyncWarmMax = 4096;
 template <int G>
 __global__ __launch_bounds__(256) void k_syncg(const DecSeg *__restrict__ sg, const DecFrame *__restrict__ fr, const uint8_t *us,
                                                const uint32_t *us_len, uint64_t *exits, uint32_t *cnts, uint64_t *used,
-                                               uint64_t *ck, uint32_t *ckrem, uint32_t *changed, int pass) {
-  constexpr uint32_t T = syncg_threads(G), kWords = kSyncgStage ? T * G * (kSubBits / 32) + kSpecPadWords : 1;
+                                               uint64_t *ck, uint32_t *ckrem, uint32_t *changed, int pass, uint32_t warm) {
+  constexpr uint32_t kWarmWords = kSyncWarmMax / 32;
+  constexpr uint32_t T = syncg_threads(G),
+                     kWords = kSyncgStage ? kWarmWords + T * G * (kSubBits / 32) + kSpecPadWords : 1;
   __shared__ SyncTab32 tabs[6];
   __shared__ uint64_t s_exit[T];
   __shared__ uint32_t s_w[kWords];
@@ -745,10 +800,16 @@ __global__ __launch_bounds__(256) void k_syncg(const DecSeg *__restrict__ sg, co
   if (blockIdx.x * T * G >= S.nsub_max) return;
   if (pass > 0 && changed[pass - 1] == 0) return;  // converged (workgroup-uniform)
   const uint32_t *gw = reinterpret_cast<const uint32_t *>(us + S.us_off);
-  const uint32_t woff = kSyncgStage ? blockIdx.x * T * G * (kSubBits / 32) : 0u;
+  // staged from kWarmWords before the workgroup's first span (the warm-up of its first thread);
+  // words before the segment's start read as 0 and are never decoded
+  const int32_t wbase = kSyncgStage ? (int32_t)(blockIdx.x * T * G * (kSubBits / 32)) - (int32_t)kWarmWords : 0;
+  const uint32_t woff = (uint32_t)wbase;  // modular: s_w[i] holds word wbase + i
   if (kSyncgStage) {
     const uint32_t fwords = (((S.in_len + 64) + 15) & ~15u) / 4;
-    for (uint32_t i = threadIdx.x; i < kWords; i += T) s_w[i] = woff + i < fwords ? gw[woff + i] : 0u;
+    for (uint32_t i = threadIdx.x; i < kWords; i += T) {
+      const int32_t gwi = wbase + (int32_t)i;
+      s_w[i] = gwi >= 0 && (uint32_t)gwi < fwords ? gw[gwi] : 0u;
+    }
   }
   const uint32_t *words = kSyncgStage ? s_w : gw;
   load_sync_tabs32(F, tabs);  // its barrier also publishes s_w
@@ -764,6 +825,13 @@ __global__ __launch_bounds__(256) void k_syncg(const DecSeg *__restrict__ sg, co
   if (live) {
     if (pass == 0) {
       entry = i0 == 0 ? 0 : pack_state(i0 * kSubBits, 0, 0);  // a guess, except at the segment's start
+      if (i0 > 0 && warm > 0) {
+        const uint32_t b = i0 * kSubBits, w0 = b > warm ? b - warm : 0u;
+        SyncLane<SyncTab32> d;
+        d.init(words, woff, pack_state(w0, 0, 0), hg);
+        while (d.pos < b) d.step(tabs, b);
+        entry = pack_state(d.pos, d.z, d.c);
+      }
       need = true;
     } else {
       entry = t == 0 ? (i0 == 0 ? 0 : exits[gi0 - 1]) : used[gi0];
@@ -1333,11 +1401,12 @@ __global__ __launch_bounds__(256) void k_finalize(const DecSeg *__restrict__ sg,
 // The workgroup's stream words are staged in LDS first (as k_spec does): every refill of a
 // thread's bit buffer is then an LDS read instead of a dependent global load, the chain a
 // subsequence's decode waits on (k_write has only ~3 waves per SIMD to hide it with).
+template <bool CHUNKS>
 __global__ __launch_bounds__(256) void k_write(const DecSeg *__restrict__ sg, const DecFrame *__restrict__ fr, const uint8_t *us, const uint32_t *us_len,
                                                const uint64_t *exits, const uint32_t *bstart, int16_t *coef,
-                                               int32_t *dcseq) {
+                                               int32_t *dcseq, uint8_t *nmask) {
   __shared__ HuffDec tabs[6];
-  __shared__ uint32_t s_w[kSpecWords];
+  __shared__ uint32_t s_w[kSpecWords + (CHUNKS ? kBlockPadWords : 0)];
   const DecSeg S = sg[blockIdx.y];  // by value: held in scalar registers
   const DecFrame &F = fr[S.frame];
   if (blockIdx.x * 256 >= S.nsub_max) return;
@@ -1346,7 +1415,8 @@ __global__ __launch_bounds__(256) void k_write(const DecSeg *__restrict__ sg, co
   const uint32_t woff = blockIdx.x * 256 * (kSubBits / 32);
   const uint32_t fwords = (((S.in_len + 64) + 15) & ~15u) / 4;
   const uint32_t *gw = reinterpret_cast<const uint32_t *>(us + S.us_off);
-  for (uint32_t k = threadIdx.x; k < kSpecWords; k += 256) s_w[k] = woff + k < fwords ? gw[woff + k] : 0u;
+  constexpr uint32_t kWords = kSpecWords + (CHUNKS ? kBlockPadWords : 0);
+  for (uint32_t k = threadIdx.x; k < kWords; k += 256) s_w[k] = woff + k < fwords ? gw[woff + k] : 0u;
   load_tables(F, tabs);  // its barrier also publishes s_w
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   const uint32_t nbits = us_len[blockIdx.y] * 8u;
@@ -1357,7 +1427,7 @@ __global__ __launch_bounds__(256) void k_write(const DecSeg *__restrict__ sg, co
   const uint32_t end = (i + 1 == nsub) ? nbits : (i + 1) * kSubBits;
   HuffGeom hg(F.g);
   hg.nblocks = S.nblocks;  // the segment's blocks (a restart interval: its whole MCUs)
-  write_span(s_w, woff, st, end, hg, tabs, bstart[gi], coef + S.blk0 * 64, dcseq, S.dcbase);
+  write_span<CHUNKS>(s_w, woff, st, end, hg, tabs, bstart[gi], coef + S.blk0 * 64, dcseq, S.dcbase, nmask + S.blk0);
 }
 
 // The write pass with 4 lanes per subsequence, for the pass-based sync (k_sync), whose
@@ -1367,12 +1437,14 @@ __global__ __launch_bounds__(256) void k_write(const DecSeg *__restrict__ sg, co
 // 0 from the entry state) up to the next lane's start: the decode of a subsequence, a chain of
 // dependent table lookups, runs as 4 shorter chains side by side.  A lane whose checkpoint is
 // missing idles and the lane before it decodes on.
+template <bool CHUNKS>
 __global__ __launch_bounds__(256) void k_write4(const DecSeg *__restrict__ sg, const DecFrame *__restrict__ fr, const uint8_t *us,
                                                 const uint32_t *us_len, const uint64_t *exits, const uint32_t *cnt,
                                                 const uint64_t *ck, const uint32_t *ckrem, const uint32_t *bstart,
-                                                int16_t *coef, int32_t *dcseq) {
+                                                int16_t *coef, int32_t *dcseq, uint8_t *nmask) {
   static_assert(kCk + 1 == 4, "one lane per checkpoint-delimited quarter");
-  constexpr uint32_t kSubsPerWg = 64, kW4Words = kSubsPerWg * (kSubBits / 32) + kSpecPadWords;
+  constexpr uint32_t kSubsPerWg = 64,
+                     kW4Words = kSubsPerWg * (kSubBits / 32) + kSpecPadWords + (CHUNKS ? kBlockPadWords : 0);
   __shared__ HuffDec tabs[6];
   __shared__ uint32_t s_w[kW4Words];
   const DecSeg S = sg[blockIdx.y];  // by value: held in scalar registers
@@ -1406,7 +1478,8 @@ __global__ __launch_bounds__(256) void k_write4(const DecSeg *__restrict__ sg, c
     }
   HuffGeom hg(F.g);
   hg.nblocks = S.nblocks;
-  write_span(s_w, woff, st, stop, hg, tabs, bstart[gi] + before, coef + S.blk0 * 64, dcseq, S.dcbase);
+  write_span<CHUNKS>(s_w, woff, st, stop, hg, tabs, bstart[gi] + before, coef + S.blk0 * 64, dcseq, S.dcbase,
+                     nmask + S.blk0);
 }
 
 // ---- decoder: IDCT -------------------------------------------------------------------------
@@ -1515,8 +1588,10 @@ __constant__ uint32_t kIdctCol[8] = {  // column c: nibble i = g(8i + c)
 // j + 8), a workgroup 4 such units: the component and its geometry are wave-uniform (scalar),
 // no lane divides, and the 8 lanes of a block read the same dequantisation entries.
 constexpr uint32_t kIdctGroup = 8 * kIdctNb;  // MCUs per wave
+// nmask (the write pass's CHUNKS form): bit r of a block's byte says its coefficient row r (zigzag
+// 8r .. 8r + 7, this lane's 16-B load) was stored; the others read as zero.  Null: a cleared buffer.
 __global__ __launch_bounds__(256) void k_idct(const DecFrame *__restrict__ fr, const int16_t *coef, const int32_t *dcseq,
-                                              uint8_t *planes) {
+                                              const uint8_t *nmask, uint8_t *planes) {
   const DecFrame &F = fr[blockIdx.y];
   const Geom &g = F.g;
   const uint32_t bpm = (uint32_t)g.bpm, nmcu = (uint32_t)g.nmcu;
@@ -1538,6 +1613,7 @@ __global__ __launch_bounds__(256) void k_idct(const DecFrame *__restrict__ fr, c
   uint32_t bxs[kIdctNb], bys[kIdctNb];
   uint4 raw[kIdctNb];
   int32_t dc[kIdctNb];
+  uint32_t nm[kIdctNb];
 #pragma unroll
   for (int h = 0; h < kIdctNb; ++h) {
     const uint32_t mcu = grp * kIdctGroup + h * 8 + lm;
@@ -1552,6 +1628,7 @@ __global__ __launch_bounds__(256) void k_idct(const DecFrame *__restrict__ fr, c
     const uint64_t di = valid[h] ? F.dcbase[k] + (uint64_t)mcu * (mh * mv) + (c - (uint32_t)g.cfirst[k]) : F.dcbase[k];
     raw[h] = *reinterpret_cast<const uint4 *>(coef + bi * 64 + r * 8);
     dc[h] = dcseq[di];
+    nm[h] = nmask ? (uint32_t)nmask[bi] : 0xFFu;
   }
   // the tables after the coefficient loads: their round trips overlap instead of the
   // coefficients waiting behind the tables' barrier
@@ -1567,7 +1644,8 @@ __global__ __launch_bounds__(256) void k_idct(const DecFrame *__restrict__ fr, c
 #pragma unroll
   for (int h = 0; h < kIdctNb; ++h) {
     if (!valid[h]) continue;
-    const uint32_t qw[4] = {raw[h].x, raw[h].y, raw[h].z, raw[h].w};
+    const bool st = (nm[h] >> r) & 1;  // a row the write pass did not store is zero
+    const uint32_t qw[4] = {st ? raw[h].x : 0u, st ? raw[h].y : 0u, st ? raw[h].z : 0u, st ? raw[h].w : 0u};
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int32_t v = (int32_t)(int16_t)(qw[j >> 1] >> (16 * (j & 1)));
@@ -1789,6 +1867,8 @@ __device__ __forceinline__ int enc_sample(uint32_t px, const EncCoef &q) {
   return __builtin_amdgcn_sdot2(pr, q.c, __mul24((int)((px >> q.sh) & 0xFF), q.m) + q.bias, false) >> 16;
 }
 
+// ONE: only row y0 (p1 unused; the encoder's chroma must not be vertically downsampled)
+template <bool ONE = false>
 __device__ __forceinline__ void enc_store_rows(const EncFrame &E, uint8_t *__restrict__ eplanes, uint32_t (&p0)[8],
                                                uint32_t (&p1)[8], int y0, int x0, int w) {
   const Geom &ge = E.g;
@@ -1823,7 +1903,7 @@ __device__ __forceinline__ void enc_store_rows(const EncFrame &E, uint8_t *__res
     const int e0 = edge ? enc_sample(l0, q) : 0, e1 = edge ? enc_sample(l1, q) : 0;
     if (ve == 1) {
 #pragma unroll
-      for (int rw = 0; rw < 2; ++rw) {
+      for (int rw = 0; rw < (ONE ? 1 : 2); ++rw) {
         const int y = y0 + rw;
         if (y >= rr) break;
         uint8_t *row = pl + (size_t)y * pitch;
@@ -1917,8 +1997,19 @@ __device__ __forceinline__ void store24(uint8_t *dst, int left, const uint8_t o[
 // with every plane load of both rows issued before any is used (color8's per-component
 // branches leave the compiler waiting on each component's loads in turn: six round trips per
 // thread at 4:2:0).  4:2:0 reads chroma rows iy - 1, iy, iy + 1 once for both output rows.
-template <int MODE, bool ENC>
-__device__ __forceinline__ void color_rows(const DecFrame &F, const Geom &g, const uint8_t *__restrict__ planes,
+// The decoder's sample planes as color_rows reads them: row(k, y) points at column 0 of
+// component k's sample row y.  GlobalPlanes: the planes k_idct wrote (k_color);
+// StripPlanes: one MCU row's strip of them in LDS (k_idct_color), indexed by frame columns.
+struct GlobalPlanes {
+  const uint8_t *__restrict__ planes;
+  const DecFrame &F;
+  __device__ __forceinline__ const uint8_t *row(int k, int y) const {
+    return planes + F.plane_off[k] + (size_t)y * F.g.pw[k];
+  }
+};
+
+template <int MODE, bool ENC, typename PL, bool ONE = false>
+__device__ __forceinline__ void color_rows(const DecFrame &F, const Geom &g, const PL &pl,
                                            uint8_t *__restrict__ pix, const EncFrame *__restrict__ efr, int y0, int x0,
                                            bool two, int bgr, int invert) {
   const int y1 = two ? y0 + 1 : y0;
@@ -1927,9 +2018,8 @@ __device__ __forceinline__ void color_rows(const DecFrame &F, const Geom &g, con
     uint2 q[3][2];
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-      const uint8_t *p = planes + F.plane_off[k];
-      q[k][0] = *reinterpret_cast<const uint2 *>(p + (size_t)y0 * g.pw[k] + x0);
-      q[k][1] = *reinterpret_cast<const uint2 *>(p + (size_t)y1 * g.pw[k] + x0);
+      q[k][0] = *reinterpret_cast<const uint2 *>(pl.row(k, y0) + x0);
+      q[k][1] = *reinterpret_cast<const uint2 *>(pl.row(k, y1) + x0);
     }
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
@@ -1937,10 +2027,9 @@ __device__ __forceinline__ void color_rows(const DecFrame &F, const Geom &g, con
       unpack8(q[k][1], v1[k]);
     }
   } else {
-    const uint8_t *pY = planes + F.plane_off[0];
-    const uint2 qa = *reinterpret_cast<const uint2 *>(pY + (size_t)y0 * g.pw[0] + x0);
-    const uint2 qb = *reinterpret_cast<const uint2 *>(pY + (size_t)y1 * g.pw[0] + x0);
-    const int dw = g.dw[1], dh = g.dh[1], pw = g.pw[1];
+    const uint2 qa = *reinterpret_cast<const uint2 *>(pl.row(0, y0) + x0);
+    const uint2 qb = *reinterpret_cast<const uint2 *>(pl.row(0, y1) + x0);
+    const int dw = g.dw[1], dh = g.dh[1];
     const bool fancy = (F.flags & 1) && dw > 2;
     const int i0 = x0 >> 1;
     int ix[6];
@@ -1969,10 +2058,9 @@ __device__ __forceinline__ void color_rows(const DecFrame &F, const Geom &g, con
     for (int m = 0; m < 4; ++m) sh[m] = 8 * min(m, e);
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
-      const uint8_t *p = planes + F.plane_off[k + 1];
 #pragma unroll
       for (int rr = 0; rr < NR; ++rr) {
-        const uint8_t *r = p + (size_t)rows[rr] * pw;
+        const uint8_t *r = pl.row(k + 1, rows[rr]);
         const uint32_t mid = *reinterpret_cast<const uint32_t *>(r + i0);
         b[k][rr][0] = r[ix[0]];
 #pragma unroll
@@ -2002,7 +2090,7 @@ __device__ __forceinline__ void color_rows(const DecFrame &F, const Geom &g, con
   if constexpr (ENC) {  // decoded YCbCr -> inverted RGB (packed) -> the encoder's samples
     uint32_t p0[8], p1[8];
 #pragma unroll
-    for (int rw = 0; rw < 2; ++rw)
+    for (int rw = 0; rw < (ONE ? 1 : 2); ++rw)
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int yy = rw ? v1[0][j] : v0[0][j], cb = rw ? v1[1][j] : v0[1][j], cr = rw ? v1[2][j] : v0[2][j];
@@ -2014,7 +2102,7 @@ __device__ __forceinline__ void color_rows(const DecFrame &F, const Geom &g, con
         if (rw) p1[j] = two ? px : p0[j];
         else p0[j] = px;
       }
-    return enc_store_rows(efr[blockIdx.z], pix, p0, p1, y0, x0, g.w);
+    return enc_store_rows<ONE>(efr[blockIdx.z], pix, p0, p1, y0, x0, g.w);
   }
   uint8_t o0[24], o1[24];
   ycc8(v0, 3, bgr, invert, o0);
@@ -2047,9 +2135,10 @@ __global__ __launch_bounds__(256) void k_color(const DecFrame *__restrict__ fr, 
   // fields would each be a vector load and a wait) take a path whose plane loads are all
   // issued up front
   const uint32_t cm = CM >= 0 ? (uint32_t)CM : (F.flags >> 1) & 3u;
-  if (cm == 1) return color_rows<0, ENC>(F, g, planes, pix, efr, y0, x0, two, bgr, invert);
-  if (cm == 2) return color_rows<1, ENC>(F, g, planes, pix, efr, y0, x0, two, bgr, invert);
-  if (cm == 3) return color_rows<2, ENC>(F, g, planes, pix, efr, y0, x0, two, bgr, invert);
+  const GlobalPlanes gp{planes, F};
+  if (cm == 1) return color_rows<0, ENC>(F, g, gp, pix, efr, y0, x0, two, bgr, invert);
+  if (cm == 2) return color_rows<1, ENC>(F, g, gp, pix, efr, y0, x0, two, bgr, invert);
+  if (cm == 3) return color_rows<2, ENC>(F, g, gp, pix, efr, y0, x0, two, bgr, invert);
   uint8_t o0[24], o1[24];
   color8(F, g, planes, y0, x0, bgr, invert, o0);
   color8(F, g, planes, two ? y0 + 1 : y0, x0, bgr, invert, o1);
@@ -2058,6 +2147,144 @@ __global__ __launch_bounds__(256) void k_color(const DecFrame *__restrict__ fr, 
   uint8_t *const d0 = pix + F.out_off + ((size_t)y0 * w + x0) * 3;
   store24(d0, w - x0, o0);
   if (two) store24(d0 + (size_t)w * 3, w - x0, o1);
+}
+
+// ---- decoder: IDCT + colour in one pass (the invert path, standard 4:2:2) ---------------------
+//
+// k_idct wrote the decoder's sample planes (133 MB per 1080p batch of 32) and k_color read them
+// straight back.  Here a workgroup decodes one MCU row's strip of kStripMcus MCUs into LDS --
+// its 30 luma blocks and the 15 + 2 blocks of each chroma component that h2v1 fancy
+// upsampling reads (one chroma column each side comes from the neighbouring MCU: its whole
+// block is transformed for it) -- 64 blocks, k_idct's workgroup; then converts the strip's
+// pixels from LDS with color_rows, the same arithmetic as k_color.  Only standard 4:2:2 frames
+// (sampling 2x1, 1x1, 1x1; bpm 4) take it: 4:2:0's vertical context would need the MCU rows
+// above and below.
+constexpr int kStripMcus = 15;                 // 2 * 15 + 2 * (15 + 2) = 64 blocks
+constexpr int kStripY = kStripMcus * 16;       // luma samples per strip row (240)
+constexpr int kStripC = (kStripMcus + 2) * 8;  // chroma samples per strip row, one block each side (136)
+
+struct StripPlanes {
+  const uint8_t *y, *cb, *cr;  // [8][kStripY], [8][kStripC] x 2 (LDS)
+  int y_base, x_base, c_base;  // frame row of strip row 0, frame column of luma / chroma column 0
+  __device__ __forceinline__ const uint8_t *row(int k, int yy) const {
+    const int r = yy - y_base;
+    return k == 0 ? y + r * kStripY - x_base : (k == 1 ? cb : cr) + r * kStripC - c_base;
+  }
+};
+
+// ONE: the encoder's chroma is not vertically downsampled (its rows are independent), so every
+// thread converts one 8-pixel row (240 threads busy); else 8 pixels x 2 rows (120 threads).
+template <bool ONE>
+__global__ __launch_bounds__(256) void k_idct_color422(const DecFrame *__restrict__ fr, const int16_t *coef,
+                                                       const int32_t *dcseq, const uint8_t *nmask,
+                                                       uint8_t *__restrict__ eplanes, const EncFrame *__restrict__ efr,
+                                                       int invert) {
+  const DecFrame &F = fr[blockIdx.z];
+  const Geom &g = F.g;
+  const int mcux = g.mcux, my = blockIdx.y, m0 = blockIdx.x * kStripMcus;
+  if (m0 >= mcux || my >= g.mcuy) return;
+  __shared__ int32_t blkv[kIdctBlocks][72];
+  __shared__ int32_t s_q[3][72];
+  __shared__ uint8_t s_pos[64];
+  __shared__ uint32_t s_col[8];
+  // the strip's samples reuse the coefficient rows once pass 2 has read them (one barrier more,
+  // 4 KB less: 8 workgroups per CU instead of 6)
+  uint8_t *const s_y = reinterpret_cast<uint8_t *>(&blkv[0][0]);
+  uint8_t *const s_cb = s_y + 8 * kStripY, *const s_cr = s_cb + 8 * kStripC;
+  static_assert(8 * (kStripY + 2 * kStripC) <= (int)sizeof(blkv), "strip fits the coefficient rows");
+  const uint32_t t = threadIdx.x, slot = t >> 3, r = t & 7;
+  // block slot b = h * 32 + slot: 0..29 luma (MCU m0 + b / 2, block b % 2), 30..46 Cb and
+  // 47..63 Cr of MCU m0 - 1 + j
+  bool valid[kIdctNb];
+  uint32_t kk[kIdctNb], lx[kIdctNb];  // component; its strip column block
+  uint4 raw[kIdctNb];
+  int32_t dc[kIdctNb];
+  uint32_t nm[kIdctNb];
+#pragma unroll
+  for (int h = 0; h < kIdctNb; ++h) {
+    const int b = h * 32 + (int)slot;
+    const int k = b < 30 ? 0 : b < 47 ? 1 : 2;
+    const int j = k == 0 ? b : k == 1 ? b - 30 : b - 47;
+    const int mx = k == 0 ? m0 + (j >> 1) : m0 - 1 + j;
+    const int c = k == 0 ? (j & 1) : k + 1;
+    kk[h] = (uint32_t)k;
+    lx[h] = (uint32_t)j;
+    valid[h] = mx >= 0 && mx < mcux;
+    const uint64_t mcu = (uint64_t)my * mcux + (valid[h] ? mx : 0);
+    const uint64_t bi = valid[h] ? F.blk0 + mcu * 4 + c : F.blk0;
+    const uint64_t di = valid[h] ? F.dcbase[k] + mcu * (k == 0 ? 2 : 1) + (k == 0 ? (j & 1) : 0) : F.dcbase[0];
+    raw[h] = *reinterpret_cast<const uint4 *>(coef + bi * 64 + r * 8);
+    dc[h] = dcseq[di];
+    nm[h] = nmask ? (uint32_t)nmask[bi] : 0xFFu;
+  }
+  if (t < 192) s_q[t >> 6][t & 63] = F.q[t >> 6][t & 63];
+  if (t < 64) s_pos[t] = kIdctPos[t];
+  if (t < 8) s_col[t] = kIdctCol[t];
+  __syncthreads();
+  const uint2 pos8 = *reinterpret_cast<const uint2 *>(&s_pos[r * 8]);
+  const uint32_t colg = s_col[r];
+#pragma unroll
+  for (int h = 0; h < kIdctNb; ++h) {
+    if (!valid[h]) continue;
+    const bool st = (nm[h] >> r) & 1;  // a row the write pass did not store is zero
+    const uint32_t qw[4] = {st ? raw[h].x : 0u, st ? raw[h].y : 0u, st ? raw[h].z : 0u, st ? raw[h].w : 0u};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int32_t v = (int32_t)(int16_t)(qw[j >> 1] >> (16 * (j & 1)));
+      const uint32_t at = ((j < 4 ? pos8.x : pos8.y) >> (8 * (j & 3))) & 0xFF;
+      blkv[h * 32 + slot][at] = (r == 0 && j == 0) ? (int32_t)(int16_t)dc[h] : v;
+    }
+  }
+  __syncthreads();
+  int32_t col[kIdctNb][8];
+#pragma unroll
+  for (int h = 0; h < kIdctNb; ++h) {  // pass 1: column r, dequantised
+    if (!valid[h]) continue;
+    int32_t in[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      in[i] = __mul24(blkv[h * 32 + slot][i * 8 + ((colg >> (4 * i)) & 7)], s_q[kk[h]][i * 8 + r]);
+    idct_line(in, col[h], 11);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int h = 0; h < kIdctNb; ++h) {
+    if (!valid[h]) continue;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) blkv[h * 32 + slot][i * 9 + r] = col[h][i];
+  }
+  __syncthreads();
+  uint2 row8[kIdctNb];
+#pragma unroll
+  for (int h = 0; h < kIdctNb; ++h) {  // pass 2: row r
+    int32_t in[8], out[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) in[i] = blkv[h * 32 + slot][r * 9 + i];
+    idct_line(in, out, 18);
+    uint32_t lo = 0, hi = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      lo |= idct_limit(out[i]) << (8 * i);
+      hi |= idct_limit(out[i + 4]) << (8 * i);
+    }
+    row8[h] = make_uint2(lo, hi);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int h = 0; h < kIdctNb; ++h) {  // into the strip
+    if (!valid[h]) continue;
+    uint8_t *dst = kk[h] == 0 ? s_y + r * kStripY : (kk[h] == 1 ? s_cb : s_cr) + r * kStripC;
+    *reinterpret_cast<uint2 *>(dst + lx[h] * 8) = row8[h];
+  }
+  __syncthreads();
+  // colour: 8 pixels x 1 row (ONE: 30 x 8 threads) or x 2 rows (30 x 4 threads)
+  constexpr int kRows = ONE ? 1 : 2;
+  if (t >= (uint32_t)(2 * kStripMcus * (8 / kRows))) return;
+  const int px = (int)t % (2 * kStripMcus), rp = (int)t / (2 * kStripMcus);
+  const int y0 = my * 8 + kRows * rp, x0 = m0 * 16 + px * 8;
+  if (y0 >= g.h || x0 >= g.w) return;
+  const StripPlanes sp{s_y, s_cb, s_cr, my * 8, m0 * 16, (m0 - 1) * 8};
+  color_rows<1, true, StripPlanes, ONE>(F, g, sp, eplanes, efr, y0, x0, !ONE && y0 + 1 < g.h, 0, invert);
 }
 
 // ---- encoder: colour + downsampling + FDCT + quantisation -----------------------------------
@@ -2848,13 +3075,14 @@ hipError_t dec_sync(const DecSeg *__restrict__ sg, const DecFrame *__restrict__ 
 
 hipError_t dec_syncg(int G, const DecSeg *__restrict__ sg, const DecFrame *__restrict__ fr, int nseg, uint32_t max_sub,
                      const uint8_t *us, const uint32_t *us_len, uint64_t *exits, uint32_t *cnts, uint64_t *used,
-                     uint64_t *ck, uint32_t *ckrem, uint32_t *changed, int pass, hipStream_t s) {
+                     uint64_t *ck, uint32_t *ckrem, uint32_t *changed, int pass, uint32_t warm, hipStream_t s) {
   if (nseg <= 0 || !max_sub) return hipSuccess;
+  warm = std::min<uint32_t>(warm, kSyncWarmMax) & ~31u;
 #define VF_SYNCG(GG)                                                                                              \
   if (G == GG) {                                                                                                  \
     const uint32_t span = syncg_threads(GG) * GG;                                                                 \
     hipLaunchKernelGGL(k_syncg<GG>, dim3((max_sub + span - 1) / span, (unsigned)nseg), dim3(syncg_threads(GG)),   \
-                       0, s, sg, fr, us, us_len, exits, cnts, used, ck, ckrem, changed, pass);                    \
+                       0, s, sg, fr, us, us_len, exits, cnts, used, ck, ckrem, changed, pass, warm);              \
     return hipGetLastError();                                                                                     \
   }
   VF_SYNCG(1)
@@ -2878,28 +3106,37 @@ hipError_t dec_sync_spec(const DecSeg *__restrict__ sg, const DecFrame *__restri
 
 hipError_t dec_write(const DecSeg *__restrict__ sg, const DecFrame *__restrict__ fr, int nseg, uint32_t max_sub, const uint8_t *us,
                      const uint32_t *us_len, const uint64_t *exits, const uint32_t *bstart, int16_t *coef,
-                     int32_t *dcseq, hipStream_t s) {
+                     int32_t *dcseq, uint8_t *nmask, hipStream_t s) {
   if (nseg <= 0 || !max_sub) return hipSuccess;
-  hipLaunchKernelGGL(k_write, dim3((max_sub + 255) / 256, (unsigned)nseg), dim3(256), 0, s, sg, fr, us, us_len, exits,
-                     bstart, coef, dcseq);
+  const dim3 grid((max_sub + 255) / 256, (unsigned)nseg);
+  if (nmask)
+    hipLaunchKernelGGL(k_write<true>, grid, dim3(256), 0, s, sg, fr, us, us_len, exits, bstart, coef, dcseq, nmask);
+  else
+    hipLaunchKernelGGL(k_write<false>, grid, dim3(256), 0, s, sg, fr, us, us_len, exits, bstart, coef, dcseq, nmask);
   return hipGetLastError();
 }
 
 hipError_t dec_write4(const DecSeg *__restrict__ sg, const DecFrame *__restrict__ fr, int nseg, uint32_t max_sub, const uint8_t *us,
                       const uint32_t *us_len, const uint64_t *exits, const uint32_t *cnt, const uint64_t *ck,
-                      const uint32_t *ckrem, const uint32_t *bstart, int16_t *coef, int32_t *dcseq, hipStream_t s) {
+                      const uint32_t *ckrem, const uint32_t *bstart, int16_t *coef, int32_t *dcseq, uint8_t *nmask,
+                      hipStream_t s) {
   if (nseg <= 0 || !max_sub) return hipSuccess;
-  hipLaunchKernelGGL(k_write4, dim3((max_sub + 63) / 64, (unsigned)nseg), dim3(256), 0, s, sg, fr, us, us_len, exits,
-                     cnt, ck, ckrem, bstart, coef, dcseq);
+  const dim3 grid((max_sub + 63) / 64, (unsigned)nseg);
+  if (nmask)
+    hipLaunchKernelGGL(k_write4<true>, grid, dim3(256), 0, s, sg, fr, us, us_len, exits, cnt, ck, ckrem, bstart, coef,
+                       dcseq, nmask);
+  else
+    hipLaunchKernelGGL(k_write4<false>, grid, dim3(256), 0, s, sg, fr, us, us_len, exits, cnt, ck, ckrem, bstart, coef,
+                       dcseq, nmask);
   return hipGetLastError();
 }
 
 hipError_t dec_idct(const DecFrame *__restrict__ fr, int n, uint32_t max_blocks, const int16_t *coef, const int32_t *dcseq,
-                    uint8_t *planes, hipStream_t s) {
+                    const uint8_t *nmask, uint8_t *planes, hipStream_t s) {
   if (n <= 0 || !max_blocks) return hipSuccess;
   // 4 units of 16 blocks per workgroup; a frame has ceil(nmcu / 16) * bpm <= (nblocks + 150) / 16 units
   hipLaunchKernelGGL(k_idct, dim3((max_blocks + 150 + 63) / 64, (unsigned)n), dim3(256), 0, s, fr,
-                     coef, dcseq, planes);
+                     coef, dcseq, nmask, planes);
   return hipGetLastError();
 }
 
@@ -2922,6 +3159,19 @@ hipError_t dec_color(const DecFrame *__restrict__ fr, int n, int max_w, int max_
     else VF_COLOR(false, -1);
   }
 #undef VF_COLOR
+  return hipGetLastError();
+}
+
+hipError_t dec_idct_color422(const DecFrame *__restrict__ fr, int n, int max_w, int max_h, const int16_t *coef,
+                             const int32_t *dcseq, const uint8_t *nmask, uint8_t *eplanes, const EncFrame *efr,
+                             int invert, int one_row, hipStream_t s) {
+  if (n <= 0 || max_w <= 0 || max_h <= 0) return hipSuccess;
+  const unsigned mcux = (unsigned)((max_w + 15) / 16), mcuy = (unsigned)((max_h + 7) / 8);
+  const dim3 grid((mcux + kStripMcus - 1) / kStripMcus, mcuy, (unsigned)n);
+  if (one_row)
+    hipLaunchKernelGGL(k_idct_color422<true>, grid, dim3(256), 0, s, fr, coef, dcseq, nmask, eplanes, efr, invert);
+  else
+    hipLaunchKernelGGL(k_idct_color422<false>, grid, dim3(256), 0, s, fr, coef, dcseq, nmask, eplanes, efr, invert);
   return hipGetLastError();
 }
 

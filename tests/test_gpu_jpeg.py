@@ -215,16 +215,19 @@ def test_concurrent_calls_lease_separate_codecs(tj):
     assert not errors, errors[:3]
 
 
+@pytest.mark.parametrize("chunks", ["1", "0"])
 @pytest.mark.parametrize("mode", ["spec", "pass", "pass-1lane"])
 @pytest.mark.parametrize("subsamp,quality", [(J.TJSAMP_420, 95), (J.TJSAMP_444, 90), (J.TJSAMP_422, 85)])
-def test_sync_modes_on_hard_content(tj, monkeypatch, mode, subsamp, quality):
+def test_sync_modes_on_hard_content(tj, monkeypatch, mode, subsamp, quality, chunks):
     """Both Huffman synchronisation paths (speculative trajectories + links, and the
     pass-based chain, whose write pass runs 4 lanes per subsequence from the converged
     checkpoints, or one with VF_JPEG_WRITE4=0) on content with long blocks (noise: links rejoin
-    late, walkers and the resolver decode explicit states) and a mixed batch, bit-exact with
-    the oracle."""
+    late, walkers and the resolver decode explicit states; blocks longer than a subsequence, so
+    the chunked write pass's owner decodes across several spans) and a mixed batch, bit-exact
+    with the oracle -- with the chunked coefficient rows + masks and with the cleared buffer."""
     monkeypatch.setenv("VF_JPEG_SYNC", mode.split("-")[0])
     monkeypatch.setenv("VF_JPEG_WRITE4", "0" if mode == "pass-1lane" else "1")
+    monkeypatch.setenv("VF_JPEG_CHUNKS", chunks)
     rng = np.random.default_rng(quality)
     imgs = [rng.integers(0, 256, (256, 320, 3), dtype=np.uint8),
             _img("scene", 3, 480, 640),
@@ -247,14 +250,18 @@ def _span_sync_batch(quality=95, subsamp=J.TJSAMP_422):
     return [J.encode(im, quality, J.TJPF_BGR, subsamp) for im in imgs]
 
 
-@pytest.mark.parametrize("g", ["0", "1", "2", "4", "8"])
-def test_span_sync_widths(tj, monkeypatch, g):
+@pytest.mark.parametrize("g,warm", [("0", "0"), ("1", "0"), ("2", "0"), ("4", "0"), ("8", "0"), ("4", "256"),
+                                    ("4", "2048"), ("8", "4096"), ("1", "1000")])
+def test_span_sync_widths(tj, monkeypatch, g, warm):
     """The pass-based sync with G subsequences per thread (k_syncg: records updated in place,
     passes queued and returning early once no workgroup's last exit changes; G = 0: the
-    host-looped one-subsequence k_sync), on frames spanning several workgroups, through the
+    host-looped one-subsequence k_sync), with and without pass 0's warm-up decode before each
+    span (VF_JPEG_SYNC_WARM bits, rounded down to 32; reaching back past the segment's start and
+    into the previous workgroup's words), on frames spanning several workgroups, through the
     fused invert and the plain decode, bit-exact with the oracle."""
     monkeypatch.setenv("VF_JPEG_SYNC", "pass")
     monkeypatch.setenv("VF_JPEG_SYNC_G", g)
+    monkeypatch.setenv("VF_JPEG_SYNC_WARM", warm)
     jpgs = _span_sync_batch()
     got = tj.invert_batch(jpgs)
     for o, j in zip(got, jpgs):
@@ -437,3 +444,25 @@ def test_bench_operating_points_on_the_auto_path(tj, monkeypatch, kind):
     t2 = tj.invert_batch_submit(jpgs[::-1])
     assert [bytes(g) for g in tj.invert_batch_result(t1)] == want
     assert [bytes(g) for g in tj.invert_batch_result(t2)] == want[::-1]
+
+
+@pytest.mark.parametrize("flags", [0, TJFLAG_FASTUPSAMPLE])
+def test_fused_idct_colour_strip_edges(tj, monkeypatch, flags):
+    """k_idct_color422 (the invert path's one-pass IDCT + colour for standard 4:2:2 input):
+    strips of 15 MCUs (240 pixels) with one chroma block of each neighbour, so widths around
+    strip multiples (the first and last strips' missing neighbours, a last strip of one MCU,
+    an odd width whose last chroma column is the clamp), heights that end inside an MCU row,
+    each encoder sampling (one-row colour for 4:2:2 / 4:4:4 / gray, two-row for 4:2:0 / 4:4:0),
+    fancy and replicating upsampling -- against the oracle, and equal to the two-pass form."""
+    monkeypatch.delenv("VF_JPEG_FUSE", raising=False)
+    sizes = [(8, 16), (9, 232), (17, 240), (8, 241), (16, 255), (23, 256), (8, 480), (31, 497), (12, 3840 // 8)]
+    jpgs = [J.encode(_img("scene" if i % 3 else "noise", 500 + i, h, w), 85, J.TJPF_BGR, J.TJSAMP_422)
+            for i, (h, w) in enumerate(sizes)]
+    for out_ss in (J.TJSAMP_422, J.TJSAMP_420, J.TJSAMP_444, J.TJSAMP_GRAY, J.TJSAMP_440):
+        want = [J.invert_jpeg(j, 85, out_ss, flags) for j in jpgs]
+        monkeypatch.setenv("VF_JPEG_FUSE_IDCT", "1")
+        got = tj.invert_batch(jpgs, 85, out_ss, flags)
+        monkeypatch.setenv("VF_JPEG_FUSE_IDCT", "0")
+        two = tj.invert_batch(jpgs, 85, out_ss, flags)
+        for i, (g, t2, w) in enumerate(zip(got, two, want)):
+            assert g == w and t2 == w, (sizes[i], out_ss, flags)
