@@ -5,7 +5,8 @@
       -d DIR -o pmc -- python3 tools/jpeg_bench.py --sizes 1080p --batch 32 --iters 3
   python tools/pmc_issue.py DIR/pmc_counter_collection.csv [--durations KERNEL_STATS.csv]
 
-Per kernel, the LAST dispatch of the run (a bench iteration, not the input encode) gives:
+Per kernel, its dispatches in the LAST batch of the run (from the last k_unstuff_count on; a
+kernel dispatched several times per batch -- the span sync's passes, the scans -- is summed) give:
   waves, VALU / LDS / SALU instructions per wave,
   clock_GHz       GRBM_GUI_ACTIVE / the dispatch's duration (the counter ticks the GPU clock
                   while the GUI is busy; rocprofv3 sums it over the XCDs, so it is divided by 8),
@@ -41,14 +42,34 @@ def per_kernel(counters_csv, durations_csv="", min_waves=1000):
         d["_name"] = short(r["Kernel_Name"])
         d["_dur_ns"] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
         d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    # the last batch: every dispatch from the last k_unstuff_count on (a batch's first kernel),
+    # summed per kernel -- the span sync runs k_syncg once per pass, and the last pass of a
+    # batch returns at once (converged), so "the last dispatch" would say nothing
+    starts = [i for i in disp if disp[i]["_name"] == "k_unstuff_count"]
+    first = max(starts) if starts else None
     last = {}
     for i in sorted(disp):
-        last[disp[i]["_name"]] = disp[i]
+        d = disp[i]
+        if first is None or i < first:
+            last[d["_name"]] = d
+            continue
+        if i == first:
+            last = {}
+        a = last.setdefault(d["_name"], {"_name": d["_name"], "_dur_ns": 0, "_long_ns": 0, "_long": d})
+        for k, v in d.items():
+            if not k.startswith("_"):
+                a[k] = a.get(k, 0.0) + v
+        a["_dur_ns"] += d["_dur_ns"]
+        if d["_dur_ns"] > a["_long_ns"]:
+            a["_long_ns"], a["_long"] = d["_dur_ns"], d
     stats = {}
     if durations_csv:
         for r in csv.DictReader(open(durations_csv)):
             stats[short(r["Name"])] = float(r["AverageNs"])
-    clk_of = {n: (d.get("GRBM_GUI_ACTIVE", 0.0) / XCDS / d["_dur_ns"] if d["_dur_ns"] else 0.0) for n, d in last.items()}
+    def clock(d):  # from the kernel's longest dispatch in the batch (or its only one)
+        d = d.get("_long", d)
+        return d.get("GRBM_GUI_ACTIVE", 0.0) / XCDS / d["_dur_ns"] if d["_dur_ns"] else 0.0
+    clk_of = {n: clock(d) for n, d in last.items()}
     longs = sorted(c for n, c in clk_of.items() if last[n]["_dur_ns"] > 50_000 and c > 0)
     clk_med = longs[len(longs) // 2] if longs else 2.4
     out = {}
@@ -56,7 +77,9 @@ def per_kernel(counters_csv, durations_csv="", min_waves=1000):
         waves = d.get("SQ_WAVES", 0.0)
         if waves < min_waves:
             continue
-        dur = stats.get(name, d["_dur_ns"])
+        # --durations gives one dispatch's average; a kernel run several times per batch keeps
+        # its summed in-batch time
+        dur = stats.get(name, d["_dur_ns"]) if "_long" not in d else d["_dur_ns"]
         clk = clk_of[name] if d["_dur_ns"] > 50_000 else clk_med
         cyc = dur * clk
         r = {"waves": int(waves), "duration_us": round(dur / 1e3, 2), "clock_GHz": round(clk, 3),
