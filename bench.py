@@ -228,7 +228,7 @@ def jpeg_issue_fractions(roofline, per_kernel):
     roofline["issue_fraction_note"] = (
         f"valu_issue_frac = VALU instructions x 2 / (1024 SIMDs x stage cycles), lds_issue_frac = LDS "
         f"instructions / (256 CUs x stage cycles); instruction counts per kernel from a rocprofv3 PMC pass "
-        f"(SQ_INSTS_VALU / SQ_INSTS_LDS, last dispatch) over the same 1080p batch, shader clock "
+        f"(SQ_INSTS_VALU / SQ_INSTS_LDS, summed over the dispatches of the last batch) over the same 1080p batch, shader clock "
         f"{clk:.2f} GHz (GRBM_GUI_ACTIVE / duration, median of the kernels above 50 us)")
 
 
