@@ -315,6 +315,9 @@ int Codec::prepare_decode(const uint8_t *const *jpegs, const size_t *sizes, int 
     }
   dsg_.clear();
   dcm_ = -2;  // the batch's common k_color layout, or -1 (mixed)
+  // VF_JPEG_IDCT24=0: every frame on the 32-bit column pass (an A/B and test selector)
+  const char *i24 = std::getenv("VF_JPEG_IDCT24");
+  const bool idct24 = !(i24 && std::strcmp(i24, "0") == 0);
   d422_ = true;  // every frame standard 4:2:2 (k_idct_color422)
   for (int f = 0; f < n; ++f) {
     const Parsed &P = parsed[(size_t)f];
@@ -326,6 +329,15 @@ int Codec::prepare_decode(const uint8_t *const *jpegs, const size_t *sizes, int 
       if (g.ncomp == 3 && g.he[0] == 1 && g.ve[0] == 1 && g.he[1] == g.he[2] && g.ve[1] == g.ve[2])
         cm = g.he[1] == 1 && g.ve[1] == 1 ? 1u : g.he[1] == 2 && g.ve[1] == 1 ? 2u : g.he[1] == 2 && g.ve[1] == 2 ? 3u : 0u;
       F.flags |= cm << 1;
+      // the bound k_idct's column pass needs for 24-bit multiplies (vf_jpeg_types.h); the AC
+      // tables' unused symbol slots are zero
+      int ac_size = 0;
+      uint32_t q_ac = 0;
+      for (int c = 0; c < g.ncomp; ++c) {
+        for (int i = 0; i < 256; ++i) ac_size = std::max(ac_size, (int)(F.ac[c].vals[i] & 15));
+        for (int i = 1; i < 64; ++i) q_ac = std::max(q_ac, (uint32_t)F.q[c][i]);
+      }
+      if (idct24 && idct_col24_ok(ac_size, q_ac)) F.flags |= kDecIdct24;
       dcm_ = dcm_ == -2 || dcm_ == (int)cm ? (int)cm : -1;
       d422_ = d422_ && g.ncomp == 3 && g.hs[0] == 2 && g.vs[0] == 1 && g.hs[1] == 1 && g.vs[1] == 1 &&
               g.hs[2] == 1 && g.vs[2] == 1 && g.bpm == 4;

@@ -711,10 +711,15 @@ __global__ __launch_bounds__(256) void k_sync(const DecSeg *__restrict__ sg, con
 // previous pass's flag and returns at once when no workgroup's last exit changed (then every
 // entry is consistent: within a workgroup by its rounds, across by the unchanged exits).
 
-// Re-decode (or first decode, check = false) of a thread's span from entry state X; returns the
+// Re-decode (or first decode, CHECK = false) of a thread's span from entry state X; returns the
 // span's last exit.  `last` is the previous decode's last exit (returned unchanged on a join).
+// A re-decode reads each mark's recorded state one mark ahead; that load is issued before the
+// current mark's record stores, because vmcnt counts stores too: loaded after them, the wait for
+// it at the next mark also waited for the stores' completion, every 64 bits.  The first decode
+// (no records yet) has no loads in its loop at all.
+template <bool CHECK>
 __device__ __forceinline__ uint64_t sync_span(const uint32_t *words, uint32_t woff, uint64_t X, uint32_t i0, uint32_t ng,
-                                              uint32_t nsub, uint32_t nbits, uint64_t gi0, bool check, uint64_t last,
+                                              uint32_t nsub, uint32_t nbits, uint64_t gi0, uint64_t last,
                                               uint64_t *exits, uint32_t *cnts, uint64_t *ck, uint32_t *ckrem,
                                               const HuffGeom &hg, const SyncTab32 *tabs) {
   SyncLane<SyncTab32> d;
@@ -725,15 +730,28 @@ __device__ __forceinline__ uint64_t sync_span(const uint32_t *words, uint32_t wo
   // m == kCk: its end.  An entry lies less than one symbol (<= 32 bits) past bj, before mark 0.
   uint32_t m = bj + kCkStep < ej ? 0u : (uint32_t)kCk;
   uint32_t mk = m < kCk ? bj + kCkStep : ej;
-  uint64_t old = check ? (m < kCk ? ck[gi0 * kCk] : exits[gi0]) : 0;
+  uint64_t old = CHECK ? (m < kCk ? ck[gi0 * kCk] : exits[gi0]) : 0;
   uint32_t n0 = 0, n1 = 0, n2 = 0;  // blocks at the checkpoints written in this decode
   static_assert(kCk == 3, "n0..n2");
   for (;;) {
     while (d.pos < mk) d.step(tabs, mk);
     const uint64_t st = pack_state(d.pos, d.z, d.c);
     const uint64_t gj = gi0 + j;
-    if (m < kCk) {
-      if (check && old == st) {  // rejoined: the rest of the span is the recorded trajectory
+    const bool joined = CHECK && old == st;
+    // the mark after this one (j2, m2 at mk2)
+    const bool send = m >= kCk;  // this mark ends subsequence j
+    const uint32_t j2 = send ? j + 1 : j, bj2 = send ? bj + kSubBits : bj;
+    const uint32_t ej2 = send ? (i0 + j2 + 1 >= nsub ? nbits : bj2 + kSubBits) : ej;
+    uint32_t m2 = send ? (bj2 + kCkStep >= ej2 ? (uint32_t)kCk : 0u) : m + 1;
+    uint32_t mk2 = m2 < kCk ? bj2 + (m2 + 1) * kCkStep : ej2;
+    if (m2 < kCk && mk2 >= ej2) {
+      m2 = kCk;
+      mk2 = ej2;
+    }
+    if (CHECK && !joined && !(send && j2 == ng))  // prefetch, ahead of this mark's stores
+      old = m2 < kCk ? ck[(gi0 + j2) * kCk + m2] : exits[gi0 + j2];
+    if (!send) {
+      if (joined) {  // rejoined: the rest of the span is the recorded trajectory
         const uint32_t cj = d.n + ckrem[gj * kCk + m];
         cnts[gj] = cj;
         if (m > 0) ckrem[gj * kCk] = cj - n0;
@@ -744,9 +762,7 @@ __device__ __forceinline__ uint64_t sync_span(const uint32_t *words, uint32_t wo
       n2 = m == 2 ? d.n : n2;
       n1 = m == 1 ? d.n : n1;
       n0 = m == 0 ? d.n : n0;
-      ++m;
     } else {
-      const bool joined = check && old == st;
       const uint32_t nw = bj + kCkStep < ej ? (bj + 2 * kCkStep < ej ? (bj + 3 * kCkStep < ej ? 3u : 2u) : 1u) : 0u;
       cnts[gj] = d.n;
       if (nw > 0) ckrem[gj * kCk] = d.n - n0;
@@ -755,20 +771,14 @@ __device__ __forceinline__ uint64_t sync_span(const uint32_t *words, uint32_t wo
       if (joined) return last;  // the exit, and every later subsequence, unchanged
       exits[gj] = st;
       for (uint32_t q = nw; q < (uint32_t)kCk; ++q) ck[gj * kCk + q] = kNoCk;  // marks past the segment's end
-      if (j + 1 == ng) return st;
-      ++j;
+      if (j2 == ng) return st;
       d.n = 0;
-      bj += kSubBits;
-      ej = i0 + j + 1 >= nsub ? nbits : bj + kSubBits;
-      m = 0;
-      if (bj + kCkStep >= ej) m = kCk;
     }
-    mk = m < kCk ? bj + (m + 1) * kCkStep : ej;
-    if (m < kCk && mk >= ej) {
-      m = kCk;
-      mk = ej;
-    }
-    if (check) old = m < kCk ? ck[(gi0 + j) * kCk + m] : exits[gi0 + j];  // one mark ahead of its use
+    j = j2;
+    bj = bj2;
+    ej = ej2;
+    m = m2;
+    mk = mk2;
   }
 }
 
@@ -843,7 +853,8 @@ __global__ __launch_bounds__(256) void k_syncg(const DecSeg *__restrict__ sg, co
   bool check = pass > 0;  // records are valid from the first decode on
   for (;;) {
     if (need) {
-      last = sync_span(words, woff, entry, i0, ng, nsub, nbits, gi0, check, last, exits, cnts, ck, ckrem, hg, tabs);
+      last = check ? sync_span<true>(words, woff, entry, i0, ng, nsub, nbits, gi0, last, exits, cnts, ck, ckrem, hg, tabs)
+                   : sync_span<false>(words, woff, entry, i0, ng, nsub, nbits, gi0, last, exits, cnts, ck, ckrem, hg, tabs);
       used[gi0] = entry;
     }
     s_exit[t] = last;
@@ -1498,18 +1509,32 @@ __global__ __launch_bounds__(256) void k_write4(const DecSeg *__restrict__ sg, c
 #define FIX_3_072711026 25172
 #define DESCALE(x, n) (((x) + ((int32_t)1 << ((n)-1))) >> (n))
 
-// jidctint.c jpeg_idct_islow, one 8-point line; `shift` 11 (pass 1) or 18 (pass 2).  32-bit
-// products, as the C code: a decoded stream's dequantised coefficients are only bounded by
-// int16 x the quantiser, so a 24-bit multiply is not exact on every legal input; guarding it
-// per wave (a range check and a ballot per line, round 3) made k_idct slower, 129.8 -> 142.5 us
-// at 1080p x 32.
+// jidctint.c jpeg_idct_islow, one 8-point line; `shift` 11 (pass 1) or 18 (pass 2), 32-bit
+// products as the C code.  M24: the products by v_mul_i32_i24 / v_mad_i32_i24 (full VALU rate;
+// v_mul_lo_u32 issues at a quarter), exact when every multiplicand -- a sum of at most four
+// inputs -- lies in [-2^23, 2^23).  The row pass's always do: its inputs are the column pass's
+// int32 results shifted right by 11, so |x| <= 2^20 and a sum of four <= 2^22, whatever the
+// stream holds.  The column pass's multiplicands are sums of dequantised AC coefficients, only
+// bounded by the frame's tables: the host sets kDecIdct24 when they fit (idct_col24_ok) and the
+// kernels take the 32-bit column pass for the frames that do not.  (Guarding it per wave with a
+// range check and a ballot per line, round 3, made k_idct slower, 129.8 -> 142.5 us.)
+template <bool B>
+struct BoolTag {
+  static constexpr bool value = B;
+};
+template <bool M24>
+__device__ __forceinline__ int32_t imul(int32_t a, int32_t c) {
+  if constexpr (M24) return __mul24(a, c);
+  else return a * c;
+}
+template <bool M24>
 __device__ __forceinline__ void idct_line(const int32_t in[8], int32_t out[8], int shift) {
   int32_t tmp0, tmp1, tmp2, tmp3, tmp10, tmp11, tmp12, tmp13, z1, z2, z3, z4, z5;
   z2 = in[2];
   z3 = in[6];
-  z1 = (z2 + z3) * FIX_0_541196100;
-  tmp2 = z1 + z3 * -FIX_1_847759065;
-  tmp3 = z1 + z2 * FIX_0_765366865;
+  z1 = imul<M24>(z2 + z3, FIX_0_541196100);
+  tmp2 = z1 + imul<M24>(z3, -FIX_1_847759065);
+  tmp3 = z1 + imul<M24>(z2, FIX_0_765366865);
   tmp0 = (in[0] + in[4]) * (1 << 13);
   tmp1 = (in[0] - in[4]) * (1 << 13);
   tmp10 = tmp0 + tmp3;
@@ -1524,15 +1549,15 @@ __device__ __forceinline__ void idct_line(const int32_t in[8], int32_t out[8], i
   z2 = tmp1 + tmp2;
   z3 = tmp0 + tmp2;
   z4 = tmp1 + tmp3;
-  z5 = (z3 + z4) * FIX_1_175875602;
-  tmp0 *= FIX_0_298631336;
-  tmp1 *= FIX_2_053119869;
-  tmp2 *= FIX_3_072711026;
-  tmp3 *= FIX_1_501321110;
-  z1 *= -FIX_0_899976223;
-  z2 *= -FIX_2_562915447;
-  z3 *= -FIX_1_961570560;
-  z4 *= -FIX_0_390180644;
+  z5 = imul<M24>(z3 + z4, FIX_1_175875602);
+  tmp0 = imul<M24>(tmp0, FIX_0_298631336);
+  tmp1 = imul<M24>(tmp1, FIX_2_053119869);
+  tmp2 = imul<M24>(tmp2, FIX_3_072711026);
+  tmp3 = imul<M24>(tmp3, FIX_1_501321110);
+  z1 = imul<M24>(z1, -FIX_0_899976223);
+  z2 = imul<M24>(z2, -FIX_2_562915447);
+  z3 = imul<M24>(z3, -FIX_1_961570560);
+  z4 = imul<M24>(z4, -FIX_0_390180644);
   z3 += z5;
   z4 += z5;
   tmp0 += z1 + z3;
@@ -1655,15 +1680,19 @@ __global__ __launch_bounds__(256) void k_idct(const DecFrame *__restrict__ fr, c
   }
   __syncthreads();
   int32_t col[kIdctNb][8];
+  const auto pass1 = [&](auto m24) {  // pass 1: column r, dequantised
 #pragma unroll
-  for (int h = 0; h < kIdctNb; ++h) {  // pass 1: column r, dequantised
-    if (!valid[h]) continue;
-    int32_t in[8];
+    for (int h = 0; h < kIdctNb; ++h) {
+      if (!valid[h]) continue;
+      int32_t in[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
-      in[i] = __mul24(blkv[h * 32 + slot][i * 8 + ((colg >> (4 * i)) & 7)], s_q[k][i * 8 + r]);  // int16 x u16: exact
-    idct_line(in, col[h], 11);
-  }
+      for (int i = 0; i < 8; ++i)
+        in[i] = __mul24(blkv[h * 32 + slot][i * 8 + ((colg >> (4 * i)) & 7)], s_q[k][i * 8 + r]);  // int16 x u16: exact
+      idct_line<decltype(m24)::value>(in, col[h], 11);
+    }
+  };
+  if (F.flags & kDecIdct24) pass1(BoolTag<true>{});  // frame-uniform (scalar) branch
+  else pass1(BoolTag<false>{});
   __syncthreads();
 #pragma unroll
   for (int h = 0; h < kIdctNb; ++h) {
@@ -1678,7 +1707,7 @@ __global__ __launch_bounds__(256) void k_idct(const DecFrame *__restrict__ fr, c
     int32_t in[8], out[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) in[i] = blkv[h * 32 + slot][r * 9 + i];
-    idct_line(in, out, 18);
+    idct_line<true>(in, out, 18);
     uint32_t lo = 0, hi = 0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -2237,15 +2266,19 @@ __global__ __launch_bounds__(256) void k_idct_color422(const DecFrame *__restric
   }
   __syncthreads();
   int32_t col[kIdctNb][8];
+  const auto pass1 = [&](auto m24) {  // pass 1: column r, dequantised
 #pragma unroll
-  for (int h = 0; h < kIdctNb; ++h) {  // pass 1: column r, dequantised
-    if (!valid[h]) continue;
-    int32_t in[8];
+    for (int h = 0; h < kIdctNb; ++h) {
+      if (!valid[h]) continue;
+      int32_t in[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
-      in[i] = __mul24(blkv[h * 32 + slot][i * 8 + ((colg >> (4 * i)) & 7)], s_q[kk[h]][i * 8 + r]);
-    idct_line(in, col[h], 11);
-  }
+      for (int i = 0; i < 8; ++i)
+        in[i] = __mul24(blkv[h * 32 + slot][i * 8 + ((colg >> (4 * i)) & 7)], s_q[kk[h]][i * 8 + r]);
+      idct_line<decltype(m24)::value>(in, col[h], 11);
+    }
+  };
+  if (F.flags & kDecIdct24) pass1(BoolTag<true>{});
+  else pass1(BoolTag<false>{});
   __syncthreads();
 #pragma unroll
   for (int h = 0; h < kIdctNb; ++h) {
@@ -2260,7 +2293,7 @@ __global__ __launch_bounds__(256) void k_idct_color422(const DecFrame *__restric
     int32_t in[8], out[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) in[i] = blkv[h * 32 + slot][r * 9 + i];
-    idct_line(in, out, 18);
+    idct_line<true>(in, out, 18);
     uint32_t lo = 0, hi = 0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {

@@ -27,6 +27,19 @@ constexpr int kLook = VF_KLOOK;        // Huffman lookahead bits
 constexpr int kAcScratchWords = 52;  // per-block AC bit scratch (63 codes of <= 26 bits + EOB)
 constexpr int kCkStep = kSubBits / 8 < 64 ? 64 : kSubBits / 8;  // Huffman-sync checkpoint spacing (bits)
 constexpr int kCk = kSubBits / kCkStep - 1;                       // checkpoints per subsequence
+// DecFrame.flags bit: every multiplicand of the IDCT's column pass fits a signed 24-bit multiply
+// (idct_col24_ok); the row pass's always do (idct_line)
+constexpr uint32_t kDecIdct24 = 8u;
+
+// The column pass of jpeg_idct_islow multiplies sums of at most four dequantised AC coefficients
+// of one column by constants (the DC only enters through a shift).  An AC coefficient is an
+// extend() of at most `ac_size` bits (the largest size nibble among the AC tables' symbols), so
+// its magnitude is under 2^ac_size; times the largest AC quantiser entry and four terms, the
+// multiplicands stay within v_mul_i32_i24's exact range when this holds.  Annex K tables (sizes
+// <= 10) with 8-bit quantisers are far inside it.
+inline bool idct_col24_ok(int ac_size, uint32_t q_ac_max) {
+  return ac_size <= 16 && 4ull * (uint64_t)q_ac_max * ((1ull << ac_size) - 1) < (1ull << 23);
+}
 
 // MCU geometry of one frame (libjpeg jdinput.c / jcmaster.c per-scan setup, restated)
 struct Geom {
@@ -109,7 +122,8 @@ struct DecFrame {
   // read, unless the first ends the block or reaches a mark
   uint16_t spair[3][1 << kLook];
   uint32_t flags;          // bit 0: fancy upsampling allowed; bits 1-2: k_color layout (0 other,
-                           // 1 4:4:4, 2 chroma 2x1, 3 chroma 2x2; three components, full-size luma)
+                           // 1 4:4:4, 2 chroma 2x1, 3 chroma 2x2; three components, full-size luma);
+                           // kDecIdct24: the IDCT's column pass may use 24-bit multiplies
   uint64_t blk0;           // first block in the batch coefficient buffer
   uint64_t dcbase[3];      // per-component DC sequences in the DC buffer
   uint64_t plane_off[3];   // component planes in the plane buffer

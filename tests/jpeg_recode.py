@@ -198,3 +198,28 @@ def long_prefixes(bits: List[int], look: int = 9) -> int:
     second-level slots a table asks for; canonical codes put them at the top of code space)."""
     space = sum(n << (16 - ln) for ln, n in enumerate(bits, 1) if ln > look)
     return -(-space // (1 << (16 - look)))
+
+
+def requant16(jpeg: bytes, scale: int) -> bytes:
+    """The same entropy-coded data under 16-bit quantisation tables (DQT Pq = 1): every entry
+    times `scale`, capped at 65535.  The coefficients are unchanged, their dequantised values
+    (hence the picture) are not: with a large scale they leave the range in which the decoder's
+    IDCT column pass may use 24-bit multiplies (vf_jpeg_types.h idct_col24_ok), which puts that
+    frame on the 32-bit path."""
+    segs, ecs, tail = _segments(jpeg)
+    hdr = bytearray(b"\xff\xd8")
+    for m, pl in segs:
+        if m == 0xDB:
+            i, new = 0, bytearray()
+            while i < len(pl):
+                pq, tq = pl[i] >> 4, pl[i] & 15
+                n = 128 if pq else 64
+                vals = ([(pl[i + 1 + 2 * k] << 8) | pl[i + 2 + 2 * k] for k in range(64)] if pq
+                        else list(pl[i + 1:i + 65]))
+                new.append(0x10 | tq)
+                for v in vals:
+                    new += min(65535, v * scale).to_bytes(2, "big")
+                i += 1 + n
+            pl = bytes(new)
+        hdr += bytes([0xFF, m]) + (len(pl) + 2).to_bytes(2, "big") + pl
+    return bytes(hdr) + ecs + tail

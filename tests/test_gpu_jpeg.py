@@ -466,3 +466,28 @@ def test_fused_idct_colour_strip_edges(tj, monkeypatch, flags):
         two = tj.invert_batch(jpgs, 85, out_ss, flags)
         for i, (g, t2, w) in enumerate(zip(got, two, want)):
             assert g == w and t2 == w, (sizes[i], out_ss, flags)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fuse", ["1", "0"])
+def test_idct_column_pass_multiplies(tj, monkeypatch, fuse):
+    """The IDCT's column pass takes 24-bit multiplies when the frame's tables bound its
+    multiplicands (vf_jpeg_types.h idct_col24_ok: Annex K sizes with 8-bit quantisers) and
+    32-bit ones otherwise; the row pass always takes 24-bit ones (its inputs are >> 11 of int32).
+    16-bit quantisation tables (tests/jpeg_recode.py requant16) scaled by 1, 20 and 255 push the
+    dequantised coefficients from inside that bound to far past it -- and past int32 in the
+    products, which both sides wrap alike -- in one batch, each frame on its own path, through
+    k_idct and the fused k_idct_color422.  Bit-exact with the oracle (decode and invert)."""
+    import jpeg_recode as R
+    monkeypatch.setenv("VF_JPEG_FUSE_IDCT", fuse)
+    jpgs = []
+    for i, ss in enumerate([J.TJSAMP_422, J.TJSAMP_420, J.TJSAMP_444]):
+        base = J.encode(_img("scene" if i else "noise", 900 + i, 48, 72), 85, J.TJPF_BGR, ss)
+        jpgs += [base] + [R.requant16(base, s) for s in (1, 20, 255)]
+    for j in jpgs:
+        assert np.array_equal(tj.decode(j), J.decode(j))
+    want = [J.invert_jpeg(j) for j in jpgs]
+    assert [bytes(g) for g in tj.invert_batch(jpgs)] == want
+    assert [bytes(g) for g in tj.invert_batch(jpgs[:4])] == want[:4]  # all 4:2:2: the fused kernel
+    monkeypatch.setenv("VF_JPEG_IDCT24", "0")  # every frame on the 32-bit column pass
+    assert [bytes(g) for g in tj.invert_batch(jpgs)] == want
