@@ -9,7 +9,7 @@ LIB       := $(PKG)/vfilter/libvfilter_hip.so
 HIPFLAGS  := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -fvisibility=hidden -Wall -Iinclude
 LDFLAGS   := -shared -Wl,-rpath,/opt/rocm/lib -Wl,--no-undefined
 
-.PHONY: all lib oracle tools clean
+.PHONY: all lib oracle tools clean exp
 all: lib oracle
 
 lib: $(LIB)
@@ -34,3 +34,9 @@ tools/tune_invert: tools/tune_invert.hip $(CSRC)/vf_kernels.hip $(CSRC)/vf_inter
 clean:
 	rm -f $(LIB) tools/tune_invert tools/pcie_probe
 	$(MAKE) -C oracle clean
+
+# Experiment libraries (timing A/Bs against the product library; never loaded by the product):
+#   make exp EXP=NAME DEFS="-DVF_EXP_...=1"  ->  tools/exp/libvf_NAME.so
+exp:
+	@mkdir -p tools/exp
+	$(HIPCC) $(HIPFLAGS) $(DEFS) $(LDFLAGS) -pthread $(SRCS) -o tools/exp/libvf_$(EXP).so

@@ -403,6 +403,10 @@ int Codec::prepare_decode(const uint8_t *const *jpegs, const size_t *sizes, int 
     *err = "more than 65535 restart intervals in one batch (split the batch)";
     return kInvalid;
   }
+  if (dcoff >= (1ull << 31)) {  // the write pass keeps DC sequence positions in 32 bits
+    *err = "more than 2^31 blocks in one batch (split the batch)";
+    return kInvalid;
+  }
   dblocks_ = blk;
   dpix_bytes_ = pix;
   {

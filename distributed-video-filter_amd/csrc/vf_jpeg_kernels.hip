@@ -265,10 +265,6 @@ __device__ __forceinline__ uint32_t long_code_len(uint32_t c16, const uint32_t *
          (c16 >= b.z);
 }
 
-__device__ __forceinline__ int extend(uint32_t v, uint32_t s) {  // jdhuff.h HUFF_EXTEND
-  return v < (1u << (s - 1)) ? (int)v - (int)((1u << s) - 1) : (int)v;
-}
-
 __device__ __forceinline__ uint64_t pack_state(uint32_t pos, uint32_t z, uint32_t c) {
   return ((uint64_t)pos << 16) | (z << 8) | c;
 }
@@ -313,6 +309,14 @@ struct HuffGeom {
 // `end` that thread decodes on to the block's end, and a thread whose entry state lies inside
 // a block skips to that block's end without storing (the block is its predecessor's).  Replaces
 // a 134 MB clear per 1080p batch and the 2-byte scatters.
+//
+// A wave runs this loop in order at ~3 waves per SIMD (k_write's grid is one workgroup per 256
+// subsequences), so every instruction of a step is on the lane's chain.  The step is kept to
+// selects: the extra bits are one bit-field extract from the buffer's upper word (a code and its
+// extra bits are at most 32 bits, and a refilled buffer holds at least 33), the DC goes to a
+// per-component running position (each component's DC sequence is in block order) instead of
+// an address rebuilt from (MCU, c) -- whose three-way selects over 64-bit bases compiled to
+// nested branches -- and the chunk and block-end bookkeeping are selects around the stores.
 template <bool CHUNKS>
 __device__ __forceinline__ void write_span(const uint32_t *w, uint32_t woff, uint64_t X, uint32_t end,
                                            const HuffGeom &g, const HuffDec *tabs, uint32_t blk, int16_t *coef,
@@ -325,10 +329,21 @@ __device__ __forceinline__ void write_span(const uint32_t *w, uint32_t woff, uin
   uint32_t nxt = w[wi];
   uint32_t z = (X >> 8) & 0xFF, c = X & 0xFF;
   uint32_t k = g.comp(c);
-  uint32_t mcu = blk / g.bpm;
-  uint64_t dcb[3];
-#pragma unroll
-  for (int q = 0; q < 3; ++q) dcb[q] = dcbase[q];
+  // DC positions: per component, its base + the blocks of it before this one (the MCUs before,
+  // and those of this MCU before c); the host keeps the DC buffer under 2^31 entries
+  uint32_t dcp0, dcp1, dcp2;
+  {
+    const uint32_t mcu = blk / g.bpm;
+    const auto at = [&](int q) {
+      const int before = min(max((int)c - (int)g.cfirst[q], 0), (int)g.bpc[q]);
+      return (uint32_t)dcbase[q] + mcu * g.bpc[q] + (uint32_t)before;
+    };
+    dcp0 = at(0);
+    dcp1 = at(1);
+    dcp2 = at(2);
+  }
+  constexpr uint32_t kTab = (uint32_t)sizeof(HuffDec);
+  uint32_t toff = __umul24(k, kTab);  // c's component's DC table (its AC table: 3 tables on)
   bool own = z == 0;            // CHUNKS: the block in progress is this thread's
   uint32_t cq = 0, m8 = 0;      // CHUNKS: the chunk being collected, chunks stored so far
   uint32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0;
@@ -339,11 +354,13 @@ __device__ __forceinline__ void write_span(const uint32_t *w, uint32_t woff, uin
     wi += f ? 1u : 0u;
     nxt = w[wi];
     const bool dc = z == 0;
-    const HuffDec &T = tabs[dc ? k : 3 + k];
-    const uint32_t e = T.fast[(uint32_t)(buf >> (64 - kLook))];
+    const HuffDec &T = *reinterpret_cast<const HuffDec *>(reinterpret_cast<const char *>(tabs) + toff +
+                                                          (dc ? 0u : 3u * kTab));
+    const uint32_t hi = (uint32_t)(buf >> 32);
+    const uint32_t e = T.fast[hi >> (32 - kLook)];
     uint32_t len = e >> 8, sym = e & 0xFF;
     if (len == 0) {
-      const uint32_t c16 = (uint32_t)(buf >> 48);
+      const uint32_t c16 = hi >> 16;
       len = long_code_len(c16, T.lim);
       if (len > 16) {
         len = 16;
@@ -354,36 +371,36 @@ __device__ __forceinline__ void write_span(const uint32_t *w, uint32_t woff, uin
     }
     const uint32_t r = dc ? 0u : sym >> 4;
     const uint32_t sz = dc ? (sym > 16 ? 16u : sym) : (sym & 15);
-    const uint64_t b2 = buf << len;
-    const int v = sz ? extend((uint32_t)(b2 >> (64 - sz)), sz) : 0;
-    buf = b2 << sz;
-    nb -= len + sz;
-    pos += len + sz;
+    const uint32_t t = len + sz;  // <= 32
+    const uint32_t xb = __builtin_amdgcn_ubfe(hi, (32 - t) & 31, sz);  // the extra bits (0 when sz = 0)
+    const int v = xb < (1u << sz >> 1) ? (int)xb - (int)((1u << sz) - 1) : (int)xb;  // jdhuff.h HUFF_EXTEND; 0 when sz = 0
+    buf <<= t;
+    nb -= t;
+    pos += t;
+    // the zigzag index after the symbol, by selects (ahead of the stores' branches, which the
+    // compiler otherwise folds it into)
+    const uint32_t zn = dc ? 1u : sz ? z + r + 1 : r == 15 ? z + 16 : 64u;
     if (dc) {
-      dcseq[HuffGeom::sel(dcb, k) + (uint64_t)mcu * HuffGeom::sel(g.bpc, k) + (c - HuffGeom::sel(g.cfirst, k))] = v;
+      dcseq[k == 0 ? dcp0 : k == 1 ? dcp1 : dcp2] = v;
     } else if (sz) {
       const uint32_t zz = z + r < 63 ? z + r : 63;
       if constexpr (CHUNKS) {
-        if (own) {
-          const uint32_t q = zz >> 3;
-          if (q != cq) {  // a new chunk: store the one collected (if any)
-            if (m8 >> cq & 1)
-              *reinterpret_cast<uint4 *>(coef + (uint64_t)blk * 64 + cq * 8) = make_uint4(q0, q1, q2, q3);
-            q0 = q1 = q2 = q3 = 0;
-            cq = q;
-          }
-          m8 |= 1u << q;
-          const uint32_t hv = ((uint32_t)v & 0xFFFFu) << (16 * (zz & 1)), wsel = (zz >> 1) & 3;
-          q0 |= wsel == 0 ? hv : 0u;
-          q1 |= wsel == 1 ? hv : 0u;
-          q2 |= wsel == 2 ? hv : 0u;
-          q3 |= wsel == 3 ? hv : 0u;
-        }
+        const uint32_t q = zz >> 3;
+        const bool nc = own && q != cq;  // a new chunk: store the one collected (if any)
+        if (nc && (m8 >> cq & 1))
+          *reinterpret_cast<uint4 *>(coef + (uint64_t)blk * 64 + cq * 8) = make_uint4(q0, q1, q2, q3);
+        const uint32_t hv = own ? ((uint32_t)v & 0xFFFFu) << (16 * (zz & 1)) : 0u, wsel = (zz >> 1) & 3;
+        q0 = (nc ? 0u : q0) | (wsel == 0 ? hv : 0u);
+        q1 = (nc ? 0u : q1) | (wsel == 1 ? hv : 0u);
+        q2 = (nc ? 0u : q2) | (wsel == 2 ? hv : 0u);
+        q3 = (nc ? 0u : q3) | (wsel == 3 ? hv : 0u);
+        cq = nc ? q : cq;
+        m8 |= own ? 1u << q : 0u;
       } else {
         coef[(uint64_t)blk * 64 + zz] = (int16_t)v;
       }
     }
-    z = dc ? 1u : sz ? z + r + 1 : r == 15 ? z + 16 : 64u;
+    z = zn;
     const bool eob = z >= 64;
     if constexpr (CHUNKS) {
       if (eob && own) {
@@ -399,12 +416,15 @@ __device__ __forceinline__ void write_span(const uint32_t *w, uint32_t woff, uin
       q2 = eob ? 0u : q2;
       q3 = eob ? 0u : q3;
     }
+    dcp0 += eob && k == 0 ? 1u : 0u;
+    dcp1 += eob && k == 1 ? 1u : 0u;
+    dcp2 += eob && k == 2 ? 1u : 0u;
     const uint32_t c1 = c + 1 == g.bpm ? 0u : c + 1;
     z = eob ? 0u : z;
-    mcu += eob && c1 == 0 ? 1u : 0u;
     blk += eob ? 1u : 0u;
     c = eob ? c1 : c;
     k = g.comp(c);
+    toff = __umul24(k, kTab);
   }
 }
 
@@ -2400,6 +2420,15 @@ __device__ __forceinline__ int16_t quantize(int32_t x, uint32_t recip, uint32_t 
   return (int16_t)(((int32_t)p ^ sg) - sg);
 }
 
+// Zero a block's AC bit image (kAcScratchWords words, a 16-B aligned row) with its 8 lanes: 16-B
+// stores, at most two per lane, instead of a loop of 4-B ones
+static_assert(kAcScratchWords % 4 == 0 && kAcScratchWords / 4 <= 16, "two 16-B stores per lane");
+__device__ __forceinline__ void clear_ac_words(uint32_t *acw_slot, uint32_t r) {
+  uint4 *a4 = reinterpret_cast<uint4 *>(acw_slot);
+  a4[r] = make_uint4(0, 0, 0, 0);
+  if (r + 8 < (uint32_t)kAcScratchWords / 4) a4[r + 8] = make_uint4(0, 0, 0, 0);
+}
+
 // The 8 * H pixels of rows py .. py + R - 1 from px that one lane converts, edges replicated
 // (jccolor.c on expand_right_edge / expand_bottom_edge input).  Loading and converting are
 // split, so a wave issues its pixel loads before it waits on anything else: inside the image
@@ -2473,7 +2502,7 @@ __device__ __forceinline__ void fdct_pass1(const uint8_t *img, const Geom &g, in
   const int px = bx * 8 * H;
   rows_load<H, R>(img, g.w, g.h, px, sy * R, real, dummy, p);
   if (threadIdx.x < 192) s_tab[threadIdx.x] = tw;
-  for (uint32_t i = r; i < (uint32_t)kAcScratchWords; i += 8) acw_slot[i] = 0;  // the block's own lanes
+  clear_ac_words(acw_slot, r);
   if (!real) return;
   if (H == 1 && R == 1) q.bias -= 128 << 16;
   int32_t v[8];
@@ -2499,7 +2528,7 @@ __device__ __forceinline__ void fdct_pass1_planes(const uint8_t *plane, int pitc
                                                   uint32_t *acw_slot, uint32_t r, int32_t *wsrow) {
   const uint2 q = *reinterpret_cast<const uint2 *>(real ? plane + (size_t)sy * pitch + bx * 8 : dummy);
   if (threadIdx.x < 192) s_tab[threadIdx.x] = tw;
-  for (uint32_t i = r; i < (uint32_t)kAcScratchWords; i += 8) acw_slot[i] = 0;  // the block's own lanes
+  clear_ac_words(acw_slot, r);
   if (!real) return;
   int32_t v[8];
 #pragma unroll
@@ -2609,7 +2638,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
   // registers and then writes its coefficient list over the slot.  Shared this way, the
   // workgroup's LDS is 18.5 KB: 8 workgroups per CU.
   __shared__ int32_t ws[32][8][9];
-  __shared__ uint32_t acw[32][kAcWords];
+  __shared__ __attribute__((aligned(16))) uint32_t acw[32][kAcWords];  // rows of 208 B: 16-B aligned
   // The table image (EncTables::fdct_lds): s_q[t][n] = {recip | corr << 16, (shift + 16) | qo
   // position of zigzag(n) for slot % 4 == j at bits 8 + 6j} (pass 2's lane reads one 8-B entry
   // per coefficient, 8 lanes 64 contiguous bytes, and uses the second word as it is for the
