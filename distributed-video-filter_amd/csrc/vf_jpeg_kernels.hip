@@ -959,12 +959,15 @@ __device__ __forceinline__ uint32_t spec_link(const uint32_t *words, uint32_t wo
 
 __global__ __launch_bounds__(256) void k_spec(const DecSeg *__restrict__ sg, const DecFrame *__restrict__ fr, const uint8_t *us, const uint32_t *us_len,
                                               SpecBufs B) {
+  // States here are kept relative to the workgroup's first bit in 32 bits (every one lies within
+  // its 16 K bits + overshoot), block counts in 16: 24.6 KB of LDS instead of 31.8, 6 workgroups
+  // per CU instead of 5 (the decodes are latency-bound chains: resident ones are what counts)
   __shared__ HuffSync tabs[6];
-  __shared__ uint64_t s_ck[kCk][256];
-  __shared__ uint32_t s_rem[kCk][256];
-  __shared__ uint64_t s_E[256];
-  __shared__ uint64_t s_X[256];
-  __shared__ uint32_t s_C[256];
+  __shared__ uint32_t s_ck[kCk][256];
+  __shared__ uint16_t s_rem[kCk][256];
+  __shared__ uint32_t s_E[256];
+  __shared__ uint32_t s_X[256];
+  __shared__ uint16_t s_C[256];
   __shared__ uint8_t s_M[256];
   __shared__ uint32_t s_w[kSpecWords];
   const DecSeg S = sg[blockIdx.y];  // by value: held in scalar registers
@@ -986,11 +989,16 @@ __global__ __launch_bounds__(256) void k_spec(const DecSeg *__restrict__ sg, con
   for (uint32_t i = t; i < NS * (kSubBits / 32) + kSpecPadWords; i += 256)
     s_w[i] = woff + i < fwords ? gw[woff + i] : 0u;
   load_sync_tables(F, tabs);  // its barrier also publishes s_w
+  // pack_state's (pos << 16 | z << 8 | c) relative to the workgroup's first bit, and back; the
+  // 32-bit kNoCk (0xFFFFFFFF) reads back as a state with z = 255, which no decode reaches
+  const uint64_t wb16 = (uint64_t)(woff * 32u) << 16;
+  const auto rel = [wb16](uint64_t st) { return (uint32_t)(st - wb16); };
+  const auto absl = [wb16](uint32_t r) { return (uint64_t)r + wb16; };
   // A: the trajectory of subsequence s from (base, z = 0, c = c0), checkpoints recorded
   uint64_t E = 0;
   uint32_t N = 0;
 #pragma unroll
-  for (int m = 0; m < kCk; ++m) s_ck[m][t] = kNoCk;
+  for (int m = 0; m < kCk; ++m) s_ck[m][t] = 0xFFFFFFFFu;
   if (live) {
     SyncLane<HuffSync> d;
     d.init(s_w, woff, pack_state(base, 0, c0), hg);
@@ -1001,15 +1009,15 @@ __global__ __launch_bounds__(256) void k_spec(const DecSeg *__restrict__ sg, con
       const uint32_t stop = cm ? mk : end;
       while (d.pos < stop) d.step(tabs, stop);
       if (!cm) break;
-      s_ck[m][t] = pack_state(d.pos, d.z, d.c);
-      s_rem[m][t] = d.n;
+      s_ck[m][t] = rel(pack_state(d.pos, d.z, d.c));
+      s_rem[m][t] = (uint16_t)d.n;
       ++m;
     }
-    for (uint32_t q = 0; q < m; ++q) s_rem[q][t] = d.n - s_rem[q][t];
+    for (uint32_t q = 0; q < m; ++q) s_rem[q][t] = (uint16_t)(d.n - s_rem[q][t]);
     E = pack_state(d.pos, d.z, d.c);
     N = d.n;
   }
-  s_E[t] = E;
+  s_E[t] = live ? rel(E) : 0u;
   __syncthreads();
   if (live) {
     B.tE[ti] = E;
@@ -1017,7 +1025,8 @@ __global__ __launch_bounds__(256) void k_spec(const DecSeg *__restrict__ sg, con
       const uint64_t wb = ((uint64_t)(S.wg0 + blockIdx.x) * kSpecLanesMax + c0) * kCk;
 #pragma unroll
       for (int m = 0; m < kCk; ++m) {
-        B.wck[wb + m] = s_ck[m][t];
+        const uint32_t r = s_ck[m][t];
+        B.wck[wb + m] = r == 0xFFFFFFFFu ? kNoCk : absl(r);
         B.wrem[wb + m] = s_rem[m][t];
       }
     }
@@ -1027,13 +1036,13 @@ __global__ __launch_bounds__(256) void k_spec(const DecSeg *__restrict__ sg, con
   uint64_t X = 0;
   if (live && sl > 0) {
     const uint32_t row = sl * L;
-    M = spec_link(s_w, woff, s_E[(sl - 1) * L + c0], base, end, s + 1 == nsub, hg, tabs,
-                  [&](uint32_t c2, int m) { return s_ck[m][row + c2]; },
-                  [&](uint32_t c2, int m) { return s_rem[m][row + c2]; }, &C, &X);
+    M = spec_link(s_w, woff, absl(s_E[(sl - 1) * L + c0]), base, end, s + 1 == nsub, hg, tabs,
+                  [&](uint32_t c2, int m) { return absl(s_ck[m][row + c2]); },
+                  [&](uint32_t c2, int m) { return (uint32_t)s_rem[m][row + c2]; }, &C, &X);
   }
   s_M[t] = (uint8_t)M;
-  s_C[t] = C;
-  s_X[t] = X;
+  s_C[t] = (uint16_t)C;
+  s_X[t] = live && sl > 0 && M >= hg.bpm ? rel(X) : 0u;  // an explicit or the frame's last end state
   __syncthreads();
   // C: the walks.  Walk e is trajectory e of the first subsequence followed through the links:
   // j_k = f_k(j_{k-1}), f_k(j) = s_M[k * L + j].  While every step is a link (no explicit
@@ -1081,7 +1090,7 @@ __global__ __launch_bounds__(256) void k_spec(const DecSeg *__restrict__ sg, con
     if (t == 0) {
       for (uint32_t q = 0; q < bpm; ++q) {
         B.tG[g0 + q] = (uint8_t)q;
-        B.tX[g0 + q] = s_E[q];
+        B.tX[g0 + q] = absl(s_E[q]);
         B.tXc[g0 + q] = s_C[q];  // trajectory count (used for the frame's first subsequence)
       }
     } else {
@@ -1089,7 +1098,7 @@ __global__ __launch_bounds__(256) void k_spec(const DecSeg *__restrict__ sg, con
         const uint32_t p = nib(gp, q);
         if (p >= bpm) continue;  // stopped (last) or explicit (the serial walk below)
         const uint32_t M2 = s_M[t * L + p];
-        const uint64_t st = M2 < bpm ? s_E[t * L + M2] : s_X[t * L + p];
+        const uint64_t st = absl(M2 < bpm ? s_E[t * L + M2] : s_X[t * L + p]);
         B.tG[g0 + t * L + q] = (uint8_t)M2;
         B.tX[g0 + t * L + q] = st;
         B.tXc[g0 + t * L + q] = s_C[t * L + p];
@@ -1119,17 +1128,17 @@ __global__ __launch_bounds__(256) void k_spec(const DecSeg *__restrict__ sg, con
       if (j < hg.bpm) {
         M2 = s_M[k * L + j];
         cnt = s_C[k * L + j];
-        xe = s_X[k * L + j];
+        xe = absl(s_X[k * L + j]);
       } else {  // explicit state: link it into subsequence k here
         const uint32_t bk = sk * kSubBits, ek = (sk + 1 >= nsub) ? nbits : (sk + 1) * kSubBits;
         const uint32_t row = k * L;
         M2 = spec_link(s_w, woff, st, bk, ek, sk + 1 == nsub, hg, tabs,
-                       [&](uint32_t c2, int m) { return s_ck[m][row + c2]; },
-                       [&](uint32_t c2, int m) { return s_rem[m][row + c2]; }, &cnt, &xe);
+                       [&](uint32_t c2, int m) { return absl(s_ck[m][row + c2]); },
+                       [&](uint32_t c2, int m) { return (uint32_t)s_rem[m][row + c2]; }, &cnt, &xe);
       }
       if (M2 < hg.bpm) {
         j = M2;
-        st = s_E[k * L + j];
+        st = absl(s_E[k * L + j]);
       } else {
         j = M2;  // kLinkNone (explicit) or kLinkLast
         st = xe;
