@@ -959,9 +959,9 @@ __device__ __forceinline__ uint32_t spec_link(const uint32_t *words, uint32_t wo
 
 __global__ __launch_bounds__(256) void k_spec(const DecSeg *__restrict__ sg, const DecFrame *__restrict__ fr, const uint8_t *us, const uint32_t *us_len,
                                               SpecBufs B) {
-  // States here are kept relative to the workgroup's first bit in 32 bits (every one lies within
-  // its 16 K bits + overshoot), block counts in 16: 24.6 KB of LDS instead of 31.8, 6 workgroups
-  // per CU instead of 5 (the decodes are latency-bound chains: resident ones are what counts)
+  // States here are kept relative to the workgroup's first bit in 32 bits (rel / absl below),
+  // block counts in 16: 24.6 KB of LDS instead of 31.8, 6 workgroups per CU instead of 5 (the
+  // decodes are latency-bound chains: the resident ones are what counts)
   __shared__ HuffSync tabs[6];
   __shared__ uint32_t s_ck[kCk][256];
   __shared__ uint16_t s_rem[kCk][256];
@@ -989,11 +989,16 @@ __global__ __launch_bounds__(256) void k_spec(const DecSeg *__restrict__ sg, con
   for (uint32_t i = t; i < NS * (kSubBits / 32) + kSpecPadWords; i += 256)
     s_w[i] = woff + i < fwords ? gw[woff + i] : 0u;
   load_sync_tables(F, tabs);  // its barrier also publishes s_w
-  // pack_state's (pos << 16 | z << 8 | c) relative to the workgroup's first bit, and back; the
-  // 32-bit kNoCk (0xFFFFFFFF) reads back as a state with z = 255, which no decode reaches
-  const uint64_t wb16 = (uint64_t)(woff * 32u) << 16;
-  const auto rel = [wb16](uint64_t st) { return (uint32_t)(st - wb16); };
-  const auto absl = [wb16](uint32_t r) { return (uint64_t)r + wb16; };
+  // pack_state's (pos << 16 | z << 8 | c) as (pos - the workgroup's first bit) << 10 | z << 4 | c
+  // (a workgroup spans at most 256 subsequences, 2^16 bits, plus a symbol's overshoot; z < 64,
+  // c < 10), and back; the 32-bit kNoCk (0xFFFFFFFF) reads back with c = 15, which no decode has
+  const uint32_t wbit = woff * 32u;
+  const auto rel = [wbit](uint64_t st) {
+    return (((uint32_t)(st >> 16) - wbit) << 10) | (((uint32_t)st >> 4) & 0x3F0u) | ((uint32_t)st & 15u);
+  };
+  const auto absl = [wbit](uint32_t r) {
+    return pack_state((r >> 10) + wbit, (r >> 4) & 63u, r & 15u);
+  };
   // A: the trajectory of subsequence s from (base, z = 0, c = c0), checkpoints recorded
   uint64_t E = 0;
   uint32_t N = 0;
