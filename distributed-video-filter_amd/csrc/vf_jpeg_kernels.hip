@@ -317,10 +317,21 @@ struct HuffGeom {
 // per-component running position (each component's DC sequence is in block order) instead of
 // an address rebuilt from (MCU, c) -- whose three-way selects over 64-bit bases compiled to
 // nested branches -- and the chunk and block-end bookkeeping are selects around the stores.
-template <bool CHUNKS>
+// k_write's LDS staging of its workgroup's DC values and chunk masks: the blocks a workgroup
+// owns are consecutive, so their per-block 4-B and 1-B stores -- scattered over the lanes, a
+// sparse store instruction nearly every step -- are collected here by block and written out
+// coalesced at the end (blocks past kStageBlocks from the first go straight to memory).
+constexpr uint32_t kStageBlocks = 4096;
+struct WriteStage {
+  int32_t *dc;     // [kStageBlocks] DC differences
+  uint16_t *nm;    // [kStageBlocks] 0x100 | chunk mask, 0 while not written
+  uint32_t first;  // the workgroup's first block (segment-relative)
+};
+template <bool CHUNKS, bool STG = false>
 __device__ __forceinline__ void write_span(const uint32_t *w, uint32_t woff, uint64_t X, uint32_t end,
                                            const HuffGeom &g, const HuffDec *tabs, uint32_t blk, int16_t *coef,
-                                           int32_t *dcseq, const uint64_t *dcbase, uint8_t *nmask) {
+                                           int32_t *dcseq, const uint64_t *dcbase, uint8_t *nmask,
+                                           const WriteStage &stg = WriteStage{nullptr, nullptr, 0}) {
   const uint32_t p = (uint32_t)(X >> 16);
   uint32_t wi = (p >> 5) - woff;
   uint64_t buf = (((uint64_t)bswap32(w[wi]) << 32) | bswap32(w[wi + 1])) << (p & 31);
@@ -381,7 +392,13 @@ __device__ __forceinline__ void write_span(const uint32_t *w, uint32_t woff, uin
     // compiler otherwise folds it into)
     const uint32_t zn = dc ? 1u : sz ? z + r + 1 : r == 15 ? z + 16 : 64u;
     if (dc) {
-      dcseq[k == 0 ? dcp0 : k == 1 ? dcp1 : dcp2] = v;
+      const uint32_t sb = blk - stg.first;
+      if (STG && sb < kStageBlocks) {
+        stg.dc[sb] = v;
+        stg.nm[sb] = 0x100;
+      } else {
+        dcseq[k == 0 ? dcp0 : k == 1 ? dcp1 : dcp2] = v;
+      }
     } else if (sz) {
       const uint32_t zz = z + r < 63 ? z + r : 63;
       if constexpr (CHUNKS) {
@@ -406,7 +423,9 @@ __device__ __forceinline__ void write_span(const uint32_t *w, uint32_t woff, uin
       if (eob && own) {
         if (m8 >> cq & 1)
           *reinterpret_cast<uint4 *>(coef + (uint64_t)blk * 64 + cq * 8) = make_uint4(q0, q1, q2, q3);
-        nmask[blk] = (uint8_t)m8;
+        const uint32_t sb = blk - stg.first;
+        if (STG && sb < kStageBlocks) stg.nm[sb] = (uint16_t)(0x100 | m8);
+        else nmask[blk] = (uint8_t)m8;
       }
       own = own || eob;  // the next block starts here: inside the span (or the loop ends)
       cq = eob ? 0u : cq;
@@ -426,6 +445,7 @@ __device__ __forceinline__ void write_span(const uint32_t *w, uint32_t woff, uin
     k = g.comp(c);
     toff = __umul24(k, kTab);
   }
+  if constexpr (STG) atomicMax(reinterpret_cast<uint32_t *>(stg.dc) + kStageBlocks, blk - stg.first);  // flush bound
 }
 
 __device__ __forceinline__ void load_tables(const DecFrame &F, HuffDec *tabs) {
@@ -1452,6 +1472,8 @@ __global__ __launch_bounds__(256) void k_write(const DecSeg *__restrict__ sg, co
                                                int32_t *dcseq, uint8_t *nmask) {
   __shared__ HuffDec tabs[6];
   __shared__ uint32_t s_w[kSpecWords + (CHUNKS ? kBlockPadWords : 0)];
+  __shared__ int32_t s_dc[kStageBlocks + 1];  // + the flush bound
+  __shared__ __attribute__((aligned(16))) uint16_t s_nm[kStageBlocks];
   const DecSeg S = sg[blockIdx.y];  // by value: held in scalar registers
   const DecFrame &F = fr[S.frame];
   if (blockIdx.x * 256 >= S.nsub_max) return;
@@ -1462,17 +1484,35 @@ __global__ __launch_bounds__(256) void k_write(const DecSeg *__restrict__ sg, co
   const uint32_t *gw = reinterpret_cast<const uint32_t *>(us + S.us_off);
   constexpr uint32_t kWords = kSpecWords + (CHUNKS ? kBlockPadWords : 0);
   for (uint32_t k = threadIdx.x; k < kWords; k += 256) s_w[k] = woff + k < fwords ? gw[woff + k] : 0u;
-  load_tables(F, tabs);  // its barrier also publishes s_w
+  for (uint32_t k = threadIdx.x; k < kStageBlocks / 8; k += 256) reinterpret_cast<uint4 *>(s_nm)[k] = make_uint4(0, 0, 0, 0);
+  if (threadIdx.x == 0) s_dc[kStageBlocks] = 0;
+  load_tables(F, tabs);  // its barrier also publishes s_w and the cleared stage
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   const uint32_t nbits = us_len[blockIdx.y] * 8u;
   const uint32_t nsub = (nbits + kSubBits - 1) / kSubBits;
-  if (i >= nsub) return;
   const uint32_t gi = S.sub0 + i;
-  const uint64_t st = i == 0 ? 0 : exits[gi - 1];
-  const uint32_t end = (i + 1 == nsub) ? nbits : (i + 1) * kSubBits;
   HuffGeom hg(F.g);
   hg.nblocks = S.nblocks;  // the segment's blocks (a restart interval: its whole MCUs)
-  write_span<CHUNKS>(s_w, woff, st, end, hg, tabs, bstart[gi], coef + S.blk0 * 64, dcseq, S.dcbase, nmask + S.blk0);
+  const uint32_t i0 = blockIdx.x * 256;  // workgroup-uniform
+  const WriteStage stg{s_dc, s_nm, i0 < nsub ? bstart[S.sub0 + i0] : 0u};
+  if (i < nsub) {
+    const uint64_t st = i == 0 ? 0 : exits[gi - 1];
+    const uint32_t end = (i + 1 == nsub) ? nbits : (i + 1) * kSubBits;
+    write_span<CHUNKS, true>(s_w, woff, st, end, hg, tabs, bstart[gi], coef + S.blk0 * 64, dcseq, S.dcbase,
+                             nmask + S.blk0, stg);
+  }
+  __syncthreads();
+  // the staged blocks, consecutive threads on consecutive blocks: the masks are one coalesced
+  // byte run, the DC values a few coalesced runs (one per component)
+  const uint32_t nst = min(s_dc[kStageBlocks] + 1, kStageBlocks);
+  uint8_t *const nm = nmask + S.blk0;
+  for (uint32_t b = threadIdx.x; b < nst; b += 256) {
+    const uint32_t f = s_nm[b];
+    if (!(f & 0x100)) continue;
+    const uint32_t blk = stg.first + b, mcu = blk / hg.bpm, c = blk - mcu * hg.bpm, k = hg.comp(c);
+    dcseq[HuffGeom::sel(S.dcbase, k) + (uint64_t)mcu * HuffGeom::sel(hg.bpc, k) + (c - HuffGeom::sel(hg.cfirst, k))] = s_dc[b];
+    if (CHUNKS) nm[blk] = (uint8_t)f;
+  }
 }
 
 // The write pass with 4 lanes per subsequence, for the pass-based sync (k_sync), whose
