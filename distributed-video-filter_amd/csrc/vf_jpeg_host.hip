@@ -674,15 +674,19 @@ int Codec::run_decode_post(int bgr, bool invert, std::string *err) {
   uint32_t *blocks_total = static_cast<uint32_t *>(dtot_dev_);
   CK(scan_u32(segs + ns, ns, (dmax_sub_ + kScanTile - 1) / kScanTile, d_cnt_[last].as<uint32_t>(),
               d_bstart_.as<uint32_t>(), d_tsum_.as<uint32_t>(), blocks_total, false, s_));
-  // After the speculative sync, the write pass stores whole 16-B coefficient rows with a
-  // per-block mask of the rows stored, which the IDCT reads: no 134 MB clear per 1080p batch
-  // (k_write + clear 118 -> 105 us).  Not after the pass-based sync: its write pass runs 4 lanes
-  // per subsequence, and with blocks of ~250 bits (hard content) nearly every lane would decode
-  // on to its last block's end and skip its first: k_write4 342 -> 1227 us
-  // (profiles/r04_jpeg_chunks_ab.txt).  VF_JPEG_CHUNKS=0 / 1 forces either form.
-  const bool chunks = [use_spec] {  // read per call: tests switch it inside one process
+  // The write pass stores whole 16-B coefficient rows with a per-block mask of the rows stored,
+  // which the IDCT reads: no clear of the coefficient buffer (134 MB per 1080p batch, 1.06 GB
+  // per 4K one).  After the speculative sync always (k_write + clear 118 -> 105 us at 1080p).
+  // After the pass-based sync only when blocks are short: its write pass runs 4 lanes per
+  // subsequence, each of which decodes on to its last block's end and skips its first, which
+  // costs a block per lane -- on hard content (~500 bits per block) k_write4 342 -> 1227 us,
+  // on 4K scenes (~22 bits per block) huffman_write 0.50 -> 0.29 ms, resident 11.1 -> 12.0 k fps
+  // (profiles/r04_jpeg_fuse_chunks_warm_ab.txt, r04_jpeg_chunks_4k_ab.txt).  VF_JPEG_CHUNKS=0 / 1
+  // forces either form.
+  constexpr uint64_t kChunkBitsPerBlock = 128;
+  const bool chunks = [use_spec, this] {  // read per call: tests switch it inside one process
     const char *v = std::getenv("VF_JPEG_CHUNKS");
-    return v && *v ? std::strcmp(v, "0") != 0 : use_spec;
+    return v && *v ? std::strcmp(v, "0") != 0 : use_spec || dbits_per_block_ <= kChunkBitsPerBlock;
   }();
   uint8_t *const nmask = chunks ? d_nmask_.as<uint8_t>() : nullptr;
   if (!chunks) CK(hipMemsetAsync(d_coef_.p, 0, dblocks_ * 128, s_));
