@@ -21,7 +21,9 @@ from __future__ import annotations
 
 import collections
 import itertools
+import os
 import select
+import selectors
 import socket
 import struct
 import threading
@@ -93,6 +95,61 @@ def _send_msg(sock: socket.socket, parts: Sequence) -> None:
             sent = 0
 
 
+class _RecvState:
+    """One peer's message being received by the select loop: u32 nparts, then per part u64
+    length + bytes, read as far as the socket has data (MSG_DONTWAIT per call, so the socket
+    itself stays blocking for the senders on other threads)."""
+
+    def __init__(self, pid: bytes, conn: socket.socket):
+        self.pid, self.conn = pid, conn
+        self._start(_HDR.size, "hdr")
+
+    def _start(self, n: int, stage: str) -> None:
+        self.stage, self.buf, self.got = stage, bytearray(n), 0
+
+    def feed(self) -> List[List[bytes]]:
+        """Read what is available; returns the messages completed (raises on disconnect)."""
+        done = []
+        while True:
+            n = len(self.buf)
+            if self.got < n:
+                try:
+                    k = self.conn.recv_into(memoryview(self.buf)[self.got:], n - self.got, socket.MSG_DONTWAIT)
+                except (BlockingIOError, InterruptedError):
+                    return done
+                if k == 0:
+                    raise ConnectionError("peer closed")
+                self.got += k
+                if self.got < n:
+                    continue
+            if self.stage == "hdr":
+                (self.nparts,) = _HDR.unpack(self.buf)
+                self.parts = []
+                if self.nparts == 0:
+                    done.append(self.parts)
+                    self._start(_HDR.size, "hdr")
+                else:
+                    self._start(_LEN.size, "len")
+            elif self.stage == "len":
+                (m,) = _LEN.unpack(self.buf)
+                self._start(m, "part")
+                if m == 0:
+                    continue
+            else:
+                self.parts.append(bytes(self.buf) if len(self.buf) < (1 << 16) else self.buf)
+                if len(self.parts) == self.nparts:
+                    done.append(self.parts)
+                    self._start(_HDR.size, "hdr")
+                else:
+                    self._start(_LEN.size, "len")
+
+
+# VF_TCP_READER=thread (default): one reader thread per peer connection; "select": one thread
+# per listener accepts and reads every peer, so N workers' messages are handled by one thread
+# instead of N contending for the GIL and the distributor's lock (profiles/r04_reader_ab.jsonl)
+_READER = os.environ.get("VF_TCP_READER", "thread")
+
+
 def _bind_addr(host: str) -> str:
     return "0.0.0.0" if host in ("*", "", None) else host
 
@@ -119,7 +176,71 @@ class _Listener:
         self._ids = itertools.count(1)
         self._lock = threading.Lock()
         self._closed = False
-        threading.Thread(target=self._accept_loop, daemon=True).start()
+        if _READER == "thread":
+            threading.Thread(target=self._accept_loop, daemon=True).start()
+        else:
+            threading.Thread(target=self._select_loop, daemon=True, name="tcp-select").start()
+
+    def _select_loop(self):
+        sel = selectors.DefaultSelector()
+        try:
+            sel.register(self.sock, selectors.EVENT_READ, None)
+        except (ValueError, OSError):  # closed before this thread started
+            sel.close()
+            return
+        try:
+            while not self._closed:
+                try:
+                    events = sel.select(timeout=0.5)
+                except (ValueError, OSError):
+                    return
+                for key, _ in events:
+                    st = key.data
+                    if st is None:  # the listening socket: a new peer
+                        try:
+                            conn, _ = self.sock.accept()
+                        except OSError:
+                            if self._closed:
+                                return
+                            continue
+                        conn.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+                        pid = b"\x00" + next(self._ids).to_bytes(4, "big")
+                        with self._lock:
+                            self.peers[pid] = (conn, threading.Lock())
+                        sel.register(conn, selectors.EVENT_READ, _RecvState(pid, conn))
+                        continue
+                    try:
+                        msgs = st.feed()
+                    except (ConnectionError, OSError):
+                        msgs = None
+                    for msg in msgs or ():
+                        h = self.handler
+                        if h is not None:
+                            h(st.pid, msg)
+                        else:
+                            self._put((st.pid, msg))
+                    if msgs is None:
+                        try:
+                            sel.unregister(st.conn)
+                        except (KeyError, ValueError, OSError):
+                            pass
+                        self._gone(st.pid, st.conn)
+        finally:
+            sel.close()
+
+    def _gone(self, pid, conn):
+        with self._lock:
+            self.peers.pop(pid, None)
+        try:
+            conn.close()
+        except OSError:
+            pass
+        if not self._closed:
+            h = self.handler
+            if h is not None:
+                h(pid, None)
+            else:
+                self._put((pid, None))  # disconnect notice (ZeroMQ gives none; see RouterEnd.recv)
 
     def _accept_loop(self):
         while not self._closed:
@@ -145,18 +266,7 @@ class _Listener:
         except (ConnectionError, OSError):
             pass
         finally:
-            with self._lock:
-                self.peers.pop(pid, None)
-            try:
-                conn.close()
-            except OSError:
-                pass
-            if not self._closed:
-                h = self.handler
-                if h is not None:
-                    h(pid, None)
-                else:
-                    self._put((pid, None))  # disconnect notice (ZeroMQ gives none; see RouterEnd.recv)
+            self._gone(pid, conn)
 
     def _put(self, item) -> None:
         with self._cond:

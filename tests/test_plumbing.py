@@ -143,7 +143,12 @@ def test_wire_v1_columns_roundtrip_every_field():
 
 # ---- transport -------------------------------------------------------------------------------
 
-def test_tcp_transport_roles():
+@pytest.mark.parametrize("reader", ["thread", "select"])
+def test_tcp_transport_roles(monkeypatch, reader):
+    """Both listener forms (VF_TCP_READER: a reader thread per peer, or one select loop per
+    listener): multipart messages in both directions, a 3 MiB part, an empty part, several peers
+    on one listener, and a peer's disconnect reported as (peer, None)."""
+    monkeypatch.setattr(tp, "_READER", reader)
     router = tp.RouterEnd("tcp", "127.0.0.1", 0)
     pull = tp.PullEnd("tcp", "127.0.0.1", 0)
     dealer = tp.DealerEnd("tcp", "127.0.0.1", router.port)
@@ -162,6 +167,29 @@ def test_tcp_transport_roles():
         assert pull.poll(2000)
         assert [bytes(x) for x in pull.recv()] == [b"a", b"", big[:10].tobytes()]
         assert not router.send(b"\x00nope", [b"x"])  # unknown peer: dropped, like ROUTER
+        # more peers on the same listeners, messages interleaved, then one disconnects
+        pushes = [tp.PushEnd("tcp", "127.0.0.1", pull.port) for _ in range(3)]
+        for r in range(5):
+            for i, q in enumerate(pushes):
+                q.send([b"m", bytes([i, r]), big[: 70000 + r].tobytes()])
+        seen = []
+        while len(seen) < 15:
+            assert pull.poll(2000)
+            got = pull.recv()
+            assert got[0] == b"m" and bytes(got[2]) == big[: 70000 + got[1][1]].tobytes()
+            seen.append(bytes(got[1]))
+        assert sorted(seen) == sorted(bytes([i, r]) for i in range(3) for r in range(5))
+        dealer.close()
+        deadline = time.time() + 5
+        gone = None
+        while gone is None and time.time() < deadline:
+            if router.poll(200):
+                p_, parts = router.recv()
+                if parts is None:
+                    gone = p_
+        assert gone == peer
+        for q in pushes:
+            q.close()
     finally:
         for s in (dealer, push, router, pull):
             s.close()
