@@ -144,10 +144,12 @@ class _RecvState:
                     self._start(_LEN.size, "len")
 
 
-# VF_TCP_READER=thread (default): one reader thread per peer connection; "select": one thread
-# per listener accepts and reads every peer, so N workers' messages are handled by one thread
-# instead of N contending for the GIL and the distributor's lock (profiles/r04_reader_ab.jsonl)
-_READER = os.environ.get("VF_TCP_READER", "thread")
+# VF_TCP_READER=select (default): one thread per listener accepts and reads every peer, so N
+# workers' messages are handled by one thread instead of N contending for the GIL and the
+# distributor's lock -- 8 echo workers with JPEG-size frames 102-104 k fps against 70-95 k, the
+# JPEG system leg 41.1-41.5 k against 38.0-41.1 k (profiles/r04_reader_ab.txt); "thread": one
+# reader thread per peer connection (rounds 1-4)
+_READER = os.environ.get("VF_TCP_READER", "select")
 
 
 def _bind_addr(host: str) -> str:
