@@ -144,12 +144,15 @@ class _RecvState:
                     self._start(_LEN.size, "len")
 
 
-# VF_TCP_READER=select (default): one thread per listener accepts and reads every peer, so N
-# workers' messages are handled by one thread instead of N contending for the GIL and the
-# distributor's lock -- 8 echo workers with JPEG-size frames 102-104 k fps against 70-95 k, the
-# JPEG system leg 41.1-41.5 k against 38.0-41.1 k (profiles/r04_reader_ab.txt); "thread": one
-# reader thread per peer connection (rounds 1-4)
-_READER = os.environ.get("VF_TCP_READER", "select")
+# VF_TCP_READER=thread (default): one reader thread per peer connection.  "select": one thread
+# per listener accepts and reads every peer, so N workers' messages are handled by one thread
+# instead of N contending for the GIL and the distributor's lock -- 8 echo workers with JPEG-size
+# frames 102-104 k fps against 70-95 k, the JPEG system leg 41.1-41.5 k against 38.0-41.1 k
+# (profiles/r04_reader_ab.txt).  Not the default: a handler runs on that one thread, and where
+# frames travel as socket payloads (no shared-memory ring) a handler's blocking send of a large
+# dispatch can wait on a worker that is itself blocked sending results nobody is reading --
+# test_configs3_mixed_resolution_pull_tcp_payloads hung that way.  Ring deployments only.
+_READER = os.environ.get("VF_TCP_READER", "thread")
 
 
 def _bind_addr(host: str) -> str:
