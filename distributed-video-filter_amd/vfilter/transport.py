@@ -216,8 +216,8 @@ class _Listener:
                         continue
                     try:
                         msgs = st.feed()
-                    except (ConnectionError, OSError):
-                        msgs = None
+                    except (ConnectionError, OSError, MemoryError, ValueError, struct.error):
+                        msgs = None  # closed, or a malformed frame (e.g. an absurd length): drop the peer
                     for msg in msgs or ():
                         h = self.handler
                         if h is not None:
