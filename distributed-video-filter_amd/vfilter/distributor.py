@@ -69,7 +69,7 @@ from .shm import FrameRing, copy_into
 class _Peer:
     __slots__ = ("pid", "version", "wid", "requests", "frames_sent", "batches_sent", "results", "errors", "home_shard", "shm",
                  "numa", "slice", "queue", "inflight", "quarantine", "batches", "alive", "gone", "evictions",
-                 "order", "last_seen", "waiting_since")
+                 "order", "last_seen", "waiting_since", "wire", "outbox", "send_lock")
 
     def __init__(self, pid: bytes, req: wire.Request, order: int):
         self.pid = pid
@@ -94,6 +94,12 @@ class _Peer:
         self.evictions = 0
         self.last_seen = time.monotonic()     # last request or result
         self.waiting_since: Optional[float] = None  # frames wait for it, it has not asked
+        self.wire = req.wire                  # newest dispatch form it reads (wire.py)
+        # dispatches built and booked under the distributor's lock, sent outside it (no socket
+        # I/O under the lock: a worker blocked sending its results must never stall a thread that
+        # holds the lock its result reader needs); send_lock keeps one peer's sends in order
+        self.outbox: Deque[tuple] = collections.deque()
+        self.send_lock = threading.Lock()
 
 
 class _Slice:
@@ -108,12 +114,17 @@ class _Slice:
 
 
 class Distributor:
+    QUARANTINE_HOLD = 4  # batch timeouts a shared-ring slot of an evicted worker is held without a disconnect notice
+
     def __init__(self, distribute_port: int = 5555, collect_port: int = 5556, frame_delay: int = 5,
                  enable_trace_export: bool = False, *, policy: str = "latest", reassembly: str = "display",
                  transport: str = "auto", host: str = "*", queue_size: int = 10, frame_buffer_size: int = 50,
                  ring_slots: int = 0, ring_slot_bytes: int = 0, ring_layout: str = "auto", shard_workers: int = 0,
                  shard_chunk: int = 1, batch_timeout: float = 30.0, max_attempts: int = 3, batch_wait: float = 0.002,
-                 trace_file: str = "webcam_frame_timing.pftrace", verbose: bool = True, zero_copy: bool = False):
+                 trace_file: str = "webcam_frame_timing.pftrace", verbose: bool = True, zero_copy: bool = False,
+                 engine: str = "auto"):
+        if engine not in ("auto", "python"):
+            raise ValueError("engine must be auto | python | native")
         if zero_copy and (ring_slots < 1 or reassembly != "ordered"):
             raise ValueError("zero_copy needs ring_slots > 0 and reassembly='ordered'")
         self.zero_copy = zero_copy
@@ -189,6 +200,7 @@ class Distributor:
         self.trace_file = trace_file
         # peers and counters
         self._peers: Dict[bytes, _Peer] = {}
+        self._dirty = set()                       # peers with dispatches queued for sending
         self._by_wid: Dict[str, _Peer] = {}
         self._shard_home: Dict[int, bytes] = {}   # shard -> the worker it belongs to
         self._shard_owner: Dict[int, bytes] = {}  # shard -> the worker serving it now
@@ -202,6 +214,8 @@ class Distributor:
         self.results_received = 0
         self.result_errors = 0
         self.quarantine_expired = 0   # slots of evicted workers' frames freed after the grace period
+        self.quarantine_forced = 0    # of which shared-ring slots freed with no disconnect notice (zmq)
+        self._disconnect_notices = self.transport == "tcp"  # zmq reports no peer disconnects
         # threads (distributor.py:42-51)
         self.running = False
         self.distribute_thread = threading.Thread(target=self.handle_distribute_requests, daemon=True)
@@ -774,6 +788,7 @@ class Distributor:
             elif not p.alive and not p.gone:
                 self._revive(p)
             p.last_seen = time.monotonic()
+            p.wire = req.wire
             if req.version == 0 and self.policy == "latest":
                 self._serve_latest_v0(p)                      # distributor.py:229-241
                 return
@@ -844,8 +859,8 @@ class Distributor:
     def _serve_latest_v0(self, p: _Peer):
         cur = self.current_frame_data
         if cur is not None and cur.get("frame_index") is not None and cur["frame_index"] > self.last_frame_sent:
-            if self._send(p, [cur]):
-                self.last_frame_sent = cur["frame_index"]
+            self._queue_dispatch(p, [cur])
+            self.last_frame_sent = cur["frame_index"]
 
     def _fill_pending(self, p: _Peer, credit: int) -> bool:
         """True while request ``credit`` of busy worker ``p`` should wait for more frames
@@ -868,9 +883,8 @@ class Distributor:
                     if not items:
                         break
                     p.requests.popleft()
-                    if not self._send(p, items):
-                        self._unsend(p, items)
-                        break
+                    self._queue_dispatch(p, items)
+        self._flush_dirty()
 
     def _lanes_of(self, p: _Peer) -> List[Deque[dict]]:
         if self.policy == "pull":
@@ -960,46 +974,103 @@ class Distributor:
             self._clone_src.pop(it["src_slot"], None)
         self._copy_done(it["frame_index"])
 
-    def _send(self, p: _Peer, items: List[dict]) -> bool:
+    def _dispatch_parts(self, p: _Peer, items: List[dict]) -> list:
+        """The dispatch message for ``items`` in the form ``p`` reads (lock held)."""
         if p.version == 0:
             it = items[0]
             payload = it["frame"] if it["slot"] is None else bytes(self.in_view(it["slot"], it["nbytes"]))
-            ok = self.distribute_socket.send(p.pid, wire.encode_dispatch_v0(it["frame_index"], payload))
-        else:
-            ring = None
-            use_ring = p.shm and any(it["slot"] is not None for it in items)
-            if use_ring:
-                sid = next(it["slot"] for it in items if it["slot"] is not None) // self.ring_slots
-                ring = {"name": self._slices[sid].ring.name, "slot_bytes": self._slices[sid].ring.slot_bytes}
-            if use_ring and all(it["slot"] is not None for it in items):  # every frame in the ring
-                rs = self.ring_slots
-                parts = wire.encode_dispatch_columns([it["frame_index"] for it in items], [it["nbytes"] for it in items],
-                                                     [it["slot"] % rs for it in items], [it["shape"] for it in items],
-                                                     [], ring)
-            else:
-                metas, payloads = [], []
-                for it in items:
-                    in_ring = use_ring and it["slot"] is not None
-                    metas.append(wire.FrameMeta(index=it["frame_index"], nbytes=it["nbytes"], shape=it["shape"],
-                                                slot=it["slot"] % self.ring_slots if in_ring else None))
-                    payloads.append(None if in_ring else (it["frame"] if it["slot"] is None else
-                                                          bytes(self.in_view(it["slot"], it["nbytes"]))))
-                parts = wire.encode_dispatch(metas, payloads, ring)
-            ok = self.distribute_socket.send(p.pid, parts)
-        if ok:
-            p.frames_sent += len(items)
-            p.batches_sent += 1
-            batch = [time.monotonic(), set()]
-            for it in items:
-                it["attempts"] += 1
-                it["_batch"] = batch
-                p.inflight[it["frame_index"]] = it
-                batch[1].add(it["frame_index"])
-            p.batches.append(batch)
-        return ok
+            return wire.encode_dispatch_v0(it["frame_index"], payload)
+        ring = None
+        rs = self.ring_slots
+        use_ring = p.shm and any(it["slot"] is not None for it in items)
+        if use_ring:
+            sid = next(it["slot"] for it in items if it["slot"] is not None) // rs
+            ring = {"name": self._slices[sid].ring.name, "slot_bytes": self._slices[sid].ring.slot_bytes}
+        payloads = [None if (use_ring and it["slot"] is not None) else
+                    (it["frame"] if it["slot"] is None else bytes(self.in_view(it["slot"], it["nbytes"])))
+                    for it in items]
+        if p.wire >= 2 and all(wire.v2_shape_ok(it["shape"]) for it in items):
+            cols = np.zeros(len(items), wire.COLS)
+            cols["index"] = [it["frame_index"] for it in items]
+            cols["nbytes"] = [it["nbytes"] for it in items]
+            cols["slot"] = [it["slot"] % rs if pl is None else -1 for it, pl in zip(items, payloads)]
+            cols["ndim"] = -1
+            for i, it in enumerate(items):
+                sh = it["shape"]
+                if sh is not None:
+                    cols["ndim"][i] = len(sh)
+                    cols["shape"][i, :len(sh)] = sh
+            return wire.encode_dispatch2(cols, [pl for pl in payloads if pl is not None], ring)
+        metas = [wire.FrameMeta(index=it["frame_index"], nbytes=it["nbytes"], shape=it["shape"],
+                                slot=it["slot"] % rs if pl is None else None) for it, pl in zip(items, payloads)]
+        return wire.encode_dispatch(metas, payloads, ring)
+
+    def _queue_dispatch(self, p: _Peer, items: List[dict]) -> None:
+        """Build and book a dispatch of ``items`` to ``p`` and queue it for sending (lock held):
+        the frames are in flight from here, so a result can never arrive before its booking."""
+        parts = self._dispatch_parts(p, items)
+        p.frames_sent += len(items)
+        p.batches_sent += 1
+        batch = [time.monotonic(), set()]
+        for it in items:
+            it["attempts"] += 1
+            it["_batch"] = batch
+            p.inflight[it["frame_index"]] = it
+            batch[1].add(it["frame_index"])
+        p.batches.append(batch)
+        p.outbox.append((parts, items))
+        self._dirty.add(p)
+
+    def _flush_dirty(self) -> None:
+        """Send every queued dispatch, outside the distributor's lock."""
+        if not self._dirty:
+            return
+        with self._lock:
+            peers = list(self._dirty)
+            self._dirty.clear()
+        for p in peers:
+            self._flush(p)
+
+    def _flush(self, p: _Peer) -> None:
+        """Drain ``p``'s outbox in order.  One thread at a time sends to a peer (``send_lock``);
+        another thread finding the lock held leaves its messages to the holder, which checks
+        the outbox again after letting go of the lock."""
+        while True:
+            if not p.send_lock.acquire(blocking=False):
+                return
+            try:
+                while True:
+                    with self._lock:
+                        if not p.outbox:
+                            break
+                        parts, items = p.outbox.popleft()
+                    if not self.distribute_socket.send(p.pid, parts):
+                        with self._cv:
+                            self._unsend(p, items)
+            finally:
+                p.send_lock.release()
+            with self._lock:
+                if not p.outbox:
+                    return
 
     def _unsend(self, p: _Peer, items: List[dict]) -> None:
-        """The transport refused a dispatch (the worker is gone): back to the queues."""
+        """The transport refused a dispatch (the worker is gone): that dispatch and every one
+        still queued behind it are un-booked and go back to the queues (lock held)."""
+        for _, more in p.outbox:
+            items = items + more
+        p.outbox.clear()
+        # only copies still booked to p: an eviction since the booking has re-queued the others
+        items = [it for it in items if p.inflight.get(it["frame_index"]) is it]
+        for it in items:
+            idx = it["frame_index"]
+            del p.inflight[idx]
+            b = it.pop("_batch", None)
+            if b is not None:
+                b[1].discard(idx)
+            it["attempts"] -= 1
+        while p.batches and not p.batches[0][1]:
+            p.batches.popleft()
+        p.frames_sent -= len(items)
         if self.policy == "latest":
             for it in items:
                 self._drop(it)
@@ -1068,7 +1139,14 @@ class Distributor:
             slot = it.get("slot")
             if slot is not None and not (self.ring_layout == "per_worker" and p.slice is not None
                                          and slot // self.ring_slots == p.slice):
-                continue  # shared ring: held until the result or the disconnect
+                # shared ring: held until the result or the disconnect -- and where the transport
+                # reports no disconnects (ZeroMQ), for at most QUARANTINE_HOLD batch timeouts, so a
+                # dead worker cannot shrink the ring for ever.  A worker that was only
+                # hung that long and then writes its stale result into the slot's output half is
+                # the documented risk of that bound.
+                if self._disconnect_notices or now - it["_evicted_at"] <= self.QUARANTINE_HOLD * self.batch_timeout:
+                    continue
+                self.quarantine_forced += 1
             p.quarantine.pop(idx)
             self._free_slot(it.get("slot"))
             self._copy_done(it["frame_index"])

@@ -68,11 +68,29 @@ def _recv_exact(sock: socket.socket, n: int, alloc=None):
     return buf
 
 
-def _recv_msg(sock: socket.socket, alloc=None) -> List[bytes]:
+# what a reader accepts before it allocates anything: a peer's length field is never trusted
+# (a u64 of 2^62 is a MemoryError, 2^63 an OverflowError in bytearray())
+MAX_PARTS = 1 << 16
+MAX_PART = int(os.environ.get("VF_TCP_MAX_PART", str(1 << 30)))
+
+
+def _check_nparts(nparts: int) -> None:
+    if nparts > MAX_PARTS:
+        raise ValueError(f"malformed message: {nparts} parts (at most {MAX_PARTS})")
+
+
+def _check_len(n: int, cap: int) -> None:
+    if n > cap:
+        raise ValueError(f"malformed message: a part of {n} B (at most {cap})")
+
+
+def _recv_msg(sock: socket.socket, alloc=None, max_part: int = MAX_PART) -> List[bytes]:
     (nparts,) = _HDR.unpack(_recv_exact(sock, _HDR.size))
+    _check_nparts(nparts)
     parts = []
     for _ in range(nparts):
         (n,) = _LEN.unpack(_recv_exact(sock, _LEN.size))
+        _check_len(n, max_part)
         parts.append(bytes(_recv_exact(sock, n)) if n < (1 << 16) else _recv_exact(sock, n, alloc))
     return parts
 
@@ -100,8 +118,8 @@ class _RecvState:
     length + bytes, read as far as the socket has data (MSG_DONTWAIT per call, so the socket
     itself stays blocking for the senders on other threads)."""
 
-    def __init__(self, pid: bytes, conn: socket.socket):
-        self.pid, self.conn = pid, conn
+    def __init__(self, pid: bytes, conn: socket.socket, max_part: int = MAX_PART):
+        self.pid, self.conn, self.max_part = pid, conn, max_part
         self._start(_HDR.size, "hdr")
 
     def _start(self, n: int, stage: str) -> None:
@@ -124,6 +142,7 @@ class _RecvState:
                     continue
             if self.stage == "hdr":
                 (self.nparts,) = _HDR.unpack(self.buf)
+                _check_nparts(self.nparts)
                 self.parts = []
                 if self.nparts == 0:
                     done.append(self.parts)
@@ -132,6 +151,7 @@ class _RecvState:
                     self._start(_LEN.size, "len")
             elif self.stage == "len":
                 (m,) = _LEN.unpack(self.buf)
+                _check_len(m, self.max_part)
                 self._start(m, "part")
                 if m == 0:
                     continue
@@ -148,10 +168,10 @@ class _RecvState:
 # per listener accepts and reads every peer, so N workers' messages are handled by one thread
 # instead of N contending for the GIL and the distributor's lock -- 8 echo workers with JPEG-size
 # frames 102-104 k fps against 70-95 k, the JPEG system leg 41.1-41.5 k against 38.0-41.1 k
-# (profiles/r04_reader_ab.txt).  Not the default: a handler runs on that one thread, and where
-# frames travel as socket payloads (no shared-memory ring) a handler's blocking send of a large
-# dispatch can wait on a worker that is itself blocked sending results nobody is reading --
-# test_configs3_mixed_resolution_pull_tcp_payloads hung that way.  Ring deployments only.
+# (profiles/r04_reader_ab.txt).  Safe with payload dispatches since round 5: the distributor
+# sends outside its lock, so a handler blocked in a large send to a worker that is itself busy
+# sending results no longer holds what the result reader needs (the round-4 hang of
+# test_configs3_mixed_resolution_pull_tcp_payloads; tests/test_plumbing.py covers both readers).
 _READER = os.environ.get("VF_TCP_READER", "thread")
 
 
@@ -177,6 +197,7 @@ class _Listener:
         # set_handler: messages are handled on the peer's reader thread as they arrive, instead
         # of queued for a polling thread (one thread hand-off less per message)
         self.handler = None
+        self.max_part = MAX_PART  # largest part a peer may announce (the distributor lowers it)
         self.peers = {}
         self._ids = itertools.count(1)
         self._lock = threading.Lock()
@@ -212,12 +233,15 @@ class _Listener:
                         pid = b"\x00" + next(self._ids).to_bytes(4, "big")
                         with self._lock:
                             self.peers[pid] = (conn, threading.Lock())
-                        sel.register(conn, selectors.EVENT_READ, _RecvState(pid, conn))
+                        sel.register(conn, selectors.EVENT_READ, _RecvState(pid, conn, self.max_part))
                         continue
                     try:
                         msgs = st.feed()
-                    except (ConnectionError, OSError, MemoryError, ValueError, struct.error):
-                        msgs = None  # closed, or a malformed frame (e.g. an absurd length): drop the peer
+                    except (ConnectionError, OSError):
+                        msgs = None  # closed
+                    except Exception as e:  # a malformed frame: drop that peer, keep serving the others
+                        print(f"transport: dropping peer {st.pid.hex()}: {type(e).__name__}: {e}")
+                        msgs = None
                     for msg in msgs or ():
                         h = self.handler
                         if h is not None:
@@ -262,7 +286,7 @@ class _Listener:
     def _read_loop(self, pid, conn):
         try:
             while not self._closed:
-                msg = _recv_msg(conn)
+                msg = _recv_msg(conn, max_part=self.max_part)
                 h = self.handler
                 if h is not None:
                     h(pid, msg)
@@ -270,6 +294,8 @@ class _Listener:
                     self._put((pid, msg))
         except (ConnectionError, OSError):
             pass
+        except Exception as e:  # a malformed frame (absurd length or part count): drop this peer
+            print(f"transport: dropping peer {pid.hex()}: {type(e).__name__}: {e}")
         finally:
             self._gone(pid, conn)
 

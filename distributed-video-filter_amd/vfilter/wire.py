@@ -10,25 +10,31 @@ v0 — the reference's own messages, byte for byte:
 
 v1 — shape-carrying and batched.  Every v1 message starts with a
 tag part that can never be a decimal index string, so a v1 peer can always tell v0 from v1:
-  request  ["READY1", json{"credit": k, "shm": bool, "wid": worker id, "numa": node of its GPU}]
-  dispatch ["FRAMES1", json{"index": [i, ...], "nbytes": [n, ...], "slot": [s | null, ...] | null,
-                             "shape1": [h, w, c] | null  (every frame's)  or  "shape": [[h, w, c] | null, ...],
+  request  ["READY1", json{"credit": k, "shm": bool, "wid": worker id, "numa": node of its GPU,
+                          "wire": 2 (the worker also reads v2 messages)}]
+  dispatch ["FRAMES1", json{"frames": [{"index", "nbytes", "shape", "slot"}, ...],
                              "ring": {"name": shm name, "slot_bytes": n} (if any slot)},
             frame_0, ..., frame_{k-1}]
            (frames whose slot is set travel in the shared-memory ring and have no part)
-  result   ["RESULT1", json{"pid": p, "wid": worker id, "index", "nbytes", "slot", "shape1" | "shape" as
-                            above, "start": t, "end": t (every frame's) or "starts", "ends": [t, ...],
-                            "errors": {"position": message} (frames that failed, if any),
+  result   ["RESULT1", json{"pid": p, "wid": worker id, "frames": [{..., "start", "end", "error"}],
                             "spans": [{"name", "begin", "end", "bytes"}...] (GPU timeline)},
             out_0, ...]
-  Columns, not a list of per-frame objects: one JSON list of ints per field encodes and parses
-  ~4-6x faster than 32 small dicts, and the metadata of a batch is what the distributor's one
-  Python process handles per message (round 3: ~6 us per frame of the control plane's ~17).
-  A decoder also accepts the earlier per-frame form ({"frames": [{"index", ...}, ...]}).
+  This per-frame form is what every earlier build of either side reads.  Decoders also accept
+  round 4's columnar v1 form ({"index": [...], "nbytes": [...], ...} under the same tags).
   "wid" ties a result to the request stream it answers (the distributor tracks every dispatched
   frame per worker, re-queues a lost worker's frames and frees their ring slots); "numa" lets
   the distributor place the worker's ring slice on its GPU's NUMA node.  A result's "nbytes" is
   the RESULT's length (a JPEG differs from its input's).
+
+v2 — binary columns, negotiated: a distributor sends v2 only to a worker whose request says
+"wire": 2, and a worker answers v2 only to a v2 dispatch, so mixed builds keep talking v1.
+  dispatch ["FRAMES2", json{"ring": {...}} (or {}), columns, frame parts of unslotted frames]
+  result   ["RESULT2", json{"pid", "wid", "start", "end" (or "starts", "ends": [...]),
+                            "errors": {"position": message}, "spans": [...]}, columns, parts]
+  columns = one little-endian 40-byte record per frame (``COLS``): index i64, nbytes i64,
+  slot i32 (-1: no slot), ndim i32 (-1: no shape), shape i32[4].  The metadata of a batch is
+  what the distributor handles per message; fixed records cost the native control plane
+  (csrc/vf_dist.cc) no parsing and the Python side one ``np.frombuffer``.
 A worker run with protocol v0 against the reference distributor sends "READY" and reads 2
 parts; this build's distributor answers a bare "READY" with a v0 dispatch.  Either side of the reference can
 therefore be swapped for this build's independently.
@@ -36,13 +42,23 @@ therefore be swapped for this build's independently.
 from __future__ import annotations
 
 import json
+from collections.abc import Sequence as _Seq
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence
+
+import numpy as np
 
 READY_V0 = b"READY"
 READY_V1 = b"READY1"
 FRAMES_V1 = b"FRAMES1"
 RESULT_V1 = b"RESULT1"
+FRAMES_V2 = b"FRAMES2"
+RESULT_V2 = b"RESULT2"
+WIRE = 2  # the newest message form this build reads
+
+# v2 per-frame record (csrc/vf_dist.cc kColsRecord mirrors it)
+COLS = np.dtype([("index", "<i8"), ("nbytes", "<i8"), ("slot", "<i4"), ("ndim", "<i4"), ("shape", "<i4", (4,))])
+assert COLS.itemsize == 40
 
 
 class FrameMeta:
@@ -84,14 +100,16 @@ class Request:
     shm: bool = False
     wid: Optional[str] = None
     numa: Optional[int] = None
+    wire: int = 1  # newest dispatch form the worker reads (v1 requests only)
 
 
 @dataclass
 class Dispatch:
-    metas: List[FrameMeta]
+    metas: Sequence[FrameMeta]
     payloads: List[Optional[bytes]] = field(default_factory=list)  # None where slot is set
     version: int = 1
     ring: Optional[dict] = None  # {"name": shm name, "slot_bytes": n} when any slot is set
+    cols: Optional[np.ndarray] = None  # v2: the COLS records as received
 
 
 @dataclass
@@ -106,32 +124,10 @@ class Result:
     spans: List[dict] = field(default_factory=list)
 
 
-def _columns(metas: Sequence[FrameMeta], timing: bool) -> dict:
-    d = {"index": [m.index for m in metas], "nbytes": [m.nbytes for m in metas]}
-    slots = [m.slot for m in metas]
-    if any(x is not None for x in slots):
-        d["slot"] = slots
-    shapes = [m.shape for m in metas]
-    if all(x == shapes[0] for x in shapes):
-        d["shape1"] = shapes[0] if shapes else None
-    else:
-        d["shape"] = shapes
-    if timing:
-        st, en = [m.start for m in metas], [m.end for m in metas]
-        if st and all(x == st[0] for x in st) and all(x == en[0] for x in en):
-            d["start"], d["end"] = st[0], en[0]
-        else:
-            d["starts"], d["ends"] = st, en
-        errs = {str(i): m.error for i, m in enumerate(metas) if m.error}
-        if errs:
-            d["errors"] = errs
-    return d
-
-
 def _metas(d: dict) -> List[FrameMeta]:
     if "frames" in d:  # the per-frame form
         return [FrameMeta.from_json(x) for x in d["frames"]]
-    idx, nb = d["index"], d["nbytes"]
+    idx, nb = d["index"], d["nbytes"]  # round 4's columnar v1 form
     n = len(idx)
     slots = d.get("slot") or [None] * n
     shapes = d["shape"] if "shape" in d else [d.get("shape1")] * n
@@ -145,10 +141,77 @@ def _metas(d: dict) -> List[FrameMeta]:
     return out
 
 
+# ---- v2 columns -------------------------------------------------------------------------
+
+def v2_shape_ok(shape) -> bool:
+    """True when ``shape`` fits a v2 record (None, or up to 4 int32 dimensions)."""
+    if shape is None:
+        return True
+    try:
+        return len(shape) <= 4 and all(0 <= int(x) < 2 ** 31 for x in shape)
+    except TypeError:
+        return False
+
+
+def columns(metas: Sequence[FrameMeta]) -> np.ndarray:
+    """COLS records of ``metas`` (every shape must pass ``v2_shape_ok``)."""
+    c = np.zeros(len(metas), COLS)
+    c["slot"] = -1
+    c["ndim"] = -1
+    for i, m in enumerate(metas):
+        c["index"][i] = m.index
+        c["nbytes"][i] = m.nbytes
+        if m.slot is not None:
+            c["slot"][i] = m.slot
+        if m.shape is not None:
+            k = len(m.shape)
+            c["ndim"][i] = k
+            c["shape"][i, :k] = m.shape
+    return c
+
+
+def _shape_of(ndim: int, row) -> Optional[List[int]]:
+    return None if ndim < 0 else [int(x) for x in row[:ndim]]
+
+
+class ColumnMetas(_Seq):
+    """The FrameMeta view of v2 records: built per frame on access (a worker that only needs the
+    slots and sizes reads ``cols`` directly)."""
+
+    def __init__(self, cols: np.ndarray, starts=None, ends=None, errors=None):
+        self.cols = cols
+        self._idx = cols["index"].tolist()
+        self._nb = cols["nbytes"].tolist()
+        self._slot = cols["slot"].tolist()
+        self._ndim = cols["ndim"].tolist()
+        self._starts, self._ends, self._errors = starts, ends, errors or {}
+
+    def __len__(self) -> int:
+        return len(self._idx)
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return [self[j] for j in range(*i.indices(len(self)))]
+        if i < 0:
+            i += len(self)
+        s = self._slot[i]
+        return FrameMeta(self._idx[i], self._nb[i], _shape_of(self._ndim[i], self.cols["shape"][i]),
+                         None if s < 0 else s,
+                         self._starts[i] if self._starts is not None else 0.0,
+                         self._ends[i] if self._ends is not None else 0.0, self._errors.get(i))
+
+
+def _cols_from(part) -> np.ndarray:
+    b = memoryview(part).cast("B")
+    if len(b) % COLS.itemsize:
+        raise ValueError(f"v2 columns of {len(b)} B are not whole {COLS.itemsize}-B records")
+    return np.frombuffer(b, COLS)
+
+
 # ---- requests -------------------------------------------------------------------------
 
 def encode_request(credit: int = 1, shm: bool = False, version: int = 1, wid: Optional[str] = None,
-                   numa: Optional[int] = None) -> List[bytes]:
+                   numa: Optional[int] = None, wire: int = 1) -> List[bytes]:
     if version == 0:
         return [READY_V0]
     d = {"credit": int(credit), "shm": bool(shm)}
@@ -156,6 +219,8 @@ def encode_request(credit: int = 1, shm: bool = False, version: int = 1, wid: Op
         d["wid"] = str(wid)
     if numa is not None:
         d["numa"] = int(numa)
+    if wire > 1:
+        d["wire"] = int(wire)
     return [READY_V1, json.dumps(d).encode()]
 
 
@@ -170,7 +235,7 @@ def decode_request(parts: Sequence[bytes]) -> Optional[Request]:
         numa = d.get("numa")
         return Request(version=1, credit=max(1, int(d.get("credit", 1))), shm=bool(d.get("shm", False)),
                        wid=None if d.get("wid") is None else str(d["wid"]),
-                       numa=None if numa is None else int(numa))
+                       numa=None if numa is None else int(numa), wire=int(d.get("wire", 1)))
     return None
 
 
@@ -181,31 +246,29 @@ def encode_dispatch_v0(index: int, frame) -> List:
 
 
 def encode_dispatch(metas: Sequence[FrameMeta], payloads: Sequence, ring: Optional[dict] = None) -> List:
-    d = _columns(metas, False)
+    """v1, per-frame form (readable by every build)."""
+    d = {"frames": [{"index": m.index, "nbytes": m.nbytes, "shape": m.shape, "slot": m.slot} for m in metas]}
     if ring is not None:
         d["ring"] = ring
     head = json.dumps(d).encode()
     return [FRAMES_V1, head] + [p for m, p in zip(metas, payloads) if m.slot is None]
 
 
-def encode_dispatch_columns(index: List[int], nbytes: List[int], slots: Optional[List[Optional[int]]],
-                            shapes: List, payloads: Sequence, ring: Optional[dict] = None) -> List:
-    """``encode_dispatch`` from columns the caller already holds (the distributor's hot path:
-    no FrameMeta per frame); ``payloads`` are the parts of the frames without a slot, in order."""
-    d = {"index": index, "nbytes": nbytes}
-    if slots is not None:
-        d["slot"] = slots
-    if all(x == shapes[0] for x in shapes):
-        d["shape1"] = shapes[0] if shapes else None
-    else:
-        d["shape"] = shapes
-    if ring is not None:
-        d["ring"] = ring
-    return [FRAMES_V1, json.dumps(d).encode()] + list(payloads)
+def encode_dispatch2(cols: np.ndarray, payloads: Sequence, ring: Optional[dict] = None) -> List:
+    """v2: ``cols`` (COLS records) and the parts of the frames without a slot, in order."""
+    head = json.dumps({"ring": ring} if ring is not None else {}).encode()
+    return [FRAMES_V2, head, cols.tobytes()] + list(payloads)
 
 
 def decode_dispatch(parts: Sequence) -> Dispatch:
     tag = bytes(parts[0])
+    if tag == FRAMES_V2:
+        head = json.loads(bytes(parts[1]))
+        cols = _cols_from(parts[2])
+        slots = cols["slot"].tolist()
+        it = iter(parts[3:])
+        payloads = [None if s >= 0 else next(it) for s in slots]
+        return Dispatch(ColumnMetas(cols), payloads, version=2, ring=head.get("ring"), cols=cols)
     if tag != FRAMES_V1:                     # v0: [index, frame]   (worker.py:50-51)
         if len(parts) != 2:
             raise ValueError(f"v0 dispatch must have 2 parts, got {len(parts)}")
@@ -227,8 +290,8 @@ def encode_result_v0(index: int, pid, start: float, end: float, frame) -> List:
 
 def encode_result(pid, metas: Sequence[FrameMeta], payloads: Sequence, spans: Optional[List[dict]] = None,
                   wid: Optional[str] = None) -> List:
-    d = _columns(metas, True)
-    d["pid"] = str(pid)
+    """v1, per-frame form (readable by every build)."""
+    d = {"pid": str(pid), "frames": [m.to_json() for m in metas]}
     if wid is not None:
         d["wid"] = str(wid)
     if spans:
@@ -237,8 +300,41 @@ def encode_result(pid, metas: Sequence[FrameMeta], payloads: Sequence, spans: Op
     return [RESULT_V1, head] + [p for m, p in zip(metas, payloads) if m.slot is None and m.error is None]
 
 
+def encode_result2(pid, cols: np.ndarray, payloads: Sequence, start: float, end: float,
+                   wid: Optional[str] = None, errors: Optional[dict] = None, spans: Optional[List[dict]] = None,
+                   starts: Optional[List[float]] = None, ends: Optional[List[float]] = None) -> List:
+    """v2: ``cols`` as dispatched with each result's own nbytes / slot (-1: the result is a part),
+    ``payloads`` the parts of unslotted, successful frames in order, ``errors`` {position: message}."""
+    d = {"pid": str(pid)}
+    if wid is not None:
+        d["wid"] = str(wid)
+    if starts is not None:
+        d["starts"], d["ends"] = starts, ends
+    else:
+        d["start"], d["end"] = start, end
+    if errors:
+        d["errors"] = {str(k): v for k, v in errors.items()}
+    if spans:
+        d["spans"] = spans
+    return [RESULT_V2, json.dumps(d).encode(), cols.tobytes()] + list(payloads)
+
+
 def decode_result(parts: Sequence) -> Result:
     tag = bytes(parts[0])
+    if tag == RESULT_V2:
+        d = json.loads(bytes(parts[1]))
+        cols = _cols_from(parts[2])
+        n = len(cols)
+        errors = {int(k): v for k, v in (d.get("errors") or {}).items()}
+        if "starts" in d:
+            st, en = [float(x) for x in d["starts"]], [float(x) for x in d["ends"]]
+        else:
+            st, en = [float(d.get("start", 0.0))] * n, [float(d.get("end", 0.0))] * n
+        metas = list(ColumnMetas(cols, st, en, errors))
+        it = iter(parts[3:])
+        payloads = [None if (m.slot is not None or m.error is not None) else next(it) for m in metas]
+        return Result(str(d["pid"]), metas, payloads, version=2, spans=list(d.get("spans", [])),
+                      wid=None if d.get("wid") is None else str(d["wid"]))
     if tag != RESULT_V1:                     # distributor.py:260-264
         if len(parts) != 5:
             raise ValueError(f"v0 result must have 5 parts, got {len(parts)}")

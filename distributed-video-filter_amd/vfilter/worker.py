@@ -217,14 +217,25 @@ class Worker:
         if d.ring is not None:
             ring = self._attach_ring(d.ring["name"], int(d.ring["slot_bytes"]))
         frames, outs = [], []
-        for m, p in zip(d.metas, d.payloads):
-            if m.slot is not None:
-                frames.append(ring.in_view(m.slot, m.nbytes))
-                # a plugin whose results have their own size (JPEG) gets the whole output half
-                outs.append(ring.out_view(m.slot, ring.slot_bytes if self.sized_results else m.nbytes))
-            else:
-                frames.append(p)
-                outs.append(None)
+        if d.cols is not None:  # v2: slots and sizes straight from the records
+            slots, nbs = d.cols["slot"].tolist(), d.cols["nbytes"].tolist()
+            whole = ring.slot_bytes if (ring is not None and self.sized_results) else None
+            for s, nb, p in zip(slots, nbs, d.payloads):
+                if s >= 0:
+                    frames.append(ring.in_view(s, nb))
+                    outs.append(ring.out_view(s, whole or nb))
+                else:
+                    frames.append(p)
+                    outs.append(None)
+        else:
+            for m, p in zip(d.metas, d.payloads):
+                if m.slot is not None:
+                    frames.append(ring.in_view(m.slot, m.nbytes))
+                    # a plugin whose results have their own size (JPEG) gets the whole output half
+                    outs.append(ring.out_view(m.slot, ring.slot_bytes if self.sized_results else m.nbytes))
+                else:
+                    frames.append(p)
+                    outs.append(None)
         if self.verbose:
             print(f"Processing frames {[m.index for m in d.metas]}")
         return d, start_time, self.submit_batch(frames, d.metas, outs), ring, outs
@@ -236,6 +247,8 @@ class Worker:
             return False
         results, spans = got
         end_time = time.time()
+        if d.cols is not None:
+            return self._finish_v2(d, start_time, end_time, results, spans, ring, outs)
         metas, payloads = [], []
         for m, r, o in zip(d.metas, results, outs):
             om = wire.FrameMeta(index=m.index, nbytes=m.nbytes, shape=m.shape, slot=m.slot,
@@ -273,10 +286,59 @@ class Worker:
         self.frames_processed += len(metas)
         return True
 
+    def _finish_v2(self, d, start_time, end_time, results, spans, ring, outs) -> bool:
+        """``_finish_job`` for a v2 dispatch: the result records are the dispatch's, with each
+        result's own length (and slot -1 where it goes back as a part)."""
+        cols = d.cols.copy()
+        slots, nbs = cols["slot"].tolist(), cols["nbytes"].tolist()
+        errors, payloads = {}, []
+        for i, (r, o) in enumerate(zip(results, outs)):
+            if r is o and o.nbytes == nbs[i]:  # written in place, the input's length
+                continue
+            if isinstance(r, Exception):
+                errors[i] = f"{type(r).__name__}: {r}"
+                self.errors += 1
+                print(f"Error in worker: frame {int(cols['index'][i])}: {r}")
+            elif slots[i] < 0:
+                payloads.append(r)
+                cols["nbytes"][i] = memoryview(r).nbytes
+            elif _same_buffer(r, o):
+                if r.nbytes != nbs[i]:  # written in place, with its own length
+                    cols["nbytes"][i] = r.nbytes
+                    cols["ndim"][i] = -1
+            else:  # a result of its own size (JPEG): into the slot when it fits, else a part
+                rb = np.frombuffer(r, dtype=np.uint8)
+                cols["nbytes"][i] = rb.nbytes
+                cols["ndim"][i] = -1
+                if rb.nbytes <= ring.slot_bytes:
+                    ring.out_view(slots[i], rb.nbytes)[:] = rb
+                else:
+                    cols["slot"][i] = -1
+                    payloads.append(r)
+        try:
+            self.collect_socket.send(wire.encode_result2(self.process_id, cols, payloads, start_time, end_time,
+                                                         wid=self.wid, errors=errors, spans=spans))
+        except Exception as e:  # the distributor re-queues frames whose result never arrives
+            self.errors += 1
+            print(f"Error in worker: could not send results {cols['index'].tolist()}: {e}")
+            return True
+        self.frames_processed += len(cols)
+        return True
+
     def _fail_job(self, job, exc: Exception) -> None:
         """A batch whose collection raised: report every frame of it as failed (so an in-order
         consumer does not wait for them) and drop the job."""
         d, start_time = job[0], job[1]
+        if d.cols is not None:
+            msg = f"{type(exc).__name__}: {exc}"
+            self.errors += len(d.cols)
+            print(f"Error in worker: batch {d.cols['index'].tolist()}: {msg}")
+            try:
+                self.collect_socket.send(wire.encode_result2(self.process_id, d.cols, [], start_time, time.time(),
+                                                             wid=self.wid, errors={i: msg for i in range(len(d.cols))}))
+            except Exception as e:  # the distributor re-queues frames whose result never arrives
+                print(f"Error in worker: could not report the failed batch: {e}")
+            return
         metas = [wire.FrameMeta(index=m.index, nbytes=m.nbytes, shape=m.shape, slot=m.slot,
                                 start=start_time, end=time.time(), error=f"{type(exc).__name__}: {exc}")
                  for m in d.metas]
@@ -316,7 +378,8 @@ class Worker:
         while self.running and (max_frames is None or self.frames_processed < max_frames):
             try:
                 while outstanding < self.depth:
-                    self.dealer_socket.send(wire.encode_request(self.batch, shm=True, wid=self.wid, numa=numa))
+                    self.dealer_socket.send(wire.encode_request(self.batch, shm=True, wid=self.wid, numa=numa,
+                                                                       wire=wire.WIRE))
                     outstanding += 1
                 self._collect_jobs(jobs, self.inflight)
                 if len(jobs) >= self.inflight:
@@ -332,7 +395,7 @@ class Worker:
                 except Exception as e:
                     print(f"Error in worker: bad dispatch message: {e}")
                     continue
-                if d.version == 1:
+                if d.version >= 1:
                     outstanding -= 1
                 jobs.append(self._start_job(d, start_time))
             except WorkerFailed:
