@@ -1,18 +1,24 @@
 # Builds the gfx950 C-ABI library (product) and the CPU oracle (test infrastructure).
-#   make            -> libvfilter_hip.so + oracle
+#   make            -> libvfilter_hip.so + libvfdist.so + oracle
 #   make tools      -> tools/tune_invert (kernel variant sweep, run on the GPU box)
 HIPCC     ?= /opt/rocm/bin/hipcc
 ARCH      ?= gfx950
 PKG       := distributed-video-filter_amd
 CSRC      := $(PKG)/csrc
 LIB       := $(PKG)/vfilter/libvfilter_hip.so
+DLIB      := $(PKG)/vfilter/libvfdist.so
+CXX       ?= g++
 HIPFLAGS  := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -fvisibility=hidden -Wall -Iinclude
 LDFLAGS   := -shared -Wl,-rpath,/opt/rocm/lib -Wl,--no-undefined
 
 .PHONY: all lib oracle tools clean exp
 all: lib oracle
 
-lib: $(LIB)
+lib: $(LIB) $(DLIB)
+
+# the distributor's native control plane: host C++ only (no HIP), so plain g++
+$(DLIB): $(CSRC)/vf_dist.cc $(CSRC)/vf_json.h include/vfdist.h
+	$(CXX) -O2 -g -std=c++17 -fPIC -shared -pthread -Wall -Wextra -Iinclude -fvisibility=hidden -Wl,--no-undefined $< -o $@ -lrt
 
 SRCS := $(CSRC)/vf_kernels.hip $(CSRC)/vf_engine.hip $(CSRC)/vf_api.hip $(CSRC)/vf_jpeg_kernels.hip $(CSRC)/vf_jpeg_host.hip
 HDRS := $(CSRC)/vf_internal.h $(CSRC)/vf_stream.h $(CSRC)/vf_host_mem.h $(CSRC)/vf_jpeg.h $(CSRC)/vf_jpeg_types.h $(CSRC)/vf_jpeg_parse.h $(CSRC)/vf_jpeg_codec.h include/vfilter.h
@@ -32,7 +38,7 @@ tools/tune_invert: tools/tune_invert.hip $(CSRC)/vf_kernels.hip $(CSRC)/vf_inter
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -Iinclude -I$(CSRC) tools/tune_invert.hip $(CSRC)/vf_kernels.hip -o $@
 
 clean:
-	rm -f $(LIB) tools/tune_invert tools/pcie_probe
+	rm -f $(LIB) $(DLIB) tools/tune_invert tools/pcie_probe
 	$(MAKE) -C oracle clean
 
 # Experiment libraries (timing A/Bs against the product library; never loaded by the product):

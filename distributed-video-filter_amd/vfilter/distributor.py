@@ -66,6 +66,39 @@ from .sharding import chunk_owner
 from .shm import FrameRing, copy_into
 
 
+class ListBatch:
+    """Released results as columns (``index``, ``nbytes``) over ``get_next_frames``' tuples."""
+
+    def __init__(self, items: list):
+        self._items = items
+        self.index = np.asarray([it[0] for it in items], np.int64)
+        self.nbytes = np.asarray([len(memoryview(it[1]).cast("B")) for it in items], np.int64)
+
+    def __len__(self) -> int:
+        return len(self._items)
+
+    def view(self, i: int):
+        return self._items[i][1]
+
+    def info(self, i: int) -> dict:
+        return self._items[i][2]
+
+    def items(self) -> list:
+        return list(self._items)
+
+
+def _native_serves(args, kw) -> bool:
+    """True when engine="auto" should pick the native control plane for these arguments."""
+    from . import native
+    try:
+        transport = tp.resolve(kw.get("transport", "auto"))
+    except ValueError:
+        return False
+    trace = kw.get("enable_trace_export", args[3] if len(args) > 3 else False)
+    return native.supports(kw.get("policy", "latest"), kw.get("reassembly", "display"), transport,
+                           int(kw.get("ring_slots", 0)), kw.get("ring_layout", "auto"), bool(trace)) is None
+
+
 class _Peer:
     __slots__ = ("pid", "version", "wid", "requests", "frames_sent", "batches_sent", "results", "errors", "home_shard", "shm",
                  "numa", "slice", "queue", "inflight", "quarantine", "batches", "alive", "gone", "evictions",
@@ -115,6 +148,20 @@ class _Slice:
 
 class Distributor:
     QUARANTINE_HOLD = 4  # batch timeouts a shared-ring slot of an evicted worker is held without a disconnect notice
+    engine = "python"
+
+    def __new__(cls, *args, **kw):
+        """``engine="native"`` -- or ``"auto"`` (the default) for the lossless ring deployment it
+        serves -- gives a ``vfilter.native.NativeDistributor``: the same API over the C++ control
+        plane (libvfdist.so).  ``"python"``, and every configuration the native engine does not
+        serve (the reference's latest-wins / display policy, ZeroMQ, socket payloads, trace
+        export), is this class."""
+        if cls is Distributor:
+            eng = kw.get("engine", "auto")
+            if eng == "native" or (eng == "auto" and _native_serves(args, kw)):
+                from .native import NativeDistributor
+                return super().__new__(NativeDistributor)
+        return super().__new__(cls)
 
     def __init__(self, distribute_port: int = 5555, collect_port: int = 5556, frame_delay: int = 5,
                  enable_trace_export: bool = False, *, policy: str = "latest", reassembly: str = "display",
@@ -123,7 +170,7 @@ class Distributor:
                  shard_chunk: int = 1, batch_timeout: float = 30.0, max_attempts: int = 3, batch_wait: float = 0.002,
                  trace_file: str = "webcam_frame_timing.pftrace", verbose: bool = True, zero_copy: bool = False,
                  engine: str = "auto"):
-        if engine not in ("auto", "python"):
+        if engine not in ("auto", "python", "native"):
             raise ValueError("engine must be auto | python | native")
         if zero_copy and (ring_slots < 1 or reassembly != "ordered"):
             raise ValueError("zero_copy needs ring_slots > 0 and reassembly='ordered'")
@@ -826,6 +873,9 @@ class Distributor:
                 other.home_shard = None
             self._shard_home[p.home_shard] = p.pid
             self._rebalance_shards()
+        elif self._orphans:  # frames that found no live worker while it was out
+            self._relane(list(self._orphans))
+            self._orphans.clear()
         self._cv.notify_all()
 
     def _rebalance_shards(self) -> None:
@@ -1381,6 +1431,16 @@ class Distributor:
             while self._released and len(out) < max_n:
                 out.append(self._released.popleft())
         return out
+
+    def get_next_batch(self, max_n: int, timeout: Optional[float] = None) -> "ListBatch":
+        """``get_next_frames`` in the columnar form of the native engine's ``get_next_batch``."""
+        return ListBatch(self.get_next_frames(max_n, timeout))
+
+    def reserve_frames_array(self, nbytes: int, n: int, block: bool = True):
+        """``reserve_frames`` as arrays: (slots, indices)."""
+        slots = self.reserve_frames(nbytes, n, block)
+        idx = [self.reserved_index(s_) for s_ in slots]
+        return np.asarray(slots, np.int32), np.asarray([-1 if i is None else i for i in idx], np.int64)
 
     def release_frame(self, index: int) -> None:
         """zero_copy: return frame ``index``'s ring slot once its result view is consumed."""

@@ -96,7 +96,13 @@ def test_configs2_4k_batch16_eight_way_shard_one_card():
 
 
 @pytest.mark.timeout(180)
-def test_configs3_mixed_resolution_pull_tcp_payloads():
+@pytest.mark.parametrize("reader", ["thread", "select"])
+def test_configs3_mixed_resolution_pull_tcp_payloads(monkeypatch, reader):
+    """Frames as socket payloads (no ring) through the Python engine, in both reader forms: the
+    select form hung here in round 4 (a handler's blocking dispatch send under the distributor's
+    lock); dispatches are now sent outside it."""
+    from vfilter import transport as tp
+    monkeypatch.setattr(tp, "_READER", reader)
     shapes = [(480, 640), (1080, 1920), (2160, 3840)]
     frames = [oracle.synthetic_frame(i, *shapes[i % 3]) for i in range(24)]
     d = Distributor(0, 0, 5, True, policy="pull", reassembly="ordered", queue_size=16, transport="tcp",

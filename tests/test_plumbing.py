@@ -298,11 +298,12 @@ def test_shard_policy_assigns_index_chunks_round_robin():
 
 
 @pytest.mark.timeout(120)
-def test_shared_memory_ring_mixed_resolutions():
+@pytest.mark.parametrize("engine", ["python", "native"])
+def test_shared_memory_ring_mixed_resolutions(engine):
     """configs[3]-shaped stream (mixed sizes) through the shared-memory ring: only slot
     numbers cross the sockets; results are read from the ring's output halves."""
     shapes = [(480, 640), (720, 1280), (1080, 1920)]
-    d = _dist(policy="pull", reassembly="ordered", queue_size=16, ring_slots=12,
+    d = _dist(engine=engine, policy="pull", reassembly="ordered", queue_size=16, ring_slots=12,
               ring_slot_bytes=1080 * 1920 * 3)
     stop, procs = spawn_workers(2, d.distribute_port, d.collect_port, protocol="v1", batch=3)
     try:
@@ -385,10 +386,11 @@ def test_perfetto_trace_reference_schema_plus_gpu_spans(tmp_path, capsys):
 
 
 @pytest.mark.timeout(120)
-def test_zero_copy_reserve_commit_and_release():
+@pytest.mark.parametrize("engine", ["python", "native"])
+def test_zero_copy_reserve_commit_and_release(engine):
     """Ring mode without host copies in the distributor: the producer fills a reserved slot
     in place; the ordered consumer reads the result view and releases the slot."""
-    d = _dist(policy="pull", reassembly="ordered", queue_size=8, ring_slots=6, ring_slot_bytes=64 * 64 * 3,
+    d = _dist(engine=engine, policy="pull", reassembly="ordered", queue_size=8, ring_slots=6, ring_slot_bytes=64 * 64 * 3,
               zero_copy=True)
     stop, procs = spawn_workers(1, d.distribute_port, d.collect_port, protocol="v1", batch=2)
     try:
@@ -415,12 +417,13 @@ def test_zero_copy_reserve_commit_and_release():
 
 
 @pytest.mark.timeout(120)
-def test_concurrent_producers_fill_the_frame_their_reservation_fixed():
+@pytest.mark.parametrize("engine", ["python", "native"])
+def test_concurrent_producers_fill_the_frame_their_reservation_fixed(engine):
     """Several producer threads reserve, fill and commit at once (tools/pipeline_bench.py's
     producer): with per-worker slices the index is fixed at reservation
     (``reserved_index``), so each thread writes the content of that index; the in-order
     consumer sees every index once, with its own content, and every slot comes back."""
-    d = _dist(policy="pull", reassembly="ordered", queue_size=12, ring_slots=6, ring_slot_bytes=48 * 40 * 3,
+    d = _dist(engine=engine, policy="pull", reassembly="ordered", queue_size=12, ring_slots=6, ring_slot_bytes=48 * 40 * 3,
               zero_copy=True)
     stop, procs = spawn_workers(2, d.distribute_port, d.collect_port, protocol="v1", batch=3)
     try:
@@ -490,11 +493,12 @@ def test_busy_worker_request_waits_to_be_filled():
 
 
 @pytest.mark.timeout(120)
-def test_grouped_reserve_commit_get_release():
+@pytest.mark.parametrize("engine", ["python", "native"])
+def test_grouped_reserve_commit_get_release(engine):
     """The grouped forms (reserve_frames / commit_frames / get_next_frames / release_frames)
     behave as their one-frame forms called in a row: every index once, in order, with its
     own content, and every slot back."""
-    d = _dist(policy="pull", reassembly="ordered", queue_size=16, ring_slots=10, ring_slot_bytes=24 * 20 * 3,
+    d = _dist(engine=engine, policy="pull", reassembly="ordered", queue_size=16, ring_slots=10, ring_slot_bytes=24 * 20 * 3,
               zero_copy=True)
     stop, procs = spawn_workers(2, d.distribute_port, d.collect_port, protocol="v1", batch=4)
     try:

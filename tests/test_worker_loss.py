@@ -57,9 +57,10 @@ def _drain(d, frames, bound_s):
 @pytest.mark.timeout(120)
 @pytest.mark.parametrize("policy", ["pull", "shard"])
 @pytest.mark.parametrize("how", ["kill", "stop"])
-def test_losing_one_of_three_workers_mid_stream(policy, how):
+@pytest.mark.parametrize("engine", ["python", "native"])
+def test_losing_one_of_three_workers_mid_stream(policy, how, engine):
     frames = [oracle.synthetic_frame(i % 7, 48, 64) for i in range(150)]
-    d = _dist(policy=policy, reassembly="ordered", queue_size=24, shard_workers=3, shard_chunk=4,
+    d = _dist(engine=engine, policy=policy, reassembly="ordered", queue_size=24, shard_workers=3, shard_chunk=4,
               ring_slots=12, ring_slot_bytes=48 * 64 * 3, batch_timeout=1.5)
     stop, procs = spawn_workers(3, d.distribute_port, d.collect_port, protocol="v1", batch=4, delay=0.004)
     try:
@@ -229,14 +230,15 @@ def test_frame_lost_after_max_attempts():
 
 
 @pytest.mark.timeout(120)
-def test_ring_results_of_their_own_size():
+@pytest.mark.parametrize("engine", ["python", "native"])
+def test_ring_results_of_their_own_size(engine):
     """A plugin whose result size differs from the input's (as a re-encoded JPEG does) through
     the shared-memory ring: smaller and larger results land in the slot's output half when
     they fit, otherwise travel back over the socket; the distributor reads each result's own
     length."""
     shapes = [(4, 4), (17, 33), (64, 64)]   # 48 B (halved), 1,683 B (+7 fits), 12,288 B (+7: no room)
     frames = [oracle.synthetic_frame(i, *shapes[i % 3]) for i in range(30)]
-    d = _dist(policy="pull", reassembly="ordered", queue_size=16, ring_slots=8, ring_slot_bytes=64 * 64 * 3)
+    d = _dist(engine=engine, policy="pull", reassembly="ordered", queue_size=16, ring_slots=8, ring_slot_bytes=64 * 64 * 3)
     stop, procs = spawn_workers(2, d.distribute_port, d.collect_port, protocol="v1", batch=3, kind="resizing")
     try:
         _wait_workers(d, 2)
@@ -261,7 +263,8 @@ def test_per_worker_slices_numa_bound():
     worker); a worker that reports a NUMA node gets its slice bound there."""
     from vfilter import numa
     d = Distributor(0, 0, policy="shard", reassembly="ordered", shard_workers=2, shard_chunk=2, queue_size=16,
-                    ring_slots=4, ring_slot_bytes=4096, transport="tcp", host="127.0.0.1", verbose=False)
+                    ring_slots=4, ring_slot_bytes=4096, transport="tcp", host="127.0.0.1", verbose=False,
+                    engine="python")  # stepped by hand (dispatch_step): the Python engine's loop
     d.running = True
     socks = [tp.DealerEnd("tcp", "127.0.0.1", d.distribute_port) for _ in range(2)]
     try:
@@ -397,7 +400,8 @@ def test_evicted_workers_slots_come_back_after_the_grace_period():
     ``batch_timeout`` they are freed (the ring does not shrink per eviction); a result that
     still arrives later is dropped."""
     d = Distributor(0, 0, policy="pull", reassembly="ordered", queue_size=16, transport="tcp",
-                    host="127.0.0.1", verbose=False, batch_timeout=0.3, ring_slots=4, ring_slot_bytes=64)
+                    host="127.0.0.1", verbose=False, batch_timeout=0.3, ring_slots=4, ring_slot_bytes=64,
+                    engine="python")  # stepped by hand (dispatch_step): the Python engine's loop
     d.running = True
     a, b = _ManualWorker(d, "A"), _ManualWorker(d, "B")
     coll = threading.Thread(target=d.check_inverter_output, daemon=True)

@@ -81,8 +81,12 @@ def main():
     ap.add_argument("--no-copy", action="store_true",
                     help="frames committed in place (no producer copy) and results left in place by the "
                          "workers: the control plane alone, at any --bytes (untouched shm pages cost no memory)")
-    ap.add_argument("--group", type=int, default=1,
-                    help="frames per reserve_frames / commit_frames / get_next_frames / release_frames call")
+    ap.add_argument("--group", type=int, default=32,
+                    help="frames per reserve_frames / commit_frames / get_next_batch / release_frames call")
+    ap.add_argument("--engine", default="auto", choices=("auto", "python", "native"),
+                    help="the distributor's control plane: the C++ engine (libvfdist.so) or the Python one")
+    ap.add_argument("--reader", default="thread", choices=("thread", "select"),
+                    help="Python engine: VF_TCP_READER (reader thread per peer, or one select loop)")
     args = ap.parse_args()
     import multiprocessing as mp
     from vfilter.shm import shm_free_bytes
@@ -93,10 +97,12 @@ def main():
     free = shm_free_bytes()
     if free is not None and not args.no_copy:  # untouched slots (--no-copy) take no memory
         slots = max(2 * args.batch, min(slots, int(free * 0.6) // (2 * slot_bytes * args.workers)))
+    from vfilter import transport as vtp
+    vtp._READER = args.reader
     d = Distributor(0, 0, policy=args.policy, reassembly="ordered", transport="tcp", host="127.0.0.1",
                     queue_size=3 * args.batch * args.workers, ring_slots=slots,
                     ring_slot_bytes=slot_bytes, shard_workers=args.workers, shard_chunk=args.batch,
-                    zero_copy=True, verbose=False)
+                    zero_copy=True, verbose=False, engine=args.engine)
     d.start()
     procs = [mctx.Process(target=run_worker, args=(d.distribute_port, d.collect_port, args.batch, args.inflight,
                                                             args.no_copy),
@@ -113,17 +119,17 @@ def main():
         warm = 4 * args.batch * args.workers
         n = args.frames
 
-        def produce():
+        size_arr = np.asarray(sizes, np.int64)
+
+        def produce():  # a group per call: arrays in, arrays out
             i = 0
             while i < warm + n:
-                got = d.reserve_frames(slot_bytes, min(args.group, warm + n - i))
-                nbs = []
-                for j, slot in enumerate(got):
-                    k = (i + j) % len(sizes)
-                    nbs.append(sizes[k])
-                    if not args.no_copy:
-                        d.frame_view(slot, sizes[k])[:] = srcs[k]
-                d.commit_frames(got, nbs)
+                got, idx = d.reserve_frames_array(slot_bytes, min(args.group, warm + n - i))
+                k = idx % len(sizes)
+                if not args.no_copy:
+                    for slot, kk in zip(got.tolist(), k.tolist()):
+                        d.frame_view(slot, sizes[kk])[:] = srcs[kk]
+                d.commit_frames(got, size_arr[k])
                 i += len(got)
 
         th = threading.Thread(target=produce, daemon=True, name="producer")
@@ -156,6 +162,7 @@ def main():
             threading.Thread(target=sampler, daemon=True).start()
         th.start()
         i = 0
+        calls = 0
         t_start = None
         while i < warm + n:
             if t_start is None and i >= warm:
@@ -163,11 +170,15 @@ def main():
                 ru0 = resource.getrusage(resource.RUSAGE_SELF)
                 th0 = thread_cpu()
                 samples.clear()
-            items = d.get_next_frames(min(args.group, warm + n - i), timeout=60)
-            if not items:
+            got = d.get_next_batch(min(args.group, warm + n - i), timeout=60)
+            if not len(got):
                 raise RuntimeError(f"frame {i} never arrived: {d.ordering_stats()}")
-            d.release_frames([it[0] for it in items])
-            i += len(items)
+            if got.index[0] != i or got.index[-1] != i + len(got) - 1:
+                raise RuntimeError(f"out of order: {got.index[:4]}... at {i}")
+            d.release_frames(got.index)
+            i += len(got)
+            if t_start is not None:
+                calls += 1
         el = time.perf_counter() - t_start
         ru1 = resource.getrusage(resource.RUSAGE_SELF)
         th1 = thread_cpu()
@@ -179,13 +190,15 @@ def main():
         th.join()
         wst = d.ordering_stats()["workers"].values()
         fpb = sum(w_["sent"] for w_ in wst) / max(1, sum(w_["batches"] for w_ in wst))
-        line = {"kind": "distributor_overhead", "frames_per_batch": round(fpb, 1), "workers": args.workers, "policy": args.policy,
+        line = {"kind": "distributor_overhead", "engine": getattr(d, "engine", "python"),
+                "reader": args.reader if getattr(d, "engine", "python") == "python" else "epoll",
+                "group": args.group, "frames_per_batch": round(fpb, 1), "workers": args.workers, "policy": args.policy,
                 "frame_bytes": "mixed 480p/1080p/4K" if args.mixed else args.bytes, "no_copy": args.no_copy,
                 "batch": args.batch, "inflight": args.inflight, "ring_slots_per_worker": slots,
                 "host_cpus": len(os.sched_getaffinity(0)),
                 "frames": n, "fps": round(n / el, 1), "us_per_frame": round(el / n * 1e6, 2),
                 "distributor_cpu_us_per_frame": round(cpu_us, 2), "of_which_sys_us": round(sys_us, 2),
-                "context_switches_per_frame": round(csw, 2),
+                "context_switches_per_frame": round(csw, 2), "frames_per_consumer_call": round(n / max(1, calls), 1),
                 "thread_cpu_us_per_frame": {k: v for k, v in sorted(per_thread.items(), key=lambda kv: -kv[1]) if v > 0.5}}
         print(json.dumps(line), flush=True)
         if args.out:
