@@ -557,6 +557,17 @@ def jpeg_mode(ctx, batch, iters=20):
     h2h_async2x = worker_form(jpgs + jpgs, reps=11)  # the worker CLI's batch of 64 frames
     outs = tj.invert_batch(jpgs)
     passes = stages.pop("sync_passes", 0.0)
+    # the reference app's own frames (webcam_app.py:17,97-111: 512 x 512 crops, PyTurboJPEG's
+    # defaults) and 480p: the rates the distributor legs jpeg_512 / jpeg_480p are compared with
+    points = {}
+    for pname, (ph, pw) in (("512sq", (512, 512)), ("480p", (480, 640))):
+        pj = tj.encode_batch([synthetic_scene(s, ph, pw) for s in range(8)])
+        pj = [pj[i % len(pj)] for i in range(batch)]
+        ctx.jpeg_bench_invert(pj, 85, 1, 0, iters=2)
+        pms, _ = ctx.jpeg_bench_invert(pj, 85, 1, 0, iters=iters)
+        points[pname] = {"frame": [ph, pw, 3], "gpu_resident_fps": round(batch / (pms / 1e3), 1),
+                         "host_to_host_worker_fps": round(batch / worker_form(pj), 1),
+                         "jpeg_bytes_mean": round(sum(len(j) for j in pj) / batch)}
     # hard content: 32 distinct noisy scenes at q95 (long blocks, dense entropy streams)
     from vfilter.synthetic import synthetic_noisy_scene
     hard = tj.encode_batch([synthetic_noisy_scene(s, H, W) for s in range(batch)], quality=95)
@@ -587,6 +598,7 @@ def jpeg_mode(ctx, batch, iters=20):
             "host_to_host_note": "1 call at a time | 2 host threads | the worker's form: 1 thread, 3 batches "
                                  "in flight (vf_jpeg_invert_submit / _wait / _fetch)",
             "jpeg_bytes_mean": round(sum(len(j) for j in jpgs) / batch),
+            "operating_points": points,
             "hard_content": hard_content}, jpgs
 
 
@@ -661,7 +673,22 @@ def cpu_baseline_jpeg(jpgs, seconds):
             "sample": f"{n} x 1080p JPEG frames ({dt:.1f} s) through libjpeg-turbo 2.1.2, 1 thread"}
 
 
-def distributor_leg(nworkers, ngpu, host_gbps=None, pcie_gbps=None, frames_scale=1.0, timeout_s=150):
+def control_plane_rate(nworkers, nbytes, frames=150000, timeout_s=120, **kw):
+    """tools/distributor_overhead.py --no-copy: the distributor's own frames/s at this frame size
+    and worker count (echo workers that leave results in place: no GPU, no host copy)."""
+    cmd = [sys.executable, os.path.join(ROOT, "tools", "distributor_overhead.py"), "--workers", str(nworkers),
+           "--no-copy", "--bytes", str(int(nbytes)), "--frames", str(frames)]
+    for k, v in kw.items():
+        cmd += [f"--{k}", str(v)]
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout_s)
+        line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+        return {k: line[k] for k in ("engine", "fps", "distributor_cpu_us_per_frame", "workers", "frame_bytes")}
+    except Exception as e:  # reported, never raised
+        return {"error": repr(e)[:200]}
+
+
+def distributor_leg(nworkers, ngpu, host_gbps=None, pcie_gbps=None, frames_scale=1.0, timeout_s=150, jpeg=None):
     """BASELINE.json configs[2] and configs[3] at this run's GPU count, host->host through the
     whole fan-out: one Distributor (lossless, in-order reassembly, one NUMA-bound shared-memory
     ring slice per worker) and one `python -m vfilter.inverter` worker process per GPU
@@ -695,7 +722,15 @@ def distributor_leg(nworkers, ngpu, host_gbps=None, pcie_gbps=None, frames_scale
                             "--frames", str(int(12288 * nworkers * frames_scale))], 181876, None),
             # the same deployment on hard content: 32 distinct noisy scenes at q95
             "jpeg_1080p_hard": (["--jpeg", "--content", "hard", "--size", "1080p", "--batch", "32", "--policy",
-                                 "pull", "--frames", str(int(1536 * nworkers * frames_scale))], None, None)}
+                                 "pull", "--frames", str(int(1536 * nworkers * frames_scale))], None, None),
+            # the reference app's own operating point (webcam_app.py:17,97-111: 512 x 512, q85 4:2:2)
+            "jpeg_512": (["--jpeg", "--size", "512sq", "--batch", "32", "--policy", "pull",
+                          "--frames", str(int(32768 * nworkers * frames_scale))], None, None),
+            "jpeg_480p": (["--jpeg", "--size", "480p", "--batch", "32", "--policy", "pull",
+                           "--frames", str(int(32768 * nworkers * frames_scale))], None, None)}
+    worker_form = {"jpeg_1080p": (jpeg or {}).get("host_to_host_worker_fps")}
+    for k_, pn in (("jpeg_512", "512sq"), ("jpeg_480p", "480p")):
+        worker_form[k_] = ((jpeg or {}).get("operating_points") or {}).get(pn, {}).get("host_to_host_worker_fps")
     out = {}
     for name, (extra, fbytes, host_x) in legs.items():
         cmd = [sys.executable, tool, "--workers", str(nworkers), "--gpus", str(ngpu)] + extra
@@ -731,6 +766,12 @@ def distributor_leg(nworkers, ngpu, host_gbps=None, pcie_gbps=None, frames_scale
             leg["ceilings"] = ceil
         else:  # JPEG: bound by the GPU codec, compared with its worker-form rate in jpeg_mode
             leg["jpeg_bytes_in_mean"] = r.get("jpeg_bytes_in_mean")
+            wf = worker_form.get(name)
+            if wf:
+                leg["worker_form_fps_per_gpu"] = wf
+                leg["of_worker_form"] = round(r["fps"] / (min(ngpu, nworkers) * wf), 3)
+            if r.get("jpeg_bytes_in_mean"):  # the distributor's own rate at this frame size beside it
+                leg["control_plane"] = control_plane_rate(nworkers, r["jpeg_bytes_in_mean"])
         leg["wall_s"] = round(time.time() - t0, 1)
         out[name] = leg
     out["note"] = ("host->host through distributor + per-worker shared-memory ring slices + one worker process "
@@ -908,7 +949,8 @@ def main():
             # one worker per rank; workers share GPUs only when rehearsing N ranks on fewer cards
             host_gbps = (cpu or {}).get("host_copy_ceiling", {}).get("GBps_r_plus_w")
             pcie_gbps = (e2e or {}).get("pinned_pipelined_GBps_each_way")
-            fanout = distributor_leg(world, max(1, min(world, torch.cuda.device_count())), host_gbps, pcie_gbps)
+            fanout = distributor_leg(world, max(1, min(world, torch.cuda.device_count())), host_gbps, pcie_gbps,
+                                     jpeg=jpeg if isinstance(jpeg, dict) else None)
             log(f"distributor leg: {fanout}")
         if world > 1:
             dist.barrier(group=cpu_group)  # host-only: the other ranks idle while rank 0 runs its legs

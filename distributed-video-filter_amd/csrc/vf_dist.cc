@@ -35,12 +35,14 @@
 #include <sys/statvfs.h>
 #include <sys/syscall.h>
 #include <sys/uio.h>
+#include <sys/un.h>
 #include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <cstddef>
 #include <cstdio>
 #include <cstring>
 #include <deque>
@@ -59,7 +61,7 @@ namespace {
 constexpr uint32_t kMaxParts = 1u << 16;
 constexpr int64_t kDefaultMaxPart = int64_t(1) << 30;
 constexpr size_t kRecord = 40;  // wire.COLS: index i64, nbytes i64, slot i32, ndim i32, shape i32[4]
-constexpr uint64_t kEvListenD = 1, kEvListenC = 2, kEvWake = 3, kFirstConn = 16;
+constexpr uint64_t kEvListenD = 1, kEvListenC = 2, kEvWake = 3, kEvListenDU = 4, kEvListenCU = 5, kFirstConn = 16;
 
 double mono() {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -286,6 +288,7 @@ struct vfd_engine {
     int64_t max_part = kDefaultMaxPart;
     int seq = 0;
     bool copy_results = false;  // zero_copy=False: results copied out, slots freed on arrival
+    bool unix_too = true;       // also listen on "\0vfd-tcp-<port>" for same-host peers
 
     std::mutex mu;
     std::condition_variable cv_in, cv_out;
@@ -323,7 +326,7 @@ struct vfd_engine {
     std::unordered_map<int64_t, std::unique_ptr<std::vector<uint8_t>>> pending_heap;  // by index, until release
 
     // I/O
-    int epfd = -1, evfd = -1, lfd[2] = {-1, -1};
+    int epfd = -1, evfd = -1, lfd[2] = {-1, -1}, ufd[2] = {-1, -1};
     int port[2] = {0, 0};
     std::thread io;
     std::unordered_map<uint64_t, std::shared_ptr<Conn>> conns;     // under mu
@@ -1438,9 +1441,26 @@ struct vfd_engine {
         return VFD_OK;
     }
 
-    void accept_all(int which) {
+    // Same-host peers: each listener also answers on an abstract Unix socket named after its TCP
+    // port ("\0vfd-tcp-<port>"), which vfilter/transport.py tries first for 127.0.0.1 / localhost
+    // (the stdlib transport's framing over AF_UNIX: no TCP stack per message; VF_TCP_UNIX=0 skips it).
+    void open_unix(int which) {
+        int fd = ::socket(AF_UNIX, SOCK_STREAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
+        if (fd < 0) return;
+        sockaddr_un a{};
+        a.sun_family = AF_UNIX;
+        int n = std::snprintf(a.sun_path + 1, sizeof a.sun_path - 1, "vfd-tcp-%d", port[which]);
+        socklen_t len = (socklen_t)(offsetof(sockaddr_un, sun_path) + 1 + n);
+        if (::bind(fd, (sockaddr*)&a, len) != 0 || ::listen(fd, 128) != 0) {
+            ::close(fd);  // another process holds the name: TCP only
+            return;
+        }
+        ufd[which] = fd;
+    }
+
+    void accept_all(int which, bool unix_side = false) {
         for (;;) {
-            int fd = ::accept4(lfd[which], nullptr, nullptr, SOCK_NONBLOCK | SOCK_CLOEXEC);
+            int fd = ::accept4(unix_side ? ufd[which] : lfd[which], nullptr, nullptr, SOCK_NONBLOCK | SOCK_CLOEXEC);
             if (fd < 0) return;
             int one = 1;
             setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
@@ -1585,6 +1605,10 @@ struct vfd_engine {
                     accept_all(0);
                 } else if (id == kEvListenC) {
                     accept_all(1);
+                } else if (id == kEvListenDU) {
+                    accept_all(0, true);
+                } else if (id == kEvListenCU) {
+                    accept_all(1, true);
                 } else if (id == kEvWake) {
                     uint64_t v;
                     ssize_t r = ::read(evfd, &v, 8);
@@ -1734,8 +1758,10 @@ struct vfd_engine {
         io_conns.clear();
         conns.clear();
         dirty.clear();
-        for (int w = 0; w < 2; ++w)
+        for (int w = 0; w < 2; ++w) {
             if (lfd[w] >= 0) ::close(lfd[w]);
+            if (ufd[w] >= 0) ::close(ufd[w]);
+        }
         if (evfd >= 0) ::close(evfd);
         if (epfd >= 0) ::close(epfd);
         auto kill_lane = [&](Lane& ln) {
@@ -1784,6 +1810,7 @@ int vfd_create(const vfd_config* cfg, vfd_engine** out) {
     e->slot_bytes = (cfg->ring_slot_bytes + 4095) / 4096 * 4096;
     e->max_part = cfg->max_part > 0 ? cfg->max_part : kDefaultMaxPart;
     e->copy_results = cfg->copy_results != 0;
+    e->unix_too = cfg->no_unix == 0;
     e->seq = g_engine_seq.fetch_add(1);
     if (e->cfg.policy == VFD_POLICY_SHARD) {
         e->shard_home.assign((size_t)e->cfg.shard_workers, 0);
@@ -1813,6 +1840,15 @@ int vfd_create(const vfd_config* cfg, vfd_engine** out) {
     epoll_ctl(e->epfd, EPOLL_CTL_ADD, e->lfd[1], &ev);
     ev.data.u64 = kEvWake;
     epoll_ctl(e->epfd, EPOLL_CTL_ADD, e->evfd, &ev);
+    if (e->unix_too) {
+        e->open_unix(0);
+        e->open_unix(1);
+        for (int w = 0; w < 2; ++w) {
+            if (e->ufd[w] < 0) continue;
+            ev.data.u64 = w == 0 ? kEvListenDU : kEvListenCU;
+            epoll_ctl(e->epfd, EPOLL_CTL_ADD, e->ufd[w], &ev);
+        }
+    }
     *out = e;
     return VFD_OK;
 }

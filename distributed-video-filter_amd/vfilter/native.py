@@ -52,7 +52,7 @@ class _Config(ctypes.Structure):
                 ("batch_timeout", ctypes.c_double), ("batch_wait", ctypes.c_double),
                 ("max_attempts", ctypes.c_int), ("verbose", ctypes.c_int), ("distribute_port", ctypes.c_int),
                 ("collect_port", ctypes.c_int), ("host", ctypes.c_char_p), ("max_part", ctypes.c_int64),
-                ("copy_results", ctypes.c_int)]
+                ("copy_results", ctypes.c_int), ("no_unix", ctypes.c_int)]
 
 
 # vfd_frame, as a numpy record (72 bytes, the C struct's natural layout)

@@ -10,6 +10,7 @@ import numpy as np
 
 SIZES = {
     "480sq": (480, 480),    # the reference raw path's hard-coded shape (inverter.py:34)
+    "512sq": (512, 512),    # the reference app's crop (webcam_app.py:17,97-101), JPEG-encoded at :110
     "480p": (480, 640),
     "1080p": (1080, 1920),
     "4k": (2160, 3840),

@@ -179,6 +179,24 @@ def _bind_addr(host: str) -> str:
     return "0.0.0.0" if host in ("*", "", None) else host
 
 
+# VF_TCP_UNIX=1: same-host peers skip the TCP stack.  A listener also answers on the abstract
+# Unix socket "\0vfd-tcp-<port>" (the native engine's listeners always do, csrc/vf_dist.cc), and a
+# connecting side whose host is 127.0.0.1 / localhost tries it before TCP.  Same framing, same
+# roles.  Not the default: a Unix socket buffers ~200 KB where loopback TCP autotunes to MBs, so a
+# sender of large socket payloads blocks sooner (harmless to the distributor, which never sends
+# under its lock, but a behaviour change for payload deployments).
+_UNIX = os.environ.get("VF_TCP_UNIX", "0") == "1" and hasattr(socket, "AF_UNIX")
+
+
+def _unix_name(port: int) -> str:
+    return f"\0vfd-tcp-{port}"
+
+
+def _nodelay(conn: socket.socket) -> None:
+    if conn.family != getattr(socket, "AF_UNIX", None):
+        conn.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+
+
 class _Listener:
     """Accepts peers; every message from any peer lands in one queue as (peer_id, parts).
     ``poll`` sleeps on a condition the readers (and ``wake``) notify: it returns the moment a
@@ -191,6 +209,15 @@ class _Listener:
         self.sock.bind((_bind_addr(host), port))
         self.sock.listen(64)
         self.port = self.sock.getsockname()[1]
+        self.usock = None
+        if _UNIX:
+            try:
+                u = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+                u.bind(_unix_name(self.port))
+                u.listen(64)
+                self.usock = u
+            except OSError:  # the name is taken: TCP only
+                self.usock = None
         self.inbox: "collections.deque[Tuple[bytes, Optional[List[bytes]]]]" = collections.deque()
         self._cond = threading.Condition(threading.Lock())
         self._woken = False
@@ -203,7 +230,9 @@ class _Listener:
         self._lock = threading.Lock()
         self._closed = False
         if _READER == "thread":
-            threading.Thread(target=self._accept_loop, daemon=True).start()
+            threading.Thread(target=self._accept_loop, args=(self.sock,), daemon=True).start()
+            if self.usock is not None:
+                threading.Thread(target=self._accept_loop, args=(self.usock,), daemon=True).start()
         else:
             threading.Thread(target=self._select_loop, daemon=True, name="tcp-select").start()
 
@@ -211,6 +240,8 @@ class _Listener:
         sel = selectors.DefaultSelector()
         try:
             sel.register(self.sock, selectors.EVENT_READ, None)
+            if self.usock is not None:
+                sel.register(self.usock, selectors.EVENT_READ, None)
         except (ValueError, OSError):  # closed before this thread started
             sel.close()
             return
@@ -222,14 +253,14 @@ class _Listener:
                     return
                 for key, _ in events:
                     st = key.data
-                    if st is None:  # the listening socket: a new peer
+                    if st is None:  # a listening socket: a new peer
                         try:
-                            conn, _ = self.sock.accept()
+                            conn, _ = key.fileobj.accept()
                         except OSError:
                             if self._closed:
                                 return
                             continue
-                        conn.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+                        _nodelay(conn)
                         pid = b"\x00" + next(self._ids).to_bytes(4, "big")
                         with self._lock:
                             self.peers[pid] = (conn, threading.Lock())
@@ -271,13 +302,13 @@ class _Listener:
             else:
                 self._put((pid, None))  # disconnect notice (ZeroMQ gives none; see RouterEnd.recv)
 
-    def _accept_loop(self):
+    def _accept_loop(self, lsock):
         while not self._closed:
             try:
-                conn, _ = self.sock.accept()
+                conn, _ = lsock.accept()
             except OSError:
                 return
-            conn.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+            _nodelay(conn)
             pid = b"\x00" + next(self._ids).to_bytes(4, "big")  # ZeroMQ-style 5-byte identity
             with self._lock:
                 self.peers[pid] = (conn, threading.Lock())
@@ -342,10 +373,17 @@ class _Listener:
 
     def close(self):
         self._closed = True
-        try:
-            self.sock.close()
-        except OSError:
-            pass
+        for ls in (self.sock, self.usock):
+            if ls is None:
+                continue
+            try:
+                ls.shutdown(socket.SHUT_RDWR)  # wakes a thread blocked in accept
+            except OSError:
+                pass
+            try:
+                ls.close()
+            except OSError:
+                pass
         with self._lock:
             for conn, _ in self.peers.values():
                 try:
@@ -369,6 +407,14 @@ class _Connection:
             return
         deadline = time.monotonic() + self.connect_timeout
         while True:
+            if _UNIX and self.addr[0] in ("127.0.0.1", "localhost"):
+                u = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+                try:
+                    u.connect(_unix_name(self.addr[1]))
+                    self.sock = u
+                    return
+                except OSError:  # no such listener on this host: TCP
+                    u.close()
             try:
                 s = socket.create_connection(self.addr, timeout=2.0)
                 s.settimeout(None)

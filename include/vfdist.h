@@ -59,6 +59,9 @@ typedef struct vfd_config {
     int copy_results;          /* 1 (zero_copy=False): a result is copied out of its slot on
                                   arrival and the slot freed at once; 0: the result is read in
                                   place and its slot held until vfd_release */
+    int no_unix;               /* 0: each listener also answers on the abstract Unix socket
+                                  "\0vfd-tcp-<port>", which same-host workers try first
+                                  (vfilter/transport.py); 1: TCP only */
 } vfd_config;
 
 /* One released result, in index order (vfd_next). */

@@ -446,6 +446,28 @@ def test_bench_operating_points_on_the_auto_path(tj, monkeypatch, kind):
     assert [bytes(g) for g in tj.invert_batch_result(t2)] == want[::-1]
 
 
+@pytest.mark.parametrize("hw", [(512, 512), (480, 640)])
+def test_reference_deployment_operating_points(tj, monkeypatch, hw):
+    """the reference app's own frames -- webcam_app.py:17,97-111 crops to 512 x 512
+    and encodes with PyTurboJPEG's defaults (q85, 4:2:2, BGR) -- and 480p, in batches of 32
+    (bench distributor.jpeg_512 / jpeg_480p), on the auto path: the synchronous call and the
+    worker's form (three batches in flight, results scattered into caller buffers), byte for
+    byte against the libjpeg-turbo-pinned oracle."""
+    from vfilter.synthetic import synthetic_scene
+    for var in ("VF_JPEG_SYNC", "VF_JPEG_SYNC_G", "VF_JPEG_SYNC_QUEUED", "VF_JPEG_WRITE4", "VF_JPEG_FUSE",
+                "VF_JPEG_FUSE_IDCT", "VF_JPEG_CHUNKS"):
+        monkeypatch.delenv(var, raising=False)
+    jpgs = [J.encode(synthetic_scene(s, *hw), 85, J.TJPF_BGR, J.TJSAMP_422) for s in range(8)]
+    jpgs = [jpgs[i % 8] for i in range(32)]
+    want = [J.invert_jpeg(j) for j in jpgs]
+    assert [bytes(g) for g in tj.invert_batch(jpgs)] == want
+    tickets = [tj.invert_batch_submit(jpgs[k:] + jpgs[:k]) for k in (0, 5, 11)]
+    for k, t in zip((0, 5, 11), tickets):
+        outs = [np.zeros(2 * len(j), np.uint8) for j in jpgs]
+        got = tj.invert_batch_result_into(t, outs)
+        assert [bytes(g) for g in got] == want[k:] + want[:k], (hw, k)
+
+
 @pytest.mark.parametrize("flags", [0, TJFLAG_FASTUPSAMPLE])
 def test_fused_idct_colour_strip_edges(tj, monkeypatch, flags):
     """k_idct_color422 (the invert path's one-pass IDCT + colour for standard 4:2:2 input):
