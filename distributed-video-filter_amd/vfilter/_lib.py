@@ -377,6 +377,20 @@ class Context:
         self._check(self._lib.vf_invert_frames_async(self._ctx, sa, da, na, n, ctypes.byref(t)))
         return t.value
 
+    def invert_frames_async_addrs(self, src_addrs: np.ndarray, dst_addrs: np.ndarray, nbytes: np.ndarray) -> int:
+        """``invert_frames_async`` from address arrays (a worker's ring slots: base + slot
+        arithmetic, no ndarray per frame; ``ndarray.ctypes`` costs ~2.5 us an access)."""
+        sa = np.ascontiguousarray(src_addrs, np.uint64)
+        da = np.ascontiguousarray(dst_addrs, np.uint64)
+        na = np.ascontiguousarray(nbytes, np.uint64)
+        n = len(sa)
+        if not (len(da) == n == len(na)):
+            raise ValueError("srcs, dsts and nbytes must have the same length")
+        t = ctypes.c_uint64(0)
+        self._check(self._lib.vf_invert_frames_async(self._ctx, sa.ctypes.data, da.ctypes.data, na.ctypes.data, n,
+                                                     ctypes.byref(t)))
+        return t.value
+
     def wait(self, ticket: int) -> float:
         """Block until ``ticket`` completes; returns its device time in ms (-1 if unknown)."""
         ms = ctypes.c_float(-1.0)
@@ -600,6 +614,54 @@ class Context:
         off = (ctypes.c_size_t * n)()
         self._check(self._lib.vf_jpeg_invert_fetch(self._ctx, ticket, buf.ctypes.data, buf.nbytes, sz, off))
         return [r if r is not None else buf[off[i]:off[i] + sz[i]] for i, r in enumerate(res)]
+
+    def jpeg_invert_submit_addrs(self, addrs: np.ndarray, sizes: np.ndarray, quality: int, subsamp: int,
+                                 flags: int = 0) -> int:
+        """``jpeg_invert_submit`` from address / size arrays (the JPEGs in a worker's ring slots)."""
+        a = np.ascontiguousarray(addrs, np.uint64)
+        z = np.ascontiguousarray(sizes, np.uint64)
+        n = len(a)
+        if n == 0 or len(z) != n:
+            raise ValueError("jpeg_invert_submit_addrs: empty batch or sizes of another length")
+        t = ctypes.c_uint64(0)
+        self._check(self._lib.vf_jpeg_invert_submit(self._ctx, a.ctypes.data, z.ctypes.data, n, quality, subsamp,
+                                                    flags, ctypes.byref(t)))
+        self.__dict__.setdefault("_jpeg_n", {})[t.value] = n
+        return t.value
+
+    def jpeg_invert_result_into_addrs(self, ticket: int, out_addrs: np.ndarray, cap: int):
+        """``jpeg_invert_result_into`` for outputs given as addresses of ``cap`` writable bytes each
+        (the output halves of ring slots): returns (sizes int64, {i: JPEG} for the frames that did
+        not fit and come back in a fresh buffer)."""
+        n = self.__dict__.get("_jpeg_n", {}).pop(ticket, None)
+        if n is None:
+            raise VFilterError(f"unknown JPEG ticket {ticket}", VF_E_INVALID)
+        oa = np.ascontiguousarray(out_addrs, np.uint64)
+        if len(oa) != n:
+            self.__dict__["_jpeg_n"][ticket] = n
+            raise ValueError(f"jpeg_invert_result_into_addrs: {len(oa)} outputs for a batch of {n}")
+        total = ctypes.c_size_t(0)
+        self._check(self._lib.vf_jpeg_invert_wait(self._ctx, ticket, ctypes.byref(total)))
+        caps = np.full(n, cap, np.uint64)
+        sz = np.zeros(n, np.uint64)
+        placed = ctypes.c_int(0)
+        try:
+            self._check(self._lib.vf_jpeg_invert_scatter(self._ctx, ticket, oa.ctypes.data, caps.ctypes.data,
+                                                         sz.ctypes.data, ctypes.byref(placed)))
+        except Exception:
+            self._lib.vf_jpeg_invert_fetch(self._ctx, ticket, None, 0, None, None)
+            raise
+        over = {}
+        if placed.value == n:
+            self._check(self._lib.vf_jpeg_invert_fetch(self._ctx, ticket, None, 0, None, None))
+        else:
+            buf = np.empty(max(1, total.value), np.uint8)
+            off = (ctypes.c_size_t * n)()
+            sz2 = (ctypes.c_size_t * n)()
+            self._check(self._lib.vf_jpeg_invert_fetch(self._ctx, ticket, buf.ctypes.data, buf.nbytes, sz2, off))
+            for i in np.flatnonzero(sz > caps).tolist():
+                over[i] = buf[off[i]:off[i] + sz2[i]]
+        return sz.astype(np.int64), over
 
     def jpeg_invert_release(self, ticket: int) -> None:
         """Drop a submitted batch without reading it."""

@@ -109,6 +109,17 @@ class TurboJPEG:
         One host thread can keep several batches in flight (each holds its own codec)."""
         return self.ctx.jpeg_invert_submit(list(jpeg_bufs), quality, jpeg_subsample, self._enc_flags(flags, quality))
 
+    def invert_batch_submit_addrs(self, addrs, sizes, quality: int = 85, jpeg_subsample: int = TJSAMP_422,
+                                  flags: int = 0) -> int:
+        """``invert_batch_submit`` for JPEGs given by address and size arrays (a worker's ring
+        slots; the memory stays valid until the result is collected)."""
+        return self.ctx.jpeg_invert_submit_addrs(addrs, sizes, quality, jpeg_subsample, self._enc_flags(flags, quality))
+
+    def invert_batch_result_into_addrs(self, ticket: int, out_addrs, cap: int):
+        """(sizes, {i: JPEG that did not fit}): each result written at ``out_addrs[i]`` (``cap``
+        writable bytes each) when it fits there."""
+        return self.ctx.jpeg_invert_result_into_addrs(ticket, out_addrs, cap)
+
     def invert_batch_ready(self, ticket: int) -> bool:
         return self.ctx.jpeg_invert_ready(ticket)
 

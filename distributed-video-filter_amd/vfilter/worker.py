@@ -46,6 +46,39 @@ def _same_buffer(r, o) -> bool:
     return r.nbytes <= o.nbytes and (r.nbytes == 0 or r.ctypes.data == o.ctypes.data)
 
 
+class RingResults:
+    """Results of a batch started from ring addresses (``Worker.submit_ring_batch``): every
+    frame's result was written at the start of its slot's output half, ``nbytes`` long (an int64
+    array), except the frames in ``errors`` ({position: message}) and in ``overflow``
+    ({position: bytes-like}: results larger than the half, sent back as socket parts)."""
+    __slots__ = ("nbytes", "errors", "overflow")
+
+    def __init__(self, nbytes, errors=None, overflow=None):
+        self.nbytes = np.asarray(nbytes, np.int64)
+        self.errors = errors or {}
+        self.overflow = overflow or {}
+
+
+def ring_results(results: Sequence, outs: Sequence) -> RingResults:
+    """``RingResults`` of per-frame results against their ring output views (a plugin's per-frame
+    fallback inside a ring batch)."""
+    nb = np.zeros(len(results), np.int64)
+    errors, over = {}, {}
+    for i, (r, o) in enumerate(zip(results, outs)):
+        if isinstance(r, Exception):
+            errors[i] = f"{type(r).__name__}: {r}"
+        elif _same_buffer(r, o):
+            nb[i] = r.nbytes
+        else:
+            rb = np.frombuffer(r, dtype=np.uint8)
+            nb[i] = rb.nbytes
+            if rb.nbytes <= o.nbytes:
+                o[:rb.nbytes] = rb
+            else:
+                over[i] = r
+    return RingResults(nb, errors, over)
+
+
 class Worker:
     # True for a plugin whose results have their own size (a re-encoded JPEG): ring frames then
     # get their slot's whole output half to write into, and the result carries its length
@@ -197,6 +230,13 @@ class Worker:
             return self._ring
 
     # -- asynchronous batch hooks (a GPU plugin overrides these) ----------------------------
+    def submit_ring_batch(self, ring: FrameRing, cols: np.ndarray):
+        """Hook: start a v2 batch whose every frame is in ``ring`` from its records (``cols``:
+        wire.COLS, slots and sizes as arrays) and return a handle whose ``poll_batch`` results
+        are a ``RingResults`` -- no Python object per frame (a GPU plugin computes the slots'
+        addresses from the ring's base).  None: use ``submit_batch`` on per-frame views."""
+        return None
+
     def submit_batch(self, frames: Sequence, metas: Sequence[wire.FrameMeta], outs: Sequence):
         """Start a batch and return a handle for ``poll_batch``.  Default: run
         ``process_batch`` now (synchronously)."""
@@ -217,6 +257,10 @@ class Worker:
         if d.ring is not None:
             ring = self._attach_ring(d.ring["name"], int(d.ring["slot_bytes"]))
         frames, outs = [], []
+        if d.cols is not None and ring is not None and len(d.cols) and bool((d.cols["slot"] >= 0).all()):
+            h = self.submit_ring_batch(ring, d.cols)
+            if h is not None:  # the whole batch from addresses
+                return d, start_time, h, ring, None
         if d.cols is not None:  # v2: slots and sizes straight from the records
             slots, nbs = d.cols["slot"].tolist(), d.cols["nbytes"].tolist()
             whole = ring.slot_bytes if (ring is not None and self.sized_results) else None
@@ -247,6 +291,8 @@ class Worker:
             return False
         results, spans = got
         end_time = time.time()
+        if isinstance(results, RingResults):
+            return self._finish_ring(d, start_time, end_time, results, spans)
         if d.cols is not None:
             return self._finish_v2(d, start_time, end_time, results, spans, ring, outs)
         metas, payloads = [], []
@@ -284,6 +330,31 @@ class Worker:
             print(f"Error in worker: could not send results {[m.index for m in metas]}: {e}")
             return True
         self.frames_processed += len(metas)
+        return True
+
+    def _finish_ring(self, d, start_time, end_time, res: RingResults, spans) -> bool:
+        """``_finish_job`` for a batch started by ``submit_ring_batch``: the records as dispatched
+        with each result's length, array operations only (plus the rare error / overflow)."""
+        cols = d.cols.copy()
+        changed = res.nbytes != cols["nbytes"]
+        cols["nbytes"] = res.nbytes
+        cols["ndim"][changed] = -1  # a result of its own size has no shape
+        payloads = []
+        for i in sorted(res.overflow):
+            if i not in res.errors:
+                cols["slot"][i] = -1
+                payloads.append(res.overflow[i])
+        for i, msg in res.errors.items():
+            self.errors += 1
+            print(f"Error in worker: frame {int(cols['index'][i])}: {msg}")
+        try:
+            self.collect_socket.send(wire.encode_result2(self.process_id, cols, payloads, start_time, end_time,
+                                                         wid=self.wid, errors=res.errors, spans=spans))
+        except Exception as e:  # the distributor re-queues frames whose result never arrives
+            self.errors += 1
+            print(f"Error in worker: could not send results {cols['index'].tolist()}: {e}")
+            return True
+        self.frames_processed += len(cols)
         return True
 
     def _finish_v2(self, d, start_time, end_time, results, spans, ring, outs) -> bool:

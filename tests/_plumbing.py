@@ -45,6 +45,36 @@ class ResizingWorker(OracleWorker):
         return x[: len(x) // 2] if len(x) <= 64 else x + b"trailer"
 
 
+class _RingMixin:
+    """The worker's ring form (Worker.submit_ring_batch): the whole batch from its records,
+    results landing in the slots' output halves (RingResults), as the GPU plugin's do."""
+
+    def submit_ring_batch(self, ring, cols):
+        from vfilter.worker import ring_results
+        slots, nbs = cols["slot"].tolist(), cols["nbytes"].tolist()
+        outs = [ring.out_view(s_, ring.slot_bytes) for s_ in slots]
+        results = []
+        for s_, n_ in zip(slots, nbs):
+            try:
+                results.append(self(ring.in_view(s_, n_)))
+            except Exception as e:
+                results.append(e)
+        return ("ring", ring_results(results, outs))
+
+    def poll_batch(self, handle, block):
+        if handle[0] == "ring":
+            return handle[1], []
+        return super().poll_batch(handle, block)
+
+
+class RingOracleWorker(_RingMixin, OracleWorker):
+    pass
+
+
+class RingResizingWorker(_RingMixin, ResizingWorker):
+    pass
+
+
 def _watch(stop_event, worker):
     stop_event.wait()
     worker.stop()
@@ -58,7 +88,8 @@ def run_worker(dport, cport, stop_event, protocol="v1", batch=4, transport="tcp"
                            install_signal_handlers=False, batch=batch, protocol=protocol,
                            transport=transport)
     else:
-        cls = ResizingWorker if kind == "resizing" else OracleWorker
+        cls = {"resizing": ResizingWorker, "ring": RingOracleWorker,
+               "ring_resizing": RingResizingWorker}.get(kind, OracleWorker)
         w = cls("127.0.0.1", dport, cport, batch=batch, protocol=protocol, transport=transport, inflight=inflight)
         w.delay = delay
         w.batch_delay = batch_delay

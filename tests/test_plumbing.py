@@ -298,14 +298,14 @@ def test_shard_policy_assigns_index_chunks_round_robin():
 
 
 @pytest.mark.timeout(120)
-@pytest.mark.parametrize("engine", ["python", "native"])
-def test_shared_memory_ring_mixed_resolutions(engine):
+@pytest.mark.parametrize("engine,kind", [("python", "oracle"), ("native", "oracle"), ("native", "ring")])
+def test_shared_memory_ring_mixed_resolutions(engine, kind):
     """configs[3]-shaped stream (mixed sizes) through the shared-memory ring: only slot
     numbers cross the sockets; results are read from the ring's output halves."""
     shapes = [(480, 640), (720, 1280), (1080, 1920)]
     d = _dist(engine=engine, policy="pull", reassembly="ordered", queue_size=16, ring_slots=12,
               ring_slot_bytes=1080 * 1920 * 3)
-    stop, procs = spawn_workers(2, d.distribute_port, d.collect_port, protocol="v1", batch=3)
+    stop, procs = spawn_workers(2, d.distribute_port, d.collect_port, protocol="v1", batch=3, kind=kind)
     try:
         frames = _frames(30, shapes)
         th = threading.Thread(target=lambda: [d.add_frame_for_distribution(f) for f in frames])

@@ -230,8 +230,8 @@ def test_frame_lost_after_max_attempts():
 
 
 @pytest.mark.timeout(120)
-@pytest.mark.parametrize("engine", ["python", "native"])
-def test_ring_results_of_their_own_size(engine):
+@pytest.mark.parametrize("engine,kind", [("python", "resizing"), ("native", "resizing"), ("native", "ring_resizing")])
+def test_ring_results_of_their_own_size(engine, kind):
     """A plugin whose result size differs from the input's (as a re-encoded JPEG does) through
     the shared-memory ring: smaller and larger results land in the slot's output half when
     they fit, otherwise travel back over the socket; the distributor reads each result's own
@@ -239,7 +239,7 @@ def test_ring_results_of_their_own_size(engine):
     shapes = [(4, 4), (17, 33), (64, 64)]   # 48 B (halved), 1,683 B (+7 fits), 12,288 B (+7: no room)
     frames = [oracle.synthetic_frame(i, *shapes[i % 3]) for i in range(30)]
     d = _dist(engine=engine, policy="pull", reassembly="ordered", queue_size=16, ring_slots=8, ring_slot_bytes=64 * 64 * 3)
-    stop, procs = spawn_workers(2, d.distribute_port, d.collect_port, protocol="v1", batch=3, kind="resizing")
+    stop, procs = spawn_workers(2, d.distribute_port, d.collect_port, protocol="v1", batch=3, kind=kind)
     try:
         _wait_workers(d, 2)
         th = threading.Thread(target=lambda: [d.add_frame_for_distribution(f) for f in frames], daemon=True)
