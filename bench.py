@@ -27,7 +27,10 @@ Prints ONE JSON line on rank 0 (contract in the task statement), including
                 a worker process runs it), per-stage roofline, libjpeg-turbo on 1 core beside it.
   distributor   configs[2] (4K, batch 16, frame-index shards, in-order reassembly) and configs[3]
                 (mixed 480p/1080p/4K stream, ordering overhead) through the distributor with one
-                worker process per GPU of this run: host->host frames/s, never the headline.
+                worker process per GPU of this run, and the JPEG deployment (1080p scenes and hard
+                content, the reference app's 512 x 512 frames, 480p) with each leg's worker-form
+                rate and the distributor's own control-plane rate beside it: host->host frames/s,
+                never the headline.
 """
 from __future__ import annotations
 

@@ -579,7 +579,7 @@ int Codec::run_decode(int bgr, bool invert, std::string *err) {
   const int sync_g = [] {  // read per call: tests switch it inside one process
     const char *v = std::getenv("VF_JPEG_SYNC_G");
     const int g = v ? std::atoi(v) : 4;
-    return g == 0 || g == 1 || g == 2 || g == 4 || g == 8 ? g : 4;
+    return g >= 0 && g <= 4 ? g : g == 8 ? 8 : 4;
   }();
   if (flag && sync_g > 0) {
     // VF_JPEG_SYNC_QUEUED = 1..kQueuedPasses (tests): fewer queued passes, so check_decode

@@ -843,11 +843,18 @@ __global__ __launch_bounds__(256) void k_syncg(const DecSeg *__restrict__ sg, co
   constexpr uint32_t T = syncg_threads(G),
                      kWords = kSyncgStage ? kWarmWords + T * G * (kSubBits / 32) + kSpecPadWords : 1;
   __shared__ SyncTab32 tabs[6];
-  __shared__ uint64_t s_exit[T];
+  // exits relative to the workgroup's first bit in 32 bits, (pos - wbit) << 10 | z << 4 | c (as
+  // k_spec's): 1 KB less LDS, which with G = 3 makes 4 workgroups per CU fit (40.7 KB)
+  __shared__ uint32_t s_exit[T];
   __shared__ uint32_t s_w[kWords];
   const DecSeg S = sg[blockIdx.y];  // by value: held in scalar registers
   const DecFrame &F = fr[S.frame];
   if (blockIdx.x * T * G >= S.nsub_max) return;
+  const uint32_t wbit = blockIdx.x * T * G * kSubBits;
+  const auto rel = [wbit](uint64_t st) {
+    return (((uint32_t)(st >> 16) - wbit) << 10) | (((uint32_t)st >> 4) & 0x3F0u) | ((uint32_t)st & 15u);
+  };
+  const auto absl = [wbit](uint32_t r) { return pack_state((r >> 10) + wbit, (r >> 4) & 63u, r & 15u); };
   if (pass > 0 && changed[pass - 1] == 0) return;  // converged (workgroup-uniform)
   const uint32_t *gw = reinterpret_cast<const uint32_t *>(us + S.us_off);
   // staged from kWarmWords before the workgroup's first span (the warm-up of its first thread);
@@ -897,11 +904,11 @@ __global__ __launch_bounds__(256) void k_syncg(const DecSeg *__restrict__ sg, co
                    : sync_span<false>(words, woff, entry, i0, ng, nsub, nbits, gi0, last, exits, cnts, ck, ckrem, hg, tabs);
       used[gi0] = entry;
     }
-    s_exit[t] = last;
+    s_exit[t] = live ? rel(last) : 0u;
     __syncthreads();
     need = false;
     if (live && t > 0) {
-      const uint64_t e = s_exit[t - 1];
+      const uint64_t e = absl(s_exit[t - 1]);
       if (e != entry) {
         entry = e;
         need = true;
@@ -3203,6 +3210,7 @@ hipError_t dec_syncg(int G, const DecSeg *__restrict__ sg, const DecFrame *__res
   }
   VF_SYNCG(1)
   VF_SYNCG(2)
+  VF_SYNCG(3)
   VF_SYNCG(4)
   VF_SYNCG(8)
 #undef VF_SYNCG

@@ -250,7 +250,7 @@ def _span_sync_batch(quality=95, subsamp=J.TJSAMP_422):
     return [J.encode(im, quality, J.TJPF_BGR, subsamp) for im in imgs]
 
 
-@pytest.mark.parametrize("g,warm", [("0", "0"), ("1", "0"), ("2", "0"), ("4", "0"), ("8", "0"), ("4", "256"),
+@pytest.mark.parametrize("g,warm", [("0", "0"), ("1", "0"), ("2", "0"), ("3", "0"), ("4", "0"), ("8", "0"), ("3", "2048"), ("4", "256"),
                                     ("4", "2048"), ("8", "4096"), ("1", "1000")])
 def test_span_sync_widths(tj, monkeypatch, g, warm):
     """The pass-based sync with G subsequences per thread (k_syncg: records updated in place,
