@@ -1590,11 +1590,13 @@ struct vfd_engine {
         double next_check = 0.0;
         while (!stopping.load()) {
             int timeout_ms;
+            bool fill_due;  // a busy worker's request waits for its batch to fill (read under mu)
             {
                 std::lock_guard<std::mutex> lk(mu);
                 double now = mono();
                 double t = cfg.batch_timeout > 0 ? 0.002 : 0.05;
-                if (fill_deadline > 0.0) t = std::min(t, std::max(0.0, fill_deadline - now));
+                fill_due = fill_deadline > 0.0;
+                if (fill_due) t = std::min(t, std::max(0.0, fill_deadline - now));
                 timeout_ms = (int)(t * 1000.0 + 0.999);
             }
             int n = epoll_wait(epfd, evs, 64, timeout_ms);
@@ -1622,7 +1624,7 @@ struct vfd_engine {
                 }
             }
             double now = mono();
-            if (now >= next_check || fill_deadline > 0.0) {
+            if (now >= next_check || fill_due) {
                 std::unique_lock<std::mutex> lk(mu);
                 check_deadlines(now);
                 serve_waiting();

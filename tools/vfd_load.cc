@@ -100,6 +100,11 @@ static bool recv_parts(int fd, std::vector<std::string>& parts) {
 
 int main(int argc, char** argv) {
     int workers = 8, batch = 32, group = 32, depth = 4;
+    // --chaos 1: worker 0 closes its connections after 40 batches (a crash), worker 1 stops
+    // answering after 60 (a hang; the engine's batch deadline evicts it): the survivors must
+    // still deliver every frame in order (re-queue, quarantine, shard-free pull policy)
+    bool chaos = false;
+    double timeout_s = 0.2;  // --chaos: the batch deadline that evicts the hung worker
     long long frames = 1000000;
     long long bytes = 181876;
     for (int i = 1; i + 1 < argc; i += 2) {
@@ -111,6 +116,8 @@ int main(int argc, char** argv) {
         else if (k == "--frames") frames = atoll(argv[i + 1]);
         else if (k == "--bytes") bytes = atoll(argv[i + 1]);
         else if (k == "--unix") g_unix = atoi(argv[i + 1]) != 0;
+        else if (k == "--chaos") chaos = atoi(argv[i + 1]) != 0;
+        else if (k == "--timeout") timeout_s = atof(argv[i + 1]);
     }
     vfd_config cfg{};
     cfg.policy = VFD_POLICY_PULL;
@@ -119,7 +126,7 @@ int main(int argc, char** argv) {
     cfg.queue_size = 3 * batch * workers;
     cfg.ring_slots = 4 * batch;
     cfg.ring_slot_bytes = bytes;
-    cfg.batch_timeout = 30.0;
+    cfg.batch_timeout = chaos ? timeout_s : 30.0;
     cfg.batch_wait = 0.002;
     cfg.max_attempts = 3;
     cfg.host = "127.0.0.1";
@@ -140,9 +147,17 @@ int main(int argc, char** argv) {
             snprintf(head, sizeof head, "{\"pid\": \"%d\", \"wid\": \"L%d\", \"start\": 0.0, \"end\": 0.0}", 1000 + w, w);
             std::string rhead = head;
             std::vector<std::string> parts;
+            int nb = 0;
             while (!stop.load() && recv_parts(d, parts)) {
                 if (parts.size() < 3 || parts[0] != "FRAMES2") continue;
-                send_parts(c, {"RESULT2", rhead, parts[2]});
+                ++nb;
+                if (chaos && w == 0 && nb == 40) break;  // crash: both connections close
+                if (chaos && w == 1 && nb >= 60) continue;  // hang: keeps reading, never answers
+                // echo: the records as dispatched; frames sent as parts (slot -1: a re-queued frame
+                // that found no room in this worker's slice) go back as parts
+                std::vector<std::string> res = {"RESULT2", rhead, parts[2]};
+                for (size_t k = 3; k < parts.size(); ++k) res.push_back(parts[k]);
+                send_parts(c, res);
                 send_parts(d, req);
             }
             close(d);
@@ -176,12 +191,12 @@ int main(int argc, char** argv) {
         int k = vfd_next(e, 256, 10.0, out.data());
         if (k <= 0) {
             fprintf(stderr, "stalled at %lld\n", got);
-            return 2;
+            _exit(2);
         }
         for (int j = 0; j < k; ++j) {
             if (out[j].index != got + j) {
                 fprintf(stderr, "order: %lld at %lld\n", (long long)out[j].index, got + j);
-                return 3;
+                _exit(3);
             }
             rel[j] = out[j].index;
         }
@@ -193,6 +208,10 @@ int main(int argc, char** argv) {
     prod.join();
     stop.store(true);
     vfd_counters(e, cnt, VFD_C_COUNT);
+    if (chaos)
+        printf("{\"chaos\": true, \"evictions\": %lld, \"requeued\": %lld, \"lost\": %lld, \"duplicates\": %lld}\n",
+               (long long)cnt[VFD_C_EVICTIONS], (long long)cnt[VFD_C_REQUEUED], (long long)cnt[VFD_C_FRAMES_LOST],
+               (long long)cnt[VFD_C_DUPLICATES]);
     printf("{\"kind\": \"vfd_load\", \"workers\": %d, \"batch\": %d, \"group\": %d, \"frame_bytes\": %lld, "
            "\"frames\": %lld, \"fps\": %.1f, \"dispatches\": %lld, \"frames_per_dispatch\": %.1f, "
            "\"unix\": %d, \"host_cpus\": %u}\n",
