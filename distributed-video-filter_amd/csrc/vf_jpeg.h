@@ -34,36 +34,27 @@ hipError_t dec_sync(const DecSeg *sg, const DecFrame *fr, int nseg, uint32_t max
                     const uint64_t *exit_in, uint64_t *exit_out, const uint32_t *cnt_in, uint32_t *cnt_out,
                     uint64_t *used, uint64_t *ck, uint32_t *ckrem, uint32_t *changed, int pass, hipStream_t s);
 // Speculative sync (one pass, no host round trip): k_spec decodes every subsequence from
-// each possible block-in-MCU and links neighbouring subsequences, k_wglink links workgroups,
-// k_resolve / k_finalize pick each subsequence's true trajectory.  *unresolved != 0 after
-// the call means some link did not rejoin a trajectory: run the pass-based dec_sync instead.
+// each possible block-in-MCU and links neighbouring subsequences (workgroups overlap by one
+// subsequence, so the links across workgroup boundaries are made there too), k_resolve /
+// k_finalize pick each subsequence's true trajectory.  *unresolved != 0 after the call means a
+// frame had more workgroups than k_resolve stages: run the pass-based dec_sync instead.
 struct SpecBufs {
-  // per lane slot [tr0 + workgroup * 256 + subsequence-in-workgroup * lanes + lane]
+  // per lane slot [tr0 + workgroup * 256 + row * lanes + lane]; row k of workgroup w is
+  // subsequence w * (256 / lanes - 1) + k
   uint64_t *tE;    // trajectory exit states
   uint8_t *tG;     // walk with entry `lane`: trajectory at the subsequence (or kLinkNone)
   uint64_t *tX;    //   its exit state
   uint32_t *tXc;   //   its block count in the subsequence
-  uint64_t *pX;    // resolved prefix records (lane 0 slots)
+  uint64_t *pX;    // prefix records of k_resolve's serial traces (lane 0 slots)
   uint32_t *pC;
   // per workgroup [wg0 + workgroup] (x kSpecLanesMax where indexed by a lane)
-  uint8_t *wF;     // walk e: trajectory at the last subsequence (kLinkNone if explicit)
-  uint64_t *wck;   // checkpoints of each workgroup's first subsequence [(wg * 16 + c) * kCk + m]
-  uint32_t *wrem;  // blocks from each of them to that subsequence's end
-  uint8_t *wB;     // boundary link from the predecessor's last trajectory j
-  uint32_t *wBC;
-  uint64_t *wBX;
+  uint8_t *wF;     // walk e: trajectory at the last row (kLinkNone if explicit)
   uint8_t *rE;     // resolved walk column
-  uint32_t *rK;    // resolved: prefix covers subsequences 0..rK
-  // traces k_wglink runs where the path may meet an explicit state (per workgroup, by lane):
-  uint8_t *wTE;    //   boundary link j missed: the walk column its trace joins (kLinkNone: none
-  uint8_t *wTK;    //   in the workgroup, kLinkLast: frame end) and at which subsequence; records in pX
-  uint8_t *wQE;    //   walk column e of the workgroup before ended explicit: the same, records in qX
-  uint8_t *wQK;
-  uint64_t *qX;    // prefix records of those traces (lane = e), like pX / pC
+  uint32_t *rK;    // resolved: the walk column from row rK on, prefix records before it
+  uint64_t *qX;    // prefix records of the traces of walk columns that ended explicit (lane = e)
   uint32_t *qC;
   uint8_t *rL;     // resolved: where the prefix records are (0x80 | lane: pX, 0xC0 | lane: qX)
-  uint32_t *stats;  // diagnostics (builds with tools/sync_stats.patch applied): [1] walker decodes [2] traced workgroups
-                    // [3] traced subsequences [4] link misses
+  uint32_t *stats;  // diagnostics (builds with tools/sync_stats.patch applied; a round-4 layout)
 };
 constexpr int kSpecLanesMax = 16;
 inline uint32_t spec_lanes_host(int bpm) { return bpm <= 1 ? 1u : bpm <= 2 ? 2u : bpm <= 4 ? 4u : bpm <= 8 ? 8u : 16u; }

@@ -371,9 +371,10 @@ int Codec::prepare_decode(const uint8_t *const *jpegs, const size_t *sizes, int 
       S.tile0 = tiles;
       S.sub0 = subs;
       S.nsub_max = (uint32_t)((len * 8 + kSubBits - 1) / kSubBits);
-      {  // speculative sync layout: spec_lanes(bpm) lanes per subsequence, 256 lanes per workgroup
+      {  // speculative sync layout: spec_lanes(bpm) lanes per subsequence, 256 lanes per workgroup,
+         // ns rows per workgroup of which the last is the next workgroup's first
         const uint32_t ns = 256 / spec_lanes_host(F.g.bpm);
-        S.nwg = (S.nsub_max + ns - 1) / ns;
+        S.nwg = S.nsub_max <= ns ? 1u : 1u + (S.nsub_max - ns + ns - 2) / (ns - 1);
         S.wg0 = wgs;
         S.tr0 = trs;
         wgs += S.nwg;
@@ -472,17 +473,8 @@ int Codec::prepare_decode(const uint8_t *const *jpegs, const size_t *sizes, int 
     CK(d_pX_.ensure(sizeof(uint64_t) * sl));
     CK(d_pC_.ensure(sizeof(uint32_t) * sl));
     CK(d_wF_.ensure(wl));
-    CK(d_wck_.ensure(sizeof(uint64_t) * wl * kCk));
-    CK(d_wrem_.ensure(sizeof(uint32_t) * wl * kCk));
-    CK(d_wB_.ensure(wl));
-    CK(d_wBC_.ensure(sizeof(uint32_t) * wl));
-    CK(d_wBX_.ensure(sizeof(uint64_t) * wl));
     CK(d_rE_.ensure(wgs));
     CK(d_rK_.ensure(sizeof(uint32_t) * wgs));
-    CK(d_wTE_.ensure(wl));
-    CK(d_wTK_.ensure(wl));
-    CK(d_wQE_.ensure(wl));
-    CK(d_wQK_.ensure(wl));
     CK(d_qX_.ensure(sizeof(uint64_t) * sl));
     CK(d_qC_.ensure(sizeof(uint32_t) * sl));
     CK(d_rL_.ensure(wgs));
@@ -543,11 +535,9 @@ int Codec::run_decode(int bgr, bool invert, std::string *err) {
   uint32_t flag = 1;
   if (use_spec) {
     SpecBufs sb{d_tE_.as<uint64_t>(), d_tG_.as<uint8_t>(), d_tX_.as<uint64_t>(), d_tXc_.as<uint32_t>(),
-                d_pX_.as<uint64_t>(), d_pC_.as<uint32_t>(), d_wF_.as<uint8_t>(), d_wck_.as<uint64_t>(),
-                d_wrem_.as<uint32_t>(), d_wB_.as<uint8_t>(), d_wBC_.as<uint32_t>(), d_wBX_.as<uint64_t>(),
-                d_rE_.as<uint8_t>(), d_rK_.as<uint32_t>(), d_wTE_.as<uint8_t>(), d_wTK_.as<uint8_t>(),
-                d_wQE_.as<uint8_t>(), d_wQK_.as<uint8_t>(), d_qX_.as<uint64_t>(), d_qC_.as<uint32_t>(),
-                d_rL_.as<uint8_t>(), d_unres_.as<uint32_t>()};
+                d_pX_.as<uint64_t>(),  d_pC_.as<uint32_t>(), d_wF_.as<uint8_t>(),  d_rE_.as<uint8_t>(),
+                d_rK_.as<uint32_t>(),  d_qX_.as<uint64_t>(), d_qC_.as<uint32_t>(), d_rL_.as<uint8_t>(),
+                d_unres_.as<uint32_t>()};
     // k_resolve reports a frame unresolved only when it has more workgroups than it stages,
     // which prepare_decode already excludes (spec_ok_), so the rest is queued without a host
     // round trip; check_decode reads the flags after its synchronisation and turns one into an
@@ -571,6 +561,8 @@ int Codec::run_decode(int bgr, bool invert, std::string *err) {
                    "%u link misses %u (workgroups %u, subsequences %u); k_resolve kcycles summed over frames: "
                    "trace %u walk %u\n", st[0], st[1], st[2], st[3], st[4],
                    dmax_wg_ * (uint32_t)ns, dmax_sub_ * (uint32_t)ns, st[5], st[6]);
+      std::fprintf(stderr, "[vf_jpeg] spec: walk columns ended explicit %u, their traces joined in one subsequence %u, "
+                   "serial traces %u (segments %d)\n", st[11], st[12], st[13], ns);
     }
   }
   // pass-based: spans of G subsequences per thread (VF_JPEG_SYNC_G = 1, 2, 4, 8; 0 = the

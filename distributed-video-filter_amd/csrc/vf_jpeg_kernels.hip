@@ -932,15 +932,18 @@ __global__ __launch_bounds__(256) void k_syncg(const DecSeg *__restrict__ sg, co
 //             rejoins (a short decode to the first matching checkpoint).  Then one lane per
 //             entry index e walks the workgroup: trajectory e of the first subsequence, the
 //             links after it, and, where a link rejoined nothing, an explicit state decoded
-//             on (the walker links it into the next subsequence itself).
-//   k_wglink  links the trajectories ending a workgroup into the next workgroup's first
-//             subsequence.
-//   k_resolve one lane per frame follows the true path across workgroups: entry e* of each
-//             workgroup from the previous one's walk, or, where the boundary link missed or a
-//             walk ended in an explicit state, by decoding on until the path rejoins a
-//             trajectory some walk column passes through (prefix records for the subsequences
-//             before that point).
-//   k_finalize writes exit state and block count per subsequence for the write pass.
+//             on (the walker links it into the next subsequence itself).  Neighbouring
+//             workgroups overlap by one subsequence (workgroup w's first is w-1's last, decoded
+//             from the same entry states, so its trajectory j IS w-1's last trajectory j): the
+//             link across a workgroup boundary is an ordinary in-workgroup link, made in k_spec.
+//   k_resolve one workgroup per frame follows the true path across workgroups: walk column
+//             e of w-1 ends at trajectory j = wF[e] of the shared subsequence, which is walk
+//             column j of w.  Where a walk ended in an explicit state (its last link rejoined
+//             nothing), the state is traced on through w first, all such traces of a frame in
+//             parallel, until it rejoins a trajectory some walk column passes through (prefix
+//             records for the subsequences before that point).
+//   k_finalize writes exit state and block count per subsequence for the write pass (a
+//             shared subsequence from its first workgroup).
 // Only a frame too long for k_resolve's tables, or a stream that never rejoins (corrupt
 // data), is reported unresolved; the caller then runs k_sync.
 
@@ -949,18 +952,27 @@ __device__ __forceinline__ uint32_t spec_lanes(uint32_t bpm) {
   return bpm <= 1 ? 1u : bpm <= 2 ? 2u : bpm <= 4 ? 4u : bpm <= 8 ? 8u : 16u;
 }
 constexpr uint32_t kSpecWords = 256 * (kSubBits / 32) + kSpecPadWords;  // NS <= 256 subsequences
+// maps of <= 16 entries packed as nibbles: (later o earlier)(e); entries >= bpm are absorbing
+__device__ __forceinline__ uint64_t map_compose(uint64_t later, uint64_t earlier, uint32_t bpm) {
+  uint64_t r = 0;
+  for (uint32_t q = 0; q < bpm; ++q) {
+    const uint32_t a = nib(earlier, q);
+    r |= (uint64_t)(a < bpm ? nib(later, a) : a) << (4 * q);
+  }
+  return r;
+}
 constexpr uint8_t kLinkNone = 0xF;  // rejoined no trajectory (explicit state follows)
 constexpr uint8_t kLinkLast = 0xE;  // the frame's last subsequence: decoded to the end
 
 // Decode from state X through subsequence [base, end); at each mark compare with the
-// checkpoints of trajectories 0..bpm-1 (ck(c, m), rem(c, m)).  Returns the trajectory joined,
-// or kLinkNone with *endst = the state at the first symbol boundary at/after `end`, or
-// kLinkLast (the frame's last subsequence, decoded to its end).  *count = blocks completed in
-// the subsequence along this path.
-template <typename CK, typename REM>
+// checkpoints of trajectories 0..bpm-1 (ck(c, m), rem(c, m)), and at the end with their exit
+// states (ex(c)).  Returns the trajectory joined, or kLinkNone with *endst = the state at the
+// first symbol boundary at/after `end`, or kLinkLast (the frame's last subsequence, decoded to
+// its end).  *count = blocks completed in the subsequence along this path.
+template <typename CK, typename REM, typename EX>
 __device__ __forceinline__ uint32_t spec_link(const uint32_t *words, uint32_t woff, uint64_t X, uint32_t base,
                                               uint32_t end, bool last, const HuffGeom &hg, const HuffSync *tabs, CK ck,
-                                              REM rem, uint32_t *count, uint64_t *endst) {
+                                              REM rem, EX ex, uint32_t *count, uint64_t *endst) {
   SyncLane<HuffSync> d;
   d.init(words, woff, X, hg);
   uint32_t m = 0;
@@ -981,7 +993,16 @@ __device__ __forceinline__ uint32_t spec_link(const uint32_t *words, uint32_t wo
   }
   *count = d.n;
   *endst = pack_state(d.pos, d.z, d.c);
-  return last ? kLinkLast : kLinkNone;
+  if (last) return kLinkLast;
+#ifndef VF_SPEC_ENDJOIN
+#define VF_SPEC_ENDJOIN 1
+#endif
+  if (!VF_SPEC_ENDJOIN) return kLinkNone;  // A/B builds only
+  // past the last mark the path may still have met a trajectory: the same state at the same
+  // boundary after `end` is the same path from there on
+  for (uint32_t c2 = 0; c2 < hg.bpm; ++c2)
+    if (ex(c2) == *endst) return c2;
+  return kLinkNone;
 }
 
 __global__ __launch_bounds__(256) void k_spec(const DecSeg *__restrict__ sg, const DecFrame *__restrict__ fr, const uint8_t *us, const uint32_t *us_len,
@@ -1001,16 +1022,17 @@ __global__ __launch_bounds__(256) void k_spec(const DecSeg *__restrict__ sg, con
   const DecFrame &F = fr[S.frame];
   if (blockIdx.x >= S.nwg) return;
   const HuffGeom hg(F.g);
-  const uint32_t L = spec_lanes(hg.bpm), NS = 256 / L;
+  const uint32_t L = spec_lanes(hg.bpm), NS = 256 / L, NSS = NS - 1;  // rows, rows not shared with w+1
   const uint32_t t = threadIdx.x, sl = t / L, c0 = t % L;
-  const uint32_t s = blockIdx.x * NS + sl;
+  const uint32_t s = blockIdx.x * NSS + sl;
   const uint32_t nbits = us_len[blockIdx.y] * 8u, nsub = (nbits + kSubBits - 1) / kSubBits;
+  if (blockIdx.x > 0 && blockIdx.x * NSS + 1 >= nsub) return;  // workgroup-uniform: owns no subsequence
   const bool live = c0 < hg.bpm && s < nsub;
   const uint32_t base = s * kSubBits, end = (s + 1 >= nsub) ? nbits : (s + 1) * kSubBits;
   const uint64_t g0 = S.tr0 + (uint64_t)blockIdx.x * 256, ti = g0 + t;
   // the workgroup's stream words (every decode here stays within them, plus overshoot and
   // lookahead), from the frame's padded unstuffed region
-  const uint32_t woff = blockIdx.x * NS * (kSubBits / 32);
+  const uint32_t woff = blockIdx.x * NSS * (kSubBits / 32);
   const uint32_t fwords = (((S.in_len + 64) + 15) & ~15u) / 4;
   const uint32_t *gw = reinterpret_cast<const uint32_t *>(us + S.us_off);
   for (uint32_t i = t; i < NS * (kSubBits / 32) + kSpecPadWords; i += 256)
@@ -1051,18 +1073,7 @@ __global__ __launch_bounds__(256) void k_spec(const DecSeg *__restrict__ sg, con
   }
   s_E[t] = live ? rel(E) : 0u;
   __syncthreads();
-  if (live) {
-    B.tE[ti] = E;
-    if (sl == 0) {  // checkpoints of the first subsequence, for k_wglink
-      const uint64_t wb = ((uint64_t)(S.wg0 + blockIdx.x) * kSpecLanesMax + c0) * kCk;
-#pragma unroll
-      for (int m = 0; m < kCk; ++m) {
-        const uint32_t r = s_ck[m][t];
-        B.wck[wb + m] = r == 0xFFFFFFFFu ? kNoCk : absl(r);
-        B.wrem[wb + m] = s_rem[m][t];
-      }
-    }
-  }
+  if (live) B.tE[ti] = E;
   // B: link trajectory c0 of s-1 into s
   uint32_t M = kLinkNone, C = N;
   uint64_t X = 0;
@@ -1070,7 +1081,8 @@ __global__ __launch_bounds__(256) void k_spec(const DecSeg *__restrict__ sg, con
     const uint32_t row = sl * L;
     M = spec_link(s_w, woff, absl(s_E[(sl - 1) * L + c0]), base, end, s + 1 == nsub, hg, tabs,
                   [&](uint32_t c2, int m) { return absl(s_ck[m][row + c2]); },
-                  [&](uint32_t c2, int m) { return (uint32_t)s_rem[m][row + c2]; }, &C, &X);
+                  [&](uint32_t c2, int m) { return (uint32_t)s_rem[m][row + c2]; },
+                  [&](uint32_t c2) { return absl(s_E[row + c2]); }, &C, &X);
   }
   s_M[t] = (uint8_t)M;
   s_C[t] = (uint16_t)C;
@@ -1083,17 +1095,10 @@ __global__ __launch_bounds__(256) void k_spec(const DecSeg *__restrict__ sg, con
   // of <= 16 entries packed as nibbles; kLinkNone and kLinkLast are absorbing).  A walk that
   // reaches an explicit state (a link that rejoined nothing, rare) continues serially from
   // there, decoding as before.
-  const uint32_t nk = blockIdx.x * NS < nsub ? min(NS, nsub - blockIdx.x * NS) : 0u;  // subsequences here
+  const uint32_t nk = blockIdx.x * NSS < nsub ? min(NS, nsub - blockIdx.x * NSS) : 0u;  // subsequences here
   if (nk == 0) return;  // workgroup-uniform
   const uint32_t bpm = hg.bpm;
-  auto compose = [bpm](uint64_t later, uint64_t earlier) {  // (later o earlier)(e)
-    uint64_t r = 0;
-    for (uint32_t q = 0; q < bpm; ++q) {
-      const uint32_t a = nib(earlier, q);
-      r |= (uint64_t)(a < bpm ? nib(later, a) : a) << (4 * q);
-    }
-    return r;
-  };
+  auto compose = [bpm](uint64_t later, uint64_t earlier) { return map_compose(later, earlier, bpm); };
   uint64_t ident = 0;
   for (uint32_t q = 0; q < bpm; ++q) ident |= (uint64_t)q << (4 * q);
   uint64_t f = ident;
@@ -1154,7 +1159,7 @@ __global__ __launch_bounds__(256) void k_spec(const DecSeg *__restrict__ sg, con
     uint32_t j = kLinkNone;  // current trajectory, or kLinkNone while explicit
     uint64_t st = s_fst[e];
     for (uint32_t k = s_first[e] + 1; k < nk; ++k) {
-      const uint32_t sk = blockIdx.x * NS + k;
+      const uint32_t sk = blockIdx.x * NSS + k;
       uint32_t cnt, M2;
       uint64_t xe = 0;
       if (j < hg.bpm) {
@@ -1166,7 +1171,8 @@ __global__ __launch_bounds__(256) void k_spec(const DecSeg *__restrict__ sg, con
         const uint32_t row = k * L;
         M2 = spec_link(s_w, woff, st, bk, ek, sk + 1 == nsub, hg, tabs,
                        [&](uint32_t c2, int m) { return absl(s_ck[m][row + c2]); },
-                       [&](uint32_t c2, int m) { return (uint32_t)s_rem[m][row + c2]; }, &cnt, &xe);
+                       [&](uint32_t c2, int m) { return (uint32_t)s_rem[m][row + c2]; },
+                       [&](uint32_t c2) { return absl(s_E[row + c2]); }, &cnt, &xe);
       }
       if (M2 < hg.bpm) {
         j = M2;
@@ -1180,35 +1186,48 @@ __global__ __launch_bounds__(256) void k_spec(const DecSeg *__restrict__ sg, con
       B.tXc[g0 + k * L + e] = cnt;
       if (j == kLinkLast) break;
     }
+    if (j == kLinkNone && nk == NS && blockIdx.x * NSS + NS < nsub) {
+      // the walk ended explicit: its decode through the next workgroup's row 1 (the subsequence
+      // after this workgroup's last, still inside the staged words), for k_resolve's trace of
+      // it (records in qX at that row, lane e)
+      const uint32_t sk = blockIdx.x * NSS + NS;
+      const uint32_t ek = (sk + 1 >= nsub) ? nbits : (sk + 1) * kSubBits;
+      const uint32_t lim = min(ek, (woff + NS * (kSubBits / 32) + kSpecPadWords - 4) * 32u);  // binds only on corrupt data
+      SyncLane<HuffSync> d;
+      d.init(s_w, woff, st, hg);
+      while (d.pos < lim) d.step(tabs, lim);
+      B.qX[g0 + 256 + L + e] = pack_state(d.pos, d.z, d.c);  // slot (w + 1, row 1, lane e)
+      B.qC[g0 + 256 + L + e] = d.n;
+    }
     B.wF[(uint64_t)(S.wg0 + blockIdx.x) * kSpecLanesMax + e] = (uint8_t)(j < hg.bpm ? j : kLinkNone);
   }
 }
 
-// Where the speculative path misses, it must be traced: decoded on from an explicit state
-// until its exit equals the exit of some walk column (tX) at a subsequence, after which it IS
-// that column.  Which explicit states the true path can meet at workgroup w is known before
-// the path is: the exit of boundary link j when it rejoined nothing (wBX), or the end state of
-// a walk column of w-1 that ended explicit (tX at w-1's last subsequence).  So those traces
-// run in parallel in k_wglink, one lane each, and k_resolve's serial walk across a frame's
-// workgroups only picks the precomputed result of the one it meets (round 2: ~2 serial traces
-// per 1080p frame were half of k_resolve's 68 us per batch).
+// Where the speculative path meets an explicit state it must be traced: decoded on until its
+// exit equals the exit of some walk column (tX) at a subsequence, after which it IS that
+// column.  Which explicit states the true path can meet at workgroup w is known before the
+// path is: the end state of a walk column of w-1 whose last link rejoined nothing (tX at
+// w-1's last subsequence, wF = kLinkNone).  So k_resolve traces all of a frame's such states
+// in parallel, one lane each, before its serial walk across the workgroups only picks the
+// result of the one it meets (round 2: ~2 serial traces per 1080p frame were half of
+// k_resolve's 68 us per batch).
 constexpr uint32_t kResolveLds = 4096;  // workgroups per frame resolved here (else fallback)
 constexpr uint32_t kTraceWords = kSubBits / 32 + 6;  // one subsequence + overshoot + lookahead
-constexpr uint8_t kNotTraced = 0xFD;   // wTE / wQE: no precomputed trace for this lane
 constexpr uint8_t kRecP = 0x80, kRecQ = 0xC0;  // rL: prefix records in pX / qX, lane = low 4 bits
 
-// Decode from explicit state X through subsequences k0.. of workgroup w (words staged per
-// subsequence into the caller's `tw` row) until the exit equals walk column q's exit tX there
-// (returns q, *kend = k), the frame ends (kLinkLast) or the workgroup does (kLinkNone, *kend =
-// its last subsequence).  Every subsequence's exit and block count go to rX / rC at lane `lane`.
+// Decode from explicit state X through rows k0.. of workgroup w (row k = subsequence
+// w * NSS + k; words staged per subsequence into the caller's `tw` row) until the exit equals
+// walk column q's exit tX there (returns q, *kend = k), the frame ends (kLinkLast) or the
+// workgroup does (kLinkNone, *kend = its last row).  Every row's exit and block count go to rX /
+// rC at lane `lane`.
 __device__ __forceinline__ uint32_t trace_on(const uint32_t *gw, uint32_t fwords, uint32_t *tw, uint64_t X,
-                                             uint32_t w, uint32_t k0, uint32_t NS, uint32_t L, uint32_t nsub,
-                                             uint32_t nbits, uint64_t tr0, const HuffGeom &hg,
+                                             uint32_t w, uint32_t k0, uint32_t NS, uint32_t NSS, uint32_t L,
+                                             uint32_t nsub, uint32_t nbits, uint64_t tr0, const HuffGeom &hg,
                                              const HuffSync *tabs, const uint64_t *tX, uint64_t *rX, uint32_t *rC,
                                              uint32_t lane, uint32_t *kend) {
   uint32_t k = k0;
-  for (; k < NS && w * NS + k < nsub; ++k) {
-    const uint32_t sk = w * NS + k;
+  for (; k < NS && w * NSS + k < nsub; ++k) {
+    const uint32_t sk = w * NSS + k;
     const uint32_t ek = (sk + 1 >= nsub) ? nbits : (sk + 1) * kSubBits;
     // the subsequence's words, fetched together (independent loads), then decoded from LDS
     const uint32_t w0 = (uint32_t)(X >> 16) >> 5;
@@ -1231,215 +1250,183 @@ __device__ __forceinline__ uint32_t trace_on(const uint32_t *gw, uint32_t fwords
   return kLinkNone;
 }
 
-// Links across workgroup boundaries: trajectory j of the last subsequence of workgroup w-1
-// into the first subsequence of w.  16 boundaries per workgroup, one lane per j.  Lanes
-// j < bpm: the link, and where it rejoined nothing, its trace on through w (records in pX lane
-// j, result in wTE / wTK).  Lanes 8 + e (bpm <= 8): walk column e of w-1 ended explicit: its
-// trace through w from subsequence 0 (records in qX lane e, result in wQE / wQK).
-__global__ __launch_bounds__(256) void k_wglink(const DecSeg *__restrict__ sg, const DecFrame *__restrict__ fr, const uint8_t *us, const uint32_t *us_len,
-                                                SpecBufs B) {
-  constexpr uint32_t kLinkWords = kSubBits / 32 + kSpecPadWords;  // as k_spec's window for one subsequence
-  __shared__ HuffSync tabs[6];
-  __shared__ uint32_t s_lw[16][kLinkWords];
-  __shared__ uint64_t s_ck[16][kSpecLanesMax * kCk];
-  __shared__ uint32_t s_rem[16][kSpecLanesMax * kCk];
-  __shared__ uint32_t s_tw[256][kTraceWords];  // each tracing lane's staged words
-  const DecSeg S = sg[blockIdx.y];  // by value: held in scalar registers
-  const DecFrame &F = fr[S.frame];
-  if (blockIdx.x * 16 >= S.nwg) return;
-  const HuffGeom hg(F.g);
-  const uint32_t L = spec_lanes(hg.bpm), NS = 256 / L;
-  const uint32_t wl = threadIdx.x / 16, w = blockIdx.x * 16 + wl, j = threadIdx.x % 16;
-  const uint32_t nbits = us_len[blockIdx.y] * 8u, nsub = (nbits + kSubBits - 1) / kSubBits;
-  const uint32_t s = w * NS;
-  const bool live = w > 0 && w < S.nwg && s < nsub;
-  const uint32_t fwords = (((S.in_len + 64) + 15) & ~15u) / 4;
-  const uint32_t *gw = reinterpret_cast<const uint32_t *>(us + S.us_off);
-  // Stage each boundary's stream words and the checkpoints it compares against (all loads
-  // issued before the decode, instead of one dependent global load per refill and per mark)
-  const uint64_t wc = (uint64_t)(S.wg0 + w) * kSpecLanesMax;
-  if (live) {
-    const uint32_t woff = s * (kSubBits / 32);
-    for (uint32_t i = j; i < kLinkWords; i += 16) s_lw[wl][i] = woff + i < fwords ? gw[woff + i] : 0u;
-    if (j < hg.bpm) {
-#pragma unroll
-      for (int m = 0; m < kCk; ++m) {
-        s_ck[wl][j * kCk + m] = B.wck[(wc + j) * kCk + m];
-        s_rem[wl][j * kCk + m] = B.wrem[(wc + j) * kCk + m];
-      }
-    }
-  }
-  load_sync_tables(F, tabs);  // its barrier also publishes the staged words and checkpoints
-  if (!live) return;
-  const uint32_t base = s * kSubBits, end = (s + 1 >= nsub) ? nbits : (s + 1) * kSubBits;
-  uint32_t *tw = s_tw[threadIdx.x];
-  if (j < hg.bpm) {
-    const uint64_t X = B.tE[S.tr0 + (uint64_t)(w - 1) * 256 + (NS - 1) * L + j];
-    uint32_t C = 0;
-    uint64_t xe = 0;
-    const uint32_t M = spec_link(s_lw[wl], s * (kSubBits / 32), X, base, end, s + 1 == nsub, hg, tabs,
-                                 [&](uint32_t c2, int m) { return s_ck[wl][c2 * kCk + m]; },
-                                 [&](uint32_t c2, int m) { return s_rem[wl][c2 * kCk + m]; }, &C, &xe);
-    const uint64_t wb = wc + j;
-    B.wB[wb] = (uint8_t)M;
-    B.wBC[wb] = C;
-    B.wBX[wb] = xe;
-    uint32_t te = kNotTraced, tk = 0;
-    if (M == kLinkNone) {  // subsequence 0 decoded without rejoining: trace on from its end
-      const uint64_t at = S.tr0 + (uint64_t)w * 256;
-      B.pX[at + j] = xe;
-      B.pC[at + j] = C;
-      te = 1 < NS && s + 1 < nsub ? trace_on(gw, fwords, tw, xe, w, 1, NS, L, nsub, nbits, S.tr0, hg, tabs, B.tX,
-                                             B.pX, B.pC, j, &tk)
-                                  : kLinkNone;
-    }
-    B.wTE[wb] = (uint8_t)te;
-    B.wTK[wb] = (uint8_t)tk;
-  } else if (hg.bpm <= 8 && j >= 8 && j - 8 < hg.bpm) {
-    const uint32_t e = j - 8;
-    const uint64_t wb = wc + e;
-    uint32_t te = kNotTraced, tk = 0;
-    if (B.wF[(uint64_t)(S.wg0 + w - 1) * kSpecLanesMax + e] == kLinkNone) {  // walk e ended explicit
-      const uint64_t X = B.tX[S.tr0 + (uint64_t)(w - 1) * 256 + (NS - 1) * L + e];
-      te = trace_on(gw, fwords, tw, X, w, 0, NS, L, nsub, nbits, S.tr0, hg, tabs, B.tX, B.qX, B.qC, e, &tk);
-    }
-    B.wQE[wb] = (uint8_t)te;
-    B.wQK[wb] = (uint8_t)tk;
-  }
-}
-
 // The true path across the workgroups of a frame (one workgroup per frame).  Per workgroup w
-// it finds the walk column e* that is the path from subsequence kj + 1 on; subsequences
-// 0..kj take prefix records (exit state, count) from pX or qX at lane rL & 15.  Where the
-// path enters w depends only on the walk column e it followed through w - 1: the boundary link
-// from that column's last trajectory rejoined trajectory e* of w's first subsequence, or it
-// missed, or the column ended explicit -- and for both misses k_wglink has already traced the
-// state on.  So every workgroup's transition e -> (e*, kj, where the records are) is made in
-// parallel first (one thread per workgroup, into LDS), and the serial walk across the frame
-// is one LDS read per workgroup.  Lane 0 decodes only where no trace was run (the path
-// crossed a whole workgroup in a trace, or an explicit walk with bpm > 8), into pX lane 0.
+// it finds the walk column e* that is the path from row rK on; rows 1..rK-1 take prefix records
+// (exit state, count) from pX or qX at lane rL & 15 (row 0 is w-1's last row, resolved there).
+// Where the path enters w depends only on the walk column e it followed through w - 1: that
+// column ended at trajectory j of the shared subsequence, which is w's walk column j; or it ended
+// explicit, and its trace through w (made first, in parallel) says which column it rejoins.  So
+// every workgroup's transition e -> (e*, rK, where the records are) is made in parallel (into
+// LDS), and the serial walk across the frame is one LDS read per workgroup.  Lane 0 decodes only
+// where the path crossed a whole workgroup in a trace without rejoining, into pX lane 0.
 constexpr uint32_t kResolveT = 16384;  // transitions staged per frame (workgroups x bpm)
-constexpr uint32_t kTrSerial = 1u << 20;
+constexpr uint32_t kTrJoined = 1u << 24;  // the path leaves the workgroup as walk column e*
+__device__ __forceinline__ uint32_t spec_nwg(uint32_t nsub, uint32_t NS) {  // workgroups owning a subsequence
+  return nsub <= NS ? 1u : 1u + (nsub - NS + NS - 2) / (NS - 1);
+}
 __global__ __launch_bounds__(256) void k_resolve(const DecSeg *__restrict__ sg, const DecFrame *__restrict__ fr, const uint8_t *us, const uint32_t *us_len,
                                                  SpecBufs B, uint32_t *unresolved) {
-  __shared__ uint32_t sT[kResolveT];  // [w * bpm + e]: e* | kj << 4 | code << 12 | kTrSerial
-  __shared__ uint8_t sE[kResolveLds], sK[kResolveLds], sJ[kResolveLds];
+  __shared__ uint32_t sT[kResolveT];  // [w * bpm + e]: e* | rK << 4 | code << 16 | kTrJoined
+  __shared__ uint8_t sE[kResolveLds], sJ[kResolveLds];
+  __shared__ uint16_t sK[kResolveLds];
   __shared__ HuffSync tabs[6];
-  __shared__ uint32_t s_tw[kTraceWords];
+  __shared__ uint32_t s_tw[256][kTraceWords];  // each tracing lane's staged words
+  __shared__ uint16_t s_xl[kResolveT];           // (workgroup, walk column) pairs to trace
+  __shared__ uint32_t s_nx, s_n1, s_abs;
+  __shared__ uint64_t s_wt[4];
   const DecSeg S = sg[blockIdx.x];  // by value: held in scalar registers
   const DecFrame &F = fr[S.frame];
   const HuffGeom hg(F.g);
-  const uint32_t bpm = hg.bpm, L = spec_lanes(bpm), NS = 256 / L;
+  const uint32_t bpm = hg.bpm, L = spec_lanes(bpm), NS = 256 / L, NSS = NS - 1;
   const uint32_t nbits = us_len[blockIdx.x] * 8u, nsub = (nbits + kSubBits - 1) / kSubBits;
-  const uint32_t nwg = min(S.nwg, (nsub + NS - 1) / NS);
+  const uint32_t nwg = min(S.nwg, spec_nwg(nsub, NS));
   const bool over = nwg > kResolveLds || nwg * bpm > kResolveT;
   if (threadIdx.x == 0)  // every segment's flag, every decode (page-locked host memory)
     __hip_atomic_store(unresolved + blockIdx.x, over ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   if (over) return;
   const uint32_t lastk = NS - 1;  // every workgroup but the frame's last is full
-  {  // the sync tables' copy is issued with the transition loads; one barrier publishes both
+  {  // the sync tables' copy; the barrier below publishes it
     const uint32_t *src = reinterpret_cast<const uint32_t *>(&F.sdc[0]);
     uint32_t *dst = reinterpret_cast<uint32_t *>(tabs);
     for (uint32_t j = threadIdx.x; j < 6 * sizeof(HuffSync) / 4; j += 256) dst[j] = src[j];
-  }
-  for (uint32_t w = threadIdx.x + 1; w < nwg; w += 256) {
-    const uint64_t rowp = (uint64_t)(S.wg0 + w - 1) * kSpecLanesMax, row = rowp + kSpecLanesMax;
-    const uint4 f4 = *reinterpret_cast<const uint4 *>(B.wF + rowp);
-    const uint4 b4 = *reinterpret_cast<const uint4 *>(B.wB + row);
-    const uint32_t fw[4] = {f4.x, f4.y, f4.z, f4.w}, bw[4] = {b4.x, b4.y, b4.z, b4.w};
-    for (uint32_t e = 0; e < bpm; ++e) {
-      const uint32_t jl = (fw[e >> 2] >> (8 * (e & 3))) & 0xF;
-      uint32_t tr = kTrSerial;
-      if (jl < bpm) {
-        const uint32_t jb = (bw[jl >> 2] >> (8 * (jl & 3))) & 0xF;
-        if (jb < bpm || jb == kLinkLast) {  // rejoined (or the frame's last subsequence)
-          tr = (jb < bpm ? jb : 0u) | ((jl | (jb < bpm ? 0u : 0x20u)) << 12);
-        } else {  // the link missed: its trace
-          const uint32_t te = B.wTE[row + jl], tk = B.wTK[row + jl];
-          if (te != kNotTraced)
-            tr = te < bpm ? te | (tk << 4) | ((kRecP | jl) << 12) : (lastk << 4) | ((kRecP | jl) << 12);
-        }
-      } else if (bpm <= 8) {  // walk column e ended explicit in w - 1: its trace
-        const uint32_t te = B.wQE[row + e], tk = B.wQK[row + e];
-        if (te != kNotTraced)
-          tr = te < bpm ? te | (tk << 4) | ((kRecQ | e) << 12) : (lastk << 4) | ((kRecQ | e) << 12);
-      }
-      sT[w * bpm + e] = tr;
-    }
   }
   __syncthreads();
   auto slot = [&](uint32_t w, uint32_t k, uint32_t lane) { return S.tr0 + (uint64_t)w * 256 + k * L + lane; };
   const uint32_t fwords = (((S.in_len + 64) + 15) & ~15u) / 4;
   const uint32_t *gw = reinterpret_cast<const uint32_t *>(us + S.us_off);
-  if (threadIdx.x == 0) {
-    sE[0] = 0;
-    sK[0] = 0;
-    sJ[0] = kRecP;  // workgroup 0: frame start = trajectory 0 (records written below)
-    B.pX[slot(0, 0, 0)] = B.tX[slot(0, 0, 0)];
-    B.pC[slot(0, 0, 0)] = B.tXc[slot(0, 0, 0)];
-    uint32_t e = 0, kj = 0;
-    uint8_t rec = kRecP;  // where workgroup w-1's prefix records are
-    for (uint32_t w = 1; w < nwg; ++w) {
-      if (kj < lastk) {
+  // transitions; every walk column that ended explicit is listed (LDS atomics) and traced,
+  // one per lane where there are at most 256 (qX lane e)
+  if (threadIdx.x == 0) s_nx = s_n1 = s_abs = 0;
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < (nwg - 1) * bpm; i += 256) {
+    const uint32_t w = 1 + i / bpm, e = i - (w - 1) * bpm;
+    const uint32_t j = B.wF[(uint64_t)(S.wg0 + w - 1) * kSpecLanesMax + e] & 0xF;
+    if (j < bpm) {
+      sT[w * bpm + e] = j | (1u << 4) | kTrJoined;
+    } else {
+      const uint32_t q = atomicAdd(&s_nx, 1u);
+      s_xl[q] = (uint16_t)i;  // q < kResolveT: one entry per (workgroup, walk column)
+    }
+  }
+  __syncthreads();
+  for (uint32_t q = threadIdx.x; q < s_nx; q += 256) {
+    const uint32_t i = s_xl[q], w = 1 + i / bpm, e = i - (w - 1) * bpm;
+    // row 1 was decoded by k_spec (w - 1's walker, into qX): compare its exit, trace on from row 2
+    const uint64_t X1 = B.qX[slot(w, 1, e)];
+    uint32_t te = kLinkNone, kf = 1;
+    if (w * NSS + 2 == nsub) {
+      te = kLinkLast;  // row 1 is the frame's last subsequence
+    } else {
+      for (uint32_t c2 = 0; c2 < bpm; ++c2)
+        if (B.tX[slot(w, 1, c2)] == X1) {
+          te = c2;
+          break;
+        }
+      if (te == kLinkNone)
+        te = trace_on(gw, fwords, s_tw[threadIdx.x], X1, w, 2, NS, NSS, L, nsub, nbits, S.tr0, hg, tabs, B.tX, B.qX,
+                      B.qC, e, &kf);
+      else
+        atomicAdd(&s_n1, 1u);
+    }
+    const uint32_t code = (uint32_t)(kRecQ | e) << 16;
+    sT[w * bpm + e] = te < bpm ? te | ((kf + 1) << 4) | code | kTrJoined : (NS << 4) | code;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {  // diagnostics (VF_JPEG_SYNC_STATS): walk columns that ended explicit, traces joined in one row
+    atomicAdd(B.stats + 11, s_nx);
+    atomicAdd(B.stats + 12, s_n1);
+  }
+  // The walk across the workgroups: the transition maps e -> e* (a path that leaves a workgroup
+  // in records is absorbing) composed by a prefix scan, lanes taking consecutive chunks of
+  // workgroups; each lane then follows its chunk from the entry the scan gives it.  A path
+  // absorbed before the frame's last workgroup (rare: a trace that rejoined nothing in a
+  // whole workgroup) is walked serially below instead.
+  {
+    const uint32_t n = nwg - 1, C = (n + 255) / 256, t = threadIdx.x;
+    const uint32_t wa = min(n, t * C) + 1, wz = min(n, (t + 1) * C) + 1;  // this lane's workgroups [wa, wz)
+    uint64_t ident = 0;
+    for (uint32_t q = 0; q < bpm; ++q) ident |= (uint64_t)q << (4 * q);
+    uint64_t f = ident;
+    for (uint32_t w = wa; w < wz; ++w) {
+      uint64_t m = 0;
+      for (uint32_t q = 0; q < bpm; ++q) {
+        const uint32_t tr = sT[w * bpm + q];
+        m |= (uint64_t)((tr & kTrJoined) ? tr & 0xF : 0xF) << (4 * q);
+      }
+      f = map_compose(m, f, bpm);
+    }
+    const uint32_t lane = t & 63, wv = t >> 6;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+      const uint64_t o = __shfl_up(f, d, 64);
+      if (lane >= d) f = map_compose(f, o, bpm);
+    }
+    if (lane == 63) s_wt[wv] = f;
+    __syncthreads();
+    uint64_t pre = ident;  // the maps of the waves before this one
+    for (uint32_t q = 0; q < wv; ++q) pre = map_compose(s_wt[q], pre, bpm);
+    uint64_t gp = __shfl_up(f, 1, 64);
+    gp = lane == 0 ? pre : map_compose(gp, pre, bpm);  // the maps of every lane before this one
+    uint32_t e = nib(gp, 0);  // the frame starts at walk column 0 of workgroup 0
+    if (wa < wz) {
+      if (e >= bpm) s_abs = 1u;
+      for (uint32_t w = wa; w < wz && e < bpm; ++w) {
         const uint32_t tr = sT[w * bpm + e];
-        if (!(tr & kTrSerial)) {
-          const uint8_t code = (uint8_t)(tr >> 12);
-          e = tr & 0xF;
-          kj = (tr >> 4) & 0xFF;
-          sE[w] = (uint8_t)e;
-          sK[w] = (uint8_t)kj;
-          sJ[w] = code;
-          rec = code < kRecP ? kRecP : code;
-          continue;
+        e = tr & 0xF;
+        sE[w] = (uint8_t)e;
+        sK[w] = (uint16_t)((tr >> 4) & 0x1FF);
+        sJ[w] = (uint8_t)(tr >> 16);
+        if (!(tr & kTrJoined)) {
+          if (w + 1 < wz) s_abs = 1u;
+          break;
         }
       }
-      // no precomputed transition: decode on serially (records into pX lane 0)
-      const uint64_t row = (uint64_t)(S.wg0 + w) * kSpecLanesMax;
-      const uint32_t jl = kj < lastk ? B.wF[row - kSpecLanesMax + e] & 0xF : kLinkNone;
-      uint64_t X;
-      uint32_t k = 0;
-      if (jl < bpm) {  // cannot happen (every missed link is traced in k_wglink); kept for safety
-        X = B.wBX[row + jl];
-        B.pX[slot(w, 0, 0)] = X;
-        B.pC[slot(w, 0, 0)] = B.wBC[row + jl];
-        k = 1;
-      } else if (kj < lastk) {
-        X = B.tX[slot(w - 1, lastk, e)];
-      } else {  // the previous workgroup's trace ran through it: continue from its last record
-        X = ((rec & 0x40) ? B.qX : B.pX)[slot(w - 1, lastk, rec & 15)];
+    }
+    if (t == 0) {
+      sE[0] = 0;
+      sK[0] = 0;
+      sJ[0] = 0;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && s_abs) {
+    uint32_t e = 0;
+    bool joined = true;
+    uint8_t rec = 0;  // where the records of a path that left w - 1 explicit are
+    for (uint32_t w = 1; w < nwg; ++w) {
+      if (joined) {
+        const uint32_t tr = sT[w * bpm + e];
+        e = tr & 0xF;
+        sE[w] = (uint8_t)e;
+        sK[w] = (uint16_t)((tr >> 4) & 0x1FF);
+        sJ[w] = rec = (uint8_t)(tr >> 16);
+        joined = (tr & kTrJoined) != 0;
+        continue;
       }
+      // the path crossed w - 1 in a trace that rejoined nothing: decode on (records into pX lane 0)
+      const uint64_t X = ((rec & 0x40) ? B.qX : B.pX)[slot(w - 1, lastk, rec & 15)];
       uint32_t kf = 0;
-      const uint32_t te = k < NS && w * NS + k < nsub
-                              ? trace_on(gw, fwords, s_tw, X, w, k, NS, L, nsub, nbits, S.tr0, hg, tabs, B.tX, B.pX,
-                                         B.pC, 0, &kf)
-                              : kLinkNone;
-      const bool found = te < bpm;
-      sE[w] = (uint8_t)(found ? te : 0);
-      sK[w] = (uint8_t)(found ? kf : lastk);
-      sJ[w] = kRecP;
-      e = found ? te : 0;
-      kj = found ? kf : lastk;
-      rec = kRecP;
+      const uint32_t te = trace_on(gw, fwords, s_tw[0], X, w, 1, NS, NSS, L, nsub, nbits, S.tr0, hg, tabs, B.tX, B.pX,
+                                   B.pC, 0, &kf);
+      atomicAdd(B.stats + 13, 1u);  // diagnostics: serial traces
+      joined = te < bpm;
+      e = joined ? te : 0;
+      sE[w] = (uint8_t)e;
+      sK[w] = (uint16_t)(joined ? kf + 1 : NS);
+      sJ[w] = rec = kRecP;
     }
   }
   __syncthreads();
   for (uint32_t w = threadIdx.x; w < nwg; w += 256) {
     B.rE[S.wg0 + w] = sE[w];
     B.rK[S.wg0 + w] = sK[w];
-    const uint8_t code = sJ[w];
-    if (code < kRecP) {  // rejoined at the boundary: prefix record of subsequence 0, into pX lane 0
-      const uint64_t wb = (uint64_t)(S.wg0 + w) * kSpecLanesMax + (code & 15);
-      B.pX[slot(w, 0, 0)] = (code & 0x20) ? B.wBX[wb] : B.tE[slot(w, 0, sE[w])];
-      B.pC[slot(w, 0, 0)] = B.wBC[wb];
-      B.rL[S.wg0 + w] = kRecP;
-    } else {
-      B.rL[S.wg0 + w] = code;
-    }
+    B.rL[S.wg0 + w] = sJ[w];
   }
 }
 
 // Exit state and block count of every subsequence along the resolved path, in the layout
-// the write pass and the block-offset scan read (exit_out / cnt_out of k_sync).
+// the write pass and the block-offset scan read (exit_out / cnt_out of k_sync).  A workgroup's
+// row 0 is its predecessor's last row, written there.
 __global__ __launch_bounds__(256) void k_finalize(const DecSeg *__restrict__ sg, const DecFrame *__restrict__ fr, const uint32_t *us_len, SpecBufs B,
                                                   uint64_t *exit_out, uint32_t *cnt_out) {
   const DecSeg S = sg[blockIdx.y];  // by value: held in scalar registers
@@ -1448,8 +1435,8 @@ __global__ __launch_bounds__(256) void k_finalize(const DecSeg *__restrict__ sg,
   const uint32_t bpm = (uint32_t)F.g.bpm, L = spec_lanes(bpm), NS = 256 / L;
   const uint32_t nbits = us_len[blockIdx.y] * 8u, nsub = (nbits + kSubBits - 1) / kSubBits;
   const uint32_t sl = threadIdx.x;
-  if (sl >= NS) return;
-  const uint32_t s = blockIdx.x * NS + sl;
+  if (sl >= NS || (blockIdx.x > 0 && sl == 0)) return;
+  const uint32_t s = blockIdx.x * (NS - 1) + sl;
   if (s >= S.nsub_max) return;
   const uint64_t gi = S.sub0 + s;
   if (s >= nsub) {
@@ -1458,8 +1445,8 @@ __global__ __launch_bounds__(256) void k_finalize(const DecSeg *__restrict__ sg,
     return;
   }
   const uint64_t g0 = S.tr0 + (uint64_t)blockIdx.x * 256;
-  const uint32_t kj = B.rK[S.wg0 + blockIdx.x], e = B.rE[S.wg0 + blockIdx.x];
-  if (sl <= kj) {
+  const uint32_t rk = B.rK[S.wg0 + blockIdx.x], e = B.rE[S.wg0 + blockIdx.x];
+  if (sl < rk) {
     const uint8_t rl = B.rL[S.wg0 + blockIdx.x];
     const uint64_t at = g0 + sl * L + (rl & 15);
     exit_out[gi] = (rl & 0x40) ? B.qX[at] : B.pX[at];
@@ -3222,7 +3209,6 @@ hipError_t dec_sync_spec(const DecSeg *__restrict__ sg, const DecFrame *__restri
                          uint32_t *unresolved, hipStream_t s) {
   if (nseg <= 0 || !max_wg) return hipSuccess;
   hipLaunchKernelGGL(k_spec, dim3(max_wg, (unsigned)nseg), dim3(256), 0, s, sg, fr, us, us_len, b);
-  hipLaunchKernelGGL(k_wglink, dim3((max_wg + 15) / 16, (unsigned)nseg), dim3(256), 0, s, sg, fr, us, us_len, b);
   hipLaunchKernelGGL(k_resolve, dim3((unsigned)nseg), dim3(256), 0, s, sg, fr, us, us_len, b, unresolved);
   hipLaunchKernelGGL(k_finalize, dim3(max_wg, (unsigned)nseg), dim3(256), 0, s, sg, fr, us_len, b, exit_out, cnt_out);
   return hipGetLastError();
