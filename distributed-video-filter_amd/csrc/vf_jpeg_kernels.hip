@@ -2011,12 +2011,18 @@ __device__ __forceinline__ void enc_store_rows(const EncFrame &E, uint8_t *__res
             lo |= (uint32_t)(rw ? c1[p] : c0[p]) << (8 * p);
             hi |= (uint32_t)(rw ? c1[p + 4] : c0[p + 4]) << (8 * p);
           }
+#if VF_ABL & 8
+          if (lo == 0x12345678u && hi == 0x9ABCDEF0u)
+#endif
           *reinterpret_cast<uint2 *>(row + x0) = make_uint2(lo, hi);
         } else {  // h2v1_downsample: bias 0, 1 alternating
           uint32_t v = 0;
 #pragma unroll
           for (int i = 0; i < 4; ++i)
             v |= (uint32_t)(((rw ? c1[2 * i] + c1[2 * i + 1] : c0[2 * i] + c0[2 * i + 1]) + (i & 1)) >> 1) << (8 * i);
+#if VF_ABL & 8
+          if (v == 0x12345678u)
+#endif
           *reinterpret_cast<uint32_t *>(row + (x0 >> 1)) = v;
         }
         if (edge) {
@@ -2570,19 +2576,32 @@ __device__ __forceinline__ void fdct_pass1(const uint8_t *img, const Geom &g, in
 // Pass 1 from the invert path's sample planes (enc_sample_rows): row sy of the block is one
 // 8-byte load; level shift and the FDCT's row pass.  The table image store and the AC-word
 // clearing sit between the load and its use, as in fdct_pass1.
+// VF_ABL (timing ablations, tools/exp builds only; outputs are wrong): bit 0 no sample-plane
+// loads in k_fdct, bit 1 no FDCT arithmetic, bit 2 no AC coding, bit 3 no sample-plane stores in
+// k_idct_color422, bit 4 no table image (only with bit 2), bit 5 no quantisation, bit 6 no
+// coefficient list (only with bit 2)
+#ifndef VF_ABL
+#define VF_ABL 0
+#endif
 template <bool FAST>
 __device__ __forceinline__ void fdct_pass1_planes(const uint8_t *plane, int pitch, int bx, int sy, bool real,
                                                   const uint4 &tw, const uint8_t *dummy, uint4 *s_tab,
                                                   uint32_t *acw_slot, uint32_t r, int32_t *wsrow) {
+#if VF_ABL & 1
+  const uint2 q = make_uint2((uint32_t)(bx * 0x01010101) ^ (uint32_t)sy, (uint32_t)(sy * 0x01030507) ^ r);
+#else
   const uint2 q = *reinterpret_cast<const uint2 *>(real ? plane + (size_t)sy * pitch + bx * 8 : dummy);
+#endif
   if (threadIdx.x < 192) s_tab[threadIdx.x] = tw;
   clear_ac_words(acw_slot, r);
   if (!real) return;
   int32_t v[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) v[j] = (int32_t)(((j < 4 ? q.x : q.y) >> (8 * (j & 3))) & 0xFF) - 128;
+#if !(VF_ABL & 2)
   if (FAST) fdct_ifast_line(v);
   else fdct_islow_line(v, 0);
+#endif
 #pragma unroll
   for (int j = 0; j < 8; ++j) wsrow[j] = v[j];
 }
@@ -2693,7 +2712,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
   // shift and through one bit-field extract for its store address), then s_ac[t][256].  Its
   // load is issued first; fdct_pass1 stores it after issuing the pixel loads.
   __shared__ uint4 s_tab[192];
+#if VF_ABL & 16
+  const uint4 tw = make_uint4(threadIdx.x, 0x3F3F3F3Fu, threadIdx.x, 0x3F3F3F3Fu);
+#else
   const uint4 tw = threadIdx.x < 192 ? reinterpret_cast<const uint4 *>(tab->fdct_lds)[threadIdx.x] : make_uint4(0, 0, 0, 0);
+#endif
   const uint2 (*const s_q)[64] = reinterpret_cast<const uint2 (*)[64]>(s_tab);
   const uint32_t (*const s_ac)[256] = reinterpret_cast<const uint32_t (*)[256]>(reinterpret_cast<const uint32_t *>(s_tab) + 256);
   const uint32_t slot = threadIdx.x >> 3, r = threadIdx.x & 7, lm = slot & (kFdctGroup - 1);
@@ -2732,13 +2755,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
     int32_t v[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) v[i] = ws[slot][i][r];
+#if !(VF_ABL & 2)
     if (FAST) fdct_ifast_line(v);
     else fdct_islow_line(v, 1);
+#endif
     const uint32_t qsel = 8 + 6 * (slot & 3);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const uint2 q = s_q[t][i * 8 + r];
+#if VF_ABL & 32
+      qo[(q.y >> qsel) & 63] = (int16_t)(v[i] >> 3);
+#else
       qo[(q.y >> qsel) & 63] = quantize(v[i], q.x & 0xFFFF, q.x >> 16, q.y);
+#endif
     }
   }
   // From here on a block's 8 lanes read only their own slot's LDS (qo, ws, acw), written by
@@ -2771,6 +2800,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
   // rounds of one code per lane instead of eight coefficient slots per lane (a 1080p q85 frame
   // averages ~4 nonzero AC coefficients per block).  The list is written without branches: a
   // zero coefficient's entry goes to the lane's own spare word (64 + r; the list uses <= 63).
+#if VF_ABL & 64
+  if (m8 != 12345u) {
+    if (real && r == 0) {
+      dcq[F.blk0 + b] = (int16_t)vz[0];
+      acbits[F.blk0 + b] = eob ? 2u : 3u;
+    }
+    return;
+  }
+#endif
   const uint32_t cnt = __popc(m8);
   const uint32_t rinc = scan8(cnt, r);
   const uint32_t nnz = last8(rinc);
@@ -2789,6 +2827,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // the group's list, read across its lanes
   uint32_t off = 0;  // the block's AC bits so far (the same in its 8 lanes)
+#if VF_ABL & 4
+  if (nnz != 12345) {
+    if (real && r == 0) {
+      dcq[F.blk0 + b] = (int16_t)vz[0];
+      acbits[F.blk0 + b] = 2u;
+    }
+    return;
+  }
+#endif
   for (uint32_t q0 = 0; __ballot(q0 < nnz) != 0; q0 += 8) {
     const uint32_t q = q0 + r;
     const bool act = q < nnz;
