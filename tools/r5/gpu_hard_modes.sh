@@ -1,5 +1,5 @@
 #!/bin/bash
-# Hard 1080p (q95 noise): speculative sync vs the pass-based default, rocprof kernel trace.
+# Speculative sync vs the auto choice (SIZES, CONTENT: default hard 1080p q95), rocprof kernel trace.
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -7,10 +7,10 @@ for mode in auto spec; do
   tag=hard_$mode
   rm -rf gpurun_out/prof_$tag
   VF_JPEG_SYNC=$mode timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$tag -o ks -- \
-      python3 tools/jpeg_bench.py --sizes ${SIZES:-1080p} --batch 32 --iters 10 --cpu-seconds 0 --resident-only --content hard \
+      python3 tools/jpeg_bench.py --sizes ${SIZES:-1080p} --batch 32 --iters 10 --cpu-seconds 0 --resident-only --content ${CONTENT:-hard} \
       --out gpurun_out/$tag.jsonl > gpurun_out/$tag.log 2>&1 || { echo PROF_FAILED $tag; tail -30 gpurun_out/$tag.log; exit 1; }
   VF_JPEG_SYNC=$mode VF_JPEG_SYNC_STATS=1 timeout -k 10 120 python3 tools/jpeg_bench.py --sizes ${SIZES:-1080p} --batch 32 --iters 1 \
-      --cpu-seconds 0 --resident-only --content hard > gpurun_out/${tag}_stats.log 2>&1 || { echo STATS_FAILED; tail -20 gpurun_out/${tag}_stats.log; exit 1; }
+      --cpu-seconds 0 --resident-only --content ${CONTENT:-hard} > gpurun_out/${tag}_stats.log 2>&1 || { echo STATS_FAILED; tail -20 gpurun_out/${tag}_stats.log; exit 1; }
   grep -m2 "spec:" gpurun_out/${tag}_stats.log
 done
 python3 - <<'PY'
