@@ -75,6 +75,10 @@ def main():
                     help="1: frame copies and full checks run on threads pinned to the NUMA node of the "
                          "slot's ring slice (per-node pools; each node gets its own copy of the source "
                          "frames); 0: on the producer / one verification pool")
+    ap.add_argument("--consume", type=int, default=64, help="results taken per get_next_batch call")
+    ap.add_argument("--verify-pool", type=int, default=-1,
+                    help="JPEG results verified and released on the verification pool (1) or inline (0); "
+                         "-1: the pool from 2 workers on")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
 
@@ -280,27 +284,12 @@ def main():
                 if not (v_[:ENDS].tobytes() == w_[:ENDS] and v_[-ENDS:].tobytes() == w_[-ENDS:]):
                     errors.append(f"frame {i_} differs")
 
-        i = 0
-        t_start = None
-        while i < warm + n:
-            if t_start is None and i >= warm:
-                if sampler is not None:
-                    sampler.clear()
-                d_stats0 = d.ordering_stats()
-                t_start = time.perf_counter()
-                i_start = i
-                started.set()
-            b = d.get_next_batch(64, timeout=120)
-            k = len(b)
-            if not k:
-                raise RuntimeError(f"frame {i} never arrived: {d.ordering_stats()}")
-            idxs = b.index
-            if idxs[0] != i or idxs[-1] != i + k - 1:
-                errors.append(f"order: got {idxs[:4].tolist()}... expected from {i}")
-            release_t[i:i + k] = time.perf_counter()
-            if args.jpeg:
-                if i >= warm:
-                    total_bytes += int(np.asarray(fbytes)[idxs % len(fbytes)].sum())
+        pool_verify = args.verify_pool == 1 or (args.verify_pool < 0 and args.workers > 1)
+
+        def verify_jpeg(b, idxs):
+            """Lengths of every JPEG result in batch ``b``, whole frames every verify_every-th, head and
+            tail of the rest; then the batch's slots go back."""
+            try:
                 bad = np.flatnonzero(b.nbytes != want_len[idxs % len(want_np)])
                 for j in bad.tolist():
                     errors.append(f"frame {int(idxs[j])}: {int(b.nbytes[j])} B, expected {int(want_len[idxs[j] % len(want_np)])}")
@@ -311,7 +300,42 @@ def main():
                 rest = np.flatnonzero(idxs % args.verify_every != 0)
                 if len(rest):
                     check_ends(b, rest, idxs[rest])
+            finally:
                 d.release_frames(idxs)
+
+        i = 0
+        t_start = None
+        while i < warm + n:
+            if t_start is None and i >= warm:
+                if sampler is not None:
+                    sampler.clear()
+                d_stats0 = d.ordering_stats()
+                t_start = time.perf_counter()
+                i_start = i
+                started.set()
+            b = d.get_next_batch(args.consume, timeout=120)
+            k = len(b)
+            if not k:
+                raise RuntimeError(f"frame {i} never arrived: {d.ordering_stats()}")
+            idxs = b.index
+            if idxs[0] != i or idxs[-1] != i + k - 1:
+                errors.append(f"order: got {idxs[:4].tolist()}... expected from {i}")
+            release_t[i:i + k] = time.perf_counter()
+            if args.jpeg:
+                if i >= warm:
+                    total_bytes += int(np.asarray(fbytes)[idxs % len(fbytes)].sum())
+                # verified and released on the verification pool, a batch per task, so the
+                # checks of several GPUs' worth of results do not serialise on this thread (with
+                # one worker the hand-off costs more than it saves: inline)
+                if not pool_verify:
+                    verify_jpeg(b, idxs)
+                    i += k
+                    continue
+                pending.append(vpool.submit(verify_jpeg, b, idxs))
+                if len(pending) >= 64:
+                    for f_ in pending[:32]:
+                        f_.result()
+                    del pending[:32]
                 i += k
                 continue
             rel = []
@@ -349,7 +373,7 @@ def main():
         st = d.ordering_stats()
         st["max_depth"] = max(st["max_depth"], d_stats0["max_depth"])
         slices = [w["slice"] for w in st["workers"].values() if w["slice"]]
-        result = {"kind": "pipeline_jpeg" if args.jpeg else "pipeline", "size": args.size, "producers": nprod,
+        result = {"kind": "pipeline_jpeg" if args.jpeg else "pipeline", "size": args.size, "producers": nprod, "consume": args.consume, "verify_pool": bool(args.jpeg and pool_verify),
                   "workers": args.workers, "gpus": min(ngpu, args.workers),
                   "inflight_per_worker": inflight,
                   "policy": args.policy, "producer": args.producer, "batch": args.batch, "frames": n_t,
