@@ -1901,7 +1901,12 @@ int vfd_destroy(vfd_engine* e) {
 
 const char* vfd_last_error(vfd_engine* e) {
     if (!e) return "engine is NULL";
-    return e->err.c_str();
+    // err is written under the engine lock (by any thread); the caller gets its own copy, valid
+    // until its next call
+    thread_local std::string copy;
+    std::lock_guard<std::mutex> lk(e->mu);
+    copy = e->err;
+    return copy.c_str();
 }
 
 int vfd_reserve(vfd_engine* e, int64_t nbytes, int n, double timeout_s, int32_t* slots, int64_t* indices) {

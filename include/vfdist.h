@@ -98,6 +98,7 @@ int vfd_start(vfd_engine* e);
 int vfd_stop(vfd_engine* e);
 /* Stop, join, close every socket, unmap and unlink every ring slice, free everything. */
 int vfd_destroy(vfd_engine* e);
+/* The engine's last error message, copied for the calling thread (valid until its next call). */
 const char* vfd_last_error(vfd_engine* e);
 
 /* Ingest (distributor.py:173-203, lossless): reserve up to n ring slots for frames of at most
