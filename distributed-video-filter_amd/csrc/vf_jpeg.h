@@ -42,8 +42,7 @@ struct SpecBufs {
   // per lane slot [tr0 + workgroup * 256 + row * lanes + lane]; row k of workgroup w is
   // subsequence w * (256 / lanes - 1) + k
   uint64_t *tE;    // trajectory exit states
-  uint8_t *tG;     // walk with entry `lane`: trajectory at the subsequence (or kLinkNone)
-  uint64_t *tX;    //   its exit state
+  uint64_t *tX;    // walk with entry `lane`: its exit state at the subsequence
   uint32_t *tXc;   //   its block count in the subsequence
   uint64_t *pX;    // prefix records of k_resolve's serial traces (lane 0 slots)
   uint32_t *pC;
@@ -54,7 +53,7 @@ struct SpecBufs {
   uint64_t *qX;    // prefix records of the traces of walk columns that ended explicit (lane = e)
   uint32_t *qC;
   uint8_t *rL;     // resolved: where the prefix records are (0x80 | lane: pX, 0xC0 | lane: qX)
-  uint32_t *stats;  // diagnostics (builds with tools/sync_stats.patch applied; a round-4 layout)
+  uint32_t *stats;  // diagnostics (VF_JPEG_SYNC_STATS; k_spec's phases in VF_SPEC_PHASES builds)
 };
 constexpr int kSpecLanesMax = 16;
 inline uint32_t spec_lanes_host(int bpm) { return bpm <= 1 ? 1u : bpm <= 2 ? 2u : bpm <= 4 ? 4u : bpm <= 8 ? 8u : 16u; }

@@ -164,7 +164,7 @@ class Codec {
   uint32_t dmax_wg_ = 0;       // speculative sync: workgroups of the largest segment
   bool spec_ok_ = true;        // every frame fits the speculative resolver
   uint64_t spec_calls_ = 0, spec_fallbacks_ = 0;
-  DevBuf d_tE_, d_tG_, d_tX_, d_tXc_, d_pX_, d_pC_, d_wF_, d_rE_, d_rK_, d_qX_, d_qC_, d_rL_,
+  DevBuf d_tE_, d_tX_, d_tXc_, d_pX_, d_pC_, d_wF_, d_rE_, d_rK_, d_qX_, d_qC_, d_rL_,
       d_unres_;
   int sync_passes_ = 0;
   DevBuf d_in_, d_dfr_, d_dsg_, d_segs_, d_tile_, d_tsum_, d_totals_, d_us_, d_exit_[2], d_cnt_[2], d_used_, d_ck_, d_ckrem_, d_bstart_,

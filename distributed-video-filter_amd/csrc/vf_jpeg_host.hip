@@ -467,7 +467,6 @@ int Codec::prepare_decode(const uint8_t *const *jpegs, const size_t *sizes, int 
   {  // speculative sync (see SpecBufs)
     const size_t sl = (size_t)trs, wl = (size_t)wgs * kSpecLanesMax;
     CK(d_tE_.ensure(sizeof(uint64_t) * sl));
-    CK(d_tG_.ensure(sl));
     CK(d_tX_.ensure(sizeof(uint64_t) * sl));
     CK(d_tXc_.ensure(sizeof(uint32_t) * sl));
     CK(d_pX_.ensure(sizeof(uint64_t) * sl));
@@ -534,7 +533,7 @@ int Codec::run_decode(int bgr, bool invert, std::string *err) {
   int pass = 0, last = 0;
   uint32_t flag = 1;
   if (use_spec) {
-    SpecBufs sb{d_tE_.as<uint64_t>(), d_tG_.as<uint8_t>(), d_tX_.as<uint64_t>(), d_tXc_.as<uint32_t>(),
+    SpecBufs sb{d_tE_.as<uint64_t>(),  d_tX_.as<uint64_t>(), d_tXc_.as<uint32_t>(),
                 d_pX_.as<uint64_t>(),  d_pC_.as<uint32_t>(), d_wF_.as<uint8_t>(),  d_rE_.as<uint8_t>(),
                 d_rK_.as<uint32_t>(),  d_qX_.as<uint64_t>(), d_qC_.as<uint32_t>(), d_rL_.as<uint8_t>(),
                 d_unres_.as<uint32_t>()};
@@ -552,17 +551,18 @@ int Codec::run_decode(int bgr, bool invert, std::string *err) {
     ++spec_calls_;
     if (stats) {
       uint32_t st[16];
+      CK(hipStreamSynchronize(s_));  // the codec's stream is non-blocking: the copy below would not wait
       CK(hipMemcpy(st, d_unres_.p, sizeof st, hipMemcpyDeviceToHost));
       st[0] = 0;
       for (int i = 0; i < ns; ++i) st[0] += h_unres_.as<uint32_t>()[i];
-      std::fprintf(stderr, "[vf_jpeg] k_spec kcycles summed over workgroups, from start: part A %u, part B %u, "
-                   "walkers end %u (x bpm)\n", st[8], st[9], st[10]);
-      std::fprintf(stderr, "[vf_jpeg] spec: unresolved %u walker decodes %u traced workgroups %u traced subsequences "
-                   "%u link misses %u (workgroups %u, subsequences %u); k_resolve kcycles summed over frames: "
-                   "trace %u walk %u\n", st[0], st[1], st[2], st[3], st[4],
-                   dmax_wg_ * (uint32_t)ns, dmax_sub_ * (uint32_t)ns, st[5], st[6]);
-      std::fprintf(stderr, "[vf_jpeg] spec: walk columns ended explicit %u, their traces joined in one subsequence %u, "
-                   "serial traces %u (segments %d)\n", st[11], st[12], st[13], ns);
+      // VF_SPEC_PHASES builds only: [8] [9] [10] wall-clock ticks / 1024 summed over workgroups from
+      // after the table load to the end of part A, of part B, and (per walker) of the serial
+      // continuations; [1] walkers, [2] their explicit rows, [3] rows they wrote
+      std::fprintf(stderr, "[vf_jpeg] k_spec phases (VF_SPEC_PHASES, 1024 wall ticks summed): part A %u, part B %u, "
+                   "walkers end %u; walkers %u explicit rows %u rows written %u (workgroups %u)\n", st[8], st[9], st[10],
+                   st[1], st[2], st[3], dmax_wg_ * (uint32_t)ns);
+      std::fprintf(stderr, "[vf_jpeg] spec: unresolved %u; walk columns ended explicit %u, their traces joined in one "
+                   "subsequence %u, serial traces %u (segments %d)\n", st[0], st[11], st[12], st[13], ns);
     }
   }
   // pass-based: spans of G subsequences per thread (VF_JPEG_SYNC_G = 1, 2, 4, 8; 0 = the

@@ -1038,6 +1038,13 @@ __global__ __launch_bounds__(256) void k_spec(const DecSeg *__restrict__ sg, con
   for (uint32_t i = t; i < NS * (kSubBits / 32) + kSpecPadWords; i += 256)
     s_w[i] = woff + i < fwords ? gw[woff + i] : 0u;
   load_sync_tables(F, tabs);  // its barrier also publishes s_w
+#ifndef VF_SPEC_PHASES
+#define VF_SPEC_PHASES 0
+#endif
+  // VF_SPEC_PHASES (exp builds; VF_JPEG_SYNC_STATS prints them): wall-clock ticks / 1024 summed
+  // over workgroups from here to the end of part A, of part B, and per walker to the end of its
+  // serial continuation; with per-row counters, so timing only
+  const uint64_t ph0 = VF_SPEC_PHASES ? wall_clock64() : 0;
   // pack_state's (pos << 16 | z << 8 | c) as (pos - the workgroup's first bit) << 10 | z << 4 | c
   // (a workgroup spans at most 256 subsequences, 2^16 bits, plus a symbol's overshoot; z < 64,
   // c < 10), and back; the 32-bit kNoCk (0xFFFFFFFF) reads back with c = 15, which no decode has
@@ -1074,6 +1081,7 @@ __global__ __launch_bounds__(256) void k_spec(const DecSeg *__restrict__ sg, con
   s_E[t] = live ? rel(E) : 0u;
   __syncthreads();
   if (live) B.tE[ti] = E;
+  if (VF_SPEC_PHASES && t == 0) atomicAdd(B.stats + 8, (uint32_t)((wall_clock64() - ph0) >> 10));
   // B: link trajectory c0 of s-1 into s
   uint32_t M = kLinkNone, C = N;
   uint64_t X = 0;
@@ -1088,6 +1096,7 @@ __global__ __launch_bounds__(256) void k_spec(const DecSeg *__restrict__ sg, con
   s_C[t] = (uint16_t)C;
   s_X[t] = live && sl > 0 && M >= hg.bpm ? rel(X) : 0u;  // an explicit or the frame's last end state
   __syncthreads();
+  if (VF_SPEC_PHASES && t == 0) atomicAdd(B.stats + 9, (uint32_t)((wall_clock64() - ph0) >> 10));
   // C: the walks.  Walk e is trajectory e of the first subsequence followed through the links:
   // j_k = f_k(j_{k-1}), f_k(j) = s_M[k * L + j].  While every step is a link (no explicit
   // state), j_k = (f_k o ... o f_1)(e), and map composition is associative, so one lane per
@@ -1126,7 +1135,6 @@ __global__ __launch_bounds__(256) void k_spec(const DecSeg *__restrict__ sg, con
   if (t < nk) {
     if (t == 0) {
       for (uint32_t q = 0; q < bpm; ++q) {
-        B.tG[g0 + q] = (uint8_t)q;
         B.tX[g0 + q] = absl(s_E[q]);
         B.tXc[g0 + q] = s_C[q];  // trajectory count (used for the frame's first subsequence)
       }
@@ -1136,7 +1144,6 @@ __global__ __launch_bounds__(256) void k_spec(const DecSeg *__restrict__ sg, con
         if (p >= bpm) continue;  // stopped (last) or explicit (the serial walk below)
         const uint32_t M2 = s_M[t * L + p];
         const uint64_t st = absl(M2 < bpm ? s_E[t * L + M2] : s_X[t * L + p]);
-        B.tG[g0 + t * L + q] = (uint8_t)M2;
         B.tX[g0 + t * L + q] = st;
         B.tXc[g0 + t * L + q] = s_C[t * L + p];
         if (M2 == kLinkNone) {  // walk q turns explicit here: its serial continuation starts at t + 1
@@ -1167,6 +1174,7 @@ __global__ __launch_bounds__(256) void k_spec(const DecSeg *__restrict__ sg, con
         cnt = s_C[k * L + j];
         xe = absl(s_X[k * L + j]);
       } else {  // explicit state: link it into subsequence k here
+        if (VF_SPEC_PHASES) atomicAdd(B.stats + 2, 1u);  // explicit rows decoded by walkers
         const uint32_t bk = sk * kSubBits, ek = (sk + 1 >= nsub) ? nbits : (sk + 1) * kSubBits;
         const uint32_t row = k * L;
         M2 = spec_link(s_w, woff, st, bk, ek, sk + 1 == nsub, hg, tabs,
@@ -1181,9 +1189,9 @@ __global__ __launch_bounds__(256) void k_spec(const DecSeg *__restrict__ sg, con
         j = M2;  // kLinkNone (explicit) or kLinkLast
         st = xe;
       }
-      B.tG[g0 + k * L + e] = (uint8_t)j;
       B.tX[g0 + k * L + e] = st;
       B.tXc[g0 + k * L + e] = cnt;
+      if (VF_SPEC_PHASES) atomicAdd(B.stats + 3, 1u);  // rows written by walkers
       if (j == kLinkLast) break;
     }
     if (j == kLinkNone && nk == NS && blockIdx.x * NSS + NS < nsub) {
@@ -1200,6 +1208,10 @@ __global__ __launch_bounds__(256) void k_spec(const DecSeg *__restrict__ sg, con
       B.qC[g0 + 256 + L + e] = d.n;
     }
     B.wF[(uint64_t)(S.wg0 + blockIdx.x) * kSpecLanesMax + e] = (uint8_t)(j < hg.bpm ? j : kLinkNone);
+    if (VF_SPEC_PHASES) {
+      atomicAdd(B.stats + 10, (uint32_t)((wall_clock64() - ph0) >> 10));
+      atomicAdd(B.stats + 1, 1u);  // walkers that ran a serial continuation
+    }
   }
 }
 

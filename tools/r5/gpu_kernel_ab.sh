@@ -26,8 +26,7 @@ for rep in os.environ["REPS"].split():
         f = glob.glob(f"gpurun_out/prof_{tag}/**/*kernel_trace.csv", recursive=True)[0]
         dd = collections.defaultdict(list)
         for r in csv.DictReader(open(f)):
-            n = re.sub(r"\(.*", "", r["Kernel_Name"].replace("(anonymous namespace)::", "")).split("::")[-1]
-            n = re.sub(r"<.*", "", n)
+            n = re.sub(r"\(.*", "", re.sub(r"<[^()]*>", "", r["Kernel_Name"].replace("(anonymous namespace)::", ""))).split("::")[-1]
             if n in kern:
                 dd[n].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
         print(f"{v:10s} rep {rep}: " + "; ".join(f"{d.get('size')} resident {d['gpu_resident_fps']} parity {d['parity_vs_oracle']} "
