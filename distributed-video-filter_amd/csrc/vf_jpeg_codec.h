@@ -163,6 +163,7 @@ class Codec {
   uint64_t dblocks_ = 0, dpix_bytes_ = 0;
   uint32_t dmax_wg_ = 0;       // speculative sync: workgroups of the largest segment
   bool spec_ok_ = true;        // every frame fits the speculative resolver
+  bool tabs4_ = true;          // every frame fits the span sync's 4-table layout (DecFrame::tabs4)
   uint64_t spec_calls_ = 0, spec_fallbacks_ = 0;
   DevBuf d_tE_, d_tX_, d_tXc_, d_pX_, d_pC_, d_wF_, d_rE_, d_rK_, d_qX_, d_qC_, d_rL_,
       d_unres_;
@@ -195,6 +196,7 @@ class Codec {
   bool spec_check_ = false;           // run_decode queued that flag's read; check_decode tests it
   bool pass_check_ = false;           // the same for the last queued sync pass's change flag
   int sync_g_ = 4;                    // span width of the queued passes (finish_sync continues them)
+  int sync_t4_ = 0;                   // and their table layout (DecFrame::tabs4)
   int queued_ = kQueuedPasses;        // span passes queued by run_decode
   bool sync_spec_ = false;            // run_decode took the speculative sync (the write pass's form)
   int sync_last_ = 0;                 // exit / count slot of the pass-based sync's result

@@ -319,6 +319,7 @@ int Codec::prepare_decode(const uint8_t *const *jpegs, const size_t *sizes, int 
   const char *i24 = std::getenv("VF_JPEG_IDCT24");
   const bool idct24 = !(i24 && std::strcmp(i24, "0") == 0);
   d422_ = true;  // every frame standard 4:2:2 (k_idct_color422)
+  tabs4_ = true;  // every frame fits the span sync's 4-table layout (DecFrame::tabs4)
   for (int f = 0; f < n; ++f) {
     const Parsed &P = parsed[(size_t)f];
     DecFrame &F = dfr_[(size_t)f];
@@ -341,6 +342,26 @@ int Codec::prepare_decode(const uint8_t *const *jpegs, const size_t *sizes, int 
       dcm_ = dcm_ == -2 || dcm_ == (int)cm ? (int)cm : -1;
       d422_ = d422_ && g.ncomp == 3 && g.hs[0] == 2 && g.vs[0] == 1 && g.hs[1] == 1 && g.vs[1] == 1 &&
               g.hs[2] == 1 && g.vs[2] == 1 && g.bpm == 4;
+    }
+    {  // the span sync's 4-table layout: components with the same (DC, AC) table ids share a
+       // slot; a frame with three distinct pairs keeps the batch on the 6-table form
+      uint32_t s4 = 0, rep = 0;
+      int key[2] = {-1, -1}, nsl = 0;
+      bool ok = true;
+      for (int c = 0; c < P.ncomp && ok; ++c) {
+        const int k = P.td[c] * 16 + P.ta[c];
+        int sl = k == key[0] ? 0 : k == key[1] ? 1 : -1;
+        if (sl < 0 && nsl == 2) ok = false;
+        if (sl < 0 && ok) {
+          key[nsl] = k;
+          rep |= (uint32_t)c << (8 + 2 * nsl);
+          sl = nsl++;
+        }
+        if (ok) s4 |= (uint32_t)sl << (2 * c);
+      }
+      if (ok && nsl == 1) rep |= (rep & 0x300u) << 2;  // slot 1 unused: a copy of slot 0
+      F.tabs4 = ok ? (s4 | rep | 0x80000000u) : 0u;
+      tabs4_ = tabs4_ && ok;
     }
     F.blk0 = blk;
     for (int c = 0; c < P.ncomp; ++c) {
@@ -568,11 +589,19 @@ int Codec::run_decode(int bgr, bool invert, std::string *err) {
   // pass-based: spans of G subsequences per thread (VF_JPEG_SYNC_G = 1, 2, 4, 8; 0 = the
   // host-looped one-subsequence k_sync), kQueuedPasses passes queued without a host round trip
   // (a pass after convergence returns at once); the last pass's flag is read at check_decode
-  const int sync_g = [] {  // read per call: tests switch it inside one process
+  // With every frame on 4 table slots (DecFrame::tabs4; VF_JPEG_SYNC_TABS4=0 turns it off) the
+  // span sync's LDS leaves room for G = 5 at 3 workgroups per CU: 25 % more stream resident.
+  const bool t4 = tabs4_ && [] {
+    const char *v = std::getenv("VF_JPEG_SYNC_TABS4");
+    return !(v && std::strcmp(v, "0") == 0);
+  }();
+  const int sync_g = [t4] {  // read per call: tests switch it inside one process
     const char *v = std::getenv("VF_JPEG_SYNC_G");
-    const int g = v ? std::atoi(v) : 4;
+    const int g = v ? std::atoi(v) : t4 ? 5 : 4;
+    if (g == 5) return t4 ? 5 : 4;
     return g >= 0 && g <= 4 ? g : g == 8 ? 8 : 4;
   }();
+  const int g_t4 = t4 && (sync_g == 4 || sync_g == 5) ? 1 : 0;
   if (flag && sync_g > 0) {
     // VF_JPEG_SYNC_QUEUED = 1..kQueuedPasses (tests): fewer queued passes, so check_decode
     // reports them unconverged and finish_sync runs the rest
@@ -582,7 +611,7 @@ int Codec::run_decode(int bgr, bool invert, std::string *err) {
     for (int p = 0; p < queued_; ++p)
       CK(dec_syncg(sync_g, sg, fr, ns, dmax_sub_, d_us_.as<uint8_t>(), us_len, d_exit_[0].as<uint64_t>(),
                    d_cnt_[0].as<uint32_t>(), d_used_.as<uint64_t>(), d_ck_.as<uint64_t>(), d_ckrem_.as<uint32_t>(),
-                   d_changed_.as<uint32_t>(), p, sync_warm(), s_));
+                   d_changed_.as<uint32_t>(), p, sync_warm(), g_t4, s_));
     CK(h_flag_.ensure(64));
     CK(hipMemcpyAsync(h_flag_.p, d_changed_.as<uint32_t>() + queued_ - 1, sizeof(uint32_t),
                       hipMemcpyDeviceToHost, s_));
@@ -625,6 +654,7 @@ int Codec::run_decode(int bgr, bool invert, std::string *err) {
   sync_spec_ = use_spec;
   sync_last_ = last;
   sync_g_ = sync_g;
+  sync_t4_ = g_t4;
   return run_decode_post(bgr, invert, err);
 }
 
@@ -643,7 +673,7 @@ int Codec::finish_sync(std::string *err) {
     }
     CK(dec_syncg(sync_g_, sg, fr, dnseg_, dmax_sub_, d_us_.as<uint8_t>(), us_len, d_exit_[0].as<uint64_t>(),
                  d_cnt_[0].as<uint32_t>(), d_used_.as<uint64_t>(), d_ck_.as<uint64_t>(), d_ckrem_.as<uint32_t>(),
-                 d_changed_.as<uint32_t>(), p, sync_warm(), s_));
+                 d_changed_.as<uint32_t>(), p, sync_warm(), sync_t4_, s_));
     uint32_t flag = 0;
     CK(hipMemcpyAsync(&flag, d_changed_.as<uint32_t>() + p, sizeof flag, hipMemcpyDeviceToHost, s_));
     CK(hipStreamSynchronize(s_));

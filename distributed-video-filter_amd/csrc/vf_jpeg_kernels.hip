@@ -537,13 +537,40 @@ __device__ __forceinline__ void load_sync_tabs32(const DecFrame &F, SyncTab32 *t
   __syncthreads();
 }
 
-template <typename Tab>
+// The span sync's 4-table layout (DecFrame::tabs4: at most two distinct (DC, AC) table pairs over
+// the components -- every frame whose chroma components share tables): slot s's DC table at
+// tabs[s], its AC table with the pairs at tabs[2 + s], from the component tabs4 names for it;
+// 9.6 KB of LDS instead of 14.4, so a workgroup stages 25 % more stream (G = 5) at 3 per CU.
+// The lanes' cpack then holds slots (tabs4_cpack), not components.  Then a barrier.
+__device__ __forceinline__ void load_sync_tabs4(const DecFrame &F, SyncTab32 *tabs) {
+  const uint32_t rep[2] = {(F.tabs4 >> 8) & 3u, (F.tabs4 >> 10) & 3u};
+  for (uint32_t j = threadIdx.x; j < 4 * (8 + 18 + 64); j += blockDim.x) {
+    const uint32_t t = j / 90, i = j - t * 90;
+    const HuffSync &S = t < 2 ? F.sdc[rep[t]] : F.sac[rep[t - 2]];
+    if (i < 8) tabs[t].lim[i] = S.lim[i];
+    else if (i < 26) tabs[t].valoff[i - 8] = S.valoff[i - 8];
+    else reinterpret_cast<uint32_t *>(tabs[t].vals)[i - 26] = reinterpret_cast<const uint32_t *>(S.vals)[i - 26];
+  }
+  for (uint32_t j = threadIdx.x; j < 4 * (1 << kLook); j += blockDim.x) {
+    const uint32_t t = j >> kLook, i = j & ((1 << kLook) - 1);
+    tabs[t].sfast[i] = t < 2 ? (uint32_t)F.sdc[rep[t]].sfast[i]
+                             : F.sac[rep[t - 2]].sfast[i] | ((uint32_t)F.spair[rep[t - 2]][i] << 16);
+  }
+  __syncthreads();
+}
+__device__ __forceinline__ uint32_t tabs4_cpack(const HuffGeom &hg, uint32_t tabs4) {  // block-in-MCU -> slot
+  uint32_t p = 0;
+  for (uint32_t c = 0; c < hg.bpm; ++c) p |= ((tabs4 >> (2 * hg.comp(c))) & 3u) << (2 * c);
+  return p;
+}
+
+template <typename Tab, uint32_t NDC = 3>  // NDC: DC tables before the AC tables in `tabs`
 struct SyncLane {
   const uint32_t *w;  // staged words, minus woff
   uint64_t buf;       // next bits, left-aligned
   uint32_t nb, wi, nxt, pos;
   uint32_t z, c, n;   // zigzag index, block-in-MCU, blocks completed
-  uint32_t toff;      // byte offset of the DC table of c's component (its AC table: 3 tables on)
+  uint32_t toff;      // byte offset of the DC table of c's component (its AC table: NDC tables on)
   uint32_t cpack, bpm;
   __device__ __forceinline__ void init(const uint32_t *words, uint32_t woff, uint64_t X, const HuffGeom &hg) {
     const uint32_t p = (uint32_t)(X >> 16);
@@ -571,7 +598,7 @@ struct SyncLane {
     wi += f ? 1u : 0u;
     nxt = w[wi];
     const Tab &T = *reinterpret_cast<const Tab *>(reinterpret_cast<const char *>(tabs) + toff +
-                                                   (z == 0 ? 0u : 3u * (uint32_t)sizeof(Tab)));
+                                                   (z == 0 ? 0u : NDC * (uint32_t)sizeof(Tab)));
     uint32_t e = T.sfast[(uint32_t)(buf >> (64 - kLook))];
     if (!e) {  // a code longer than kLook bits: jdhuff.c's slow path (rare)
       const uint32_t c16 = (uint32_t)(buf >> 48);
@@ -757,12 +784,12 @@ __global__ __launch_bounds__(256) void k_sync(const DecSeg *__restrict__ sg, con
 // current mark's record stores, because vmcnt counts stores too: loaded after them, the wait for
 // it at the next mark also waited for the stores' completion, every 64 bits.  The first decode
 // (no records yet) has no loads in its loop at all.
-template <bool CHECK>
+template <bool CHECK, uint32_t NDC>
 __device__ __forceinline__ uint64_t sync_span(const uint32_t *words, uint32_t woff, uint64_t X, uint32_t i0, uint32_t ng,
                                               uint32_t nsub, uint32_t nbits, uint64_t gi0, uint64_t last,
                                               uint64_t *exits, uint32_t *cnts, uint64_t *ck, uint32_t *ckrem,
                                               const HuffGeom &hg, const SyncTab32 *tabs) {
-  SyncLane<SyncTab32> d;
+  SyncLane<SyncTab32, NDC> d;
   d.init(words, woff, X, hg);
   uint32_t j = 0, bj = i0 * kSubBits;
   uint32_t ej = i0 + 1 >= nsub ? nbits : bj + kSubBits;  // end of subsequence j
@@ -830,19 +857,19 @@ __device__ __forceinline__ uint64_t sync_span(const uint32_t *words, uint32_t wo
 #define VF_SYNCG_STAGE 1
 #endif
 constexpr bool kSyncgStage = VF_SYNCG_STAGE;
-constexpr uint32_t syncg_threads(int G) { return !kSyncgStage || G <= 4 ? 256u : 1024u / (uint32_t)G; }
+constexpr uint32_t syncg_threads(int G) { return !kSyncgStage || G <= 5 ? 256u : 1024u / (uint32_t)G; }
 // Pass 0's guessed entries can be warmed: a thread first decodes the `warm` bits before its span
 // from a guessed state (nothing recorded), so its entry is the state at the first symbol boundary
 // at or past the span's start, usually the true one already (tools/sync_sim.py --warm).
 constexpr uint32_t kSyncWarmMax = 4096;
-template <int G>
+template <int G, uint32_t NDC>  // NDC 3: six tables (one per component); 2: DecFrame::tabs4's four
 __global__ __launch_bounds__(256) void k_syncg(const DecSeg *__restrict__ sg, const DecFrame *__restrict__ fr, const uint8_t *us,
                                                const uint32_t *us_len, uint64_t *exits, uint32_t *cnts, uint64_t *used,
                                                uint64_t *ck, uint32_t *ckrem, uint32_t *changed, int pass, uint32_t warm) {
   constexpr uint32_t kWarmWords = kSyncWarmMax / 32;
   constexpr uint32_t T = syncg_threads(G),
                      kWords = kSyncgStage ? kWarmWords + T * G * (kSubBits / 32) + kSpecPadWords : 1;
-  __shared__ SyncTab32 tabs[6];
+  __shared__ SyncTab32 tabs[2 * NDC];
   // exits relative to the workgroup's first bit in 32 bits, (pos - wbit) << 10 | z << 4 | c (as
   // k_spec's): 1 KB less LDS, which with G = 3 makes 4 workgroups per CU fit (40.7 KB)
   __shared__ uint32_t s_exit[T];
@@ -869,8 +896,10 @@ __global__ __launch_bounds__(256) void k_syncg(const DecSeg *__restrict__ sg, co
     }
   }
   const uint32_t *words = kSyncgStage ? s_w : gw;
-  load_sync_tabs32(F, tabs);  // its barrier also publishes s_w
-  const HuffGeom hg(F.g);
+  if constexpr (NDC == 2) load_sync_tabs4(F, tabs);  // its barrier also publishes s_w
+  else load_sync_tabs32(F, tabs);
+  HuffGeom hg(F.g);
+  if constexpr (NDC == 2) hg.cpack = tabs4_cpack(hg, F.tabs4);
   const uint32_t t = threadIdx.x;
   const uint32_t nbits = us_len[blockIdx.y] * 8u, nsub = (nbits + kSubBits - 1) / kSubBits;
   const uint32_t i0 = (blockIdx.x * T + t) * G;
@@ -884,7 +913,7 @@ __global__ __launch_bounds__(256) void k_syncg(const DecSeg *__restrict__ sg, co
       entry = i0 == 0 ? 0 : pack_state(i0 * kSubBits, 0, 0);  // a guess, except at the segment's start
       if (i0 > 0 && warm > 0) {
         const uint32_t b = i0 * kSubBits, w0 = b > warm ? b - warm : 0u;
-        SyncLane<SyncTab32> d;
+        SyncLane<SyncTab32, NDC> d;
         d.init(words, woff, pack_state(w0, 0, 0), hg);
         while (d.pos < b) d.step(tabs, b);
         entry = pack_state(d.pos, d.z, d.c);
@@ -900,8 +929,8 @@ __global__ __launch_bounds__(256) void k_syncg(const DecSeg *__restrict__ sg, co
   bool check = pass > 0;  // records are valid from the first decode on
   for (;;) {
     if (need) {
-      last = check ? sync_span<true>(words, woff, entry, i0, ng, nsub, nbits, gi0, last, exits, cnts, ck, ckrem, hg, tabs)
-                   : sync_span<false>(words, woff, entry, i0, ng, nsub, nbits, gi0, last, exits, cnts, ck, ckrem, hg, tabs);
+      last = check ? sync_span<true, NDC>(words, woff, entry, i0, ng, nsub, nbits, gi0, last, exits, cnts, ck, ckrem, hg, tabs)
+                   : sync_span<false, NDC>(words, woff, entry, i0, ng, nsub, nbits, gi0, last, exits, cnts, ck, ckrem, hg, tabs);
       used[gi0] = entry;
     }
     s_exit[t] = live ? rel(last) : 0u;
@@ -3244,21 +3273,25 @@ hipError_t dec_sync(const DecSeg *__restrict__ sg, const DecFrame *__restrict__ 
 
 hipError_t dec_syncg(int G, const DecSeg *__restrict__ sg, const DecFrame *__restrict__ fr, int nseg, uint32_t max_sub,
                      const uint8_t *us, const uint32_t *us_len, uint64_t *exits, uint32_t *cnts, uint64_t *used,
-                     uint64_t *ck, uint32_t *ckrem, uint32_t *changed, int pass, uint32_t warm, hipStream_t s) {
+                     uint64_t *ck, uint32_t *ckrem, uint32_t *changed, int pass, uint32_t warm, int tabs4,
+                     hipStream_t s) {
   if (nseg <= 0 || !max_sub) return hipSuccess;
   warm = std::min<uint32_t>(warm, kSyncWarmMax) & ~31u;
-#define VF_SYNCG(GG)                                                                                              \
-  if (G == GG) {                                                                                                  \
+#define VF_SYNCG(GG, ND)                                                                                          \
+  if (G == GG && (ND == 2) == (tabs4 != 0)) {                                                                     \
     const uint32_t span = syncg_threads(GG) * GG;                                                                 \
-    hipLaunchKernelGGL(k_syncg<GG>, dim3((max_sub + span - 1) / span, (unsigned)nseg), dim3(syncg_threads(GG)),   \
-                       0, s, sg, fr, us, us_len, exits, cnts, used, ck, ckrem, changed, pass, warm);              \
+    hipLaunchKernelGGL((k_syncg<GG, ND>), dim3((max_sub + span - 1) / span, (unsigned)nseg),                      \
+                       dim3(syncg_threads(GG)), 0, s, sg, fr, us, us_len, exits, cnts, used, ck, ckrem, changed,  \
+                       pass, warm);                                                                               \
     return hipGetLastError();                                                                                     \
   }
-  VF_SYNCG(1)
-  VF_SYNCG(2)
-  VF_SYNCG(3)
-  VF_SYNCG(4)
-  VF_SYNCG(8)
+  VF_SYNCG(1, 3)
+  VF_SYNCG(2, 3)
+  VF_SYNCG(3, 3)
+  VF_SYNCG(4, 3)
+  VF_SYNCG(8, 3)
+  VF_SYNCG(4, 2)
+  VF_SYNCG(5, 2)
 #undef VF_SYNCG
   return hipErrorInvalidValue;
 }

@@ -124,6 +124,10 @@ struct DecFrame {
   uint32_t flags;          // bit 0: fancy upsampling allowed; bits 1-2: k_color layout (0 other,
                            // 1 4:4:4, 2 chroma 2x1, 3 chroma 2x2; three components, full-size luma);
                            // kDecIdct24: the IDCT's column pass may use 24-bit multiplies
+  // The span sync's 4-table layout (vf_jpeg_kernels.hip load_sync_tabs4): bits 0-5 the table
+  // slot (0 / 1) of each component, 2 bits each; bits 8-9 / 10-11 the component whose tables
+  // fill slot 0 / 1; bit 31: the frame has at most two distinct (DC, AC) table pairs
+  uint32_t tabs4;
   uint64_t blk0;           // first block in the batch coefficient buffer
   uint64_t dcbase[3];      // per-component DC sequences in the DC buffer
   uint64_t plane_off[3];   // component planes in the plane buffer

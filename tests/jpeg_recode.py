@@ -87,8 +87,9 @@ class _Bits:
         raise ValueError("bad Huffman code")
 
 
-def tokens(jpeg: bytes):
-    """The scan's symbols in order: (class, table id, symbol, extra value, extra bits)."""
+def tokens(jpeg: bytes, with_comp: bool = False):
+    """The scan's symbols in order: (class, table id, symbol, extra value, extra bits), plus the
+    component with ``with_comp``."""
     segs, ecs, _ = _segments(jpeg)
     tabs = _dht_tables(segs)
     sof = next(pl for m, pl in segs if m in (0xC0, 0xC1))
@@ -110,12 +111,12 @@ def tokens(jpeg: bytes):
     out = []
     for c in order:
         s = br.sym(dec[(0, td[c])])
-        out.append((0, td[c], s, br.read(s), s))
+        out.append((0, td[c], s, br.read(s), s) + ((c,) if with_comp else ()))
         k = 1
         while k < 64:
             rs = br.sym(dec[(1, ta[c])])
             r, s = rs >> 4, rs & 15
-            out.append((1, ta[c], rs, br.read(s), s))
+            out.append((1, ta[c], rs, br.read(s), s) + ((c,) if with_comp else ()))
             if s:
                 k += r + 1
             elif r == 15:
@@ -139,14 +140,23 @@ def long_tables(freq: Counter, short_len: int, nshort: int, long_len: int) -> Tu
     return bits, [s for ln in sorted(vals_by_len) for s in vals_by_len[ln]]
 
 
-def recode(jpeg: bytes, dc_long: int = 10, ac_long: int = 12, share: bool = False) -> bytes:
+# split=True: table ids per component (DC, AC) -- three distinct pairs, so the components share
+# no slot of the span sync's 4-table layout (DecFrame::tabs4) and a batch with such a frame
+# takes the 6-table form
+SPLIT_IDS = [(0, 0), (1, 1), (1, 0)]
+
+
+def recode(jpeg: bytes, dc_long: int = 10, ac_long: int = 12, share: bool = False, split: bool = False) -> bytes:
     """The same image with new tables: per table id, the 2 (DC) / 8 (AC) most frequent
     symbols get 2 / 4-bit codes, every other symbol dc_long / ac_long bits.  share=True puts
-    every component on table 0 of each class."""
+    every component on table 0 of each class; split=True gives components 0, 1, 2 the table ids
+    SPLIT_IDS (three components only)."""
     segs, _, tail = _segments(jpeg)
-    toks = tokens(jpeg)
+    toks = tokens(jpeg, with_comp=split)
     if share:
         toks = [(cl, 0, s, v, n) for cl, _, s, v, n in toks]
+    if split:
+        toks = [(cl, SPLIT_IDS[c][cl], s, v, n) for cl, _, s, v, n, c in toks]
     freq: Dict[Tuple[int, int], Counter] = {}
     for cl, th, s, _, _ in toks:
         freq.setdefault((cl, th), Counter())[s] += 1
@@ -184,10 +194,10 @@ def recode(jpeg: bytes, dc_long: int = 10, ac_long: int = 12, share: bool = Fals
             continue
         if m == 0xDA:
             hdr += b"\xff\xc4" + (len(dht) + 2).to_bytes(2, "big") + dht
-            if share:
+            if share or split:
                 pl = bytearray(pl)
                 for c in range(pl[0]):
-                    pl[2 + 2 * c] = 0
+                    pl[2 + 2 * c] = (SPLIT_IDS[c][0] << 4) | SPLIT_IDS[c][1] if split else 0
                 pl = bytes(pl)
         hdr += bytes([0xFF, m]) + (len(pl) + 2).to_bytes(2, "big") + pl
     return bytes(hdr) + bytes(out) + tail

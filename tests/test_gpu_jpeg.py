@@ -250,8 +250,8 @@ def _span_sync_batch(quality=95, subsamp=J.TJSAMP_422):
     return [J.encode(im, quality, J.TJPF_BGR, subsamp) for im in imgs]
 
 
-@pytest.mark.parametrize("g,warm", [("0", "0"), ("1", "0"), ("2", "0"), ("3", "0"), ("4", "0"), ("8", "0"), ("3", "2048"), ("4", "256"),
-                                    ("4", "2048"), ("8", "4096"), ("1", "1000")])
+@pytest.mark.parametrize("g,warm", [("0", "0"), ("1", "0"), ("2", "0"), ("3", "0"), ("4", "0"), ("5", "0"), ("8", "0"), ("3", "2048"),
+                                    ("4", "256"), ("4", "2048"), ("5", "2048"), ("8", "4096"), ("1", "1000")])
 def test_span_sync_widths(tj, monkeypatch, g, warm):
     """The pass-based sync with G subsequences per thread (k_syncg: records updated in place,
     passes queued and returning early once no workgroup's last exit changes; G = 0: the
@@ -268,6 +268,27 @@ def test_span_sync_widths(tj, monkeypatch, g, warm):
         assert o == J.invert_jpeg(j)
     for j in jpgs[:2]:
         assert np.array_equal(tj.decode(j), J.decode(j))
+
+
+@pytest.mark.parametrize("tabs4", ["1", "0"])
+def test_span_sync_table_layouts(tj, monkeypatch, tabs4):
+    """The span sync's two table layouts: four tables (components with the same (DC, AC) table
+    ids share a slot: Annex K frames, shared tables, grayscale), which leave the LDS for G = 5,
+    and six (a batch holding a frame with three distinct table pairs, jpeg_recode's split=True,
+    or VF_JPEG_SYNC_TABS4=0; G = 5 is then run as 4), through several workgroups per frame and
+    the unconverged-pass continuation, bit-exact with the oracle."""
+    import jpeg_recode as R
+    monkeypatch.setenv("VF_JPEG_SYNC", "pass")
+    monkeypatch.setenv("VF_JPEG_SYNC_TABS4", tabs4)
+    monkeypatch.delenv("VF_JPEG_SYNC_G", raising=False)
+    base = _span_sync_batch()
+    small = J.encode(_img("scene", 10, 96, 128), 85, J.TJPF_BGR, J.TJSAMP_444)
+    extra = [R.recode(small, split=True), R.recode(small, ac_long=16, share=True),
+             J.encode(_img("scene", 9, 120, 200), 85, J.TJPF_BGR, J.TJSAMP_GRAY)]
+    for batch, queued in ((base, "4"), (base + extra, "4"), (extra[1:], "4"), (base, "1")):
+        monkeypatch.setenv("VF_JPEG_SYNC_QUEUED", queued)
+        assert [bytes(g) for g in tj.invert_batch(batch)] == [J.invert_jpeg(j) for j in batch]
+    assert np.array_equal(tj.decode(extra[0]), J.decode(extra[0]))
 
 
 @pytest.mark.parametrize("queued", ["1", "2"])

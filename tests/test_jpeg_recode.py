@@ -16,10 +16,12 @@ def _srcs():
             J.encode(J.synthetic_scene(6, 40, 56), 85, J.TJPF_BGR, J.TJSAMP_GRAY)]
 
 
-@pytest.mark.parametrize("kw", [{}, {"dc_long": 11, "ac_long": 10}, {"ac_long": 16, "share": True}])
+@pytest.mark.parametrize("kw", [{}, {"dc_long": 11, "ac_long": 10}, {"ac_long": 16, "share": True}, {"split": True}])
 def test_recode_keeps_pixels(kw):
     have_lib = J.libjpeg_available()[0]
     for j in _srcs():
+        if kw.get("split") and J.info(j)["ncomp"] != 3:
+            continue  # three components only
         r = R.recode(j, **kw)
         assert r != j
         want = J.decode(j)
@@ -35,3 +37,13 @@ def test_recoded_tables_have_many_long_codes():
     assert need > 12
     annex_k = R._dht_tables(R._segments(_srcs()[0])[0])
     assert sum(R.long_prefixes(bits) for bits, _ in annex_k.values()) == 11  # 5 + 5 + 1 + 0
+
+
+def test_split_tables_give_three_distinct_pairs():
+    """recode(split=True): components 0, 1, 2 on (DC, AC) table ids (0, 0), (1, 1), (1, 0) --
+    the case the span sync's 4-table layout cannot hold (vf_jpeg_host.hip, DecFrame::tabs4)."""
+    r = R.recode(_srcs()[0], split=True)
+    segs, _, _ = R._segments(r)
+    sos = next(pl for m, pl in segs if m == 0xDA)
+    assert [(sos[2 + 2 * c] >> 4, sos[2 + 2 * c] & 15) for c in range(3)] == R.SPLIT_IDS
+    assert set(R._dht_tables(segs)) == {(0, 0), (0, 1), (1, 0), (1, 1)}

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Per-kernel timing A/B over libraries (VARIANTS="name=path ..."), rocprofv3 kernel trace of
+# Per-kernel timing A/B over libraries (VARIANTS="name=path[@VAR=VAL,...] ..."), rocprofv3 kernel trace of
 # tools/jpeg_bench.py (SIZES, CONTENT, resident only), REPS reps, means of the kernels in KERNELS.
 set -o pipefail
 mkdir -p gpurun_out
@@ -8,9 +8,10 @@ export VARIANTS KERNELS=${KERNELS:-"k_idct_color422 k_fdct"} SIZES=${SIZES:-1080
 for rep in $REPS; do
 for nv in $VARIANTS; do
   v=${nv%%=*}; lib=${nv#*=}
+  envs=""; case "$lib" in *@*) envs=${lib#*@}; lib=${lib%%@*};; esac  # name=path@VAR=VAL,VAR=VAL
   tag=kab_${v}_$rep
   rm -rf gpurun_out/prof_$tag
-  VFILTER_LIB=$lib timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$tag -o ks -- \
+  env ${envs//,/ } VFILTER_LIB=$lib timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$tag -o ks -- \
       python3 tools/jpeg_bench.py --sizes $SIZES --batch 32 --iters 10 --cpu-seconds 0 --resident-only --content $CONTENT \
       --out gpurun_out/$tag.jsonl > gpurun_out/$tag.log 2>&1 || { echo PROF_FAILED $tag; tail -30 gpurun_out/$tag.log; exit 1; }
 done
