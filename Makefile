@@ -29,16 +29,20 @@ $(LIB): $(SRCS) $(HDRS)
 oracle:
 	$(MAKE) -C oracle
 
-tools: tools/tune_invert tools/pcie_probe
+tools: tools/tune_invert tools/pcie_probe tools/vfd_load
 
 tools/pcie_probe: tools/pcie_probe.hip
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 $< -o $@
+
+# the native control plane driven from C++ alone (load generator, --chaos; host only)
+tools/vfd_load: tools/vfd_load.cc $(DLIB) include/vfdist.h
+	$(CXX) -O2 -std=c++17 -Iinclude tools/vfd_load.cc -o $@ -L$(dir $(DLIB)) -lvfdist -Wl,-rpath,$(abspath $(dir $(DLIB))) -pthread
 
 tools/tune_invert: tools/tune_invert.hip $(CSRC)/vf_kernels.hip $(CSRC)/vf_internal.h $(CSRC)/vf_stream.h
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -Iinclude -I$(CSRC) tools/tune_invert.hip $(CSRC)/vf_kernels.hip -o $@
 
 clean:
-	rm -f $(LIB) $(DLIB) tools/tune_invert tools/pcie_probe
+	rm -f $(LIB) $(DLIB) tools/tune_invert tools/pcie_probe tools/vfd_load
 	$(MAKE) -C oracle clean
 
 # Experiment libraries (timing A/Bs against the product library; never loaded by the product):
