@@ -154,7 +154,11 @@ class Codec {
   hipEvent_t done_ = nullptr;  // the last call's downloads have landed
 
   // decode layout
-  std::vector<DecFrame> dfr_;
+  // the batch's frames (21 KB each, mostly tables), built by the parse tasks straight into
+  // page-locked memory and uploaded from there: no 21 KB-per-frame zero fill and copy on the
+  // submitting thread
+  HostBuf h_dfr_;
+  DecFrame *dfr_ = nullptr;
   std::vector<DecSeg> dsg_;    // entropy-coded segments: one per frame, or one per restart interval
   std::vector<const uint8_t *> seg_src_;  // each segment's raw bytes in the caller's JPEG
   int dn_ = 0, dnseg_ = 0, ndcseg_ = 0;

@@ -15,6 +15,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <new>
 #include <string>
 #include <vector>
 
@@ -290,7 +291,8 @@ int Codec::prepare_decode(const uint8_t *const *jpegs, const size_t *sizes, int 
     *err = "empty batch";
     return kInvalid;
   }
-  dfr_.assign((size_t)n, DecFrame());
+  CK(h_dfr_.ensure(sizeof(DecFrame) * (size_t)n));
+  dfr_ = h_dfr_.as<DecFrame>();
   seg_src_.clear();
   std::vector<Parsed> parsed((size_t)n);
   uint64_t in_off = 0, us_off = 0, blk = 0, dcoff = 0, plane = 0, pix = 0;
@@ -304,7 +306,7 @@ int Codec::prepare_decode(const uint8_t *const *jpegs, const size_t *sizes, int 
   pool_.run(n, [&](int f) {
     Parsed &P = parsed[(size_t)f];
     std::string &e = ferr[(size_t)f];
-    DecFrame &F = dfr_[(size_t)f];
+    DecFrame &F = *new (&dfr_[(size_t)f]) DecFrame();  // value-initialised, by the frame's own task
     parse_frame(jpegs[f], sizes[f], max_pixels_, &P, &F.g, F.dc, F.ac, F.sdc, F.sac, F.spair, &e);  // vf_jpeg_parse.h
     for (int c = 0; c < P.ncomp && e.empty(); ++c) std::memcpy(F.q[c], P.qt[P.tq[c]], sizeof F.q[c]);
   });
@@ -511,14 +513,13 @@ int Codec::prepare_decode(const uint8_t *const *jpegs, const size_t *sizes, int 
   // codec's next call, which starts after this one has synchronised)
   const size_t dsz = sizeof(DecFrame) * (size_t)n, gsz = sizeof(DecSeg) * (size_t)dnseg_,
                ssz = sizeof(ScanSeg) * segs.size();
-  CK(h_ddesc_.ensure(dsz + gsz + ssz));
-  std::memcpy(h_ddesc_.as<uint8_t>(), dfr_.data(), dsz);
-  std::memcpy(h_ddesc_.as<uint8_t>() + dsz, dsg_.data(), gsz);
-  std::memcpy(h_ddesc_.as<uint8_t>() + dsz + gsz, segs.data(), ssz);
+  CK(h_ddesc_.ensure(gsz + ssz));
+  std::memcpy(h_ddesc_.as<uint8_t>(), dsg_.data(), gsz);
+  std::memcpy(h_ddesc_.as<uint8_t>() + gsz, segs.data(), ssz);
   CK(hipMemcpyAsync(d_in_.p, h_stage_.p, in_off, hipMemcpyHostToDevice, s_));
-  CK(hipMemcpyAsync(d_dfr_.p, h_ddesc_.p, dsz, hipMemcpyHostToDevice, s_));
-  CK(hipMemcpyAsync(d_dsg_.p, h_ddesc_.as<uint8_t>() + dsz, gsz, hipMemcpyHostToDevice, s_));
-  CK(hipMemcpyAsync(d_segs_.p, h_ddesc_.as<uint8_t>() + dsz + gsz, ssz, hipMemcpyHostToDevice, s_));
+  CK(hipMemcpyAsync(d_dfr_.p, h_dfr_.p, dsz, hipMemcpyHostToDevice, s_));
+  CK(hipMemcpyAsync(d_dsg_.p, h_ddesc_.p, gsz, hipMemcpyHostToDevice, s_));
+  CK(hipMemcpyAsync(d_segs_.p, h_ddesc_.as<uint8_t>() + gsz, ssz, hipMemcpyHostToDevice, s_));
   return kOk;
 }
 

@@ -12,7 +12,7 @@ from vfilter import Context  # noqa: E402
 from vfilter.jpeg import TurboJPEG  # noqa: E402
 
 size = sys.argv[1] if len(sys.argv) > 1 else "1080p"
-h, w = {"480p": (480, 640), "1080p": (1080, 1920), "4k": (2160, 3840)}[size]
+h, w = {"512sq": (512, 512), "480p": (480, 640), "1080p": (1080, 1920), "4k": (2160, 3840)}[size]
 ctx = Context(0)
 tj = TurboJPEG(ctx=ctx)
 frames = [J.synthetic_scene(s, h, w) for s in range(8)]
