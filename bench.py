@@ -722,15 +722,15 @@ def distributor_leg(nworkers, ngpu, host_gbps=None, pcie_gbps=None, frames_scale
                            (640 * 480 + 1920 * 1080 + 3840 * 2160) * 3 // 3, 4.25),
             # the reference's default deployment: JPEG frames, workers in JPEG mode
             "jpeg_1080p": (["--jpeg", "--size", "1080p", "--batch", "32", "--policy", "pull",
-                            "--frames", str(int(12288 * nworkers * frames_scale))], 181876, None),
+                            "--frames", str(int(24576 * nworkers * frames_scale))], 181876, None),
             # the same deployment on hard content: 32 distinct noisy scenes at q95
             "jpeg_1080p_hard": (["--jpeg", "--content", "hard", "--size", "1080p", "--batch", "32", "--policy",
-                                 "pull", "--frames", str(int(1536 * nworkers * frames_scale))], None, None),
+                                 "pull", "--frames", str(int(4608 * nworkers * frames_scale))], None, None),
             # the reference app's own operating point (webcam_app.py:17,97-111: 512 x 512, q85 4:2:2)
             "jpeg_512": (["--jpeg", "--size", "512sq", "--batch", "32", "--policy", "pull",
-                          "--frames", str(int(32768 * nworkers * frames_scale))], None, None),
+                          "--frames", str(int(98304 * nworkers * frames_scale))], None, None),
             "jpeg_480p": (["--jpeg", "--size", "480p", "--batch", "32", "--policy", "pull",
-                           "--frames", str(int(32768 * nworkers * frames_scale))], None, None)}
+                           "--frames", str(int(98304 * nworkers * frames_scale))], None, None)}
     worker_form = {"jpeg_1080p": (jpeg or {}).get("host_to_host_worker_fps")}
     for k_, pn in (("jpeg_512", "512sq"), ("jpeg_480p", "480p")):
         worker_form[k_] = ((jpeg or {}).get("operating_points") or {}).get(pn, {}).get("host_to_host_worker_fps")
