@@ -517,6 +517,9 @@ def end_to_end_ring(device, host_batch, batch, np, reps=16):
                               "pinned_pipelined_GBps_each_way")}
 
 
+SMALL_BATCH = 64  # JPEG frames of the reference app's size (512 x 512, 480p): worker batch
+
+
 def jpeg_mode(ctx, batch, iters=20):
     """The reference's default mode (use_jpeg=True): decode -> bitwise_not -> encode per frame
     (inverter.py:32 -> :41 -> :44) on 1080p JPEGs made with the PyTurboJPEG defaults (q85,
@@ -562,15 +565,18 @@ def jpeg_mode(ctx, batch, iters=20):
     passes = stages.pop("sync_passes", 0.0)
     # the reference app's own frames (webcam_app.py:17,97-111: 512 x 512 crops, PyTurboJPEG's
     # defaults) and 480p: the rates the distributor legs jpeg_512 / jpeg_480p are compared with
+    # in batches of SMALL_BATCH: a worker's per-batch host costs (parse, ~25 launches) halve per
+    # frame against 32, +30-50 % through the system at these sizes (profiles/r05_small_batch_ab.txt)
     points = {}
     for pname, (ph, pw) in (("512sq", (512, 512)), ("480p", (480, 640))):
         pj = tj.encode_batch([synthetic_scene(s, ph, pw) for s in range(8)])
-        pj = [pj[i % len(pj)] for i in range(batch)]
+        pj = [pj[i % len(pj)] for i in range(SMALL_BATCH)]
         ctx.jpeg_bench_invert(pj, 85, 1, 0, iters=2)
         pms, _ = ctx.jpeg_bench_invert(pj, 85, 1, 0, iters=iters)
-        points[pname] = {"frame": [ph, pw, 3], "gpu_resident_fps": round(batch / (pms / 1e3), 1),
-                         "host_to_host_worker_fps": round(batch / worker_form(pj), 1),
-                         "jpeg_bytes_mean": round(sum(len(j) for j in pj) / batch)}
+        points[pname] = {"frame": [ph, pw, 3], "batch": SMALL_BATCH,
+                         "gpu_resident_fps": round(SMALL_BATCH / (pms / 1e3), 1),
+                         "host_to_host_worker_fps": round(SMALL_BATCH / worker_form(pj), 1),
+                         "jpeg_bytes_mean": round(sum(len(j) for j in pj) / SMALL_BATCH)}
     # hard content: 32 distinct noisy scenes at q95 (long blocks, dense entropy streams)
     from vfilter.synthetic import synthetic_noisy_scene
     hard = tj.encode_batch([synthetic_noisy_scene(s, H, W) for s in range(batch)], quality=95)
@@ -703,6 +709,8 @@ def distributor_leg(nworkers, ngpu, host_gbps=None, pcie_gbps=None, frames_scale
                            producer copy, reporting the ordering overhead
       jpeg_1080p           the reference's default deployment: 1080p JPEG frames (q85 4:2:2),
                            workers in JPEG mode (3 batches of 32 in flight), pull policy
+      jpeg_1080p_hard      the same on hard content (noisy scenes at q95)
+      jpeg_512, jpeg_480p  the reference app's own frame sizes, in batches of SMALL_BATCH (64)
     Every 8th frame is verified in full, the others on their first and last 4 KiB.  Beside each
     leg: the ceilings for this many GPUs — PCIe (the pinned pipelined rate measured in
     end_to_end, each way, per GPU) and host DRAM (the host's measured r+w bandwidth from the
@@ -727,9 +735,9 @@ def distributor_leg(nworkers, ngpu, host_gbps=None, pcie_gbps=None, frames_scale
             "jpeg_1080p_hard": (["--jpeg", "--content", "hard", "--size", "1080p", "--batch", "32", "--policy",
                                  "pull", "--frames", str(int(4608 * nworkers * frames_scale))], None, None),
             # the reference app's own operating point (webcam_app.py:17,97-111: 512 x 512, q85 4:2:2)
-            "jpeg_512": (["--jpeg", "--size", "512sq", "--batch", "32", "--policy", "pull",
+            "jpeg_512": (["--jpeg", "--size", "512sq", "--batch", str(SMALL_BATCH), "--policy", "pull",
                           "--frames", str(int(98304 * nworkers * frames_scale))], None, None),
-            "jpeg_480p": (["--jpeg", "--size", "480p", "--batch", "32", "--policy", "pull",
+            "jpeg_480p": (["--jpeg", "--size", "480p", "--batch", str(SMALL_BATCH), "--policy", "pull",
                            "--frames", str(int(98304 * nworkers * frames_scale))], None, None)}
     worker_form = {"jpeg_1080p": (jpeg or {}).get("host_to_host_worker_fps")}
     for k_, pn in (("jpeg_512", "512sq"), ("jpeg_480p", "480p")):

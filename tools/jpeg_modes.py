@@ -19,7 +19,7 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "distributed-video-filter_amd")]
 
-SIZES = {"480p": (480, 640), "1080p": (1080, 1920), "4k": (2160, 3840)}
+SIZES = {"512sq": (512, 512), "480p": (480, 640), "1080p": (1080, 1920), "4k": (2160, 3840)}
 
 
 def run(size, mode, batch=32, reps=24):
