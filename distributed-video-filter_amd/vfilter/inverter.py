@@ -35,6 +35,19 @@ from .jpeg import TurboJPEG
 from .worker import RingResults, Worker, WorkerFailed, ring_results
 
 
+# JPEG frames up to this many bytes on average are asked for in batches of SMALL_CREDIT: a
+# batch's host work (parse, ~25 launches) is then spread over twice the frames (the reference
+# app's 512 x 512 crops: +30-50 % through the system); larger frames in batches
+# of CREDIT
+SMALL_JPEG_BYTES = 64 * 1024
+CREDIT, SMALL_CREDIT = 32, 64
+
+
+def auto_credit(mean_jpeg_bytes: float) -> int:
+    """The batch a JPEG worker started with ``batch=0`` asks for, from its frames' mean size."""
+    return SMALL_CREDIT if 0 < mean_jpeg_bytes <= SMALL_JPEG_BYTES else CREDIT
+
+
 class InverterWorker(Worker):
     def __init__(self, host: str = "localhost", distribute_port: int = 5555, collect_port: int = 5556,
                  delay: float = 0.0, use_jpeg: bool = True, *, device: Optional[int] = None,
@@ -45,10 +58,16 @@ class InverterWorker(Worker):
         # form 24.6 k fps with 3 in flight vs 21.4 k with 2: profiles/r02_jpeg_depth.jsonl)
         if worker_kw.get("inflight") is None:
             worker_kw["inflight"] = 3 if use_jpeg else 2
+        # batch=0: JPEG requests adapt to the frames (auto_credit); raw frames in batches of 32
+        self.auto_credit = use_jpeg and worker_kw.get("batch") == 0
+        if worker_kw.get("batch") == 0:
+            worker_kw["batch"] = CREDIT
+        self._jpeg_bytes = 0.0  # running mean of the JPEG frames submitted (auto_credit)
         super().__init__(host, distribute_port, collect_port, **worker_kw)
         self.delay = delay
         self.device = default_device() if device is None else device
-        self.ctx = Context(self.device, max_frame_bytes=max_frame_bytes, max_batch=max(1, self.batch))
+        self.ctx = Context(self.device, max_frame_bytes=max_frame_bytes,
+                           max_batch=max(1, SMALL_CREDIT if self.auto_credit else self.batch))
         # inverter.py:13 — TurboJPEG() with PyTurboJPEG's defaults, on this worker's GPU
         self.jpeg = TurboJPEG(ctx=self.ctx, tj_version=tj_version) if use_jpeg else None
         # re-encoded JPEGs written straight into their ring slots (VF_JPEG_SCATTER=0: copied by the loop)
@@ -122,6 +141,8 @@ class InverterWorker(Worker):
         Ring frames (page-locked) are inverted in place (zero-copy); socket payloads are staged.
         JPEG batches are queued on a codec of their own (vf_jpeg_invert_submit: fused decode ->
         invert -> encode) and collected later, ring frames' results straight into their slots."""
+        if self.jpeg:
+            self._note_jpeg_bytes(float(sum(len(f) for f in frames)), len(frames))
         if self.jpeg and self.delay <= 0:
             try:  # staged and queued now; the loop receives the next batch while this one runs
                 return ("jpeg", self.jpeg.invert_batch_submit(list(frames)), list(frames), list(outs))
@@ -140,6 +161,14 @@ class InverterWorker(Worker):
             return ("done", [e] * len(frames), [])
         return ("gpu", ticket, srcs, dsts)  # srcs kept alive until the ticket completes
 
+    def _note_jpeg_bytes(self, total: float, n: int) -> None:
+        if n:
+            m = total / n
+            self._jpeg_bytes = m if not self._jpeg_bytes else 0.75 * self._jpeg_bytes + 0.25 * m
+
+    def request_credit(self) -> int:
+        return auto_credit(self._jpeg_bytes) if self.auto_credit else self.batch
+
     def submit_ring_batch(self, ring, cols):
         """The worker's ring form: every frame of the batch in this worker's page-locked ring
         slice, so the inputs and outputs are base + slot arithmetic -- one address array each,
@@ -152,6 +181,7 @@ class InverterWorker(Worker):
         ina = np.uint64(ring.base_address) + cols["slot"].astype(np.uint64) * np.uint64(2 * sb)
         nb = cols["nbytes"]
         if self.jpeg:
+            self._note_jpeg_bytes(float(nb.sum()), len(nb))
             try:
                 t = self.jpeg.invert_batch_submit_addrs(ina, nb)
             except Exception:  # a frame the host parser refuses: the per-frame views path
@@ -261,10 +291,10 @@ def main(argv=None):
                     help="raw H x W x 3 frames (use_jpeg=False); default JPEG frames, as the reference CLI")
     ap.add_argument("--jpeg", action="store_true", help=argparse.SUPPRESS)  # the default; kept for old scripts
     ap.add_argument("--device", type=int, default=None, help="GPU ordinal (default: VF_DEVICE / LOCAL_RANK / 0)")
-    ap.add_argument("--batch", type=int, default=32,
-                    help="frames per request (protocol v1; default 32, the batch every distributor "
-                         "leg of bench.py measures; 64 moves 1080p JPEG through the system by no more "
-                         "than run-to-run spread: profiles/r02_pipeline_jpeg_batch64.txt)")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="frames per request (protocol v1); default 0: JPEG 64 while the frames average "
+                         "<= 64 KB (the reference app's 512 x 512 crops), else 32 (inverter.auto_credit); "
+                         "raw 32")
     ap.add_argument("--inflight", type=int, default=None,
                     help="batches in progress at once (protocol v1; default 3 for JPEG, 2 for raw)")
     ap.add_argument("--protocol", choices=("v0", "v1"), default="v1",

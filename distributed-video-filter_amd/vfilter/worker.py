@@ -230,6 +230,11 @@ class Worker:
             return self._ring
 
     # -- asynchronous batch hooks (a GPU plugin overrides these) ----------------------------
+    def request_credit(self) -> int:
+        """Frames asked for by the next request (protocol v1): ``batch``; a plugin may adapt it
+        to the frames it sees (InverterWorker with ``batch=0``)."""
+        return self.batch
+
     def submit_ring_batch(self, ring: FrameRing, cols: np.ndarray):
         """Hook: start a v2 batch whose every frame is in ``ring`` from its records (``cols``:
         wire.COLS, slots and sizes as arrays) and return a handle whose ``poll_batch`` results
@@ -449,8 +454,8 @@ class Worker:
         while self.running and (max_frames is None or self.frames_processed < max_frames):
             try:
                 while outstanding < self.depth:
-                    self.dealer_socket.send(wire.encode_request(self.batch, shm=True, wid=self.wid, numa=numa,
-                                                                       wire=wire.WIRE))
+                    self.dealer_socket.send(wire.encode_request(self.request_credit(), shm=True, wid=self.wid,
+                                                                numa=numa, wire=wire.WIRE))
                     outstanding += 1
                 self._collect_jobs(jobs, self.inflight)
                 if len(jobs) >= self.inflight:

@@ -76,6 +76,9 @@ def main():
                          "slot's ring slice (per-node pools; each node gets its own copy of the source "
                          "frames); 0: on the producer / one verification pool")
     ap.add_argument("--consume", type=int, default=64, help="results taken per get_next_batch call")
+    ap.add_argument("--worker-batch", type=int, default=None,
+                    help="the workers' --batch (default: --batch; 0: the worker's own choice, "
+                         "vfilter.inverter.auto_credit); --batch still sizes the ring slices")
     ap.add_argument("--verify-pool", type=int, default=-1,
                     help="JPEG results verified and released on the verification pool (1) or inline (0); "
                          "-1: the pool from 2 workers on")
@@ -125,7 +128,8 @@ def main():
                     ["-m", "vfilter.inverter"])
         cmd = [sys.executable] + launcher + ["--host", "127.0.0.1",
                "--distribute-port", str(d.distribute_port), "--collect-port",
-               str(d.collect_port), "--batch", str(args.batch), "--transport", "tcp"]
+               str(d.collect_port), "--batch", str(args.batch if args.worker_batch is None else args.worker_batch),
+               "--transport", "tcp"]
         if not args.jpeg:
             cmd.append("--raw")
         if args.inflight:
@@ -373,7 +377,7 @@ def main():
         st = d.ordering_stats()
         st["max_depth"] = max(st["max_depth"], d_stats0["max_depth"])
         slices = [w["slice"] for w in st["workers"].values() if w["slice"]]
-        result = {"kind": "pipeline_jpeg" if args.jpeg else "pipeline", "size": args.size, "producers": nprod, "consume": args.consume, "verify_pool": bool(args.jpeg and pool_verify),
+        result = {"kind": "pipeline_jpeg" if args.jpeg else "pipeline", "size": args.size, "producers": nprod, "consume": args.consume, "worker_batch": args.worker_batch, "verify_pool": bool(args.jpeg and pool_verify),
                   "workers": args.workers, "gpus": min(ngpu, args.workers),
                   "inflight_per_worker": inflight,
                   "policy": args.policy, "producer": args.producer, "batch": args.batch, "frames": n_t,
