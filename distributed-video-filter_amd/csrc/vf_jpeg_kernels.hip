@@ -511,14 +511,6 @@ struct SyncTab32 {
   int32_t valoff[18];
   uint8_t vals[256];
 };
-template <typename Tab>
-struct SyncPairs {
-  static constexpr bool v = false;
-};
-template <>
-struct SyncPairs<SyncTab32> {
-  static constexpr bool v = true;
-};
 
 // F's six sync tables (sdc[3], sac[3]) with the AC pairs into LDS, then a barrier (which also
 // publishes whatever the caller staged before the call)
@@ -564,13 +556,15 @@ __device__ __forceinline__ uint32_t tabs4_cpack(const HuffGeom &hg, uint32_t tab
   return p;
 }
 
-template <typename Tab, uint32_t NDC = 3>  // NDC: DC tables before the AC tables in `tabs`
+// k_spec's lane (six HuffSync tables: three DC, then three AC; no pairs): a 64-bit bit buffer
+// refilled with selects, one table read per symbol.  The span sync's lane is SpanLane, below.
+template <typename Tab>
 struct SyncLane {
   const uint32_t *w;  // staged words, minus woff
   uint64_t buf;       // next bits, left-aligned
   uint32_t nb, wi, nxt, pos;
   uint32_t z, c, n;   // zigzag index, block-in-MCU, blocks completed
-  uint32_t toff;      // byte offset of the DC table of c's component (its AC table: NDC tables on)
+  uint32_t toff;      // byte offset of the DC table of c's component (its AC table: 3 tables on)
   uint32_t cpack, bpm;
   __device__ __forceinline__ void init(const uint32_t *words, uint32_t woff, uint64_t X, const HuffGeom &hg) {
     const uint32_t p = (uint32_t)(X >> 16);
@@ -588,17 +582,15 @@ struct SyncLane {
     bpm = hg.bpm;
     toff = __umul24((cpack >> (2 * c)) & 3, (uint32_t)sizeof(Tab));
   }
-  // one step: a symbol, or two (an AC table's pair entry) when the first leaves the block open
-  // and ends before `stop` -- so a mark's state is still taken at the first symbol boundary at
-  // or past it, whichever symbol a decoder's pairing started from
-  __device__ __forceinline__ void step(const Tab *tabs, uint32_t stop) {
+  // one step: one symbol (`stop` is SpanLane's pair bound; a single symbol never needs it)
+  __device__ __forceinline__ void step(const Tab *tabs, uint32_t /*stop*/) {
     const bool f = nb <= 32;
     buf |= f ? (uint64_t)bswap32(nxt) << (32 - nb) : 0ull;
     nb += f ? 32u : 0u;
     wi += f ? 1u : 0u;
     nxt = w[wi];
     const Tab &T = *reinterpret_cast<const Tab *>(reinterpret_cast<const char *>(tabs) + toff +
-                                                   (z == 0 ? 0u : NDC * (uint32_t)sizeof(Tab)));
+                                                   (z == 0 ? 0u : 3u * (uint32_t)sizeof(Tab)));
     uint32_t e = T.sfast[(uint32_t)(buf >> (64 - kLook))];
     if (!e) {  // a code longer than kLook bits: jdhuff.c's slow path (rare)
       const uint32_t c16 = (uint32_t)(buf >> 48);
@@ -615,19 +607,88 @@ struct SyncLane {
       }
       e = (adv << 8) | (len + extra);
     }
-    const uint32_t len1 = e & 0xFF, adv1 = (e >> 8) & 0xFF;
-    const bool two = SyncPairs<Tab>::v && (e >> 16) != 0 && z + adv1 < 64 && pos + len1 < stop;
-    const uint32_t len = two ? (e >> 16) & 0xFF : len1;  // pair word: (advance << 24) | (length << 16)
+    const uint32_t len = e & 0xFF;
     buf <<= len;
     nb -= len;
     pos += len;
-    z += two ? e >> 24 : adv1;
+    z += (e >> 8) & 0xFF;
     const bool eob = z >= 64;
     const uint32_t c1 = c + 1 == bpm ? 0u : c + 1;
     c = eob ? c1 : c;
     z = eob ? 0u : z;
     n += eob ? 1u : 0u;
     toff = __umul24((cpack >> (2 * c)) & 3, (uint32_t)sizeof(Tab));
+  }
+};
+
+// k_syncg's lane.  One step decodes a symbol, or two (an AC table's pair entry) when the first
+// leaves the block open and ends before `stop` -- so a mark's state is still taken at the first
+// symbol boundary at or past it, whichever symbol a decoder's pairing started from.  It takes
+// about two thirds of the instructions of the buffered step it replaced (SyncLane's reader, 60
+// per step; the span sync issues VALU back to back, so its time follows the step's instruction
+// count).  There is no bit buffer to refill: a step reads the two staged words
+// holding bits pos-1 .. pos+62 with one ds_read2 and aligns them with v_alignbit (a three-word
+// window sliding a read ahead, so that the table read is the only LDS read on the chain, was no
+// faster).  The words are staged byte-swapped, and the position is kept negated relative to
+// the staged words, q = 32 * wbase - pos, so the word index (-(q >> 5) - 1: the word of bit pos-1)
+// and the alignment shift (q & 31 = 31 - (pos-1) % 32, v_alignbit reads its low 5 bits) are
+// direct functions of q.  Staged word 0 must lie before every position decoded (pos - 32 * wbase
+// >= 1).  The block-in-MCU is kept doubled (c2): its table slot is one bit-field extract.
+template <uint32_t NDC>  // tabs: NDC DC tables, then NDC AC tables with the pairs
+struct SpanLane {
+  const uint32_t *wl;  // staged words, byte-swapped
+  uint32_t base;       // 32 * wbase (modular)
+  int32_t q;           // base - pos
+  uint32_t z, c2, n;   // zigzag index, 2 x block-in-MCU, blocks completed
+  uint32_t cpack, bpm2;
+  __device__ __forceinline__ void init(const uint32_t *s_w, uint32_t base_, uint64_t X, const HuffGeom &hg) {
+    wl = s_w;
+    base = base_;
+    q = (int32_t)(base - (uint32_t)(X >> 16));
+    z = (X >> 8) & 0xFF;
+    c2 = (uint32_t)(X & 0xFF) * 2u;
+    n = 0;
+    cpack = hg.cpack;
+    bpm2 = hg.bpm * 2u;
+  }
+  __device__ __forceinline__ uint32_t pos() const { return base - (uint32_t)q; }
+  __device__ __forceinline__ uint32_t c() const { return c2 >> 1; }
+  __device__ __forceinline__ uint64_t state() const { return pack_state(pos(), z, c()); }
+  // steps while pos < stop
+  __device__ __forceinline__ void run(const SyncTab32 *tabs, uint32_t stop) {
+    const int32_t qs = (int32_t)(base - stop);  // pos < stop <=> q > qs
+    while (q > qs) step(tabs, qs);
+  }
+  __device__ __forceinline__ void step(const SyncTab32 *tabs, int32_t qs) {
+    const uint32_t *p = wl + (-(q >> 5) - 1);
+    const uint32_t r = __builtin_amdgcn_alignbit(p[0], p[1], (uint32_t)q);  // bits pos .. pos+31
+    const SyncTab32 &T = tabs[((cpack >> c2) & 3u) + min(z, 1u) * NDC];
+    uint32_t e = T.sfast[r >> (32 - kLook)];
+    if (!e) {  // a code longer than kLook bits (rare): as SyncLane
+      const uint32_t c16 = r >> 16;
+      uint32_t len = long_code_len(c16, T.lim), sym = 0;
+      if (len > 16) len = 16;
+      else sym = T.vals[(uint32_t)((int32_t)(c16 >> (16 - len)) + T.valoff[len]) & 255];
+      uint32_t extra, adv;
+      if (z == 0) {
+        extra = sym > 16 ? 16 : sym;
+        adv = 1;
+      } else {
+        extra = sym & 15;
+        adv = extra ? (sym >> 4) + 1 : ((sym >> 4) == 15 ? 16 : 64);
+      }
+      e = (adv << 8) | (len + extra);
+    }
+    const int32_t q1 = q - (int32_t)(e & 0xFF);
+    const uint32_t z1 = z + ((e >> 8) & 0xFF);
+    const bool two = (e >> 16) != 0 && z1 < 64 && q1 > qs;  // pair word: (advance << 24) | (length << 16)
+    q = two ? q - (int32_t)((e >> 16) & 0xFF) : q1;
+    z = two ? z + (e >> 24) : z1;
+    const bool eob = z >= 64;
+    const uint32_t c2n = c2 + 2 == bpm2 ? 0u : c2 + 2;
+    c2 = eob ? c2n : c2;
+    z = eob ? 0u : z;
+    n += eob ? 1u : 0u;
   }
 };
 
@@ -785,12 +846,12 @@ __global__ __launch_bounds__(256) void k_sync(const DecSeg *__restrict__ sg, con
 // it at the next mark also waited for the stores' completion, every 64 bits.  The first decode
 // (no records yet) has no loads in its loop at all.
 template <bool CHECK, uint32_t NDC>
-__device__ __forceinline__ uint64_t sync_span(const uint32_t *words, uint32_t woff, uint64_t X, uint32_t i0, uint32_t ng,
+__device__ __forceinline__ uint64_t sync_span(const uint32_t *words, uint32_t wb32, uint64_t X, uint32_t i0, uint32_t ng,
                                               uint32_t nsub, uint32_t nbits, uint64_t gi0, uint64_t last,
                                               uint64_t *exits, uint32_t *cnts, uint64_t *ck, uint32_t *ckrem,
                                               const HuffGeom &hg, const SyncTab32 *tabs) {
-  SyncLane<SyncTab32, NDC> d;
-  d.init(words, woff, X, hg);
+  SpanLane<NDC> d;
+  d.init(words, wb32, X, hg);
   uint32_t j = 0, bj = i0 * kSubBits;
   uint32_t ej = i0 + 1 >= nsub ? nbits : bj + kSubBits;  // end of subsequence j
   // next mark of subsequence j: checkpoint m < kCk at bj + (m + 1) * kCkStep (if inside it), or
@@ -801,8 +862,8 @@ __device__ __forceinline__ uint64_t sync_span(const uint32_t *words, uint32_t wo
   uint32_t n0 = 0, n1 = 0, n2 = 0;  // blocks at the checkpoints written in this decode
   static_assert(kCk == 3, "n0..n2");
   for (;;) {
-    while (d.pos < mk) d.step(tabs, mk);
-    const uint64_t st = pack_state(d.pos, d.z, d.c);
+    d.run(tabs, mk);
+    const uint64_t st = d.state();
     const uint64_t gj = gi0 + j;
     const bool joined = CHECK && old == st;
     // the mark after this one (j2, m2 at mk2)
@@ -849,15 +910,12 @@ __device__ __forceinline__ uint64_t sync_span(const uint32_t *words, uint32_t wo
   }
 }
 
-// T threads per workgroup, T * G subsequences: the workgroup's stream words (32 KB at most) are
-// staged in LDS first, so a refill is an LDS read (global loads one word ahead exposed their
-// latency every few symbols: ~500-700 shader cycles per symbol on an idle GPU, counted with
-// tools/build_syncg_stats.sh).
-#ifndef VF_SYNCG_STAGE
-#define VF_SYNCG_STAGE 1
-#endif
-constexpr bool kSyncgStage = VF_SYNCG_STAGE;
-constexpr uint32_t syncg_threads(int G) { return !kSyncgStage || G <= 5 ? 256u : 1024u / (uint32_t)G; }
+// T threads per workgroup, T * G subsequences: the workgroup's stream words (40 KB at most) are
+// staged in LDS first, byte-swapped for SpanLane, so a step's words are an LDS read (global
+// loads exposed their latency every few symbols: ~500-700 shader cycles per symbol on an idle
+// GPU, counted with tools/build_syncg_stats.sh; unstaged, at twice the occupancy, a pass took
+// 2.4x as long).
+constexpr uint32_t syncg_threads(int G) { return G <= 5 ? 256u : 1024u / (uint32_t)G; }
 // Pass 0's guessed entries can be warmed: a thread first decodes the `warm` bits before its span
 // from a guessed state (nothing recorded), so its entry is the state at the first symbol boundary
 // at or past the span's start, usually the true one already (tools/sync_sim.py --warm).
@@ -867,8 +925,7 @@ __global__ __launch_bounds__(256) void k_syncg(const DecSeg *__restrict__ sg, co
                                                const uint32_t *us_len, uint64_t *exits, uint32_t *cnts, uint64_t *used,
                                                uint64_t *ck, uint32_t *ckrem, uint32_t *changed, int pass, uint32_t warm) {
   constexpr uint32_t kWarmWords = kSyncWarmMax / 32;
-  constexpr uint32_t T = syncg_threads(G),
-                     kWords = kSyncgStage ? kWarmWords + T * G * (kSubBits / 32) + kSpecPadWords : 1;
+  constexpr uint32_t T = syncg_threads(G), kWords = 1 + kWarmWords + T * G * (kSubBits / 32) + kSpecPadWords;
   __shared__ SyncTab32 tabs[2 * NDC];
   // exits relative to the workgroup's first bit in 32 bits, (pos - wbit) << 10 | z << 4 | c (as
   // k_spec's): 1 KB less LDS, which with G = 3 makes 4 workgroups per CU fit (40.7 KB)
@@ -884,18 +941,18 @@ __global__ __launch_bounds__(256) void k_syncg(const DecSeg *__restrict__ sg, co
   const auto absl = [wbit](uint32_t r) { return pack_state((r >> 10) + wbit, (r >> 4) & 63u, r & 15u); };
   if (pass > 0 && changed[pass - 1] == 0) return;  // converged (workgroup-uniform)
   const uint32_t *gw = reinterpret_cast<const uint32_t *>(us + S.us_off);
-  // staged from kWarmWords before the workgroup's first span (the warm-up of its first thread);
-  // words before the segment's start read as 0 and are never decoded
-  const int32_t wbase = kSyncgStage ? (int32_t)(blockIdx.x * T * G * (kSubBits / 32)) - (int32_t)kWarmWords : 0;
-  const uint32_t woff = (uint32_t)wbase;  // modular: s_w[i] holds word wbase + i
-  if (kSyncgStage) {
+  // staged from kWarmWords + 1 before the workgroup's first span (the warm-up of its first
+  // thread, and the word before it: SpanLane reads the word of bit pos-1); words before the
+  // segment's start read as 0 and are never decoded
+  const int32_t wbase = (int32_t)(blockIdx.x * T * G * (kSubBits / 32)) - (int32_t)kWarmWords - 1;
+  const uint32_t wb32 = (uint32_t)wbase * 32u;  // modular: s_w[i] holds word wbase + i
+  {
     const uint32_t fwords = (((S.in_len + 64) + 15) & ~15u) / 4;
     for (uint32_t i = threadIdx.x; i < kWords; i += T) {
       const int32_t gwi = wbase + (int32_t)i;
-      s_w[i] = gwi >= 0 && (uint32_t)gwi < fwords ? gw[gwi] : 0u;
+      s_w[i] = gwi >= 0 && (uint32_t)gwi < fwords ? bswap32(gw[gwi]) : 0u;
     }
   }
-  const uint32_t *words = kSyncgStage ? s_w : gw;
   if constexpr (NDC == 2) load_sync_tabs4(F, tabs);  // its barrier also publishes s_w
   else load_sync_tabs32(F, tabs);
   HuffGeom hg(F.g);
@@ -913,10 +970,10 @@ __global__ __launch_bounds__(256) void k_syncg(const DecSeg *__restrict__ sg, co
       entry = i0 == 0 ? 0 : pack_state(i0 * kSubBits, 0, 0);  // a guess, except at the segment's start
       if (i0 > 0 && warm > 0) {
         const uint32_t b = i0 * kSubBits, w0 = b > warm ? b - warm : 0u;
-        SyncLane<SyncTab32, NDC> d;
-        d.init(words, woff, pack_state(w0, 0, 0), hg);
-        while (d.pos < b) d.step(tabs, b);
-        entry = pack_state(d.pos, d.z, d.c);
+        SpanLane<NDC> d;
+        d.init(s_w, wb32, pack_state(w0, 0, 0), hg);
+        d.run(tabs, b);
+        entry = d.state();
       }
       need = true;
     } else {
@@ -929,8 +986,8 @@ __global__ __launch_bounds__(256) void k_syncg(const DecSeg *__restrict__ sg, co
   bool check = pass > 0;  // records are valid from the first decode on
   for (;;) {
     if (need) {
-      last = check ? sync_span<true, NDC>(words, woff, entry, i0, ng, nsub, nbits, gi0, last, exits, cnts, ck, ckrem, hg, tabs)
-                   : sync_span<false, NDC>(words, woff, entry, i0, ng, nsub, nbits, gi0, last, exits, cnts, ck, ckrem, hg, tabs);
+      last = check ? sync_span<true, NDC>(s_w, wb32, entry, i0, ng, nsub, nbits, gi0, last, exits, cnts, ck, ckrem, hg, tabs)
+                   : sync_span<false, NDC>(s_w, wb32, entry, i0, ng, nsub, nbits, gi0, last, exits, cnts, ck, ckrem, hg, tabs);
       used[gi0] = entry;
     }
     s_exit[t] = live ? rel(last) : 0u;
