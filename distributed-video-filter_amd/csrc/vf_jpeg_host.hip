@@ -270,14 +270,16 @@ int Codec::init(std::string *err) {
 // The invert path's fused colour pass (k_color writes the encoder's sample planes, k_fdct reads
 // them); VF_JPEG_FUSE=0 keeps the pixel round trip (read per call: tests switch it).
 // Bits a span-sync thread decodes before its span in pass 0, so that its entry is (usually)
-// synchronised already: 8 blocks' worth of the batch's bits per block -- the full state (bit
+// synchronised already: 12 blocks' worth of the batch's bits per block -- the full state (bit
 // position, zigzag index, block-in-MCU) resynchronises at block boundaries (hard 1080p: ~250
-// bits per block, 2,024 bits of warm-up; 4K scenes: ~20, 160).  VF_JPEG_SYNC_WARM=<bits>
-// overrides (0: guessed entries), read per call: tests and A/Bs switch it inside one process.
+// bits per block, 3,008 bits of warm-up; 4K scenes: ~20, 240).  12 rather than 8 blocks: hard
+// 1080p sync 4-9 % shorter on each of four content seeds, 4K scenes unchanged
+// (profiles/r05_jpeg_sync_warm_ab.txt).  VF_JPEG_SYNC_WARM=<bits> overrides (0: guessed
+// entries), read per call: tests and A/Bs switch it inside one process.
 uint32_t Codec::sync_warm() const {
   const char *v = std::getenv("VF_JPEG_SYNC_WARM");
   if (v && *v && std::strcmp(v, "auto") != 0) return (uint32_t)std::strtoul(v, nullptr, 10);
-  return (uint32_t)std::min<uint64_t>(4096, 8 * dbits_per_block_) & ~31u;
+  return (uint32_t)std::min<uint64_t>(4096, 12 * dbits_per_block_) & ~31u;
 }
 
 static bool fuse_enabled() {

@@ -40,6 +40,7 @@ def main():
     ap.add_argument("--content", default="scene", choices=("scene", "hard"),
                     help="scene: 8 camera-like scenes at q85; hard: 32 distinct noisy scenes at q95 "
                          "(vfilter.synthetic.synthetic_noisy_scene)")
+    ap.add_argument("--seed0", type=int, default=0, help="first content seed (frames use seed0 .. seed0 + 31)")
     ap.add_argument("--out", default="")
     ap.add_argument("--resident-only", action="store_true",
                     help="only the GPU-resident batches (kernel profiles without the concurrent host forms)")
@@ -52,10 +53,10 @@ def main():
         h, w = SIZES[name]
         if args.content == "hard":
             from vfilter.synthetic import synthetic_noisy_scene
-            frames = [synthetic_noisy_scene(s, h, w) for s in range(min(args.batch, 32))]
+            frames = [synthetic_noisy_scene(args.seed0 + s, h, w) for s in range(min(args.batch, 32))]
             jpgs = [J.encode(frames[i % len(frames)], 95, J.TJPF_BGR, args.subsamp) for i in range(args.batch)]
         else:
-            frames = [J.synthetic_scene(s, h, w) for s in range(min(args.batch, 8))]
+            frames = [J.synthetic_scene(args.seed0 + s, h, w) for s in range(min(args.batch, 8))]
             jpgs = [J.encode(frames[i % len(frames)], 85, J.TJPF_BGR, args.subsamp) for i in range(args.batch)]
         in_bytes = sum(len(j) for j in jpgs)
         ms, stages = ctx.jpeg_bench_invert(jpgs, 85, args.subsamp, 0, iters=2)  # warm

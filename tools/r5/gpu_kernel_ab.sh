@@ -1,6 +1,6 @@
 #!/bin/bash
 # Per-kernel timing A/B over libraries (VARIANTS="name=path[@VAR=VAL,...] ..."), rocprofv3 kernel trace of
-# tools/jpeg_bench.py (SIZES, CONTENT, resident only), REPS reps, means of the kernels in KERNELS.
+# tools/jpeg_bench.py (SIZES, CONTENT, resident only, JB_ARGS extra arguments), REPS reps, means of the kernels in KERNELS.
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -13,7 +13,7 @@ for nv in $VARIANTS; do
   rm -rf gpurun_out/prof_$tag
   env ${envs//,/ } VFILTER_LIB=$lib timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$tag -o ks -- \
       python3 tools/jpeg_bench.py --sizes $SIZES --batch 32 --iters 10 --cpu-seconds 0 --resident-only --content $CONTENT \
-      --out gpurun_out/$tag.jsonl > gpurun_out/$tag.log 2>&1 || { echo PROF_FAILED $tag; tail -30 gpurun_out/$tag.log; exit 1; }
+      $JB_ARGS --out gpurun_out/$tag.jsonl > gpurun_out/$tag.log 2>&1 || { echo PROF_FAILED $tag; tail -30 gpurun_out/$tag.log; exit 1; }
 done
 done
 python3 - <<'PY'
