@@ -634,7 +634,8 @@ struct SyncLane {
 // and the alignment shift (q & 31 = 31 - (pos-1) % 32, v_alignbit reads its low 5 bits) are
 // direct functions of q.  Staged word 0 must lie before every position decoded (pos - 32 * wbase
 // >= 1).  The block-in-MCU is kept doubled (c2): its table slot is one bit-field extract.
-template <uint32_t NDC>  // tabs: NDC DC tables, then NDC AC tables with the pairs
+// k_spec runs it on its six HuffSync tables without pairs (PAIRS = false).
+template <typename Tab, uint32_t NDC, bool PAIRS = true>  // tabs: NDC DC tables, then NDC AC tables
 struct SpanLane {
   const uint32_t *wl;  // staged words, byte-swapped
   uint32_t base;       // 32 * wbase (modular)
@@ -655,14 +656,14 @@ struct SpanLane {
   __device__ __forceinline__ uint32_t c() const { return c2 >> 1; }
   __device__ __forceinline__ uint64_t state() const { return pack_state(pos(), z, c()); }
   // steps while pos < stop
-  __device__ __forceinline__ void run(const SyncTab32 *tabs, uint32_t stop) {
+  __device__ __forceinline__ void run(const Tab *tabs, uint32_t stop) {
     const int32_t qs = (int32_t)(base - stop);  // pos < stop <=> q > qs
     while (q > qs) step(tabs, qs);
   }
-  __device__ __forceinline__ void step(const SyncTab32 *tabs, int32_t qs) {
+  __device__ __forceinline__ void step(const Tab *tabs, int32_t qs) {
     const uint32_t *p = wl + (-(q >> 5) - 1);
     const uint32_t r = __builtin_amdgcn_alignbit(p[0], p[1], (uint32_t)q);  // bits pos .. pos+31
-    const SyncTab32 &T = tabs[((cpack >> c2) & 3u) + min(z, 1u) * NDC];
+    const Tab &T = tabs[((cpack >> c2) & 3u) + min(z, 1u) * NDC];
     uint32_t e = T.sfast[r >> (32 - kLook)];
     if (!e) {  // a code longer than kLook bits (rare): as SyncLane
       const uint32_t c16 = r >> 16;
@@ -681,9 +682,14 @@ struct SpanLane {
     }
     const int32_t q1 = q - (int32_t)(e & 0xFF);
     const uint32_t z1 = z + ((e >> 8) & 0xFF);
-    const bool two = (e >> 16) != 0 && z1 < 64 && q1 > qs;  // pair word: (advance << 24) | (length << 16)
-    q = two ? q - (int32_t)((e >> 16) & 0xFF) : q1;
-    z = two ? z + (e >> 24) : z1;
+    if constexpr (PAIRS) {
+      const bool two = (e >> 16) != 0 && z1 < 64 && q1 > qs;  // pair word: (advance << 24) | (length << 16)
+      q = two ? q - (int32_t)((e >> 16) & 0xFF) : q1;
+      z = two ? z + (e >> 24) : z1;
+    } else {
+      q = q1;
+      z = z1;
+    }
     const bool eob = z >= 64;
     const uint32_t c2n = c2 + 2 == bpm2 ? 0u : c2 + 2;
     c2 = eob ? c2n : c2;
@@ -850,7 +856,7 @@ __device__ __forceinline__ uint64_t sync_span(const uint32_t *words, uint32_t wb
                                               uint32_t nsub, uint32_t nbits, uint64_t gi0, uint64_t last,
                                               uint64_t *exits, uint32_t *cnts, uint64_t *ck, uint32_t *ckrem,
                                               const HuffGeom &hg, const SyncTab32 *tabs) {
-  SpanLane<NDC> d;
+  SpanLane<SyncTab32, NDC> d;
   d.init(words, wb32, X, hg);
   uint32_t j = 0, bj = i0 * kSubBits;
   uint32_t ej = i0 + 1 >= nsub ? nbits : bj + kSubBits;  // end of subsequence j
@@ -970,7 +976,7 @@ __global__ __launch_bounds__(256) void k_syncg(const DecSeg *__restrict__ sg, co
       entry = i0 == 0 ? 0 : pack_state(i0 * kSubBits, 0, 0);  // a guess, except at the segment's start
       if (i0 > 0 && warm > 0) {
         const uint32_t b = i0 * kSubBits, w0 = b > warm ? b - warm : 0u;
-        SpanLane<NDC> d;
+        SpanLane<SyncTab32, NDC> d;
         d.init(s_w, wb32, pack_state(w0, 0, 0), hg);
         d.run(tabs, b);
         entry = d.state();
@@ -1056,20 +1062,20 @@ constexpr uint8_t kLinkLast = 0xE;  // the frame's last subsequence: decoded to 
 // first symbol boundary at/after `end`, or kLinkLast (the frame's last subsequence, decoded to
 // its end).  *count = blocks completed in the subsequence along this path.
 template <typename CK, typename REM, typename EX>
-__device__ __forceinline__ uint32_t spec_link(const uint32_t *words, uint32_t woff, uint64_t X, uint32_t base,
+__device__ __forceinline__ uint32_t spec_link(const uint32_t *words, uint32_t wb32, uint64_t X, uint32_t base,
                                               uint32_t end, bool last, const HuffGeom &hg, const HuffSync *tabs, CK ck,
                                               REM rem, EX ex, uint32_t *count, uint64_t *endst) {
-  SyncLane<HuffSync> d;
-  d.init(words, woff, X, hg);
+  SpanLane<HuffSync, 3, false> d;
+  d.init(words, wb32, X, hg);
   uint32_t m = 0;
-  while (m < kCk && base + (m + 1) * kCkStep <= d.pos) ++m;
+  while (m < kCk && base + (m + 1) * kCkStep <= d.pos()) ++m;
   for (;;) {  // decode to the next mark (a checkpoint inside the subsequence) or to its end
     const uint32_t mk = base + (m + 1) * kCkStep;
     const bool cm = !last && m < kCk && mk < end;
     const uint32_t stop = cm ? mk : end;
-    while (d.pos < stop) d.step(tabs, stop);
+    d.run(tabs, stop);
     if (!cm) break;
-    const uint64_t st = pack_state(d.pos, d.z, d.c);
+    const uint64_t st = d.state();
     for (uint32_t c2 = 0; c2 < hg.bpm; ++c2)
       if (ck(c2, m) == st) {
         *count = d.n + rem(c2, m);
@@ -1078,7 +1084,7 @@ __device__ __forceinline__ uint32_t spec_link(const uint32_t *words, uint32_t wo
     ++m;
   }
   *count = d.n;
-  *endst = pack_state(d.pos, d.z, d.c);
+  *endst = d.state();
   if (last) return kLinkLast;
 #ifndef VF_SPEC_ENDJOIN
 #define VF_SPEC_ENDJOIN 1
@@ -1103,7 +1109,7 @@ __global__ __launch_bounds__(256) void k_spec(const DecSeg *__restrict__ sg, con
   __shared__ uint32_t s_X[256];
   __shared__ uint16_t s_C[256];
   __shared__ uint8_t s_M[256];
-  __shared__ uint32_t s_w[kSpecWords];
+  __shared__ uint32_t s_w[1 + kSpecWords];
   const DecSeg S = sg[blockIdx.y];  // by value: held in scalar registers
   const DecFrame &F = fr[S.frame];
   if (blockIdx.x >= S.nwg) return;
@@ -1117,12 +1123,14 @@ __global__ __launch_bounds__(256) void k_spec(const DecSeg *__restrict__ sg, con
   const uint32_t base = s * kSubBits, end = (s + 1 >= nsub) ? nbits : (s + 1) * kSubBits;
   const uint64_t g0 = S.tr0 + (uint64_t)blockIdx.x * 256, ti = g0 + t;
   // the workgroup's stream words (every decode here stays within them, plus overshoot and
-  // lookahead), from the frame's padded unstuffed region
+  // lookahead), from the frame's padded unstuffed region, byte-swapped for SpanLane from the
+  // word before the first (s_w[i] is word woff - 1 + i: SpanLane reads the word of bit pos-1)
   const uint32_t woff = blockIdx.x * NSS * (kSubBits / 32);
+  const uint32_t wb32 = (woff - 1u) * 32u;  // modular
   const uint32_t fwords = (((S.in_len + 64) + 15) & ~15u) / 4;
   const uint32_t *gw = reinterpret_cast<const uint32_t *>(us + S.us_off);
-  for (uint32_t i = t; i < NS * (kSubBits / 32) + kSpecPadWords; i += 256)
-    s_w[i] = woff + i < fwords ? gw[woff + i] : 0u;
+  for (uint32_t i = t; i < 1 + NS * (kSubBits / 32) + kSpecPadWords; i += 256)
+    s_w[i] = woff - 1u + i < fwords ? bswap32(gw[woff - 1u + i]) : 0u;
   load_sync_tables(F, tabs);  // its barrier also publishes s_w
 #ifndef VF_SPEC_PHASES
 #define VF_SPEC_PHASES 0
@@ -1147,21 +1155,21 @@ __global__ __launch_bounds__(256) void k_spec(const DecSeg *__restrict__ sg, con
 #pragma unroll
   for (int m = 0; m < kCk; ++m) s_ck[m][t] = 0xFFFFFFFFu;
   if (live) {
-    SyncLane<HuffSync> d;
-    d.init(s_w, woff, pack_state(base, 0, c0), hg);
+    SpanLane<HuffSync, 3, false> d;
+    d.init(s_w, wb32, pack_state(base, 0, c0), hg);
     uint32_t m = 0;
     for (;;) {  // decode to the next checkpoint mark inside the subsequence, or to its end
       const uint32_t mk = base + (m + 1) * kCkStep;
       const bool cm = m < kCk && mk < end;
       const uint32_t stop = cm ? mk : end;
-      while (d.pos < stop) d.step(tabs, stop);
+      d.run(tabs, stop);
       if (!cm) break;
-      s_ck[m][t] = rel(pack_state(d.pos, d.z, d.c));
+      s_ck[m][t] = rel(d.state());
       s_rem[m][t] = (uint16_t)d.n;
       ++m;
     }
     for (uint32_t q = 0; q < m; ++q) s_rem[q][t] = (uint16_t)(d.n - s_rem[q][t]);
-    E = pack_state(d.pos, d.z, d.c);
+    E = d.state();
     N = d.n;
   }
   s_E[t] = live ? rel(E) : 0u;
@@ -1173,7 +1181,7 @@ __global__ __launch_bounds__(256) void k_spec(const DecSeg *__restrict__ sg, con
   uint64_t X = 0;
   if (live && sl > 0) {
     const uint32_t row = sl * L;
-    M = spec_link(s_w, woff, absl(s_E[(sl - 1) * L + c0]), base, end, s + 1 == nsub, hg, tabs,
+    M = spec_link(s_w, wb32, absl(s_E[(sl - 1) * L + c0]), base, end, s + 1 == nsub, hg, tabs,
                   [&](uint32_t c2, int m) { return absl(s_ck[m][row + c2]); },
                   [&](uint32_t c2, int m) { return (uint32_t)s_rem[m][row + c2]; },
                   [&](uint32_t c2) { return absl(s_E[row + c2]); }, &C, &X);
@@ -1263,7 +1271,7 @@ __global__ __launch_bounds__(256) void k_spec(const DecSeg *__restrict__ sg, con
         if (VF_SPEC_PHASES) atomicAdd(B.stats + 2, 1u);  // explicit rows decoded by walkers
         const uint32_t bk = sk * kSubBits, ek = (sk + 1 >= nsub) ? nbits : (sk + 1) * kSubBits;
         const uint32_t row = k * L;
-        M2 = spec_link(s_w, woff, st, bk, ek, sk + 1 == nsub, hg, tabs,
+        M2 = spec_link(s_w, wb32, st, bk, ek, sk + 1 == nsub, hg, tabs,
                        [&](uint32_t c2, int m) { return absl(s_ck[m][row + c2]); },
                        [&](uint32_t c2, int m) { return (uint32_t)s_rem[m][row + c2]; },
                        [&](uint32_t c2) { return absl(s_E[row + c2]); }, &cnt, &xe);
@@ -1287,10 +1295,10 @@ __global__ __launch_bounds__(256) void k_spec(const DecSeg *__restrict__ sg, con
       const uint32_t sk = blockIdx.x * NSS + NS;
       const uint32_t ek = (sk + 1 >= nsub) ? nbits : (sk + 1) * kSubBits;
       const uint32_t lim = min(ek, (woff + NS * (kSubBits / 32) + kSpecPadWords - 4) * 32u);  // binds only on corrupt data
-      SyncLane<HuffSync> d;
-      d.init(s_w, woff, st, hg);
-      while (d.pos < lim) d.step(tabs, lim);
-      B.qX[g0 + 256 + L + e] = pack_state(d.pos, d.z, d.c);  // slot (w + 1, row 1, lane e)
+      SpanLane<HuffSync, 3, false> d;
+      d.init(s_w, wb32, st, hg);
+      d.run(tabs, lim);
+      B.qX[g0 + 256 + L + e] = d.state();  // slot (w + 1, row 1, lane e)
       B.qC[g0 + 256 + L + e] = d.n;
     }
     B.wF[(uint64_t)(S.wg0 + blockIdx.x) * kSpecLanesMax + e] = (uint8_t)(j < hg.bpm ? j : kLinkNone);
