@@ -251,14 +251,15 @@ def _span_sync_batch(quality=95, subsamp=J.TJSAMP_422):
 
 
 @pytest.mark.parametrize("g,warm", [("0", "0"), ("1", "0"), ("2", "0"), ("3", "0"), ("4", "0"), ("5", "0"), ("8", "0"), ("3", "2048"),
-                                    ("4", "256"), ("4", "2048"), ("5", "2048"), ("8", "4096"), ("1", "1000")])
+                                    ("4", "256"), ("4", "2048"), ("5", "2048"), ("5", "4096"), ("8", "4096"), ("1", "1000")])
 def test_span_sync_widths(tj, monkeypatch, g, warm):
     """The pass-based sync with G subsequences per thread (k_syncg: records updated in place,
     passes queued and returning early once no workgroup's last exit changes; G = 0: the
     host-looped one-subsequence k_sync), with and without pass 0's warm-up decode before each
     span (VF_JPEG_SYNC_WARM bits, rounded down to 32; reaching back past the segment's start and
-    into the previous workgroup's words), on frames spanning several workgroups, through the
-    fused invert and the plain decode, bit-exact with the oracle."""
+    into the previous workgroup's words -- at 4096, the staged maximum, a workgroup's first warm-up
+    starts in the word after SpanLane's leading one), on frames spanning several workgroups,
+    through the fused invert and the plain decode, bit-exact with the oracle."""
     monkeypatch.setenv("VF_JPEG_SYNC", "pass")
     monkeypatch.setenv("VF_JPEG_SYNC_G", g)
     monkeypatch.setenv("VF_JPEG_SYNC_WARM", warm)
