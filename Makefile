@@ -11,10 +11,12 @@ CXX       ?= g++
 HIPFLAGS  := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -fvisibility=hidden -Wall -Iinclude
 LDFLAGS   := -shared -Wl,-rpath,/opt/rocm/lib -Wl,--no-undefined
 
-.PHONY: all lib oracle tools clean exp
+.PHONY: all lib vfdist oracle tools clean exp
 all: lib oracle
 
 lib: $(LIB) $(DLIB)
+
+vfdist: $(DLIB)
 
 # the distributor's native control plane: host C++ only (no HIP), so plain g++
 $(DLIB): $(CSRC)/vf_dist.cc $(CSRC)/vf_json.h include/vfdist.h

@@ -59,6 +59,7 @@
 namespace {
 
 constexpr uint32_t kMaxParts = 1u << 16;
+constexpr size_t kReadBurst = 8u << 20;  // bytes read from one connection before parsing
 constexpr int64_t kDefaultMaxPart = int64_t(1) << 30;
 constexpr size_t kRecord = 40;  // wire.COLS: index i64, nbytes i64, slot i32, ndim i32, shape i32[4]
 constexpr uint64_t kEvListenD = 1, kEvListenC = 2, kEvWake = 3, kEvListenDU = 4, kEvListenCU = 5, kFirstConn = 16;
@@ -1260,10 +1261,16 @@ struct vfd_engine {
         }
         if (sender) sender->last_seen = mono();
         // the common message: every frame a ring result of the sender's own dispatch, in flight
-        // once, no error -- booked in one pass
+        // once, no error, indices strictly increasing (so none repeats) -- booked in one pass;
+        // anything else (a repeated index included) takes the per-record path below
         bool fast = sender != nullptr;
         if (fast)
-            for (auto& m : metas) {
+            for (size_t i = 0; i < metas.size(); ++i) {
+                const ResMeta& m = metas[i];
+                if (i && m.index <= metas[i - 1].index) {
+                    fast = false;
+                    break;
+                }
                 auto f = sender->inflight.find(m.index);
                 if (m.error || m.slot < 0 || f == sender->inflight.end() || f->second->slot < 0 ||
                     settled.count(m.index) || m.nbytes < 0 || m.nbytes > slot_bytes) {
@@ -1279,6 +1286,7 @@ struct vfd_engine {
         if (fast) {
             for (auto& m : metas) {
                 auto f = sender->inflight.find(m.index);
+                if (f == sender->inflight.end()) continue;  // unreachable after the pre-check
                 Frame* it = f->second;
                 sender->inflight.erase(f);
                 if (it->batch) --it->batch->remaining;
@@ -1507,7 +1515,14 @@ struct vfd_engine {
     void on_readable(const std::shared_ptr<Conn>& c) {
         bool closed = false;
         for (;;) {
-            if (c->rlen == c->rbuf.size()) c->rbuf.resize(c->rbuf.size() * 2);
+            if (c->rlen == c->rbuf.size()) {
+                // a full buffer past the burst cap is parsed before reading more (epoll is
+                // level-triggered, so the rest is read on the next wakeup): a peer that writes
+                // without pause cannot grow the buffer past max(burst, its pending message)
+                // or hold the I/O thread; a pending message's size is reserved below
+                if (c->rbuf.size() >= kReadBurst) break;
+                c->rbuf.resize(std::min(c->rbuf.size() * 2, kReadBurst));
+            }
             ssize_t r = ::recv(c->fd, c->rbuf.data() + c->rlen, c->rbuf.size() - c->rlen, MSG_DONTWAIT);
             if (r > 0) {
                 c->rlen += (size_t)r;

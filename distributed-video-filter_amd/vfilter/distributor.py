@@ -52,6 +52,7 @@ import collections
 import json
 import os
 import queue
+import sys
 import threading
 import time
 from typing import Sequence, Deque, Dict, List, Optional
@@ -95,8 +96,20 @@ def _native_serves(args, kw) -> bool:
     except ValueError:
         return False
     trace = kw.get("enable_trace_export", args[3] if len(args) > 3 else False)
-    return native.supports(kw.get("policy", "latest"), kw.get("reassembly", "display"), transport,
-                           int(kw.get("ring_slots", 0)), kw.get("ring_layout", "auto"), bool(trace)) is None
+    if native.supports(kw.get("policy", "latest"), kw.get("reassembly", "display"), transport,
+                       int(kw.get("ring_slots", 0)), kw.get("ring_layout", "auto"), bool(trace)) is not None:
+        return False
+    if not native.available():  # auto never fails for a missing library: the Python engine serves
+        global _auto_notice_shown
+        if not _auto_notice_shown:
+            _auto_notice_shown = True
+            print(f"vfilter.distributor: engine='auto' uses the Python engine ({native.LIB_NAME} not loadable "
+                  f"at {native.library_path()}; `make lib` builds it)", file=sys.stderr, flush=True)
+        return False
+    return True
+
+
+_auto_notice_shown = False
 
 
 class _Peer:
@@ -1122,8 +1135,15 @@ class Distributor:
             p.batches.popleft()
         p.frames_sent -= len(items)
         if self.policy == "latest":
+            cur = self.current_frame_data
             for it in items:
-                self._drop(it)
+                if it is cur and it["frame_index"] == self.last_frame_sent:
+                    # the reference books last_frame_sent only after a successful send
+                    # (distributor.py:238-241): the frame still in the dispatch slot stays there
+                    # for the next READY instead of being dropped
+                    self.last_frame_sent = it["frame_index"] - 1
+                else:
+                    self._drop(it)
         else:
             self._relane(items)
         self._evict(p, "dispatch refused (worker disconnected)", gone=True)

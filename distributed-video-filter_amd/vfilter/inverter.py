@@ -178,6 +178,10 @@ class InverterWorker(Worker):
         if self.delay > 0:
             return None
         sb = ring.slot_bytes
+        slots, nbs = cols["slot"], cols["nbytes"]
+        if len(slots) and (int(slots.min()) < 0 or int(slots.max()) >= ring.nslots or int(nbs.min()) < 0
+                           or int(nbs.max()) > sb):
+            return None  # a record outside this ring slice: never a raw GPU address; the views path
         ina = np.uint64(ring.base_address) + cols["slot"].astype(np.uint64) * np.uint64(2 * sb)
         nb = cols["nbytes"]
         if self.jpeg:

@@ -62,6 +62,26 @@ def test_engine_selection():
         Distributor(0, 0, policy="latest", engine="native", **kw)
 
 
+def test_auto_engine_falls_back_when_the_library_cannot_load(monkeypatch, capsys):
+    """engine='auto' never fails for a missing libvfdist.so: the Python engine serves, with one
+    notice; engine='native' still refuses loudly."""
+    from vfilter import distributor as dmod
+    monkeypatch.setattr(native, "available", lambda: False)
+    monkeypatch.setattr(dmod, "_auto_notice_shown", False)
+    kw = dict(transport="tcp", host="127.0.0.1", verbose=False, policy="pull", reassembly="ordered",
+              ring_slots=4, ring_slot_bytes=4096)
+    d = Distributor(0, 0, **kw)
+    try:
+        assert type(d) is Distributor and d.engine == "python"
+    finally:
+        d.cleanup()
+    assert "uses the Python engine" in capsys.readouterr().err
+    monkeypatch.setenv("VFDIST_LIB", "/nonexistent/libvfdist.so")
+    monkeypatch.setattr(native, "_lib", None)
+    with pytest.raises(native.NativeError, match="not found"):
+        Distributor(0, 0, engine="native", **kw)
+
+
 def _native(**kw):
     kw.setdefault("transport", "tcp")
     kw.setdefault("host", "127.0.0.1")
@@ -308,6 +328,44 @@ def test_malformed_peer_is_dropped_alone(bad):
         assert item is not None and bytes(item[1]) == b"\xf8" * 8
     finally:
         raw.close()
+        a.close()
+        d.cleanup()
+
+
+@pytest.mark.timeout(60)
+@pytest.mark.parametrize("order", [[0, 0, 1], [1, 0, 1], [0, 1, 1, 0]])
+def test_result_with_a_repeated_index(order):
+    """A RESULT2 whose records repeat a frame index (a buggy or malicious worker) must not take
+    the one-pass fast path (it would free that frame twice): each index is booked once, the
+    repeat is dropped, and the engine keeps serving."""
+    d = _native(policy="pull", queue_size=16, ring_slots=8, ring_slot_bytes=4096, zero_copy=True)
+    a = _Manual(d, "A")
+    try:
+        a.request(2)
+        _wait(lambda: d.num_workers() == 1)
+        frames = [b"\x01" * 16, b"\x02" * 16]
+        _commit_all(d, frames)
+        disp = a.recv()
+        assert [m.index for m in disp.metas] == [0, 1]
+        if a.ring is None or a.ring.name != disp.ring["name"]:
+            a.ring = FrameRing(name=disp.ring["name"], slot_bytes=int(disp.ring["slot_bytes"]))
+        by_index = {m.index: m for m in disp.metas}
+        for m in disp.metas:
+            a.ring.out_view(m.slot, m.nbytes)[:] = np.bitwise_not(a.ring.in_view(m.slot, m.nbytes))
+        metas = [wire.FrameMeta(i, by_index[i].nbytes, by_index[i].shape, by_index[i].slot, 1.0, 2.0) for i in order]
+        a.push.send(wire.encode_result2(os.getpid(), wire.columns(metas), [], 1.0, 2.0, wid="A"))
+        for i in range(2):
+            item = d.get_next_frame(timeout=5)
+            assert item is not None and item[0] == i and bytes(item[1]) == oracle.invert_bytes(frames[i])
+            d.release_frame(i)
+        d.add_frame_for_distribution(b"\x07" * 8)               # index 2: the engine still serves
+        a.request(1)
+        a.answer(a.recv())
+        item = d.get_next_frame(timeout=5)
+        assert item is not None and item[0] == 2 and bytes(item[1]) == b"\xf8" * 8
+        d.release_frame(2)
+        _wait(lambda: d.free_slots() == d.total_slots(), 5, "slots back")
+    finally:
         a.close()
         d.cleanup()
 

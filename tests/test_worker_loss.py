@@ -495,3 +495,43 @@ def test_shared_ring_slots_of_an_evicted_worker_wait_for_its_result():
         a.close()
         b.close()
         d.cleanup()
+
+
+@pytest.mark.timeout(60)
+def test_latest_policy_keeps_the_slot_frame_after_a_refused_send():
+    """Reference policy (latest-wins, v0 READY): a dispatch the transport refuses (the worker
+    is gone) does not consume the frame -- distributor.py:238-241 books last_frame_sent only
+    after a successful send -- so the next READY still gets it."""
+    d = _dist(engine="python")
+    a = tp.DealerEnd("tcp", "127.0.0.1", d.distribute_port)
+    b = tp.DealerEnd("tcp", "127.0.0.1", d.distribute_port)
+    try:
+        real_send = d.distribute_socket.send
+        refused = []
+
+        def send_once_refused(pid, parts):
+            if not refused:
+                refused.append(pid)
+                return False
+            return real_send(pid, parts)
+
+        d.distribute_socket.send = send_once_refused
+        d.add_frame_for_distribution(b"\x11" * 32)
+        t0 = time.time()
+        while d.current_frame_data is None:                 # in the latest-wins slot
+            assert time.time() - t0 < 10
+            time.sleep(0.01)
+        a.send(wire.encode_request(version=0))              # served, but the send is refused
+        t0 = time.time()
+        while not refused:
+            assert time.time() - t0 < 10, "no dispatch attempted"
+            time.sleep(0.01)
+        b.send(wire.encode_request(version=0))
+        assert b.poll(5000), "the frame in the dispatch slot was dropped with the refused send"
+        disp = wire.decode_dispatch(b.recv())
+        assert [m.index for m in disp.metas] == [0] and bytes(disp.payloads[0]) == b"\x11" * 32
+        assert d.frames_dropped == 0
+    finally:
+        a.close()
+        b.close()
+        d.cleanup()
