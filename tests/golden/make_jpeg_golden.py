@@ -51,6 +51,10 @@ CASES = [  # (name, kind, seed, h, w, quality, subsamp, fastdct)
      {"restart_interval": 7, "optimize": True}),
     ("scene_96x128_q75_440_opt", "scene", 14, 96, 128, 75, J.TJSAMP_440, False, {"optimize": True}),
     ("scene_33x9_q85_422_dri2", "scene", 15, 33, 9, 85, J.TJSAMP_422, False, {"restart_interval": 2}),
+    # the reference app's own operating point: webcam_app.py:17,97-111 centre-crops to 512 x 512
+    # and encodes with PyTurboJPEG's defaults (q85, 4:2:2)
+    ("scene_512sq_q85_422", "scene", 16, 512, 512, 85, J.TJSAMP_422, False),
+    ("noise_512sq_q85_422", "noise", 17, 512, 512, 85, J.TJSAMP_422, False),
 ]
 
 
