@@ -30,7 +30,8 @@ hipError_t dec_unstuff_write(const DecSeg *sg, int nseg, uint32_t max_tiles, con
 hipError_t dec_syncg(int G, const DecSeg *sg, const DecFrame *fr, int nseg, uint32_t max_sub, const uint8_t *us,
                      const uint32_t *us_len, uint64_t *exits, uint32_t *cnts, uint64_t *used, uint64_t *ck,
                      uint32_t *ckrem, uint32_t *changed, int pass, uint32_t warm, int tabs4, hipStream_t s);
-// tabs4: every frame's DecFrame::tabs4 is set (G = 4 or 5 then; else G = 1, 2, 3, 4 or 8)
+// tabs4: every frame's DecFrame::tabs4 is set (G = 4 or 5 then; else G = 1, 2, 3, 4 or 8); 2: and every
+// frame's bpm divides 32 (the LSB-first lane)
 hipError_t dec_sync(const DecSeg *sg, const DecFrame *fr, int nseg, uint32_t max_sub, const uint8_t *us, const uint32_t *us_len,
                     const uint64_t *exit_in, uint64_t *exit_out, const uint32_t *cnt_in, uint32_t *cnt_out,
                     uint64_t *used, uint64_t *ck, uint32_t *ckrem, uint32_t *changed, int pass, hipStream_t s);

@@ -324,6 +324,7 @@ int Codec::prepare_decode(const uint8_t *const *jpegs, const size_t *sizes, int 
   const bool idct24 = !(i24 && std::strcmp(i24, "0") == 0);
   d422_ = true;  // every frame standard 4:2:2 (k_idct_color422)
   tabs4_ = true;  // every frame fits the span sync's 4-table layout (DecFrame::tabs4)
+  pow2bpm_ = true;  // every frame's blocks per MCU divide 32 (k_syncg's SpanLaneR)
   for (int f = 0; f < n; ++f) {
     const Parsed &P = parsed[(size_t)f];
     DecFrame &F = dfr_[(size_t)f];
@@ -366,6 +367,7 @@ int Codec::prepare_decode(const uint8_t *const *jpegs, const size_t *sizes, int 
       if (ok && nsl == 1) rep |= (rep & 0x300u) << 2;  // slot 1 unused: a copy of slot 0
       F.tabs4 = ok ? (s4 | rep | 0x80000000u) : 0u;
       tabs4_ = tabs4_ && ok;
+      pow2bpm_ = pow2bpm_ && F.g.bpm >= 1 && F.g.bpm <= 16 && (F.g.bpm & (F.g.bpm - 1)) == 0;
     }
     F.blk0 = blk;
     for (int c = 0; c < P.ncomp; ++c) {
@@ -604,7 +606,12 @@ int Codec::run_decode(int bgr, bool invert, std::string *err) {
     if (g == 5) return t4 ? 5 : 4;
     return g >= 0 && g <= 4 ? g : g == 8 ? 8 : 4;
   }();
-  const int g_t4 = t4 && (sync_g == 4 || sync_g == 5) ? 1 : 0;
+  // 2: the LSB-first lane (SpanLaneR) when every frame's block cycle divides 32 (VF_JPEG_SYNC_LSB=0: off)
+  const bool lsb = pow2bpm_ && [] {  // read per call: tests switch it inside one process
+    const char *v = std::getenv("VF_JPEG_SYNC_LSB");
+    return !(v && std::strcmp(v, "0") == 0);
+  }();
+  const int g_t4 = t4 && (sync_g == 4 || sync_g == 5) ? (lsb ? 2 : 1) : 0;
   if (flag && sync_g > 0) {
     // VF_JPEG_SYNC_QUEUED = 1..kQueuedPasses (tests): fewer queued passes, so check_decode
     // reports them unconverged and finish_sync runs the rest

@@ -323,6 +323,32 @@ def test_span_sync_table_layouts(tj, monkeypatch, tabs4):
     assert np.array_equal(tj.decode(extra[0]), J.decode(extra[0]))
 
 
+@pytest.mark.parametrize("lsb", ["1", "0"])
+@pytest.mark.parametrize("g,warm", [("5", "3008"), ("4", "0"), ("5", "4096")])
+def test_span_sync_lsb_lane(tj, monkeypatch, lsb, g, warm):
+    """k_syncg's LSB-first lane (SpanLaneR: every frame's block cycle divides 32 -- 4:2:2 and
+    grayscale here -- on the four-table layout): table slots from a per-lane bit pattern by block
+    count, fast entries at bit-reversed indices, "no pair" stored as the first symbol again,
+    codes longer than the lookahead (jpeg_recode's 16-bit AC codes) through the bit-reversed
+    slow path; across workgroups, with and without the warm-up, against the MSB-first lane
+    (VF_JPEG_SYNC_LSB=0) and the oracle, bit-exact.  A batch with a 4:2:0 frame (6 blocks per
+    MCU) takes the MSB-first lane."""
+    import jpeg_recode as R
+    monkeypatch.setenv("VF_JPEG_SYNC", "pass")
+    monkeypatch.setenv("VF_JPEG_SYNC_LSB", lsb)
+    monkeypatch.setenv("VF_JPEG_SYNC_G", g)
+    monkeypatch.setenv("VF_JPEG_SYNC_WARM", warm)
+    monkeypatch.delenv("VF_JPEG_SYNC_TABS4", raising=False)
+    base = _span_sync_batch()
+    long16 = R.recode(J.encode(_img("scene", 12, 200, 320), 90, J.TJPF_BGR, J.TJSAMP_422), ac_long=16, share=True)
+    gray = J.encode(np.clip(_img("scene", 13, 400, 512).astype(np.int16) + 30, 0, 255).astype(np.uint8), 95,
+                    J.TJPF_BGR, J.TJSAMP_GRAY)
+    b420 = J.encode(_img("scene", 14, 96, 128), 90, J.TJPF_BGR, J.TJSAMP_420)
+    for batch in (base + [long16, gray], [long16], [gray, long16], base + [b420]):
+        assert [bytes(o) for o in tj.invert_batch(batch)] == [J.invert_jpeg(j) for j in batch]
+    assert np.array_equal(tj.decode(long16), J.decode(long16))
+
+
 @pytest.mark.parametrize("queued", ["1", "2"])
 def test_span_sync_unconverged_passes_resume(tj, monkeypatch, queued):
     """When the queued span passes leave a workgroup's last exit changing (forced here with
