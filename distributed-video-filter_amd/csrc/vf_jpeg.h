@@ -61,7 +61,7 @@ constexpr int kSpecLanesMax = 16;
 inline uint32_t spec_lanes_host(int bpm) { return bpm <= 1 ? 1u : bpm <= 2 ? 2u : bpm <= 4 ? 4u : bpm <= 8 ? 8u : 16u; }
 hipError_t dec_sync_spec(const DecSeg *sg, const DecFrame *fr, int nseg, uint32_t max_wg, const uint8_t *us, const uint32_t *us_len,
                          const SpecBufs &b, uint64_t *exit_out, uint32_t *cnt_out, uint32_t *unresolved,
-                         hipStream_t s);
+                         int lsb, hipStream_t s);  // lsb: every frame's blocks per MCU divide 16
 hipError_t dec_write(const DecSeg *sg, const DecFrame *fr, int nseg, uint32_t max_sub, const uint8_t *us, const uint32_t *us_len,
                      const uint64_t *exits, const uint32_t *bstart, int16_t *coef, int32_t *dcseq,
                      uint8_t *nmask, hipStream_t s);  // nmask: chunked coefficient rows (else a cleared buffer)

@@ -168,7 +168,7 @@ class Codec {
   uint32_t dmax_wg_ = 0;       // speculative sync: workgroups of the largest segment
   bool spec_ok_ = true;        // every frame fits the speculative resolver
   bool tabs4_ = true;          // every frame fits the span sync's 4-table layout (DecFrame::tabs4)
-  bool pow2bpm_ = true;        // every frame's blocks per MCU divide 32 (k_syncg's SpanLaneR)
+  bool pow2bpm_ = true;        // every frame's blocks per MCU divide 16 (the syncs' LSB-first lanes)
   uint64_t spec_calls_ = 0, spec_fallbacks_ = 0;
   DevBuf d_tE_, d_tX_, d_tXc_, d_pX_, d_pC_, d_wF_, d_rE_, d_rK_, d_qX_, d_qC_, d_rL_,
       d_unres_;

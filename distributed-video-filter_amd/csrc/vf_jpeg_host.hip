@@ -324,7 +324,7 @@ int Codec::prepare_decode(const uint8_t *const *jpegs, const size_t *sizes, int 
   const bool idct24 = !(i24 && std::strcmp(i24, "0") == 0);
   d422_ = true;  // every frame standard 4:2:2 (k_idct_color422)
   tabs4_ = true;  // every frame fits the span sync's 4-table layout (DecFrame::tabs4)
-  pow2bpm_ = true;  // every frame's blocks per MCU divide 32 (k_syncg's SpanLaneR)
+  pow2bpm_ = true;  // every frame's blocks per MCU divide 16 (the span and speculative syncs' LSB-first lanes)
   for (int f = 0; f < n; ++f) {
     const Parsed &P = parsed[(size_t)f];
     DecFrame &F = dfr_[(size_t)f];
@@ -554,6 +554,12 @@ int Codec::run_decode(int bgr, bool invert, std::string *err) {
     if (v && std::strcmp(v, "spec") == 0) return 2;
     return 0;
   }();
+  // the LSB-first lanes (SpanLaneRT) when every frame's block cycle divides 16 (k_spec's
+  // 2-bit component slots; k_syncg's 1-bit table slots need it to divide 32); VF_JPEG_SYNC_LSB=0: off
+  const bool lsb = pow2bpm_ && [] {  // read per call: tests switch it inside one process
+    const char *v = std::getenv("VF_JPEG_SYNC_LSB");
+    return !(v && std::strcmp(v, "0") == 0);
+  }();
   constexpr uint32_t kSpecAutoSubs = 12288;
   const bool use_spec = spec_ok_ && (mode == 2 || (mode == 0 && dmax_sub_ <= kSpecAutoSubs));
   int pass = 0, last = 0;
@@ -571,7 +577,7 @@ int Codec::run_decode(int bgr, bool invert, std::string *err) {
     const bool stats = std::getenv("VF_JPEG_SYNC_STATS") != nullptr;
     if (stats) CK(hipMemsetAsync(d_unres_.p, 0, sizeof(uint32_t) * 16, s_));  // SpecBufs::stats
     CK(dec_sync_spec(sg, fr, ns, dmax_wg_, d_us_.as<uint8_t>(), us_len, sb, d_exit_[0].as<uint64_t>(),
-                     d_cnt_[0].as<uint32_t>(), static_cast<uint32_t *>(unres_dev_), s_));
+                     d_cnt_[0].as<uint32_t>(), static_cast<uint32_t *>(unres_dev_), lsb ? 1 : 0, s_));
     spec_check_ = true;
     flag = 0;  // exits / counts are in slot 0
     ++spec_calls_;
@@ -606,11 +612,7 @@ int Codec::run_decode(int bgr, bool invert, std::string *err) {
     if (g == 5) return t4 ? 5 : 4;
     return g >= 0 && g <= 4 ? g : g == 8 ? 8 : 4;
   }();
-  // 2: the LSB-first lane (SpanLaneR) when every frame's block cycle divides 32 (VF_JPEG_SYNC_LSB=0: off)
-  const bool lsb = pow2bpm_ && [] {  // read per call: tests switch it inside one process
-    const char *v = std::getenv("VF_JPEG_SYNC_LSB");
-    return !(v && std::strcmp(v, "0") == 0);
-  }();
+
   const int g_t4 = t4 && (sync_g == 4 || sync_g == 5) ? (lsb ? 2 : 1) : 0;
   if (flag && sync_g > 0) {
     // VF_JPEG_SYNC_QUEUED = 1..kQueuedPasses (tests): fewer queued passes, so check_decode

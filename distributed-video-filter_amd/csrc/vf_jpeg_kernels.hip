@@ -718,62 +718,66 @@ struct SpanLane {
 //    by the block count -- no block-in-MCU is carried, it is (c0 + n) & (bpm - 1) at the marks.
 // Same symbols, pairs, marks and states as SpanLane (the long-code path reads the code MSB-first
 // through a bit reversal).
-struct SpanLaneR {
-  uint32_t Q;     // bit position - 2, relative to LDS byte 0 (8 * address + bit)
+// Tab: SyncTab32 (32-bit fast entries, pairs in the upper half; k_syncg) or HuffSync (16-bit, one
+// symbol; k_spec); NT DC tables then NT AC tables; SB bits per block's table slot in the pattern.
+template <typename Tab, uint32_t NT, uint32_t SB, bool PAIRS>
+struct SpanLaneRT {
+  static constexpr uint32_t kEnt = sizeof(Tab{}.sfast[0]);     // bytes per fast entry: 4 or 2
+  static constexpr uint32_t kLead = kEnt == 4 ? 2u : 1u;       // window read from bit pos - kLead
+  uint32_t Q;     // bit position - kLead, relative to LDS byte 0 (8 * address + bit)
   uint32_t qofs;  // Q - pos (modular)
   uint32_t z, n, tb, cpl, c0, bpmm, dc0, ac0;
-  // s_w: the LSB-first staged words, word i at stream position 32 * (wbase + i) = wb32 + 32 i;
-  // pat: bit j = slot of block-in-MCU (j mod bpm); tabs: DC slots 0, 1 then AC slots 0, 1
+  // s_w: the LSB-first staged words, word i at stream position wb32 + 32 i; pat: bits SB j ..
+  // SB j + SB - 1 = table slot of block-in-MCU (j mod bpm); tabs: the NT DC tables, then NT AC
   __device__ __forceinline__ void init(const uint32_t *s_w, uint32_t wb32, uint64_t X, uint32_t pat, uint32_t bpm,
-                                       const SyncTab32 *tabs) {
-    qofs = 8u * (uint32_t)(uintptr_t)s_w - wb32 - 2u;
+                                       const Tab *tabs) {
+    qofs = 8u * (uint32_t)(uintptr_t)s_w - wb32 - kLead;
     Q = (uint32_t)(X >> 16) + qofs;
     z = (X >> 8) & 0xFF;
     c0 = (uint32_t)(X & 0xFF);
     n = 0;
     bpmm = bpm - 1;
-    cpl = __builtin_amdgcn_alignbit(pat, pat, c0);  // rotate right by c0: bit k = slot of block c0 + k
+    cpl = __builtin_amdgcn_alignbit(pat, pat, SB * c0);  // rotate right: field k = slot of block c0 + k
     dc0 = (uint32_t)(uintptr_t)tabs;
-    ac0 = dc0 + 2u * (uint32_t)sizeof(SyncTab32);
-    tb = (cpl & 1u) * (uint32_t)sizeof(SyncTab32) + (z == 0 ? dc0 : ac0);
+    ac0 = dc0 + NT * (uint32_t)sizeof(Tab);
+    tb = (cpl & ((1u << SB) - 1)) * (uint32_t)sizeof(Tab) + (z == 0 ? dc0 : ac0);
   }
   __device__ __forceinline__ uint32_t pos() const { return Q - qofs; }
   __device__ __forceinline__ uint32_t c() const { return (c0 + n) & bpmm; }
   // n = 0 for the next subsequence's count; the slot pattern and c0 move on by the blocks counted
   __device__ __forceinline__ void restart_count() {
     c0 = (c0 + n) & bpmm;
-    cpl = __builtin_amdgcn_alignbit(cpl, cpl, n);
+    cpl = __builtin_amdgcn_alignbit(cpl, cpl, SB * n);
     n = 0;
   }
   __device__ __forceinline__ uint64_t state() const { return pack_state(pos(), z, c()); }
-  __device__ __forceinline__ static uint32_t lds(uint32_t a) {
-    return *reinterpret_cast<const __attribute__((address_space(3))) uint32_t *>((size_t)a);
+  template <typename T>
+  __device__ __forceinline__ static T lds(uint32_t a) {
+    return *reinterpret_cast<const __attribute__((address_space(3))) T *>((size_t)a);
   }
   // steps while pos < stop
-  __device__ __forceinline__ void run(const SyncTab32 *, uint32_t stop) {
+  __device__ __forceinline__ void run(const Tab *, uint32_t stop) {
     const uint32_t Qs = stop + qofs;
     while (Q < Qs) step(Qs);
   }
-  // The window is read from bit pos - 2 on, so the fast table's byte offset is r & (4 * 511).
-  // The fast entries' upper half is the pair entry, or a copy of the lower half where there is
-  // none (load_sync_tabs4<true>), so taking "the pair" needs no test of whether there is one.
+  // The window is read from bit pos - kLead on, so the fast table's byte offset is r & (kEnt * 511).
+  // PAIRS: the fast entries' upper half is the pair entry, or a copy of the lower half where there
+  // is none (load_sync_tabs4<true>), so taking "the pair" needs no test of whether there is one.
   __device__ __forceinline__ void step(uint32_t Qs) {
     const uint32_t a = (Q >> 3) & ~3u;
-    const uint32_t r = __builtin_amdgcn_alignbit(lds(a + 4), lds(a), Q);  // bits pos-2 .. pos+29, LSB-first
-    uint32_t e = lds(tb + (uint32_t)offsetof(SyncTab32, sfast) + (r & (((1u << kLook) - 1) << 2)));
+    const uint32_t r = __builtin_amdgcn_alignbit(lds<uint32_t>(a + 4), lds<uint32_t>(a), Q);  // LSB-first
+    const uint32_t ea = tb + (uint32_t)offsetof(Tab, sfast) + (r & (((1u << kLook) - 1) * kEnt));
+    uint32_t e = kEnt == 4 ? lds<uint32_t>(ea) : (uint32_t)lds<uint16_t>(ea);
+    if constexpr (kEnt == 2) asm("" : "+v"(e));  // a 32-bit value from here (else the branch below compiles as an if / else on 16 bits)
     if (!e) {  // a code longer than kLook bits (rare): as SpanLane
-      const uint32_t c16 = (__builtin_bitreverse32(r) >> 14) & 0xFFFFu;
-      const __attribute__((address_space(3))) uint32_t *lim =
-          reinterpret_cast<const __attribute__((address_space(3))) uint32_t *>((size_t)tb);
+      const uint32_t c16 = (__builtin_bitreverse32(r) >> (16 - kLead)) & 0xFFFFu;
       uint32_t len = kLook + 1, sym = 0;
 #pragma unroll
-      for (int i = 0; i < 7; ++i) len += c16 >= lim[i] ? 1u : 0u;
+      for (int i = 0; i < 7; ++i) len += c16 >= lds<uint32_t>(tb + (uint32_t)offsetof(Tab, lim) + 4u * i) ? 1u : 0u;
       if (len > 16) len = 16;
       else {
-        const int32_t vo = *reinterpret_cast<const __attribute__((address_space(3))) int32_t *>(
-            (size_t)(tb + (uint32_t)offsetof(SyncTab32, valoff) + 4u * len));
-        sym = *reinterpret_cast<const __attribute__((address_space(3))) uint8_t *>(
-            (size_t)(tb + (uint32_t)offsetof(SyncTab32, vals) + ((uint32_t)((int32_t)(c16 >> (16 - len)) + vo) & 255u)));
+        const int32_t vo = lds<int32_t>(tb + (uint32_t)offsetof(Tab, valoff) + 4u * len);
+        sym = lds<uint8_t>(tb + (uint32_t)offsetof(Tab, vals) + ((uint32_t)((int32_t)(c16 >> (16 - len)) + vo) & 255u));
       }
       uint32_t extra, adv;
       if (z == 0) {
@@ -784,25 +788,39 @@ struct SpanLaneR {
         adv = extra ? (sym >> 4) + 1 : ((sym >> 4) == 15 ? 16 : 64);
       }
       e = (adv << 8) | (len + extra);
-      e |= e << 16;  // no pair
+      if constexpr (PAIRS) e |= e << 16;  // no pair
     }
-    const uint32_t Q1 = Q + (e & 0xFF);
-    const uint32_t z1 = z + ((e >> 8) & 0xFF);
-    const bool two = z1 < 64 && Q1 < Qs;  // (advance << 24) | (length << 16): both symbols, or the first again
-    Q = two ? Q + ((e >> 16) & 0xFF) : Q1;
-    z = two ? z + (e >> 24) : z1;
+    if constexpr (PAIRS) {
+      const uint32_t Q1 = Q + (e & 0xFF);
+      const uint32_t z1 = z + ((e >> 8) & 0xFF);
+      const bool two = z1 < 64 && Q1 < Qs;  // (advance << 24) | (length << 16): both symbols, or the first again
+      Q = two ? Q + ((e >> 16) & 0xFF) : Q1;
+      z = two ? z + (e >> 24) : z1;
+    } else {
+      Q += e & 0xFF;
+      z += (e >> 8) & 0xFF;
+    }
     const bool eob = z >= 64;
     z = eob ? 0u : z;
     n += eob ? 1u : 0u;
-    tb = __builtin_amdgcn_ubfe(cpl, n, 1u) * (uint32_t)sizeof(SyncTab32) + (eob ? dc0 : ac0);
+    tb = __builtin_amdgcn_ubfe(cpl, SB * n, SB) * (uint32_t)sizeof(Tab) + (eob ? dc0 : ac0);
   }
 };
+using SpanLaneR = SpanLaneRT<SyncTab32, 2, 1, true>;
 
+template <bool REV = false>  // REV: fast entries at bit-reversed indices (SpanLaneRT)
 __device__ __forceinline__ void load_sync_tables(const DecFrame &F, HuffSync *tabs) {
   const uint32_t *src = reinterpret_cast<const uint32_t *>(&F.sdc[0]);
   uint32_t *dst = reinterpret_cast<uint32_t *>(tabs);
   constexpr uint32_t nw = 6 * sizeof(HuffSync) / 4;
   for (uint32_t j = threadIdx.x; j < nw; j += blockDim.x) dst[j] = src[j];
+  if constexpr (REV) {
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < 6 * (1u << kLook); j += blockDim.x) {
+      const uint32_t t = j >> kLook, i = j & ((1u << kLook) - 1);
+      tabs[t].sfast[__builtin_bitreverse32(i) >> (32 - kLook)] = (t < 3 ? F.sdc[t] : F.sac[t - 3]).sfast[i];
+    }
+  }
   __syncthreads();
 }
 
@@ -1169,12 +1187,22 @@ constexpr uint8_t kLinkLast = 0xE;  // the frame's last subsequence: decoded to 
 // states (ex(c)).  Returns the trajectory joined, or kLinkNone with *endst = the state at the
 // first symbol boundary at/after `end`, or kLinkLast (the frame's last subsequence, decoded to
 // its end).  *count = blocks completed in the subsequence along this path.
-template <typename CK, typename REM, typename EX>
+// k_spec's lanes: SpanLane, or on LSB-first words the six-table SpanLaneRT (2-bit component slots)
+template <bool LSB>
+using SpecLane = std::conditional_t<LSB, SpanLaneRT<HuffSync, 3, 2, false>, SpanLane<HuffSync, 3, false>>;
+template <bool LSB>
+__device__ __forceinline__ void spec_lane_init(SpecLane<LSB> &d, const uint32_t *words, uint32_t wb32, uint64_t X,
+                                               const HuffGeom &hg, const HuffSync *tabs) {
+  if constexpr (LSB) d.init(words, wb32, X, hg.pat, hg.bpm, tabs);
+  else d.init(words, wb32, X, hg);
+}
+
+template <bool LSB, typename CK, typename REM, typename EX>
 __device__ __forceinline__ uint32_t spec_link(const uint32_t *words, uint32_t wb32, uint64_t X, uint32_t base,
                                               uint32_t end, bool last, const HuffGeom &hg, const HuffSync *tabs, CK ck,
                                               REM rem, EX ex, uint32_t *count, uint64_t *endst) {
-  SpanLane<HuffSync, 3, false> d;
-  d.init(words, wb32, X, hg);
+  SpecLane<LSB> d;
+  spec_lane_init<LSB>(d, words, wb32, X, hg, tabs);
   uint32_t m = 0;
   while (m < kCk && base + (m + 1) * kCkStep <= d.pos()) ++m;
   for (;;) {  // decode to the next mark (a checkpoint inside the subsequence) or to its end
@@ -1205,6 +1233,7 @@ __device__ __forceinline__ uint32_t spec_link(const uint32_t *words, uint32_t wb
   return kLinkNone;
 }
 
+template <bool LSB>  // LSB: every frame's blocks per MCU divide 16 (SpanLaneRT on LSB-first words)
 __global__ __launch_bounds__(256) void k_spec(const DecSeg *__restrict__ sg, const DecFrame *__restrict__ fr, const uint8_t *us, const uint32_t *us_len,
                                               SpecBufs B) {
   // States here are kept relative to the workgroup's first bit in 32 bits (rel / absl below),
@@ -1221,7 +1250,9 @@ __global__ __launch_bounds__(256) void k_spec(const DecSeg *__restrict__ sg, con
   const DecSeg S = sg[blockIdx.y];  // by value: held in scalar registers
   const DecFrame &F = fr[S.frame];
   if (blockIdx.x >= S.nwg) return;
-  const HuffGeom hg(F.g);
+  HuffGeom hg(F.g);
+  if constexpr (LSB)  // 2-bit component of block-in-MCU (j mod bpm) at bits 2j, 2j + 1
+    for (uint32_t j = 0, c = 0; j < 16; ++j, c = c + 1 == hg.bpm ? 0u : c + 1) hg.pat |= hg.comp(c) << (2 * j);
   const uint32_t L = spec_lanes(hg.bpm), NS = 256 / L, NSS = NS - 1;  // rows, rows not shared with w+1
   const uint32_t t = threadIdx.x, sl = t / L, c0 = t % L;
   const uint32_t s = blockIdx.x * NSS + sl;
@@ -1237,9 +1268,11 @@ __global__ __launch_bounds__(256) void k_spec(const DecSeg *__restrict__ sg, con
   const uint32_t wb32 = (woff - 1u) * 32u;  // modular
   const uint32_t fwords = (((S.in_len + 64) + 15) & ~15u) / 4;
   const uint32_t *gw = reinterpret_cast<const uint32_t *>(us + S.us_off);
-  for (uint32_t i = t; i < 1 + NS * (kSubBits / 32) + kSpecPadWords; i += 256)
-    s_w[i] = woff - 1u + i < fwords ? bswap32(gw[woff - 1u + i]) : 0u;
-  load_sync_tables(F, tabs);  // its barrier also publishes s_w
+  for (uint32_t i = t; i < 1 + NS * (kSubBits / 32) + kSpecPadWords; i += 256) {
+    const uint32_t v = woff - 1u + i < fwords ? gw[woff - 1u + i] : 0u;
+    s_w[i] = LSB ? bswap32(__builtin_bitreverse32(v)) : bswap32(v);  // LSB-first / byte-swapped
+  }
+  load_sync_tables<LSB>(F, tabs);  // its barrier also publishes s_w
 #ifndef VF_SPEC_PHASES
 #define VF_SPEC_PHASES 0
 #endif
@@ -1263,8 +1296,8 @@ __global__ __launch_bounds__(256) void k_spec(const DecSeg *__restrict__ sg, con
 #pragma unroll
   for (int m = 0; m < kCk; ++m) s_ck[m][t] = 0xFFFFFFFFu;
   if (live) {
-    SpanLane<HuffSync, 3, false> d;
-    d.init(s_w, wb32, pack_state(base, 0, c0), hg);
+    SpecLane<LSB> d;
+    spec_lane_init<LSB>(d, s_w, wb32, pack_state(base, 0, c0), hg, tabs);
     uint32_t m = 0;
     for (;;) {  // decode to the next checkpoint mark inside the subsequence, or to its end
       const uint32_t mk = base + (m + 1) * kCkStep;
@@ -1289,7 +1322,7 @@ __global__ __launch_bounds__(256) void k_spec(const DecSeg *__restrict__ sg, con
   uint64_t X = 0;
   if (live && sl > 0) {
     const uint32_t row = sl * L;
-    M = spec_link(s_w, wb32, absl(s_E[(sl - 1) * L + c0]), base, end, s + 1 == nsub, hg, tabs,
+    M = spec_link<LSB>(s_w, wb32, absl(s_E[(sl - 1) * L + c0]), base, end, s + 1 == nsub, hg, tabs,
                   [&](uint32_t c2, int m) { return absl(s_ck[m][row + c2]); },
                   [&](uint32_t c2, int m) { return (uint32_t)s_rem[m][row + c2]; },
                   [&](uint32_t c2) { return absl(s_E[row + c2]); }, &C, &X);
@@ -1379,7 +1412,7 @@ __global__ __launch_bounds__(256) void k_spec(const DecSeg *__restrict__ sg, con
         if (VF_SPEC_PHASES) atomicAdd(B.stats + 2, 1u);  // explicit rows decoded by walkers
         const uint32_t bk = sk * kSubBits, ek = (sk + 1 >= nsub) ? nbits : (sk + 1) * kSubBits;
         const uint32_t row = k * L;
-        M2 = spec_link(s_w, wb32, st, bk, ek, sk + 1 == nsub, hg, tabs,
+        M2 = spec_link<LSB>(s_w, wb32, st, bk, ek, sk + 1 == nsub, hg, tabs,
                        [&](uint32_t c2, int m) { return absl(s_ck[m][row + c2]); },
                        [&](uint32_t c2, int m) { return (uint32_t)s_rem[m][row + c2]; },
                        [&](uint32_t c2) { return absl(s_E[row + c2]); }, &cnt, &xe);
@@ -1403,8 +1436,8 @@ __global__ __launch_bounds__(256) void k_spec(const DecSeg *__restrict__ sg, con
       const uint32_t sk = blockIdx.x * NSS + NS;
       const uint32_t ek = (sk + 1 >= nsub) ? nbits : (sk + 1) * kSubBits;
       const uint32_t lim = min(ek, (woff + NS * (kSubBits / 32) + kSpecPadWords - 4) * 32u);  // binds only on corrupt data
-      SpanLane<HuffSync, 3, false> d;
-      d.init(s_w, wb32, st, hg);
+      SpecLane<LSB> d;
+      spec_lane_init<LSB>(d, s_w, wb32, st, hg, tabs);
       d.run(tabs, lim);
       B.qX[g0 + 256 + L + e] = d.state();  // slot (w + 1, row 1, lane e)
       B.qC[g0 + 256 + L + e] = d.n;
@@ -3473,9 +3506,10 @@ hipError_t dec_syncg(int G, const DecSeg *__restrict__ sg, const DecFrame *__res
 
 hipError_t dec_sync_spec(const DecSeg *__restrict__ sg, const DecFrame *__restrict__ fr, int nseg, uint32_t max_wg, const uint8_t *us,
                          const uint32_t *us_len, const SpecBufs &b, uint64_t *exit_out, uint32_t *cnt_out,
-                         uint32_t *unresolved, hipStream_t s) {
+                         uint32_t *unresolved, int lsb, hipStream_t s) {
   if (nseg <= 0 || !max_wg) return hipSuccess;
-  hipLaunchKernelGGL(k_spec, dim3(max_wg, (unsigned)nseg), dim3(256), 0, s, sg, fr, us, us_len, b);
+  if (lsb) hipLaunchKernelGGL(k_spec<true>, dim3(max_wg, (unsigned)nseg), dim3(256), 0, s, sg, fr, us, us_len, b);
+  else hipLaunchKernelGGL(k_spec<false>, dim3(max_wg, (unsigned)nseg), dim3(256), 0, s, sg, fr, us, us_len, b);
   hipLaunchKernelGGL(k_resolve, dim3((unsigned)nseg), dim3(256), 0, s, sg, fr, us, us_len, b, unresolved);
   hipLaunchKernelGGL(k_finalize, dim3(max_wg, (unsigned)nseg), dim3(256), 0, s, sg, fr, us_len, b, exit_out, cnt_out);
   return hipGetLastError();

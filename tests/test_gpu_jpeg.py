@@ -349,6 +349,27 @@ def test_span_sync_lsb_lane(tj, monkeypatch, lsb, g, warm):
     assert np.array_equal(tj.decode(long16), J.decode(long16))
 
 
+@pytest.mark.parametrize("lsb", ["1", "0"])
+def test_speculative_sync_lsb_lane(tj, monkeypatch, lsb):
+    """k_spec on LSB-first words (SpanLaneRT over the six 16-bit HuffSync tables, 2-bit component
+    slots; every frame's block cycle divides 16): scenes, noise with long blocks, 16-bit AC codes
+    (the bit-reversed slow path), grayscale, several workgroups per frame, in one batch and
+    alone; a batch with a 4:2:0 frame takes the MSB-first lane.  Bit-exact with the oracle and
+    equal with VF_JPEG_SYNC_LSB=0."""
+    import jpeg_recode as R
+    monkeypatch.setenv("VF_JPEG_SYNC", "spec")
+    monkeypatch.setenv("VF_JPEG_SYNC_LSB", lsb)
+    rng = np.random.default_rng(21)
+    frames = [J.encode(_img("scene", 20, 480, 640), 85, J.TJPF_BGR, J.TJSAMP_422),
+              J.encode(rng.integers(0, 256, (128, 160, 3), dtype=np.uint8), 90, J.TJPF_BGR, J.TJSAMP_422),
+              R.recode(J.encode(_img("scene", 21, 160, 200), 85, J.TJPF_BGR, J.TJSAMP_422), ac_long=16),
+              J.encode(_img("scene", 22, 270, 360), 85, J.TJPF_BGR, J.TJSAMP_GRAY)]
+    b420 = J.encode(_img("scene", 23, 64, 80), 85, J.TJPF_BGR, J.TJSAMP_420)
+    for batch in (frames, frames[2:3], frames + [b420]):
+        assert [bytes(o) for o in tj.invert_batch(batch)] == [J.invert_jpeg(j) for j in batch]
+    assert np.array_equal(tj.decode(frames[2]), J.decode(frames[2]))
+
+
 @pytest.mark.parametrize("queued", ["1", "2"])
 def test_span_sync_unconverged_passes_resume(tj, monkeypatch, queued):
     """When the queued span passes leave a workgroup's last exit changing (forced here with
