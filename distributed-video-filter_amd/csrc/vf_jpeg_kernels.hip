@@ -1842,8 +1842,9 @@ __device__ __forceinline__ int32_t imul(int32_t a, int32_t c) {
   if constexpr (M24) return __mul24(a, c);
   else return a * c;
 }
-template <bool M24>
-__device__ __forceinline__ void idct_line(const int32_t in[8], int32_t out[8], int shift) {
+// jidctint.c's butterflies; emit(i, v) receives output i before its descale
+template <bool M24, typename Emit>
+__device__ __forceinline__ void idct_core(const int32_t in[8], Emit emit) {
   int32_t tmp0, tmp1, tmp2, tmp3, tmp10, tmp11, tmp12, tmp13, z1, z2, z3, z4, z5;
   z2 = in[2];
   z3 = in[6];
@@ -1879,21 +1880,31 @@ __device__ __forceinline__ void idct_line(const int32_t in[8], int32_t out[8], i
   tmp1 += z2 + z4;
   tmp2 += z2 + z3;
   tmp3 += z1 + z4;
+  emit(0, tmp10 + tmp3);
+  emit(7, tmp10 - tmp3);
+  emit(1, tmp11 + tmp2);
+  emit(6, tmp11 - tmp2);
+  emit(2, tmp12 + tmp1);
+  emit(5, tmp12 - tmp1);
+  emit(3, tmp13 + tmp0);
+  emit(4, tmp13 - tmp0);
+}
+template <bool M24>
+__device__ __forceinline__ void idct_line(const int32_t in[8], int32_t out[8], int shift) {
   const int32_t r = (int32_t)1 << (shift - 1);
-  out[0] = (tmp10 + tmp3 + r) >> shift;
-  out[7] = (tmp10 - tmp3 + r) >> shift;
-  out[1] = (tmp11 + tmp2 + r) >> shift;
-  out[6] = (tmp11 - tmp2 + r) >> shift;
-  out[2] = (tmp12 + tmp1 + r) >> shift;
-  out[5] = (tmp12 - tmp1 + r) >> shift;
-  out[3] = (tmp13 + tmp0 + r) >> shift;
-  out[4] = (tmp13 - tmp0 + r) >> shift;
+  idct_core<M24>(in, [&](int i, int32_t v) { out[i] = (v + r) >> shift; });
 }
 
-// jdmaster.c prepare_range_limit_table, post-IDCT part (RANGE_MASK 1023)
-__device__ __forceinline__ uint32_t idct_limit(int32_t x) {
-  const int32_t m = x & 1023;
-  return m < 128 ? (uint32_t)(m + 128) : m < 512 ? 255u : m < 896 ? 0u : (uint32_t)(m - 896);
+// The row pass (descale by 18) with jdmaster.c prepare_range_limit_table's post-IDCT limit
+// (RANGE_MASK 1023) in three instructions: the table maps
+// m = x & 1023 to m + 128 (m < 128), 255 (< 512), 0 (< 896), m - 896, which for every x is
+// clamp(((x + 512) & 1023) - 384, 0, 255); with 512 << 18 added to the rounding constant, the
+// descale and the mask are one bit-field extract of the 32-bit sum (bits 18..27).
+__device__ __forceinline__ void idct_row_limited(const int32_t in[8], uint32_t out[8]) {
+  idct_core<true>(in, [&](int i, int32_t v) {
+    const int32_t m = (int32_t)__builtin_amdgcn_ubfe((uint32_t)v + ((1u << 17) + (512u << 18)), 18, 10) - 384;
+    out[i] = (uint32_t)min(max(m, 0), 255);
+  });
 }
 
 // Measured (tools/gpu_jpeg_variants.sh, profiles/r01_jpeg_idct_variants.txt; dc + idct ms at
@@ -2019,15 +2030,16 @@ __global__ __launch_bounds__(256) void k_idct(const DecFrame *__restrict__ fr, c
 #pragma unroll
   for (int h = 0; h < kIdctNb; ++h) {  // pass 2: row r
     if (!valid[h]) continue;
-    int32_t in[8], out[8];
+    int32_t in[8];
+    uint32_t out[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) in[i] = blkv[h * 32 + slot][r * 9 + i];
-    idct_line<true>(in, out, 18);
+    idct_row_limited(in, out);
     uint32_t lo = 0, hi = 0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      lo |= idct_limit(out[i]) << (8 * i);
-      hi |= idct_limit(out[i + 4]) << (8 * i);
+      lo |= out[i] << (8 * i);
+      hi |= out[i + 4] << (8 * i);
     }
     uint8_t *p = plane + (uint64_t)(bys[h] * 8 + r) * pw + bxs[h] * 8;
     *reinterpret_cast<uint2 *>(p) = make_uint2(lo, hi);
@@ -2534,7 +2546,9 @@ __global__ __launch_bounds__(256) void k_idct_color422(const DecFrame *__restric
   const int mcux = g.mcux, my = blockIdx.y, m0 = blockIdx.x * kStripMcus;
   if (m0 >= mcux || my >= g.mcuy) return;
   __shared__ int32_t blkv[kIdctBlocks][72];
-  __shared__ int32_t s_q[3][72];
+  // dequantisation in zigzag order: lane r multiplies its 8 coefficients (zigzag 8r .. 8r + 7) as
+  // it stores them, so pass 1 reads dequantised values (jidctint.c's DEQUANTIZE, moved earlier)
+  __shared__ __attribute__((aligned(16))) uint16_t s_qz[3][64];
   __shared__ uint8_t s_pos[64];
   __shared__ uint32_t s_col[8];
   // the strip's samples reuse the coefficient rows once pass 2 has read them (one barrier more,
@@ -2567,7 +2581,7 @@ __global__ __launch_bounds__(256) void k_idct_color422(const DecFrame *__restric
     dc[h] = dcseq[di];
     nm[h] = nmask ? (uint32_t)nmask[bi] : 0xFFu;
   }
-  if (t < 192) s_q[t >> 6][t & 63] = F.q[t >> 6][t & 63];
+  if (t < 192) s_qz[t >> 6][kZigOf[t & 63]] = F.q[t >> 6][t & 63];
   if (t < 64) s_pos[t] = kIdctPos[t];
   if (t < 8) s_col[t] = kIdctCol[t];
   __syncthreads();
@@ -2578,11 +2592,13 @@ __global__ __launch_bounds__(256) void k_idct_color422(const DecFrame *__restric
     if (!valid[h]) continue;
     const bool st = (nm[h] >> r) & 1;  // a row the write pass did not store is zero
     const uint32_t qw[4] = {st ? raw[h].x : 0u, st ? raw[h].y : 0u, st ? raw[h].z : 0u, st ? raw[h].w : 0u};
+    const uint4 q4 = *reinterpret_cast<const uint4 *>(&s_qz[kk[h]][r * 8]);
+    const uint32_t qq[4] = {q4.x, q4.y, q4.z, q4.w};
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int32_t v = (int32_t)(int16_t)(qw[j >> 1] >> (16 * (j & 1)));
+      const int32_t v = (r == 0 && j == 0) ? (int32_t)(int16_t)dc[h] : (int32_t)(int16_t)(qw[j >> 1] >> (16 * (j & 1)));
       const uint32_t at = ((j < 4 ? pos8.x : pos8.y) >> (8 * (j & 3))) & 0xFF;
-      blkv[h * 32 + slot][at] = (r == 0 && j == 0) ? (int32_t)(int16_t)dc[h] : v;
+      blkv[h * 32 + slot][at] = __mul24(v, (int32_t)((qq[j >> 1] >> (16 * (j & 1))) & 0xFFFF));
     }
   }
   __syncthreads();
@@ -2593,8 +2609,7 @@ __global__ __launch_bounds__(256) void k_idct_color422(const DecFrame *__restric
       if (!valid[h]) continue;
       int32_t in[8];
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
-        in[i] = __mul24(blkv[h * 32 + slot][i * 8 + ((colg >> (4 * i)) & 7)], s_q[kk[h]][i * 8 + r]);
+      for (int i = 0; i < 8; ++i) in[i] = blkv[h * 32 + slot][i * 8 + ((colg >> (4 * i)) & 7)];
       idct_line<decltype(m24)::value>(in, col[h], 11);
     }
   };
@@ -2611,15 +2626,16 @@ __global__ __launch_bounds__(256) void k_idct_color422(const DecFrame *__restric
   uint2 row8[kIdctNb];
 #pragma unroll
   for (int h = 0; h < kIdctNb; ++h) {  // pass 2: row r
-    int32_t in[8], out[8];
+    int32_t in[8];
+    uint32_t out[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) in[i] = blkv[h * 32 + slot][r * 9 + i];
-    idct_line<true>(in, out, 18);
+    idct_row_limited(in, out);
     uint32_t lo = 0, hi = 0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      lo |= idct_limit(out[i]) << (8 * i);
-      hi |= idct_limit(out[i + 4]) << (8 * i);
+      lo |= out[i] << (8 * i);
+      hi |= out[i + 4] << (8 * i);
     }
     row8[h] = make_uint2(lo, hi);
   }
