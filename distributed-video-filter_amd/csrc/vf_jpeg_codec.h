@@ -207,6 +207,10 @@ class Codec {
   int sync_last_ = 0;                 // exit / count slot of the pass-based sync's result
   bool enc_fast_ = false;             // submit_invert's DCT (wait_invert re-encodes after finish_sync)
   TaskPool pool_{4};
+  double prep_ms_[3] = {0, 0, 0};  // VF_JPEG_TRACE: prepare_decode's parse / descriptor loop / staging
+  std::vector<uint64_t> ekey_;     // prepare_encode's last batch shape (n, settings, sizes, offsets)
+  bool ekey_valid_ = false;        // ... and its device-side descriptors are current
+  uint64_t enc_prep_reused_ = 0;
 };
 
 }  // namespace jpeg

@@ -305,13 +305,26 @@ int Codec::prepare_decode(const uint8_t *const *jpegs, const size_t *sizes, int 
   dmax_w_ = dmax_h_ = 0;
   // per frame, in parallel: markers, scan end, geometry and decode tables
   std::vector<std::string> ferr((size_t)n);
+  using clk = std::chrono::steady_clock;
+  const auto tp0 = clk::now();
+  // the bound k_idct's column pass needs for 24-bit multiplies (vf_jpeg_types.h), per frame on its
+  // parse task: the largest AC size over its tables (unused symbol slots are zero) and AC quantiser
+  std::vector<uint8_t> m24ok((size_t)n);
   pool_.run(n, [&](int f) {
     Parsed &P = parsed[(size_t)f];
     std::string &e = ferr[(size_t)f];
     DecFrame &F = *new (&dfr_[(size_t)f]) DecFrame();  // value-initialised, by the frame's own task
     parse_frame(jpegs[f], sizes[f], max_pixels_, &P, &F.g, F.dc, F.ac, F.sdc, F.sac, F.spair, &e);  // vf_jpeg_parse.h
     for (int c = 0; c < P.ncomp && e.empty(); ++c) std::memcpy(F.q[c], P.qt[P.tq[c]], sizeof F.q[c]);
+    int ac_size = 0;
+    uint32_t q_ac = 0;
+    for (int c = 0; c < F.g.ncomp && e.empty(); ++c) {
+      for (int i = 0; i < 256; ++i) ac_size = std::max(ac_size, (int)(F.ac[c].vals[i] & 15));
+      for (int i = 1; i < 64; ++i) q_ac = std::max(q_ac, (uint32_t)F.q[c][i]);
+    }
+    m24ok[(size_t)f] = e.empty() && idct_col24_ok(ac_size, q_ac) ? 1 : 0;
   });
+  const auto tp1 = clk::now();
   for (int f = 0; f < n; ++f)
     if (!ferr[(size_t)f].empty()) {
       *err = "frame " + std::to_string(f) + ": " + ferr[(size_t)f];
@@ -335,15 +348,7 @@ int Codec::prepare_decode(const uint8_t *const *jpegs, const size_t *sizes, int 
       if (g.ncomp == 3 && g.he[0] == 1 && g.ve[0] == 1 && g.he[1] == g.he[2] && g.ve[1] == g.ve[2])
         cm = g.he[1] == 1 && g.ve[1] == 1 ? 1u : g.he[1] == 2 && g.ve[1] == 1 ? 2u : g.he[1] == 2 && g.ve[1] == 2 ? 3u : 0u;
       F.flags |= cm << 1;
-      // the bound k_idct's column pass needs for 24-bit multiplies (vf_jpeg_types.h); the AC
-      // tables' unused symbol slots are zero
-      int ac_size = 0;
-      uint32_t q_ac = 0;
-      for (int c = 0; c < g.ncomp; ++c) {
-        for (int i = 0; i < 256; ++i) ac_size = std::max(ac_size, (int)(F.ac[c].vals[i] & 15));
-        for (int i = 1; i < 64; ++i) q_ac = std::max(q_ac, (uint32_t)F.q[c][i]);
-      }
-      if (idct24 && idct_col24_ok(ac_size, q_ac)) F.flags |= kDecIdct24;
+      if (idct24 && m24ok[(size_t)f]) F.flags |= kDecIdct24;
       dcm_ = dcm_ == -2 || dcm_ == (int)cm ? (int)cm : -1;
       d422_ = d422_ && g.ncomp == 3 && g.hs[0] == 2 && g.vs[0] == 1 && g.hs[1] == 1 && g.vs[1] == 1 &&
               g.hs[2] == 1 && g.vs[2] == 1 && g.bpm == 4;
@@ -463,6 +468,7 @@ int Codec::prepare_decode(const uint8_t *const *jpegs, const size_t *sizes, int 
       ++ndcseg_;
     }
   }
+  const auto tp2 = clk::now();
   // staging: inputs packed, then uploaded in one copy
   CK(h_stage_.ensure(in_off));
   pool_.run(dnseg_, [&](int i) {
@@ -524,6 +530,12 @@ int Codec::prepare_decode(const uint8_t *const *jpegs, const size_t *sizes, int 
   CK(hipMemcpyAsync(d_dfr_.p, h_dfr_.p, dsz, hipMemcpyHostToDevice, s_));
   CK(hipMemcpyAsync(d_dsg_.p, h_ddesc_.p, gsz, hipMemcpyHostToDevice, s_));
   CK(hipMemcpyAsync(d_segs_.p, h_ddesc_.as<uint8_t>() + gsz, ssz, hipMemcpyHostToDevice, s_));
+  {  // VF_JPEG_TRACE's split of prep_dec: parse tasks | descriptor loop | staging, buffers, uploads
+    auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    prep_ms_[0] = ms(tp0, tp1);
+    prep_ms_[1] = ms(tp1, tp2);
+    prep_ms_[2] = ms(tp2, clk::now());
+  }
   return kOk;
 }
 
@@ -803,6 +815,27 @@ int Codec::prepare_encode(const int *ws, const int *hs, const uint64_t *img_offs
     return kInvalid;
   }
   fuse_ = false;  // the invert paths turn it on after both prepares
+  // Everything below depends only on the frames' sizes and layout and the settings: a batch shaped
+  // like this codec's previous one (a worker's steady state) reuses its descriptors, tables,
+  // headers and buffers, already on the device (nothing else writes them).
+  {
+    std::vector<uint64_t> key;
+    key.reserve(3 * (size_t)n + 4);
+    key.push_back((uint64_t)n);
+    key.push_back((uint64_t)quality);
+    key.push_back((uint64_t)subsamp);
+    key.push_back(fastdct ? 1u : 0u);
+    for (int f = 0; f < n; ++f) {
+      key.push_back((uint64_t)(uint32_t)ws[f] << 32 | (uint32_t)hs[f]);
+      key.push_back(img_offs[f]);
+    }
+    if (ekey_valid_ && key == ekey_) {
+      ++enc_prep_reused_;
+      return kOk;
+    }
+    ekey_valid_ = false;  // until this prepare completes
+    ekey_.swap(key);
+  }
   efr_.assign((size_t)n, EncFrame());
   std::vector<uint8_t> hdr;
   uint64_t blk = 0, bits = 0, out = 0, epl = 0;
@@ -885,6 +918,7 @@ int Codec::prepare_encode(const int *ws, const int *hs, const uint64_t *img_offs
   CK(hipMemcpyAsync(d_etab_.p, hb + o_tab, sizeof tab, hipMemcpyHostToDevice, s_));
   CK(hipMemcpyAsync(d_hdr_.p, hb + o_hdr, hdr.size(), hipMemcpyHostToDevice, s_));
   CK(hipMemcpyAsync(d_esegs_.p, hb + o_seg, ssz, hipMemcpyHostToDevice, s_));
+  ekey_valid_ = true;
   return kOk;
 }
 
@@ -1101,8 +1135,9 @@ int Codec::submit_invert(const uint8_t *const *jpegs, const size_t *jsizes, int 
   if (trace) {
     auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
     static const clk::time_point origin = t0;
-    std::fprintf(stderr, "[vf_jpeg] submit codec %p n=%d at %.3f: prep_dec %.3f prep_enc %.3f queue %.3f ms\n",
-                 (void *)this, n, ms(origin, t0), ms(t0, t1), ms(t1, t2), ms(t2, clk::now()));
+    std::fprintf(stderr, "[vf_jpeg] submit codec %p n=%d at %.3f: prep_dec %.3f (parse %.3f loop %.3f stage %.3f) "
+                 "prep_enc %.3f queue %.3f ms\n", (void *)this, n, ms(origin, t0), ms(t0, t1), prep_ms_[0], prep_ms_[1],
+                 prep_ms_[2], ms(t1, t2), ms(t2, clk::now()));
   }
   return kOk;
 }
