@@ -159,6 +159,7 @@ class Codec {
   // submitting thread
   HostBuf h_dfr_;
   DecFrame *dfr_ = nullptr;
+  int ntabs_ = 0;  // distinct Huffman table sets (DecTabs) of the batch, after its DecFrames
   std::vector<DecSeg> dsg_;    // entropy-coded segments: one per frame, or one per restart interval
   std::vector<const uint8_t *> seg_src_;  // each segment's raw bytes in the caller's JPEG
   int dn_ = 0, dnseg_ = 0, ndcseg_ = 0;

@@ -293,7 +293,9 @@ int Codec::prepare_decode(const uint8_t *const *jpegs, const size_t *sizes, int 
     *err = "empty batch";
     return kInvalid;
   }
-  CK(h_dfr_.ensure(sizeof(DecFrame) * (size_t)n));
+  // [n DecFrames][the batch's distinct DecTabs], one pinned buffer and one upload
+  const size_t toff = align_up(sizeof(DecFrame) * (size_t)n, 256);
+  CK(h_dfr_.ensure(toff + sizeof(DecTabs) * (size_t)n));
   dfr_ = h_dfr_.as<DecFrame>();
   seg_src_.clear();
   std::vector<Parsed> parsed((size_t)n);
@@ -307,22 +309,25 @@ int Codec::prepare_decode(const uint8_t *const *jpegs, const size_t *sizes, int 
   std::vector<std::string> ferr((size_t)n);
   using clk = std::chrono::steady_clock;
   const auto tp0 = clk::now();
-  // the bound k_idct's column pass needs for 24-bit multiplies (vf_jpeg_types.h), per frame on its
-  // parse task: the largest AC size over its tables (unused symbol slots are zero) and AC quantiser
-  std::vector<uint8_t> m24ok((size_t)n);
+  // per frame on its parse task: markers, geometry, quantisers, the largest AC quantiser (the
+  // bound k_idct's column pass needs for 24-bit multiplies, vf_jpeg_types.h) and the key of its
+  // Huffman tables; the tables themselves are built once per distinct key below
+  std::vector<uint32_t> qmax((size_t)n);
+  std::vector<uint64_t> khash((size_t)n);
+  std::vector<std::vector<uint8_t>> keys((size_t)n);
   pool_.run(n, [&](int f) {
     Parsed &P = parsed[(size_t)f];
     std::string &e = ferr[(size_t)f];
     DecFrame &F = *new (&dfr_[(size_t)f]) DecFrame();  // value-initialised, by the frame's own task
-    parse_frame(jpegs[f], sizes[f], max_pixels_, &P, &F.g, F.dc, F.ac, F.sdc, F.sac, F.spair, &e);  // vf_jpeg_parse.h
-    for (int c = 0; c < P.ncomp && e.empty(); ++c) std::memcpy(F.q[c], P.qt[P.tq[c]], sizeof F.q[c]);
-    int ac_size = 0;
+    parse_frame(jpegs[f], sizes[f], max_pixels_, &P, &F.g, nullptr, nullptr, nullptr, nullptr, nullptr, &e);  // vf_jpeg_parse.h
+    if (!e.empty()) return;
     uint32_t q_ac = 0;
-    for (int c = 0; c < F.g.ncomp && e.empty(); ++c) {
-      for (int i = 0; i < 256; ++i) ac_size = std::max(ac_size, (int)(F.ac[c].vals[i] & 15));
+    for (int c = 0; c < P.ncomp; ++c) {
+      std::memcpy(F.q[c], P.qt[P.tq[c]], sizeof F.q[c]);
       for (int i = 1; i < 64; ++i) q_ac = std::max(q_ac, (uint32_t)F.q[c][i]);
     }
-    m24ok[(size_t)f] = e.empty() && idct_col24_ok(ac_size, q_ac) ? 1 : 0;
+    qmax[(size_t)f] = q_ac;
+    khash[(size_t)f] = table_key(P, &keys[(size_t)f]);
   });
   const auto tp1 = clk::now();
   for (int f = 0; f < n; ++f)
@@ -330,6 +335,33 @@ int Codec::prepare_decode(const uint8_t *const *jpegs, const size_t *sizes, int 
       *err = "frame " + std::to_string(f) + ": " + ferr[(size_t)f];
       return kJpeg;
     }
+  // the distinct table sets (a batch of one stream has one): built into the buffer after the frames
+  std::vector<int> uniq;      // first frame of each distinct set
+  std::vector<int> acmax;     // its largest AC size (unused symbol slots are zero)
+  std::vector<uint8_t> m24ok((size_t)n);  // the frame's tables and quantisers fit kDecIdct24
+  for (int f = 0; f < n; ++f) {
+    int u = 0;
+    for (; u < (int)uniq.size(); ++u)
+      if (khash[(size_t)uniq[(size_t)u]] == khash[(size_t)f] && keys[(size_t)uniq[(size_t)u]] == keys[(size_t)f]) break;
+    if (u == (int)uniq.size()) {
+      const Parsed &P = parsed[(size_t)f];
+      DecTabs &T = *new (h_dfr_.as<uint8_t>() + toff + sizeof(DecTabs) * uniq.size()) DecTabs();
+      for (int c = 0; c < P.ncomp; ++c)
+        if (!build_tables(P.dcbits[P.td[c]], P.dcvals[P.td[c]], true, &T.dc[c], &T.sdc[c]) ||
+            !build_tables(P.acbits[P.ta[c]], P.acvals[P.ta[c]], false, &T.ac[c], &T.sac[c], T.spair[c])) {
+          *err = "frame " + std::to_string(f) + ": bad Huffman table";
+          return kJpeg;
+        }
+      int a = 0;
+      for (int c = 0; c < P.ncomp; ++c)
+        for (int i = 0; i < 256; ++i) a = std::max(a, (int)(T.ac[c].vals[i] & 15));
+      uniq.push_back(f);
+      acmax.push_back(a);
+    }
+    dfr_[(size_t)f].tabs_off = toff + sizeof(DecTabs) * (size_t)u;
+    m24ok[(size_t)f] = idct_col24_ok(acmax[(size_t)u], qmax[(size_t)f]) ? 1 : 0;
+  }
+  ntabs_ = (int)uniq.size();
   dsg_.clear();
   dcm_ = -2;  // the batch's common k_color layout, or -1 (mixed)
   // VF_JPEG_IDCT24=0: every frame on the 32-bit column pass (an A/B and test selector)
@@ -477,7 +509,7 @@ int Codec::prepare_decode(const uint8_t *const *jpegs, const size_t *sizes, int 
   });
   CK(hipSetDevice(device_));
   CK(d_in_.ensure(in_off));
-  CK(d_dfr_.ensure(sizeof(DecFrame) * (size_t)n));
+  CK(d_dfr_.ensure(toff + sizeof(DecTabs) * (size_t)ntabs_));
   CK(d_dsg_.ensure(sizeof(DecSeg) * (size_t)dnseg_));
   CK(d_segs_.ensure(sizeof(ScanSeg) * segs.size()));
   CK(d_tile_.ensure(sizeof(uint32_t) * tiles));
@@ -521,7 +553,7 @@ int Codec::prepare_decode(const uint8_t *const *jpegs, const size_t *sizes, int 
   // descriptors go through pinned memory too, so every upload stays asynchronous and nothing
   // waits for the GPU before the kernels are queued (the pinned buffers are reused only by the
   // codec's next call, which starts after this one has synchronised)
-  const size_t dsz = sizeof(DecFrame) * (size_t)n, gsz = sizeof(DecSeg) * (size_t)dnseg_,
+  const size_t dsz = toff + sizeof(DecTabs) * (size_t)ntabs_, gsz = sizeof(DecSeg) * (size_t)dnseg_,
                ssz = sizeof(ScanSeg) * segs.size();
   CK(h_ddesc_.ensure(gsz + ssz));
   std::memcpy(h_ddesc_.as<uint8_t>(), dsg_.data(), gsz);

@@ -452,7 +452,12 @@ __device__ __forceinline__ void write_span(const uint32_t *w, uint32_t woff, uin
   if constexpr (STG) atomicMax(reinterpret_cast<uint32_t *>(stg.dc) + kStageBlocks, blk - stg.first);  // flush bound
 }
 
-__device__ __forceinline__ void load_tables(const DecFrame &F, HuffDec *tabs) {
+// frame F's Huffman tables (DecFrame::tabs_off, from the DecFrame array fr)
+__device__ __forceinline__ const DecTabs &tabs_of(const DecFrame *fr, const DecFrame &F) {
+  return *reinterpret_cast<const DecTabs *>(reinterpret_cast<const char *>(fr) + F.tabs_off);
+}
+
+__device__ __forceinline__ void load_tables(const DecTabs &F, HuffDec *tabs) {
   const uint32_t *src = reinterpret_cast<const uint32_t *>(&F.dc[0]);
   uint32_t *dst = reinterpret_cast<uint32_t *>(tabs);
   constexpr uint32_t nw = 6 * sizeof(HuffDec) / 4;
@@ -518,7 +523,7 @@ struct SyncTab32 {
 
 // F's six sync tables (sdc[3], sac[3]) with the AC pairs into LDS, then a barrier (which also
 // publishes whatever the caller staged before the call)
-__device__ __forceinline__ void load_sync_tabs32(const DecFrame &F, SyncTab32 *tabs) {
+__device__ __forceinline__ void load_sync_tabs32(const DecTabs &F, SyncTab32 *tabs) {
   for (uint32_t j = threadIdx.x; j < 6 * (8 + 18 + 64); j += blockDim.x) {
     const uint32_t t = j / 90, i = j - t * 90;
     const HuffSync &S = t < 3 ? F.sdc[t] : F.sac[t - 3];
@@ -539,8 +544,8 @@ __device__ __forceinline__ void load_sync_tabs32(const DecFrame &F, SyncTab32 *t
 // 9.6 KB of LDS instead of 14.4, so a workgroup stages 25 % more stream (G = 5) at 3 per CU.
 // The lanes' cpack then holds slots (tabs4_cpack), not components.  Then a barrier.
 template <bool REV = false>  // REV: fast entries at bit-reversed indices (SpanLaneR)
-__device__ __forceinline__ void load_sync_tabs4(const DecFrame &F, SyncTab32 *tabs) {
-  const uint32_t rep[2] = {(F.tabs4 >> 8) & 3u, (F.tabs4 >> 10) & 3u};
+__device__ __forceinline__ void load_sync_tabs4(const DecTabs &F, uint32_t tabs4, SyncTab32 *tabs) {
+  const uint32_t rep[2] = {(tabs4 >> 8) & 3u, (tabs4 >> 10) & 3u};
   for (uint32_t j = threadIdx.x; j < 4 * (8 + 18 + 64); j += blockDim.x) {
     const uint32_t t = j / 90, i = j - t * 90;
     const HuffSync &S = t < 2 ? F.sdc[rep[t]] : F.sac[rep[t - 2]];
@@ -809,7 +814,7 @@ struct SpanLaneRT {
 using SpanLaneR = SpanLaneRT<SyncTab32, 2, 1, true>;
 
 template <bool REV = false>  // REV: fast entries at bit-reversed indices (SpanLaneRT)
-__device__ __forceinline__ void load_sync_tables(const DecFrame &F, HuffSync *tabs) {
+__device__ __forceinline__ void load_sync_tables(const DecTabs &F, HuffSync *tabs) {
   const uint32_t *src = reinterpret_cast<const uint32_t *>(&F.sdc[0]);
   uint32_t *dst = reinterpret_cast<uint32_t *>(tabs);
   constexpr uint32_t nw = 6 * sizeof(HuffSync) / 4;
@@ -857,7 +862,7 @@ __global__ __launch_bounds__(256) void k_sync(const DecSeg *__restrict__ sg, con
   const DecSeg S = sg[blockIdx.y];  // by value: held in scalar registers
   const DecFrame &F = fr[S.frame];
   if (blockIdx.x * 256 >= S.nsub_max) return;
-  load_sync_tables(F, tabs);
+  load_sync_tables(tabs_of(fr, F), tabs);
   const HuffGeom hg(F.g);
   const uint32_t t = threadIdx.x;
   const uint32_t i = blockIdx.x * 256 + t;
@@ -1080,8 +1085,8 @@ __global__ __launch_bounds__(256) void k_syncg(const DecSeg *__restrict__ sg, co
       s_w[i] = LSB ? bswap32(__builtin_bitreverse32(v)) : bswap32(v);  // LSB-first / byte-swapped
     }
   }
-  if constexpr (NDC == 2) load_sync_tabs4<LSB>(F, tabs);  // its barrier also publishes s_w
-  else load_sync_tabs32(F, tabs);
+  if constexpr (NDC == 2) load_sync_tabs4<LSB>(tabs_of(fr, F), F.tabs4, tabs);  // its barrier also publishes s_w
+  else load_sync_tabs32(tabs_of(fr, F), tabs);
   HuffGeom hg(F.g);
   if constexpr (NDC == 2) hg.cpack = tabs4_cpack(hg, F.tabs4);
   if constexpr (LSB) {
@@ -1272,7 +1277,7 @@ __global__ __launch_bounds__(256) void k_spec(const DecSeg *__restrict__ sg, con
     const uint32_t v = woff - 1u + i < fwords ? gw[woff - 1u + i] : 0u;
     s_w[i] = LSB ? bswap32(__builtin_bitreverse32(v)) : bswap32(v);  // LSB-first / byte-swapped
   }
-  load_sync_tables<LSB>(F, tabs);  // its barrier also publishes s_w
+  load_sync_tables<LSB>(tabs_of(fr, F), tabs);  // its barrier also publishes s_w
 #ifndef VF_SPEC_PHASES
 #define VF_SPEC_PHASES 0
 #endif
@@ -1533,7 +1538,7 @@ __global__ __launch_bounds__(256) void k_resolve(const DecSeg *__restrict__ sg, 
   if (over) return;
   const uint32_t lastk = NS - 1;  // every workgroup but the frame's last is full
   {  // the sync tables' copy; the barrier below publishes it
-    const uint32_t *src = reinterpret_cast<const uint32_t *>(&F.sdc[0]);
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(&tabs_of(fr, F).sdc[0]);
     uint32_t *dst = reinterpret_cast<uint32_t *>(tabs);
     for (uint32_t j = threadIdx.x; j < 6 * sizeof(HuffSync) / 4; j += 256) dst[j] = src[j];
   }
@@ -1727,7 +1732,7 @@ __global__ __launch_bounds__(256) void k_write(const DecSeg *__restrict__ sg, co
   for (uint32_t k = threadIdx.x; k < kWords; k += 256) s_w[k] = woff + k < fwords ? gw[woff + k] : 0u;
   for (uint32_t k = threadIdx.x; k < kStageBlocks / 8; k += 256) reinterpret_cast<uint4 *>(s_nm)[k] = make_uint4(0, 0, 0, 0);
   if (threadIdx.x == 0) s_dc[kStageBlocks] = 0;
-  load_tables(F, tabs);  // its barrier also publishes s_w and the cleared stage
+  load_tables(tabs_of(fr, F), tabs);  // its barrier also publishes s_w and the cleared stage
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   const uint32_t nbits = us_len[blockIdx.y] * 8u;
   const uint32_t nsub = (nbits + kSubBits - 1) / kSubBits;
@@ -1780,7 +1785,7 @@ __global__ __launch_bounds__(256) void k_write4(const DecSeg *__restrict__ sg, c
   const uint32_t fwords = (((S.in_len + 64) + 15) & ~15u) / 4;
   const uint32_t *gw = reinterpret_cast<const uint32_t *>(us + S.us_off);
   for (uint32_t k = threadIdx.x; k < kW4Words; k += 256) s_w[k] = woff + k < fwords ? gw[woff + k] : 0u;
-  load_tables(F, tabs);  // its barrier also publishes s_w
+  load_tables(tabs_of(fr, F), tabs);  // its barrier also publishes s_w
   const uint32_t i = blockIdx.x * kSubsPerWg + (threadIdx.x >> 2), q = threadIdx.x & 3;
   const uint32_t nbits = us_len[blockIdx.y] * 8u;
   const uint32_t nsub = (nbits + kSubBits - 1) / kSubBits;

@@ -475,6 +475,27 @@ inline bool check_segments(const uint8_t *jpeg, Parsed *P, const Geom &g, std::s
 
 // Everything the decoder's host side derives from one frame's bytes, in order: markers, the
 // size limits, geometry, restart layout, and the six Huffman tables (DecFrame's tables).
+// The bytes that determine a frame's Huffman tables (per component: its DC and AC tables' code
+// counts and symbols), and their FNV-1a hash: frames with equal keys share a DecTabs.
+inline uint64_t table_key(const Parsed &P, std::vector<uint8_t> *key) {
+  key->clear();
+  key->push_back((uint8_t)P.ncomp);
+  auto put = [&](const uint8_t bits[17], const uint8_t *vals) {
+    int nv = 0;
+    for (int l = 1; l <= 16; ++l) nv += bits[l];
+    key->insert(key->end(), bits, bits + 17);
+    key->insert(key->end(), vals, vals + std::min(nv, 256));
+  };
+  for (int c = 0; c < P.ncomp; ++c) {
+    put(P.dcbits[P.td[c]], P.dcvals[P.td[c]]);
+    put(P.acbits[P.ta[c]], P.acvals[P.ta[c]]);
+  }
+  uint64_t h = 1469598103934665603ull;
+  for (uint8_t b : *key) h = (h ^ b) * 1099511628211ull;
+  return h;
+}
+
+// tables null: markers, geometry and segments only (the Huffman tables are the caller's to build)
 inline bool parse_frame(const uint8_t *jpeg, size_t size, uint64_t max_pixels, Parsed *P, Geom *g,
                         HuffDec dc[3], HuffDec ac[3], HuffSync sdc[3], HuffSync sac[3], uint16_t spair[3][1 << kLook],
                         std::string *err) {
@@ -489,6 +510,7 @@ inline bool parse_frame(const uint8_t *jpeg, size_t size, uint64_t max_pixels, P
     return false;
   }
   if (!check_segments(jpeg, P, *g, err)) return false;
+  if (!dc) return true;  // tables built by the caller (Codec::prepare_decode: one set per distinct DHT)
   for (int c = 0; c < P->ncomp; ++c)
     if (!build_tables(P->dcbits[P->td[c]], P->dcvals[P->td[c]], true, &dc[c], &sdc[c]) ||
         !build_tables(P->acbits[P->ta[c]], P->acvals[P->ta[c]], false, &ac[c], &sac[c], spair[c])) {

@@ -111,9 +111,10 @@ struct HuffSync {
   uint8_t vals[256];
 };
 
-struct DecFrame {
-  Geom g;
-  uint16_t q[3][64];       // dequantisation per component, natural order
+// A frame's Huffman tables, 20.5 KB.  The frames of a batch that share their tables (one encoder,
+// one set of settings: a stream's every frame) share one DecTabs; the batch's distinct ones follow
+// its DecFrame array in the same buffer, and DecFrame::tabs_off locates a frame's.
+struct DecTabs {
   HuffDec dc[3], ac[3];    // per component (kept adjacent: loaded into LDS as one block)
   HuffSync sdc[3], sac[3];  // the same, for the synchronisation decoders (adjacent too)
   // AC pairs for the span sync: spair[k][next kLook bits] = (advance << 8) | length of an AC
@@ -121,6 +122,12 @@ struct DecFrame {
   // lie inside the kLook bits (0: no pair); a step then moves over two symbols with one table
   // read, unless the first ends the block or reaches a mark
   uint16_t spair[3][1 << kLook];
+};
+
+struct DecFrame {
+  Geom g;
+  uint16_t q[3][64];       // dequantisation per component, natural order
+  uint64_t tabs_off;       // its DecTabs, in bytes from the start of the DecFrame array
   uint32_t flags;          // bit 0: fancy upsampling allowed; bits 1-2: k_color layout (0 other,
                            // 1 4:4:4, 2 chroma 2x1, 3 chroma 2x2; three components, full-size luma);
                            // kDecIdct24: the IDCT's column pass may use 24-bit multiplies
