@@ -770,7 +770,13 @@ def distributor_leg(nworkers, ngpu, host_gbps=None, pcie_gbps=None, frames_scale
         t0 = time.time()
         # JPEG legs swing between runs (host scheduling of the worker's submit thread): the
         # median of `reps` runs is reported, with every run's rate beside it
-        runs = [run_once(cmd) for _ in range(reps if host_x is None else 1)]
+        runs = []
+        for i in range(reps if host_x is None else 1):
+            runs.append(run_once(cmd))
+            # a progress line per run: a leg at N > 1 can run for minutes
+            log(f"distributor {name} run {i}: " + (f"{runs[-1]['fps']:.1f} fps" if "fps" in runs[-1]
+                                                     else str(runs[-1].get("error"))[:200])
+                + f" ({time.time() - t0:.1f} s)")
         good = sorted((r for r in runs if "error" not in r), key=lambda r: r["fps"])
         if not good:
             out[name] = runs[-1]
@@ -923,7 +929,8 @@ def headline(line):
         h["cpu_baseline"] = cpu
     sz = line.get("sizes")
     if isinstance(sz, dict):  # whole-job fps and the slowest rank's HBM fraction per size
-        h["sizes"] = {k: _pick(v, "fps", "frac_of_hbm_peak") for k, v in sz.items() if isinstance(v, dict)}
+        h["sizes"] = {k: _pick(v, "fps", "batch_per_rank", "kernel_GBps_per_gpu", "frac_of_hbm_peak")
+                      for k, v in sz.items() if isinstance(v, dict)}
     sw = line.get("configs4_sweep")
     if isinstance(sw, dict):
         h["configs4_sweep"] = {k: _pick(v, "fps", "frac_of_hbm_peak") for k, v in sw.items() if isinstance(v, dict)}
