@@ -18,9 +18,13 @@
 // concurrently (profiles/r01_pcie_probe_pipelines.txt).  IN and OUT are separate streams, so
 // the two directions run on separate SDMA engines at once.
 #include <hip/hip_runtime.h>
+#include <linux/futex.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <chrono>
+#include <climits>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -32,6 +36,11 @@ namespace vf {
 
 namespace {
 constexpr int kStatusHip = -2;  // VF_E_HIP
+// run_gated: pieces of at least 32 KiB, at most 254 of them (32 MiB of staging = 128 x 256 KiB),
+// their landed marks and the status word in one page-locked page
+constexpr uint32_t kGateMinShift = 15;
+constexpr size_t kGateFlagBytes = 4096;
+constexpr size_t kGateStatus = 1023;  // index of the status word in the flag page
 
 size_t env_or(const char *name, size_t dflt) {
   const char *v = std::getenv(name);
@@ -51,18 +60,42 @@ bool fired(hipEvent_t e, hipError_t *err) {
 }  // namespace
 
 // ---- host copy pool -----------------------------------------------------------------------
+// Workers sleep on a futex over the task generation, not on a condition variable: a condition
+// variable's waiters re-take its mutex one after another when woken, so the ninth worker of a
+// drop-in frame's copy started tens of microseconds after the first.  Each worker now wakes
+// straight into the task, and the caller waits for the last one on the pending count.
+namespace {
+long futex_wait(std::atomic<uint32_t> *a, uint32_t v) {
+  return syscall(SYS_futex, reinterpret_cast<uint32_t *>(a), FUTEX_WAIT_PRIVATE, v, nullptr, nullptr, 0);
+}
+long futex_wake(std::atomic<uint32_t> *a, int n) {
+  return syscall(SYS_futex, reinterpret_cast<uint32_t *>(a), FUTEX_WAKE_PRIVATE, n, nullptr, nullptr, 0);
+}
+}  // namespace
+
 CopyPool::CopyPool(int nthreads, size_t split_min) : split_min_(split_min), n_(std::max(1, nthreads)) {
   for (int i = 1; i < n_; ++i) threads_.emplace_back([this, i] { run(i); });
 }
 
 CopyPool::~CopyPool() {
-  {
-    std::lock_guard<std::mutex> lk(mu_);
-    stop_ = true;
-    ++gen_;
-  }
-  cv_.notify_all();
+  stop_.store(true, std::memory_order_relaxed);
+  gen_.fetch_add(1, std::memory_order_release);
+  futex_wake(&gen_, INT32_MAX);
   for (auto &t : threads_) t.join();
+}
+
+void CopyPool::post() {  // the task fields are set: publish a new generation and wake every worker
+  pending_.store((uint32_t)(n_ - 1), std::memory_order_relaxed);
+  gen_.fetch_add(1, std::memory_order_release);
+  futex_wake(&gen_, INT32_MAX);
+}
+
+void CopyPool::wait_all() {
+  for (int spin = 0; spin < 4096; ++spin) {  // the workers usually finish within microseconds of the caller
+    if (pending_.load(std::memory_order_acquire) == 0) return;
+    __builtin_ia32_pause();
+  }
+  for (uint32_t p; (p = pending_.load(std::memory_order_acquire)) != 0;) futex_wait(&pending_, p);
 }
 
 void CopyPool::copy(uint8_t *dst, const uint8_t *src, size_t len) {
@@ -70,18 +103,13 @@ void CopyPool::copy(uint8_t *dst, const uint8_t *src, size_t len) {
     std::memcpy(dst, src, len);
     return;
   }
-  {
-    std::lock_guard<std::mutex> lk(mu_);
-    dst_ = dst;
-    src_ = src;
-    len_ = len;
-    pending_ = n_ - 1;
-    ++gen_;
-  }
-  cv_.notify_all();
+  fn_ = nullptr;
+  dst_ = dst;
+  src_ = src;
+  len_ = len;
+  post();
   part(0);
-  std::unique_lock<std::mutex> lk(mu_);
-  done_cv_.wait(lk, [this] { return pending_ == 0; });
+  wait_all();
 }
 
 void CopyPool::start(std::function<void(int, int)> fn) {
@@ -89,19 +117,13 @@ void CopyPool::start(std::function<void(int, int)> fn) {
     fn(0, 1);
     return;
   }
-  {
-    std::lock_guard<std::mutex> lk(mu_);
-    fn_ = std::move(fn);
-    pending_ = n_ - 1;
-    ++gen_;
-  }
-  cv_.notify_all();
+  fn_ = std::move(fn);
+  post();
 }
 
 void CopyPool::join() {
   if (n_ == 1) return;
-  std::unique_lock<std::mutex> lk(mu_);
-  done_cv_.wait(lk, [this] { return pending_ == 0; });
+  wait_all();
   fn_ = nullptr;
 }
 
@@ -113,20 +135,15 @@ void CopyPool::part(int i) {
 }
 
 void CopyPool::run(int i) {
-  uint64_t seen = 0;
+  uint32_t seen = 0;  // the generation the pool was built with: a task posted before this thread ran is still seen
   for (;;) {
-    {
-      std::unique_lock<std::mutex> lk(mu_);
-      cv_.wait(lk, [&] { return gen_ != seen; });
-      seen = gen_;
-      if (stop_) return;
-    }
+    uint32_t g;
+    while ((g = gen_.load(std::memory_order_acquire)) == seen) futex_wait(&gen_, seen);
+    seen = g;
+    if (stop_.load(std::memory_order_relaxed)) return;
     if (fn_) fn_(i - 1, n_ - 1);
     else part(i);
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      if (--pending_ == 0) done_cv_.notify_one();
-    }
+    if (pending_.fetch_sub(1, std::memory_order_acq_rel) == 1) futex_wake(&pending_, 1);
   }
 }
 
@@ -154,6 +171,8 @@ Engine::~Engine() {
   for (hipEvent_t e : free_events_) (void)hipEventDestroy(e);
   (void)numa_pinned_free(stg_in_);
   (void)numa_pinned_free(stg_out_);
+  (void)numa_pinned_free(stg_flags_);
+  if (stg_frontier_) (void)hipFree(stg_frontier_);
   if (s_in_) (void)hipStreamDestroy(s_in_);
   if (s_out_) (void)hipStreamDestroy(s_out_);
   if (s_map_) (void)hipStreamDestroy(s_map_);
@@ -319,7 +338,13 @@ bool Engine::run_now(const std::vector<Seg> &segs, JobResult *out) {
     (void)hipGetLastError();
     return false;
   }
-  if (!all_mapped) return run_staged(segs, total, out);
+  if (!all_mapped) {
+    if (segs.size() == 1) {
+      const int g = run_gated(segs[0], out);
+      if (g >= 0) return g != 0;
+    }
+    return run_staged(segs, total, out);
+  }
   hipEvent_t a = take_event(), b = take_event();
   if (!a || !b) {
     give_event(a);
@@ -365,17 +390,134 @@ hipError_t Engine::ensure_staging() {
   const int node = device_numa_node(device_);
   hipError_t e;
   if ((!stg_in_ && (e = numa_pinned_alloc((void **)&stg_in_, kStagedMax, node)) != hipSuccess) ||
-      (!stg_out_ && (e = numa_pinned_alloc((void **)&stg_out_, kStagedMax, node)) != hipSuccess))
+      (!stg_out_ && (e = numa_pinned_alloc((void **)&stg_out_, kStagedMax, node)) != hipSuccess) ||
+      (!stg_flags_ && (e = numa_pinned_alloc((void **)&stg_flags_, kGateFlagBytes, node)) != hipSuccess))
     return e;
-  void *di = nullptr, *dout = nullptr;
+  void *di = nullptr, *dout = nullptr, *dfl = nullptr;
   if ((e = hipHostGetDevicePointer(&di, stg_in_, 0)) != hipSuccess ||
-      (e = hipHostGetDevicePointer(&dout, stg_out_, 0)) != hipSuccess)
+      (e = hipHostGetDevicePointer(&dout, stg_out_, 0)) != hipSuccess ||
+      (e = hipHostGetDevicePointer(&dfl, stg_flags_, 0)) != hipSuccess)
     return e;
+  stg_dflags_ = static_cast<uint32_t *>(dfl);
+  if (!stg_frontier_) {
+    if ((e = hipMalloc((void **)&stg_frontier_, 256)) != hipSuccess) return e;
+    if ((e = hipMemset(stg_frontier_, 0, 256)) != hipSuccess) return e;
+  }
+  int khz = 0;
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device_) == hipSuccess && khz > 0)
+    clock_khz_ = (uint64_t)khz;
+  (void)hipGetLastError();
   stg_din_ = static_cast<uint8_t *>(di);
   stg_dout_ = static_cast<uint8_t *>(dout);
   if (!cpool_) cpool_.reset(new CopyPool((int)env_or("VF_HOST_THREADS", 8) + 1, (size_t)256 << 10));
   stg_ready_ = true;
   return hipSuccess;
+}
+
+// The drop-in's own shape, one pageable frame (vfilter.bitwise_not(frame) for
+// cv2.bitwise_not(frame), inverter.py:41), with the copy overlapped by the launch: the kernel
+// is queued first and its tiles wait for their piece of the staging copy (invert_gated_kernel),
+// while the pool's workers copy the pieces in order and count each one in page-locked memory.
+// run_staged instead launches after the copy (one piece up to 8 MiB), so the frame paid
+// copy + launch + PCIe in series.  -1: not this shape (a mapped source, an unaligned side, more
+// than kStagedMax bytes, VF_STAGE_GATED=0, or the staging is busy on another thread).
+int Engine::run_gated(const Seg &sg, JobResult *out) {
+  // Read per call (tools/r6/gated_ab.py, the tests).  Frames above 8 MiB only by default: a 4K
+  // frame takes 0.60-0.66 ms instead of 0.73-0.76 (run_staged copies it whole, then launches 3
+  // pieces), within 2-12 % of a page-locked source; at 480p and 1080p the two forms measured
+  // within noise of each other (profiles/r06_dropin_gated_ab.txt).
+  const bool enabled = env_or("VF_STAGE_GATED", 1) != 0;
+  const size_t min_len = env_or("VF_STAGE_GATE_MIN", (size_t)8 << 20);
+  if (!enabled || sg.len == 0 || sg.len <= min_len || sg.len > kStagedMax || mapped(sg.src, sg.len)) return -1;
+  uint8_t *dd = mapped(sg.dst, sg.len);
+  const bool stage_out = dd == nullptr;
+  if ((((uintptr_t)sg.dst) & 15) != 0) return -1;
+  std::unique_lock<std::mutex> lk(stg_mu_, std::try_to_lock);
+  if (!lk.owns_lock()) return -1;
+  if (ensure_staging() != hipSuccess) {
+    (void)hipGetLastError();
+    return -1;
+  }
+  if (stage_out) dd = stg_dout_;
+  // pieces of 32 KiB and up, at most 254 (the relay reads their marks in one round trip; 255 is
+  // its give-up mark)
+  uint32_t shift = kGateMinShift;
+  while (((sg.len - 1) >> shift) >= 254) ++shift;
+  const size_t piece = (size_t)1 << shift;
+  const size_t np = ((sg.len - 1) >> shift) + 1;
+  volatile uint32_t *flags = stg_flags_;
+  for (size_t i = 0; i < np; ++i) flags[i] = 0;
+  flags[kGateStatus] = 0;
+  std::atomic_thread_fence(std::memory_order_seq_cst);
+  // The pieces go to whichever thread asks next: the pool's workers are woken before the launch
+  // and join as they wake (a wake-up costs microseconds to tens of them), this thread right after
+  // the launch; each copies whole pieces and marks each one landed.  Also after a failed launch:
+  // the copy completes either way, and nothing waits on it.
+  const uint8_t *src = sg.src;
+  uint8_t *stg = stg_in_;
+  uint32_t *cnt = stg_flags_;
+  const size_t len = sg.len;
+  std::atomic<size_t> next{0};
+  // (non-temporal stores for this copy, so the GPU's reads would not be served from the copying
+  // cores' caches, measured the same: profiles/r06_dropin_gated_ab.txt)
+  auto copy_pieces = [&next, src, stg, cnt, len, piece, shift, np] {
+    for (size_t i; (i = next.fetch_add(1, std::memory_order_relaxed)) < np;) {
+      const size_t off = i << shift;
+      std::memcpy(stg + off, src + off, std::min(piece, len - off));
+      __atomic_store_n(cnt + i, 1u, __ATOMIC_RELEASE);
+    }
+  };
+  cpool_->start([&copy_pieces](int, int) { copy_pieces(); });  // wakes the workers first
+  hipEvent_t a = take_event(), b = take_event();
+  hipError_t e = (a && b) ? hipEventRecord(a, s_map_) : hipErrorOutOfMemory;
+  // 100 ms without a piece: the copy stalled (it never waits on the GPU); the kernel gives up.
+  // VF_STAGE_GATE_BUDGET_US overrides (tests drive the give-up path with 0).
+  const uint64_t budget_us = env_or("VF_STAGE_GATE_BUDGET_US", 100000);
+  const uint64_t budget = clock_khz_ * budget_us / 1000;
+  if (e == hipSuccess) {
+    gate_gen_ = (gate_gen_ + 1) & 0xFFFFFFu;
+    if (gate_gen_ == 0) gate_gen_ = 1;
+    e = launch_invert_gated(stg_din_, dd, sg.len, stg_dflags_, shift, 1u, stg_frontier_, gate_gen_,
+                            stg_dflags_ + kGateStatus, budget, s_map_);
+  }
+  if (e == hipSuccess) e = hipEventRecord(b, s_map_);
+  copy_pieces();
+  // the GPU first, then the pool: a worker that woke late (after the pieces ran out) still has to
+  // check in before this frame's task may go out of scope, and that wait now overlaps the kernel
+  if (e == hipSuccess) e = hipEventSynchronize(b);
+  cpool_->join();
+  bool gave_up = false;
+  if (e == hipSuccess && flags[kGateStatus] != 0) {  // a wave gave up: the staging copy is complete now
+    gave_up = true;
+    MappedBatch mb;
+    mb.src[0] = stg_din_;
+    mb.dst[0] = dd;
+    mb.n[0] = sg.len;
+    e = launch_invert_mapped(mb, 1, sg.len, s_map_);
+    if (e == hipSuccess) e = hipEventRecord(b, s_map_);
+    if (e == hipSuccess) e = hipEventSynchronize(b);
+  }
+  if (e == hipSuccess && stage_out) cpool_->copy(sg.dst, stg_out_, sg.len);
+  *out = JobResult();
+  if (e != hipSuccess) {
+    (void)hipStreamSynchronize(s_map_);  // nothing may land in the caller's buffers later
+    (void)hipGetLastError();
+    out->status = kStatusHip;
+    out->hip = e;
+    out->msg = std::string("gated zero-copy launch failed: ") + hipGetErrorString(e);
+  } else {
+    float ms = -1.f;
+    if (hipEventElapsedTime(&ms, a, b) != hipSuccess) ms = -1.f;
+    out->kernel_ms = out->gpu_ms = ms;
+    out->zero_copy = true;
+    out->timeline.push_back(ChunkTime{sg.len, 0.f, 0.f, ms, ms});
+    if (env_or("VF_STAGE_TRACE", 0) != 0)  // read per call: tests switch it on
+      std::fprintf(stderr, "vf_stage: gated %zu B, %zu pieces, %d pool workers, GPU %.1f us%s\n", sg.len, np, cpool_->workers(),
+                   ms * 1000.f, gave_up ? ", re-run ungated after a give-up" : "");
+  }
+  give_event(a);
+  give_event(b);
+  return 1;
 }
 
 // A small synchronous job with a side outside the mapped ranges (a pageable frame: the

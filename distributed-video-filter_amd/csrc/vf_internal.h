@@ -42,6 +42,12 @@ struct MappedBatch {
   uint32_t tile0[kMappedMax + 1];  // first 4-KiB tile of each range (set by the launcher)
 };
 hipError_t launch_invert_mapped(const MappedBatch &b, int n, size_t total_bytes, hipStream_t stream);
+// One mapped range whose source is still being copied into it by the host: tile t waits until
+// landed[piece of t] == nw, relayed through the device word `frontier` tagged with gen (24 bits,
+// not 0) (vf_kernels.hip invert_gated_kernel); src and dst 16-B aligned, at most 254 pieces.
+hipError_t launch_invert_gated(const uint8_t *src, uint8_t *dst, size_t n, const uint32_t *landed,
+                               uint32_t piece_shift, uint32_t nw, uint32_t *frontier, uint32_t gen, uint32_t *status,
+                               uint64_t budget_ticks, hipStream_t stream);
 
 // ---- host -> host pipeline (vf_engine.hip) --------------------------------------------------
 
@@ -66,13 +72,14 @@ class CopyPool {
   std::function<void(int, int)> fn_;  // start(): the workers' task
   void part(int i);
   void run(int i);
+  void post();
+  void wait_all();
   int n_;
   std::vector<std::thread> threads_;
-  std::mutex mu_;
-  std::condition_variable cv_, done_cv_;
-  uint64_t gen_ = 0;
-  bool stop_ = false;
-  int pending_ = 0;
+  // one task at a time: the caller sets the task fields, then post() bumps gen_ (futex) and
+  // the workers count pending_ down (futex for the caller's wait)
+  std::atomic<uint32_t> gen_{0}, pending_{0};
+  std::atomic<bool> stop_{false};
   uint8_t *dst_ = nullptr;
   const uint8_t *src_ = nullptr;
   size_t len_ = 0;
@@ -166,6 +173,7 @@ class Engine {
   bool step_retire();
   bool launch_mapped(Job *job);
   bool run_staged(const std::vector<Seg> &segs, size_t total, JobResult *out);
+  int run_gated(const Seg &sg, JobResult *out);  // -1: not this job's shape (run_staged takes it)
   hipError_t ensure_staging();
   bool step_mapped_retire();
   void fail_all(hipError_t e, const char *what);
@@ -192,6 +200,11 @@ class Engine {
   uint8_t *stg_in_ = nullptr, *stg_out_ = nullptr;    // host addresses
   uint8_t *stg_din_ = nullptr, *stg_dout_ = nullptr;  // their device addresses
   bool stg_ready_ = false;
+  // run_gated: per-piece landed counts (host-written) and the kernel's give-up flag, page-locked
+  uint32_t *stg_flags_ = nullptr, *stg_dflags_ = nullptr;
+  uint32_t *stg_frontier_ = nullptr;  // device memory: the relay's published piece count
+  uint32_t gate_gen_ = 0;
+  uint64_t clock_khz_ = 100000;  // wall_clock64() rate
   std::mutex stg_mu_;                           // one staged job at a time
   std::unique_ptr<CopyPool> cpool_;
   std::mutex ev_mu_;             // free_events_: the engine thread and run_now's caller both take and give

@@ -192,7 +192,110 @@ __global__ __launch_bounds__(kBlock) void invert_mapped_kernel(MappedBatch b, ui
   }
 }
 
+// ---- the drop-in's pageable frame, launched before its bytes have landed ----------------------
+// vf_invert_host on an ordinary (pageable) frame (inverter.py:41's call shape): the host pool
+// copies the frame into mapped staging in pieces of 2^piece_shift bytes while this kernel
+// already runs, so the launch and the PCIe traffic of the first pieces overlap the copy of the
+// later ones.  Whole pieces go to whichever host thread asks next, which then sets landed[p]
+// (page-locked memory) to nw = 1, so pieces may complete out of order.
+// One wave (workgroup 0's first) relays: it reads all the counts in one round trip over PCIe,
+// publishes how many leading pieces are complete as (gen << 8) | count in a device-memory word,
+// sleeps about a microsecond and reads again until every piece is in.  The other workgroups
+// stride over the tiles and, before a tile whose piece is past what they saw complete, read the
+// device word (on-chip, not PCIe: polling host memory from every wave flooded the link with
+// reads, 0.39 ms for a 480p frame).  A relay or tile wave that waits `budget` wall-clock ticks
+// sets *status and leaves (the relay also publishes count 255, which sends every tile wave
+// home); the caller then inverts the whole frame again, ungated, from the complete staging
+// copy.  The counts are read relaxed: the host writes a piece before its count (x86 stores are
+// ordered), a tile reads the staging copy only after the relay saw its count, and no line of a
+// piece can sit in a cache before it landed (the launch's acquire dropped the previous frame's
+// lines; no earlier tile of this launch touches it).  src is the staging buffer, 16-B aligned
+// like dst; the last tile also does the n % 16 tail bytes.  gen tells this launch's word from
+// the previous one's (the word is never reset).
+__global__ __launch_bounds__(kBlock) void invert_gated_kernel(const u32x4 *__restrict__ s, u32x4 *__restrict__ d,
+                                                              uint64_t n, const uint32_t *landed, uint32_t piece_shift,
+                                                              uint32_t nw, uint32_t *frontier, uint32_t gen,
+                                                              uint32_t *status, uint64_t budget) {
+  const uint32_t np = (uint32_t)((n - 1) >> piece_shift) + 1;  // <= 254 (the launcher checks)
+  const uint32_t t = threadIdx.x;
+  const uint64_t t0 = wall_clock64();
+  if (blockIdx.x == 0) {  // the relay
+    if (t >= 64) return;
+    uint32_t k = 0;
+    while (k < np) {
+      uint32_t f[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)  // issued together: one PCIe round trip
+        f[j] = 64 * j + t < np ? __hip_atomic_load(landed + 64 * j + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : nw;
+      uint32_t c = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint64_t m = __ballot(f[j] >= nw);
+        if (c == 64u * j) c += ~m ? (uint32_t)__builtin_ctzll(~m) : 64u;
+      }
+      const uint32_t kn = min(c, np);
+      if (kn != k) {
+        k = kn;
+        if (t == 0) __hip_atomic_store(frontier, (gen << 8) | k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (k < np) {
+        if (wall_clock64() - t0 > budget) {
+          if (t == 0) {
+            __hip_atomic_store(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(frontier, (gen << 8) | 255u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+          return;
+        }
+        __builtin_amdgcn_s_sleep(32);
+      }
+    }
+    return;
+  }
+  const uint64_t n16 = n >> 4;
+  const uint64_t tiles = (n + kBlock * 16 - 1) / (kBlock * 16);
+  uint32_t ready = 0;  // pieces [0, ready) seen complete (wave-uniform)
+  for (uint64_t tile = blockIdx.x - 1; tile < tiles; tile += gridDim.x - 1) {
+    const uint64_t end = min((tile + 1) * (uint64_t)(kBlock * 16), n);
+    const uint32_t need = (uint32_t)((end - 1) >> piece_shift);
+    while (ready <= need) {
+      const uint32_t v = __hip_atomic_load(frontier, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((v >> 8) == (gen & 0xFFFFFFu)) {
+        if ((v & 255u) == 255u) return;  // the relay gave up
+        ready = v & 255u;
+      }
+      if (ready <= need) {
+        if (wall_clock64() - t0 > budget) {
+          __hip_atomic_store(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          return;
+        }
+        __builtin_amdgcn_s_sleep(8);
+      }
+    }
+    const uint64_t i = tile * kBlock + t;
+    if (i < n16) st16<true>(d + i, ~ld16<true>(s + i));
+    if (tile == tiles - 1 && t < (uint32_t)(n & 15)) {
+      const uint8_t *sb = reinterpret_cast<const uint8_t *>(s) + (n16 << 4);
+      reinterpret_cast<uint8_t *>(d)[(n16 << 4) + t] = (uint8_t)~sb[t];
+    }
+  }
+}
+
 // ---- launchers ----------------------------------------------------------------------
+
+hipError_t launch_invert_gated(const uint8_t *src, uint8_t *dst, size_t n, const uint32_t *landed,
+                               uint32_t piece_shift, uint32_t nw, uint32_t *frontier, uint32_t gen, uint32_t *status,
+                               uint64_t budget_ticks, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  if ((((uintptr_t)src | (uintptr_t)dst) & 15) != 0 || ((n - 1) >> piece_shift) >= 254 || (gen & 0xFFFFFFu) == 0)
+    return hipErrorInvalidValue;
+  const uint64_t tiles = (n + kBlock * 16 - 1) / (kBlock * 16);
+  // the relay + tile workgroups, as many as launch_invert_mapped's
+  const uint64_t grid = 1 + std::min<uint64_t>(tiles, n < (16ull << 20) ? 256 : 128);
+  hipLaunchKernelGGL(invert_gated_kernel, dim3((unsigned)grid), dim3(kBlock), 0, stream,
+                     reinterpret_cast<const u32x4 *>(src), reinterpret_cast<u32x4 *>(dst), (uint64_t)n, landed,
+                     piece_shift, nw, frontier, gen, status, budget_ticks);
+  return hipGetLastError();
+}
 
 // src and dst at different offsets mod 16: dst's head bytewise, then the shifting body.
 static hipError_t launch_shift(const uint8_t *s, uint8_t *d, size_t nbytes, int max_blocks, hipStream_t stream) {

@@ -496,6 +496,44 @@ def test_staged_jobs_without_copy_threads(monkeypatch, threads):
             assert np.array_equal(vfilter.bitwise_not(x[3:3 + n], ctx=ctx), want)
 
 
+@pytest.mark.parametrize("budget", [None, "0"])
+def test_gated_dropin_frames(vf_ctx, monkeypatch, capfd, budget):
+    """The drop-in's pageable frame with an aligned destination takes the gated launch
+    (Engine::run_gated; by default above 8 MiB, here at every size): the kernel is queued
+    before the staging copy and each tile waits for its piece (32 KiB and up).  Ragged sizes
+    around the piece and tile edges up to a 4K frame and the 32-MiB staging cap, into the pinned
+    arena and into a pageable array, and in place; with a give-up budget of 0 the waves leave at
+    their first missing piece and the frame is inverted again, ungated -- bit-exact either way,
+    nothing outside the destination touched."""
+    monkeypatch.setenv("VF_STAGE_TRACE", "1")
+    monkeypatch.setenv("VF_STAGE_GATE_MIN", "0")  # every size (the default gates frames above 8 MiB)
+    if budget is not None:
+        monkeypatch.setenv("VF_STAGE_GATE_BUDGET_US", budget)
+    sizes = [1, 15, 16, 4097, 262143, 262144, 262145, FB_1080, 2160 * 3840 * 3 + 3, 32 << 20]
+    rng = np.random.default_rng(7)
+    x = rng.integers(0, 256, (32 << 20) + 64, dtype=np.uint8)
+    for n in sizes:
+        src = x[5:5 + n]
+        want = ~src
+        r = vfilter.bitwise_not(src, ctx=vf_ctx)                 # pageable -> pinned arena
+        assert np.array_equal(r, want), n
+        d = np.full(n + 32, 0x5A, np.uint8)
+        dv = d[16:16 + n]
+        if dv.ctypes.data % 16:
+            dv = d[16 - dv.ctypes.data % 16:][:n]
+        off = dv.ctypes.data - d.ctypes.data
+        vf_ctx.invert_host(src, dv, n)                            # pageable -> pageable
+        assert np.array_equal(dv, want), n
+        assert (d[:off] == 0x5A).all() and (d[off + n:] == 0x5A).all(), n
+    w = x[:FB_1080 + 16].copy()
+    vf_ctx.invert_host(w, w, w.nbytes)                            # in place
+    assert np.array_equal(w, ~x[:FB_1080 + 16])
+    err = capfd.readouterr().err
+    assert err.count("vf_stage: gated") >= 2 * len(sizes), err[-2000:]
+    if budget == "0":
+        assert "re-run ungated" in err
+
+
 def _zero_copy(tl):
     """A zero-copy call reports one record whose H2D start = kernel start = 0 and kernel end =
     D2H end (one launch read the source and wrote the destination over PCIe)."""

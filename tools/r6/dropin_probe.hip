@@ -11,6 +11,7 @@
 //
 //   tools/r6/dropin_probe [reps]      (one JSON object per row on stdout)
 #include <hip/hip_runtime.h>
+#include <sys/mman.h>
 
 #include <algorithm>
 #include <chrono>
@@ -18,6 +19,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <vector>
+
+#include "../../include/vfilter.h"
 
 #define CK(x)                                                                        \
   do {                                                                               \
@@ -57,6 +60,26 @@ __global__ __launch_bounds__(256) void k_zc(const v4 *__restrict__ s, v4 *__rest
     stamps[2 * blockIdx.x + 1] = wall_clock64();
   }
 }
+
+
+// page-locked host memory of one kind: hipHostMalloc, or mmap + hipHostRegister on 4 KiB pages
+// (the product's numa_pinned_alloc), or the same on transparent huge pages
+static uint8_t *host_alloc(int kind, size_t n) {
+  if (kind == 0) {
+    void *p = nullptr;
+    CK(hipHostMalloc(&p, n, hipHostMallocMapped));
+    return (uint8_t *)p;
+  }
+  const size_t len = (n + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1);
+  void *raw = mmap(nullptr, len + (2u << 20), PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+  if (raw == MAP_FAILED) std::exit(2);
+  uint8_t *p = (uint8_t *)(((uintptr_t)raw + (2u << 20) - 1) & ~(uintptr_t)((2u << 20) - 1));
+  madvise(p, len, kind == 2 ? MADV_HUGEPAGE : MADV_NOHUGEPAGE);
+  std::memset(p, 0, len);
+  CK(hipHostRegister(p, len, hipHostRegisterMapped));
+  return p;
+}
+static const char *kind_name(int k) { return k == 0 ? "hostmalloc" : k == 1 ? "registered_4k" : "registered_thp"; }
 
 static double now_us() {
   return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -167,6 +190,56 @@ int main(int argc, char **argv) {
   for (Wait w : {kEventSync, kStreamSync, kSpin}) run_zc(256, 1, w, "zc_wait");
   for (int grid : {128, 256, 512, 1024, 2048})
     for (int u : {1, 2, 4}) run_zc(grid, u, kSpin, "zc_grid");
+
+  // allocation kinds under the best launch shapes
+  for (int kind : {1, 2}) {
+    uint8_t *ks = host_alloc(kind, nbytes), *kd = host_alloc(kind, nbytes);
+    std::memcpy(ks, hs, nbytes);
+    CK(hipHostGetDevicePointer((void **)&ds, ks, 0));
+    CK(hipHostGetDevicePointer((void **)&dd, kd, 0));
+    uint8_t *save_s = hs, *save_d = hd;
+    hs = ks, hd = kd;
+    char tag[64];
+    std::snprintf(tag, sizeof tag, "zc_%s", kind_name(kind));
+    for (int grid : {128, 256}) run_zc(grid, 1, kSpin, tag);
+    hs = save_s, hd = save_d;
+  }
+  CK(hipHostGetDevicePointer((void **)&ds, hs, 0));
+  CK(hipHostGetDevicePointer((void **)&dd, hd, 0));
+
+  // the product: vf_invert_host on page-locked buffers (vf_alloc_host), and with a pageable
+  // source (the drop-in's shape: an ordinary numpy frame in, a page-locked result out)
+  {
+    vf_ctx *ctx = nullptr;
+    if (vf_create(0, nbytes, 1, &ctx) != 0) {
+      std::fprintf(stderr, "vf_create: %s\n", vf_last_error(nullptr));
+      return 1;
+    }
+    void *ps = nullptr, *pd = nullptr;
+    if (vf_alloc_host(ctx, nbytes, &ps) != 0 || vf_alloc_host(ctx, nbytes, &pd) != 0) return 1;
+    std::vector<uint8_t> pageable(hs, hs + nbytes);
+    for (int src_kind = 0; src_kind < 2; ++src_kind) {
+      const uint8_t *src = src_kind == 0 ? (const uint8_t *)ps : pageable.data();
+      if (src_kind == 0) std::memcpy(ps, hs, nbytes);
+      std::vector<double> wall;
+      for (int r = 0; r < reps + 10; ++r) {
+        const double t = now_us();
+        if (vf_invert_host(ctx, src, (uint8_t *)pd, nbytes) != 0) {
+          std::fprintf(stderr, "vf_invert_host: %s\n", vf_last_error(ctx));
+          return 1;
+        }
+        if (r >= 10) wall.push_back(now_us() - t);
+      }
+      bool ok = true;
+      for (size_t i = 0; i < nbytes && ok; i += 4099) ok = ((uint8_t *)pd)[i] == (uint8_t)~hs[i];
+      std::printf("{\"row\": \"product_vf_invert_host\", \"src\": \"%s\", \"wall_us\": %.1f, \"ok\": %s}\n",
+                  src_kind == 0 ? "pinned" : "pageable", median(wall), ok ? "true" : "false");
+      std::fflush(stdout);
+    }
+    vf_free_host(ctx, ps);
+    vf_free_host(ctx, pd);
+    vf_destroy(ctx);
+  }
 
   // SDMA one way each (same frame), the copy engines' fixed cost
   for (int dir = 0; dir < 2; ++dir) {
