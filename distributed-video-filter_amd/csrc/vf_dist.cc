@@ -2056,6 +2056,30 @@ int vfd_reserved_index(vfd_engine* e, int32_t slot, int64_t* index) {
     return VFD_OK;
 }
 
+int vfd_fill(vfd_engine* e, int n, const int32_t* slots, const uint64_t* src_addrs, const int64_t* nbytes) {
+    if (!e || n < 0 || (n > 0 && (!slots || !src_addrs || !nbytes))) return VFD_E_INVALID;
+    std::vector<uint8_t*> dst((size_t)n);
+    {
+        std::lock_guard<std::mutex> lk(e->mu);
+        for (int i = 0; i < n; ++i) {
+            if (!e->reserved.count(slots[i])) {
+                e->err = "slot " + std::to_string(slots[i]) + " was not reserved";
+                return VFD_E_INVALID;
+            }
+            if (nbytes[i] < 0 || nbytes[i] > e->slot_bytes || (nbytes[i] > 0 && !src_addrs[i])) {
+                e->err = "frame " + std::to_string(i) + " of " + std::to_string(nbytes[i]) + " B does not fit a slot of " +
+                         std::to_string(e->slot_bytes) + " B";
+                return VFD_E_INVALID;
+            }
+            dst[(size_t)i] = e->in_addr(slots[i]);
+        }
+    }
+    // the reservations are the caller's until vfd_commit: the copies run outside the lock
+    for (int i = 0; i < n; ++i)
+        if (nbytes[i] > 0) std::memcpy(dst[(size_t)i], reinterpret_cast<const void*>((uintptr_t)src_addrs[i]), (size_t)nbytes[i]);
+    return VFD_OK;
+}
+
 int vfd_next(vfd_engine* e, int max_n, double timeout_s, vfd_frame* out) {
     if (!e || max_n < 0 || (max_n > 0 && !out)) return VFD_E_INVALID;
     std::unique_lock<std::mutex> lk(e->mu);

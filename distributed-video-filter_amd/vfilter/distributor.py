@@ -49,6 +49,7 @@ All shared state sits behind one lock (the reference relies on the GIL, SURVEY Â
 from __future__ import annotations
 
 import collections
+import ctypes
 import json
 import os
 import queue
@@ -1461,6 +1462,23 @@ class Distributor:
         slots = self.reserve_frames(nbytes, n, block)
         idx = [self.reserved_index(s_) for s_ in slots]
         return np.asarray(slots, np.int32), np.asarray([-1 if i is None else i for i in idx], np.int64)
+
+    def fill_frames(self, slots, src_addrs, nbytes) -> None:
+        """The native engine's columnar copy (vfd_fill) for this engine: frame i's ``nbytes[i]``
+        bytes at address ``src_addrs[i]`` into reserved slot ``slots[i]`` (one copy per frame)."""
+        if not (len(slots) == len(src_addrs) == len(nbytes)):
+            raise ValueError("fill_frames: slots, src_addrs and nbytes differ in length")
+        cols = list(zip(np.asarray(slots).tolist(), np.asarray(src_addrs, np.uint64).tolist(),
+                        np.asarray(nbytes).tolist()))
+        for s_, a, nb in cols:  # refused before anything is copied, as vfd_fill
+            if self.reserved_index(s_) is None:
+                raise ValueError(f"fill_frames: slot {s_} was not reserved")
+            if nb < 0 or nb > self.ring_slot_bytes:
+                raise ValueError(f"fill_frames: a frame of {nb} B does not fit a slot of {self.ring_slot_bytes} B")
+        for s_, a, nb in cols:
+            if nb:
+                src = np.ctypeslib.as_array((ctypes.c_uint8 * nb).from_address(a))
+                self.in_view(s_, nb)[:] = src
 
     def release_frame(self, index: int) -> None:
         """zero_copy: return frame ``index``'s ring slot once its result view is consumed."""

@@ -110,6 +110,11 @@ int vfd_reserve(vfd_engine* e, int64_t nbytes, int n, double timeout_s, int32_t*
  * NULL) and write their indices to out_indices (may be NULL).  Returns VFD_OK. */
 int vfd_commit(vfd_engine* e, int n, const int32_t* slots, const int64_t* nbytes, const int32_t* ndims,
                const int32_t* shapes, int64_t* out_indices);
+/* Columnar fill of n reservations (a producer at hundreds of thousands of small frames per
+ * second, e.g. 512 x 512 JPEGs, cannot afford a per-frame call): copy nbytes[i] from src_addrs[i]
+ * into slot slots[i]'s input half.  Every slot must be reserved and every size fit a slot, else
+ * VFD_E_INVALID and nothing is copied.  Replaces the per-frame copy of distributor.py:173-203. */
+int vfd_fill(vfd_engine* e, int n, const int32_t* slots, const uint64_t* src_addrs, const int64_t* nbytes);
 /* Give back a reservation that will not be committed; its index is counted lost. */
 int vfd_cancel(vfd_engine* e, int32_t slot);
 /* The index a reservation carries. */

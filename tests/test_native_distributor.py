@@ -371,6 +371,64 @@ def test_result_with_a_repeated_index(order):
 
 
 @pytest.mark.timeout(120)
+@pytest.mark.parametrize("engine", ["native", "python"])
+def test_fill_frames_columnar_copy(engine):
+    """fill_frames (vfd_fill): every frame of a reservation group copied into its slot by one
+    call, from an address column -- the producer form of the bench's small-JPEG legs.  Frames of
+    several sizes, 2 worker processes, every result in order and bit-exact; an unreserved slot
+    or an oversized frame is refused before anything is copied."""
+    kw = dict(policy="pull", queue_size=64, ring_slots=24, ring_slot_bytes=32 * 32 * 3, zero_copy=True)
+    if engine == "native":
+        d = _native(**kw)
+    else:
+        d = Distributor(0, 0, engine="python", transport="tcp", host="127.0.0.1", verbose=False,
+                        reassembly="ordered", **kw)
+        d.start()
+    stop, procs = spawn_workers(2, d.distribute_port, d.collect_port, protocol="v1", batch=8)
+    try:
+        _wait(lambda: d.num_workers() == 2, 60, "register")
+        kinds = [oracle.synthetic_frame(k, 32, 32).reshape(-1)[: 32 * 32 * 3 - 97 * k].copy() for k in range(5)]
+        addr = np.array([k_.ctypes.data for k_ in kinds], np.uint64)
+        nbk = np.array([k_.nbytes for k_ in kinds], np.int64)
+        n = 400
+
+        def produce():
+            done = 0
+            while done < n:
+                slots, idx = d.reserve_frames_array(kinds[0].nbytes, min(16, n - done))
+                d.fill_frames(slots, addr[idx % 5], nbk[idx % 5])
+                assert d.commit_frames(slots, nbk[idx % 5]) == idx.tolist()
+                done += len(slots)
+
+        th = threading.Thread(target=produce, daemon=True)
+        th.start()
+        i = 0
+        while i < n:
+            b = d.get_next_batch(32, timeout=20)
+            assert len(b), d.ordering_stats()
+            assert b.index.tolist() == list(range(i, i + len(b)))
+            for k in range(len(b)):
+                assert bytes(b.view(k)) == oracle.invert_bytes(kinds[(i + k) % 5].tobytes())
+            d.release_frames(b.index)
+            i += len(b)
+        th.join(5)
+        slots, idx = d.reserve_frames_array(kinds[0].nbytes, 2)
+        view = d.frame_view(int(slots[0]), 64)
+        view[:] = 0x5A
+        big = np.zeros(1 << 20, np.uint8)  # past the slot (ring_slot_bytes rounded up to pages)
+        with pytest.raises((native.NativeError, ValueError), match="does not fit"):
+            d.fill_frames(slots, [addr[0], big.ctypes.data], [int(nbk[0]), big.nbytes])
+        with pytest.raises((native.NativeError, ValueError), match="not reserved"):
+            d.fill_frames([int(slots[0]), 10 ** 6], [addr[0], addr[1]], [64, 64])
+        assert (view == 0x5A).all()  # refused calls copied nothing
+        for s_ in slots.tolist():
+            d.cancel_frame(s_)
+    finally:
+        stop_workers(stop, procs)
+        d.cleanup()
+
+
+@pytest.mark.timeout(120)
 def test_grouped_array_calls_and_batches():
     """reserve_frames_array / commit_frames / get_next_batch / release_frames: the consumer's
     columnar form, with 2 worker processes, every frame in order and bit-exact."""

@@ -199,6 +199,28 @@ def main():
         # a 1080p / 4K raw frame's copy (0.3-2 ms) still goes to its slice's node pool
         INLINE_COPY = 1 << 20
 
+        # JPEG frames through the native engine: the producer works in columns -- one reservation,
+        # one vfd_fill (every frame's copy into its slot) and one commit per group -- where a
+        # Python step per frame (index lookup, view, copy call) held the leg at 100-160 k fps on
+        # one producer thread (r06_small_legs_profile.txt)
+        columnar = args.jpeg and args.producer == "copy" and getattr(d, "engine", "python") == "native"
+        if columnar:
+            group = max(1, args.batch)
+            src_addr = np.array([p_.ctypes.data for p_ in pregen], np.uint64)
+            src_nb = np.array([p_.nbytes for p_ in pregen], np.int64)
+
+        def produce_columns(i0, g):
+            done_ = 0
+            while done_ < g:
+                slots, idxs = d.reserve_frames_array(max_nb, g - done_)
+                if not len(slots):
+                    return
+                nb = src_nb[idxs % len(shapes)]
+                d.fill_frames(slots, src_addr[idxs % len(shapes)], nb)
+                commit_t[idxs] = time.perf_counter()
+                d.commit_frames(slots, nb)
+                done_ += len(slots)
+
         def produce():
             while True:
                 with count_lock:
@@ -209,6 +231,9 @@ def main():
                     counter[0] += g
                 if i0 >= warm:
                     started.wait()
+                if columnar:
+                    produce_columns(i0, g)
+                    continue
                 done_ = 0
                 while done_ < g:
                     slots = d.reserve_frames(max_nb, g - done_)
@@ -380,7 +405,8 @@ def main():
         result = {"kind": "pipeline_jpeg" if args.jpeg else "pipeline", "size": args.size, "producers": nprod, "consume": args.consume, "worker_batch": args.worker_batch, "verify_pool": bool(args.jpeg and pool_verify),
                   "workers": args.workers, "gpus": min(ngpu, args.workers),
                   "inflight_per_worker": inflight,
-                  "policy": args.policy, "producer": args.producer, "batch": args.batch, "frames": n_t,
+                  "policy": args.policy, "producer": args.producer, "producer_form": "columns" if columnar else "per frame",
+                  "batch": args.batch, "frames": n_t,
                   "ring_slots_per_worker": slots, "verify_full_every": args.verify_every,
                   "slice_bytes_per_worker": slices[0]["bytes"] if slices else None,
                   "slice_numa": [sl["numa"] for sl in slices], "slice_numa_bound": [sl["numa_bound"] for sl in slices],

@@ -13,3 +13,10 @@ for sz in 512sq 480p; do
 done
 done
 for sz in 512sq 480p; do timeout -k 10 120 python3 tools/r6/worker_form_phases.py $sz 64; done
+if [ "${PROFILE:-0}" = 1 ]; then
+for sz in 512sq 480p; do
+  timeout -k 10 200 python3 tools/pipeline_bench.py --workers 1 --gpus 1 --jpeg --size $sz --batch 64 --policy pull \
+      --frames 98304 --profile gpurun_out/r6_prof_$sz > gpurun_out/r6_leg_${sz}_prof.json 2> gpurun_out/r6_leg_${sz}_prof.err || { echo PROF_FAILED $sz; tail -20 gpurun_out/r6_leg_${sz}_prof.err; exit 1; }
+  python3 -c "import json,sys; d=json.loads([l for l in open('gpurun_out/r6_leg_${sz}_prof.json') if l.startswith('{')][-1]); print('$sz profiled', d['fps'])"
+done
+fi
