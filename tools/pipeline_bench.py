@@ -203,7 +203,9 @@ def main():
         # one vfd_fill (every frame's copy into its slot) and one commit per group -- where a
         # Python step per frame (index lookup, view, copy call) held the leg at 100-160 k fps on
         # one producer thread (r06_small_legs_profile.txt)
-        columnar = args.jpeg and args.producer == "copy" and getattr(d, "engine", "python") == "native"
+        # (frames of 1 MiB and more -- hard q95 1080p JPEGs are 2 MB -- keep the node pools' parallel copies)
+        columnar = (args.jpeg and args.producer == "copy" and getattr(d, "engine", "python") == "native"
+                    and max(fbytes) < INLINE_COPY)
         if columnar:
             group = max(1, args.batch)
             src_addr = np.array([p_.ctypes.data for p_ in pregen], np.uint64)
