@@ -94,10 +94,7 @@ hipError_t enc_ff_count(const EncFrame *fr, int n, uint32_t max_tiles, const uin
                         const uint8_t *stream, uint32_t *tile_cnt, hipStream_t s);
 hipError_t enc_ff_write(const EncFrame *fr, int n, uint32_t max_tiles, const uint32_t *total_bits,
                         const uint8_t *stream, const uint32_t *tile_off, const uint32_t *nff,
-                        const uint8_t *hdr, uint8_t *out, uint64_t *out_size, hipStream_t s);
-// the batch's finished JPEGs packed back to back (each at a 64-B aligned offset) for one D2H
-hipError_t enc_compact(const EncFrame *fr, int n, const uint64_t *out_size, const uint8_t *out, uint8_t *pack,
-                       hipStream_t s);
+                        const uint8_t *hdr, uint8_t *pack, uint64_t *out_size, hipStream_t s);
 
 }  // namespace jpeg
 }  // namespace vf

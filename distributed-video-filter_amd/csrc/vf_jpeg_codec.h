@@ -175,7 +175,7 @@ class Codec {
       d_unres_;
   int sync_passes_ = 0;
   DevBuf d_in_, d_dfr_, d_dsg_, d_segs_, d_tile_, d_tsum_, d_totals_, d_us_, d_exit_[2], d_cnt_[2], d_used_, d_ck_, d_ckrem_, d_bstart_,
-      d_changed_, d_coef_, d_nmask_, d_dcseq_, d_planes_, d_pix_;
+      d_changed_, d_coef_, d_nmask_, d_dcseq_, d_dcpred_, d_planes_, d_pix_;
 
   // encode layout
   std::vector<EncFrame> efr_;
@@ -190,7 +190,7 @@ class Codec {
   uint64_t dbits_per_block_ = 0;  // the batch's entropy-coded bits per block (span-sync warm-up)
   uint32_t sync_warm() const;
   DevBuf d_efr_, d_etab_, d_hdr_, d_esegs_, d_etsum_, d_etotals_, d_dcq_, d_acbits_, d_acscr_, d_bits_, d_pre_, d_bitoff_, d_stream_, d_ffcnt_,
-      d_out_, d_outsize_, d_pack_;
+      d_outsize_, d_pack_;
 
   HostBuf h_unres_;            // k_resolve's per-segment unresolved flags (stored through the mapping)
   void *unres_dev_ = nullptr, *dtot_dev_ = nullptr;  // device addresses of h_unres_ / h_dtot_

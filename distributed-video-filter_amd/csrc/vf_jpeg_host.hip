@@ -548,6 +548,7 @@ int Codec::prepare_decode(const uint8_t *const *jpegs, const size_t *sizes, int 
   CK(d_coef_.ensure(blk * 128));
   CK(d_nmask_.ensure(blk + 16));
   CK(d_dcseq_.ensure(sizeof(int32_t) * (dcoff + 1)));
+  CK(d_dcpred_.ensure(sizeof(int32_t) * (dcoff + 1)));  // the scan's output: out of place, so short sequences scan in one pass
   CK(d_planes_.ensure(plane));
   CK(d_pix_.ensure(pix));
   // descriptors go through pinned memory too, so every upload stays asynchronous and nothing
@@ -783,7 +784,7 @@ int Codec::run_decode_post(int bgr, bool invert, std::string *err) {
                  d_bstart_.as<uint32_t>(), d_coef_.as<int16_t>(), d_dcseq_.as<int32_t>(), nmask, s_));
   CK(stage_event(3));
   // 4. DC prediction (inclusive scan per component sequence)
-  CK(scan_i32(segs + 2 * ns, ndcseg_, dc_max_tiles_, d_dcseq_.as<int32_t>(), d_dcseq_.as<int32_t>(),
+  CK(scan_i32(segs + 2 * ns, ndcseg_, dc_max_tiles_, d_dcseq_.as<int32_t>(), d_dcpred_.as<int32_t>(),
               d_tsum_.as<int32_t>(), nullptr, true, s_));
   // 5. IDCT, 6. upsample + colour (+ invert).  The invert path on standard 4:2:2 frames does both
   // in one pass with the decoder planes in LDS (k_idct_color422; VF_JPEG_FUSE_IDCT=0: two passes)
@@ -793,13 +794,13 @@ int Codec::run_decode_post(int bgr, bool invert, std::string *err) {
   }();
   if (fuse_idct) {
     CK(stage_event(4));  // the DC scan above is the dc_idct stage; the fused pass the colour stage
-    CK(dec_idct_color422(fr, n, dmax_w_, dmax_h_, d_coef_.as<int16_t>(), d_dcseq_.as<int32_t>(), nmask,
+    CK(dec_idct_color422(fr, n, dmax_w_, dmax_h_, d_coef_.as<int16_t>(), d_dcpred_.as<int32_t>(), nmask,
                          d_eplanes_.as<uint8_t>(), d_efr_.as<EncFrame>(), invert ? 1 : 0, kSampV[esub_] == 1 ? 1 : 0,
                          s_));
     CK(stage_event(5));
     return kOk;
   }
-  CK(dec_idct(fr, n, dmax_blocks_, d_coef_.as<int16_t>(), d_dcseq_.as<int32_t>(), nmask, d_planes_.as<uint8_t>(), s_));
+  CK(dec_idct(fr, n, dmax_blocks_, d_coef_.as<int16_t>(), d_dcpred_.as<int32_t>(), nmask, d_planes_.as<uint8_t>(), s_));
   CK(stage_event(4));
   // the invert path (fuse_): the encoder's sample planes instead of pixels (enc_sample_rows)
   CK(dec_color(fr, n, dmax_w_, dmax_h_, d_planes_.as<uint8_t>(), fuse_ ? d_eplanes_.as<uint8_t>() : d_pix_.as<uint8_t>(),
@@ -932,7 +933,6 @@ int Codec::prepare_encode(const int *ws, const int *hs, const uint64_t *img_offs
   CK(d_bitoff_.ensure(sizeof(uint32_t) * blk));
   CK(d_stream_.ensure(bits));
   CK(d_ffcnt_.ensure(sizeof(uint32_t) * tiles));
-  CK(d_out_.ensure(out));
   CK(d_pack_.ensure(out));
   CK(d_outsize_.ensure(sizeof(uint64_t) * (size_t)n));
   CK(d_eplanes_.ensure(epl));
@@ -976,8 +976,7 @@ int Codec::run_encode(int bgr, bool fastdct, std::string *err) {
   CK(scan_u32(segs + n, n, (emax_tiles_ + kScanTile - 1) / kScanTile, d_ffcnt_.as<uint32_t>(),
               d_ffcnt_.as<uint32_t>(), d_etsum_.as<uint32_t>(), nff, false, s_));
   CK(enc_ff_write(fr, n, emax_tiles_, total_bits, d_stream_.as<uint8_t>(), d_ffcnt_.as<uint32_t>(), nff,
-                  d_hdr_.as<uint8_t>(), d_out_.as<uint8_t>(), d_outsize_.as<uint64_t>(), s_));
-  CK(enc_compact(fr, n, d_outsize_.as<uint64_t>(), d_out_.as<uint8_t>(), d_pack_.as<uint8_t>(), s_));
+                  d_hdr_.as<uint8_t>(), d_pack_.as<uint8_t>(), d_outsize_.as<uint64_t>(), s_));  // packed in place
   CK(stage_event(8));
   return kOk;
 }

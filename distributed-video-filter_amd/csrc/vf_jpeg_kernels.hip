@@ -99,7 +99,11 @@ __global__ __launch_bounds__(256) void seg_tile_sum(const ScanSeg *segs, const T
 // of a separate one-workgroup-per-segment kernel scanning them in between: one launch and one
 // dependent kernel boundary fewer per scan (five scans per batch).  The segment's last tile
 // writes the segment total; a segment with no tiles has its total written as 0 by tile 0.
-template <typename T, bool INCL>
+// PRE_IN: no seg_tile_sum before it -- a tile adds up the inputs of the tiles before it in its
+// segment itself (out of place only: another tile may be writing out meanwhile), for segments of
+// a few tiles, where the second launch (~4.5 us of a small batch's GPU time) costs more than
+// re-reading up to three tiles from L2.  A scan whose segments are all one tile needs neither.
+template <typename T, bool INCL, bool PRE_IN = false>
 __global__ __launch_bounds__(256) void seg_apply(const ScanSeg *segs, const T *in, const T *tsum, T *out, T *totals) {
   const ScanSeg sg = segs[blockIdx.y];
   const uint64_t t0 = (uint64_t)blockIdx.x * kScanTile;
@@ -117,7 +121,17 @@ __global__ __launch_bounds__(256) void seg_apply(const ScanSeg *segs, const T *i
     acc += v[j];
   }
   T pre = 0;  // this thread's share of the preceding tiles' sums
-  for (uint32_t i = threadIdx.x; i < blockIdx.x; i += 256) pre += tsum[sg.tile0 + i];
+  if constexpr (PRE_IN) {
+    for (uint64_t i = (uint64_t)threadIdx.x * kScanPerThread; i < t0; i += kScanTile) {
+      T w[kScanPerThread];
+#pragma unroll
+      for (int j = 0; j < kScanPerThread; ++j) w[j] = in[sg.base + i + j];  // i + j < t0 <= len
+#pragma unroll
+      for (int j = 0; j < kScanPerThread; ++j) pre += w[j];
+    }
+  } else {
+    for (uint32_t i = threadIdx.x; i < blockIdx.x; i += 256) pre += tsum[sg.tile0 + i];
+  }
   // one barrier for both: the exclusive scan of acc and the sum of pre over the workgroup
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const T x = wave_incl_scan(acc);
@@ -149,6 +163,16 @@ hipError_t seg_scan(const ScanSeg *segs, int nseg, uint32_t max_tiles, const T *
                     T *totals, bool inclusive, hipStream_t s) {
   if (nseg <= 0 || max_tiles == 0) return hipSuccess;
   const dim3 g(max_tiles, (unsigned)nseg);
+  static const uint32_t one_pass_max = [] {  // VF_SCAN_ONE_PASS_TILES (0: always two kernels)
+    const char *v = std::getenv("VF_SCAN_ONE_PASS_TILES");
+    return v && *v ? (uint32_t)std::atoi(v) : 4u;
+  }();
+  const bool one = max_tiles == 1 ? one_pass_max > 0 : (in != out && max_tiles <= one_pass_max);
+  if (one) {  // tile 0 of a segment reads no tile sums, so one tile per segment is the PRE_IN form too
+    if (inclusive) hipLaunchKernelGGL((seg_apply<T, true, true>), g, dim3(256), 0, s, segs, in, tsum, out, totals);
+    else hipLaunchKernelGGL((seg_apply<T, false, true>), g, dim3(256), 0, s, segs, in, tsum, out, totals);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(seg_tile_sum<T>, g, dim3(256), 0, s, segs, in, tsum);
   if (inclusive) hipLaunchKernelGGL((seg_apply<T, true>), g, dim3(256), 0, s, segs, in, tsum, out, totals);
   else hipLaunchKernelGGL((seg_apply<T, false>), g, dim3(256), 0, s, segs, in, tsum, out, totals);
@@ -3343,27 +3367,6 @@ __global__ __launch_bounds__(256) void k_zero_stream(const EncFrame *__restrict_
   for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < nw; i += gridDim.x * 256) w[i] = 0;
 }
 
-// Frame f's JPEG to pack + sum over g < f of align64(size g): the host then fetches the batch
-// with one copy of the packed total instead of one copy per frame (~10 us of DMA set-up each).
-__global__ __launch_bounds__(256) void k_compact(const EncFrame *__restrict__ fr, const uint64_t *out_size, const uint8_t *out,
-                                                 uint8_t *pack) {
-  const uint32_t f = blockIdx.y;
-  uint64_t off = 0;
-  for (uint32_t g = 0; g < f; ++g) off += (out_size[g] + 63) & ~63ull;
-  const uint64_t sz = out_size[f];
-  const uint8_t *src = out + fr[f].out_off;
-  uint8_t *dst = pack + off;
-  const uint64_t stride = (uint64_t)gridDim.x * 256, i0 = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  uint64_t done = 0;
-  if ((reinterpret_cast<uintptr_t>(src) & 15) == 0) {  // dst is 64-B aligned
-    const uint64_t n16 = sz >> 4;
-    for (uint64_t i = i0; i < n16; i += stride)
-      reinterpret_cast<uint4 *>(dst)[i] = reinterpret_cast<const uint4 *>(src)[i];
-    done = n16 << 4;
-  }
-  for (uint64_t i = done + i0; i < sz; i += stride) dst[i] = src[i];
-}
-
 // ---- encoder: byte stuffing, header, EOI ------------------------------------------------------
 
 // the 16 bytes of the packed stream at i0, the final partial byte padded with ones
@@ -3411,17 +3414,31 @@ __global__ __launch_bounds__(256) void k_ff_count(const EncFrame *__restrict__ f
   }
 }
 
+// Writes the finished JPEGs packed back to back, frame f at the sum over g < f of align64(size
+// of g), so the host fetches a batch with one copy (a separate compaction kernel used to move
+// them there: 6-8 us per batch and a second pass over the output).  Every size is known here:
+// the header, the stream bytes (total_bits) and the stuffed bytes (nff).
 __global__ __launch_bounds__(256) void k_ff_write(const EncFrame *__restrict__ fr, const uint32_t *total_bits,
                                                   const uint8_t *stream, const uint32_t *off, const uint32_t *nff,
-                                                  const uint8_t *hdr, uint8_t *out, uint64_t *out_size) {
+                                                  const uint8_t *hdr, uint8_t *pack, uint64_t *out_size) {
   const EncFrame &F = fr[blockIdx.y];
   // the frame's fields in registers (k_ff_count)
   const uint32_t hdr_len = F.hdr_len, hdr_off = F.hdr_off, tile0 = F.tile0;
   const uint8_t *src = stream + F.bits_off;
-  uint8_t *o = out + F.out_off;
   const uint32_t tb = total_bits[blockIdx.y], nbytes = (tb + 7) >> 3;
   const uint32_t ntiles = (nbytes + kTile - 1) / kTile;
   __shared__ uint32_t sh[4];
+  __shared__ uint64_t s_pack;
+  if (threadIdx.x < 64) {  // the frame's packed offset (one wave; a batch has <= 65535 frames)
+    uint64_t acc = 0;
+    for (uint32_t g = threadIdx.x; g < blockIdx.y; g += 64)
+      acc += ((uint64_t)fr[g].hdr_len + ((total_bits[g] + 7) >> 3) + nff[g] + 2 + 63) & ~63ull;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    if (threadIdx.x == 0) s_pack = acc;
+  }
+  __syncthreads();
+  uint8_t *o = pack + s_pack;
   __shared__ uint8_t s_out[2 * kTile];  // a tile's bytes after stuffing (at most every byte 0xFF)
   for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {  // grid-stride over the stream's tiles
     if (t == 0)
@@ -3665,17 +3682,10 @@ hipError_t enc_ff_count(const EncFrame *__restrict__ fr, int n, uint32_t max_til
 
 hipError_t enc_ff_write(const EncFrame *__restrict__ fr, int n, uint32_t max_tiles, const uint32_t *total_bits,
                         const uint8_t *stream, const uint32_t *tile_off, const uint32_t *nff, const uint8_t *hdr,
-                        uint8_t *out, uint64_t *out_size, hipStream_t s) {
+                        uint8_t *pack, uint64_t *out_size, hipStream_t s) {
   if (n <= 0 || !max_tiles) return hipSuccess;
   hipLaunchKernelGGL(k_ff_write, dim3(max_tiles < kFFGrid ? max_tiles : kFFGrid, (unsigned)n), dim3(256), 0, s, fr,
-                     total_bits, stream, tile_off, nff, hdr, out, out_size);
-  return hipGetLastError();
-}
-
-hipError_t enc_compact(const EncFrame *__restrict__ fr, int n, const uint64_t *out_size, const uint8_t *out, uint8_t *pack,
-                       hipStream_t s) {
-  if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_compact, dim3(32, (unsigned)n), dim3(256), 0, s, fr, out_size, out, pack);
+                     total_bits, stream, tile_off, nff, hdr, pack, out_size);
   return hipGetLastError();
 }
 

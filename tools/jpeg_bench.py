@@ -27,7 +27,7 @@ import numpy as np  # noqa: E402
 
 from oracle import jpeg as J  # noqa: E402
 
-SIZES = {"480p": (480, 640), "720p": (720, 1280), "1080p": (1080, 1920), "4k": (2160, 3840)}
+SIZES = {"512sq": (512, 512), "480p": (480, 640), "720p": (720, 1280), "1080p": (1080, 1920), "4k": (2160, 3840)}
 
 
 def main():
