@@ -3170,21 +3170,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
 
 // ---- encoder: DC coding, bit offsets, packing --------------------------------------------------
 
+// Stream positions [a, b) of a word (position 0 = its first bit on the wire) as a mask of the word
+// in memory (big-endian bytes).  A word two writers share is merged with an AND of the writer's
+// positions cleared and an OR of its bits: the writers' positions are disjoint, so any order of
+// the four atomics leaves both writers' bits and nothing stale -- the stream needs no zeroing
+// first (it used to take a kernel of its own per batch).
+__device__ __forceinline__ uint32_t wire_mask(uint32_t a, uint32_t b) {
+  const uint32_t m = (0xFFFFFFFFu >> a) & (b >= 32 ? 0xFFFFFFFFu : ~(0xFFFFFFFFu >> b));
+  return bswap32(m);
+}
+__device__ __forceinline__ void merge_word(uint32_t *w, uint32_t mask, uint32_t v) {
+  atomicAnd(w, ~mask);
+  atomicOr(w, v);
+}
+
 struct BitSink {  // MSB-first bits into big-endian words at a bit offset
   uint32_t *w;
   uint32_t wi;
   uint64_t acc;
-  uint32_t n;
+  uint32_t n, s;  // s: the first word's first position
   bool first;
   __device__ __forceinline__ BitSink(uint32_t *words, uint32_t off)
-      : w(words), wi(off >> 5), acc(0), n(off & 31), first(true) {}
+      : w(words), wi(off >> 5), acc(0), n(off & 31), s(off & 31), first(true) {}
   __device__ __forceinline__ void put(uint32_t code, uint32_t size) {  // size <= 32
     acc = (acc << size) | code;
     n += size;
     if (n >= 32) {
       n -= 32;
       const uint32_t v = (uint32_t)(acc >> n);
-      if (first) atomicOr(w + wi, bswap32(v));  // shares its leading bits with the previous block
+      if (first) merge_word(w + wi, wire_mask(s, 32), bswap32(v));  // shares its leading bits with the previous block
       else w[wi] = bswap32(v);
       first = false;
       ++wi;
@@ -3192,7 +3206,7 @@ struct BitSink {  // MSB-first bits into big-endian words at a bit offset
     }
   }
   __device__ __forceinline__ void finish() {
-    if (n) atomicOr(w + wi, bswap32((uint32_t)(acc << (32 - n))));
+    if (n) merge_word(w + wi, wire_mask(first ? s : 0u, n), bswap32((uint32_t)(acc << (32 - n))));
   }
 };
 
@@ -3311,7 +3325,8 @@ __device__ __forceinline__ void pack_block(Sink &out, uint32_t p, uint32_t n, ui
 // Every block writes its bits at its offset.  The 64 blocks of a wave are consecutive, so
 // their bits are one contiguous span: the wave assembles it in an LDS image (LDS atomics
 // where neighbouring blocks share a word) and stores it as whole words, with global atomics
-// only on the span's first and last words (shared with the neighbouring waves).  Writing
+// only on the span's first and last words (shared with the neighbouring waves; merged under
+// their masks, wire_mask).  Writing
 // each block straight to memory took two global atomics per block, most of them on words a
 // neighbouring lane of the same instruction also hit.  A span over kPackWords (very detailed
 // content) takes that direct path.
@@ -3352,19 +3367,12 @@ __global__ __launch_bounds__(256) void k_pack(const EncFrame *__restrict__ fr, c
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const uint32_t s0 = __shfl(off, 0) & 31, e1 = __shfl(off + len, (int)last) - (w1 - 1) * 32;  // 1..32
   for (uint32_t i = lane; i < nw; i += 64) {
     const uint32_t v = img[i];
-    if (i == 0 || i == nw - 1) atomicOr(words + w0 + i, v);
+    if (i == 0 || i == nw - 1) merge_word(words + w0 + i, wire_mask(i == 0 ? s0 : 0u, i == nw - 1 ? e1 : 32u), v);
     else words[w0 + i] = v;
   }
-}
-
-// zero the words the packed stream of each frame will occupy (boundary words are OR-ed)
-__global__ __launch_bounds__(256) void k_zero_stream(const EncFrame *__restrict__ fr, const uint32_t *total_bits, uint8_t *stream) {
-  const EncFrame &F = fr[blockIdx.y];
-  const uint32_t nw = (total_bits[blockIdx.y] >> 5) + 2;
-  uint32_t *w = reinterpret_cast<uint32_t *>(stream + F.bits_off);
-  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < nw; i += gridDim.x * 256) w[i] = 0;
 }
 
 // ---- encoder: byte stuffing, header, EOI ------------------------------------------------------
@@ -3664,7 +3672,6 @@ hipError_t enc_pack(const EncFrame *__restrict__ fr, int n, uint32_t max_blocks,
                     const uint32_t *acscr, const uint32_t *bitoff, const uint32_t *total_bits, uint8_t *stream,
                     hipStream_t s) {
   if (n <= 0 || !max_blocks) return hipSuccess;
-  hipLaunchKernelGGL(k_zero_stream, dim3(64, (unsigned)n), dim3(256), 0, s, fr, total_bits, stream);
   hipLaunchKernelGGL(k_pack, dim3((max_blocks + 255) / 256, (unsigned)n), dim3(256), 0, s, fr, pre, acbits, acscr,
                      bitoff, stream);
   return hipGetLastError();
