@@ -1426,7 +1426,10 @@ __global__ __launch_bounds__(256) void k_spec(const DecSeg *__restrict__ sg, con
   // serial continuations, walkers 256 / L lanes apart so their divergent decodes run in
   // different waves where possible
   const uint32_t wsp = 256 / L, e = t / wsp;
-  if (t % wsp == 0 && e < bpm && s_first[e] != 0) {
+#ifndef VF_SPEC_NOSERIAL
+#define VF_SPEC_NOSERIAL 0  // timing-only builds: skip the serial continuations (outputs wrong)
+#endif
+  if (!VF_SPEC_NOSERIAL && t % wsp == 0 && e < bpm && s_first[e] != 0) {
     uint32_t j = kLinkNone;  // current trajectory, or kLinkNone while explicit
     uint64_t st = s_fst[e];
     for (uint32_t k = s_first[e] + 1; k < nk; ++k) {
