@@ -757,8 +757,8 @@ def distributor_leg(nworkers, ngpu, host_gbps=None, pcie_gbps=None, frames_scale
             so, se = p.communicate(timeout=timeout_s)
         except subprocess.TimeoutExpired:
             os.killpg(p.pid, signal.SIGKILL)
-            p.communicate()
-            return {"error": f"timed out after {timeout_s} s"}
+            so, se = p.communicate()
+            return {"error": f"timed out after {timeout_s} s: " + (se or "")[-300:]}
         lines = [ln for ln in so.splitlines() if ln.startswith("{")]
         if p.returncode != 0 or not lines:
             return {"error": f"rc={p.returncode}: {se[-300:]}"}
@@ -1096,6 +1096,14 @@ def main():
         sweep = sweep_leg(ctx, np, host_batch, args.batch, rank, world, barrier_sync, reduce_max)
         if rank == 0:
             log(f"configs[4] sweep: {sweep}")
+    if world > 1 and rank != 0:
+        # No collective follows: the other ranks leave here, so that their idle GPU contexts
+        # (and their hardware queues) are gone while rank 0 runs the JPEG, per-frame and
+        # distributor legs.  Rehearsing N ranks on one card, the idle contexts' queues slowed the
+        # workers' JPEG kernels about 4x, past the legs' time limits.
+        ctx.close()
+        dist.destroy_process_group()
+        return
     jpeg = None
     if rank == 0 and not args.no_jpeg:
         jpeg = run_jpeg_child(device, args.batch, args.cpu_seconds)
@@ -1106,8 +1114,8 @@ def main():
             jpeg_issue_fractions(hc["roofline"], jpeg_pmc_hard)
         log(f"jpeg mode: {jpeg}")
     if rank == 0 and args.cpu_seconds > 0:
-        # after every timed region (the other ranks wait at the distributor leg's barrier); at
-        # N > 1 a shorter sample without the process-count series keeps the run bounded
+        # after every timed region (the other ranks have left); at N > 1 a shorter sample
+        # without the process-count series keeps the run bounded
         full = world == 1
         cpu = cpu_baseline(host_batch, args.batch, args.cpu_seconds if full else min(3.0, args.cpu_seconds), np)
         procs = min(args.cpu_procs, len(os.sched_getaffinity(0)))
@@ -1142,8 +1150,6 @@ def main():
             fanout = distributor_leg(world, max(1, min(world, torch.cuda.device_count())), host_gbps, pcie_gbps,
                                      jpeg=jpeg if isinstance(jpeg, dict) else None, reps=max(1, args.dist_reps))
             log(f"distributor leg: {fanout}")
-        if world > 1:
-            dist.barrier(group=cpu_group)  # host-only: the other ranks idle while rank 0 runs its legs
 
     if rank == 0:
         frames = world * args.steps * args.batch
