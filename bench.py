@@ -1102,7 +1102,10 @@ def main():
         # distributor legs.  Rehearsing N ranks on one card, the idle contexts' queues slowed the
         # workers' JPEG kernels about 4x, past the legs' time limits.
         ctx.close()
-        dist.destroy_process_group()
+        try:  # local teardown: rank 0 runs no collective after this point
+            dist.destroy_process_group()
+        except Exception as e:  # reported, never raised
+            log(f"rank {rank}: destroy_process_group: {e!r}"[:200])
         return
     jpeg = None
     if rank == 0 and not args.no_jpeg:
@@ -1191,7 +1194,10 @@ def main():
         }
         emit(line)
     if world > 1:
-        dist.destroy_process_group()
+        try:  # the other ranks have left (after the last collective); the line is out already
+            dist.destroy_process_group()
+        except Exception as e:
+            log(f"destroy_process_group: {e!r}"[:200])
 
 
 if __name__ == "__main__":
