@@ -281,6 +281,25 @@ def gpu_spans(timeline, t_call: float) -> List[dict]:
     return spans
 
 
+def pin_to_gpu_node(device=None) -> bool:
+    """Keep the worker process on the CPUs of its GPU's NUMA node (VF_WORKER_PIN=0: leave it).
+    Done before the context exists, so the codec's and the copy pool's threads inherit it: the
+    host half of a batch (parsing, staging, the ring slice the distributor bound to that node)
+    then stays on one socket instead of wherever the scheduler last put the thread."""
+    if os.environ.get("VF_WORKER_PIN", "1") == "0":
+        return False
+    from . import numa
+    from ._lib import default_device
+    cpus = numa.node_cpus(numa.gpu_numa_node(default_device() if device is None else device))
+    if not cpus:
+        return False
+    try:
+        os.sched_setaffinity(0, cpus)
+    except OSError:
+        return False
+    return True
+
+
 def main(argv=None):
     """inverter.py:48-61 plus the GPU worker's knobs."""
     ap = argparse.ArgumentParser(description="Inverter worker for video processing (MI355X backend)")
@@ -306,6 +325,7 @@ def main(argv=None):
     ap.add_argument("--transport", choices=("auto", "zmq", "tcp"), default="auto")
     ap.add_argument("--verbose", action="store_true")
     args = ap.parse_args(argv)
+    pin_to_gpu_node(args.device)
     worker = InverterWorker(args.host, args.distribute_port, args.collect_port, args.delay,
                             use_jpeg=not args.raw, device=args.device, batch=args.batch, inflight=args.inflight,
                             protocol=args.protocol, transport=args.transport, verbose=args.verbose)
