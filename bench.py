@@ -825,6 +825,8 @@ def jpeg_child(args):
     """The JPEG leg in a fresh interpreter without torch, as a worker process runs it
     (`python -m vfilter.inverter` imports no torch); prints one JSON object."""
     from vfilter import Context
+    from vfilter.inverter import pin_to_gpu_node
+    pin_to_gpu_node(args.jpeg_child)  # as the worker process pins itself (its "worker form" is measured here)
     ctx = Context(args.jpeg_child)
     jpeg, jpgs = jpeg_mode(ctx, args.batch)
     ctx.close()
