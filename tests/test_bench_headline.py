@@ -84,3 +84,31 @@ def test_headline_with_failed_legs():
     assert len(s) <= bench.HEADLINE_MAX_BYTES
     assert h["distributor"]["jpeg_512"]["error"].startswith("timed out")
     assert h["cpu_baseline"] is None
+
+
+R06_RUNS = [("profiles/r06_bench_detail_end.json", "profiles/r06_bench_end.json"),
+            ("profiles/r06_bench_detail_confirm.json", "profiles/r06_bench_confirm.json"),
+            ("profiles/r06_bench_n2_rehearsal_1card_detail.json", "profiles/r06_bench_n2_rehearsal_1card.json"),
+            ("profiles/r06_bench_n4_rehearsal_1card_detail.json", "profiles/r06_bench_n4_rehearsal_1card.json")]
+
+
+@pytest.mark.parametrize("detail,headline", R06_RUNS)
+def test_round6_headlines_are_what_emit_makes_of_their_detail(detail, headline, tmp_path):
+    """The committed round-6 GPU runs (N=1 end and confirmation, the N=2 and N=4 one-card
+    rehearsals): emit() on each detail record gives back, key for key, the headline that run
+    printed last -- so the evidence under profiles/ is one record seen two ways, and the
+    headline stays under the driver's limit at every N rehearsed."""
+    path = os.path.join(ROOT, detail)
+    if not os.path.exists(path):
+        pytest.skip(f"{detail} not in this tree")
+    rec = json.load(open(path))
+    out = io.StringIO()
+    with redirect_stdout(out), redirect_stderr(io.StringIO()):
+        bench.emit(dict(rec), str(tmp_path / "bench_detail.json"))
+    last = out.getvalue().splitlines()[-1]
+    assert len(last.encode()) <= bench.HEADLINE_MAX_BYTES
+    got, want = json.loads(last), _record(headline)
+    got.pop("detail"), want.pop("detail")
+    assert got == want
+    assert all(k in got for k in REQUIRED)
+    assert got["n_gpus"] == rec["n_gpus"] and got["value"] == rec["value"]
