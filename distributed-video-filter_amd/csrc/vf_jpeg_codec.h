@@ -207,6 +207,11 @@ class Codec {
   bool sync_spec_ = false;            // run_decode took the speculative sync (the write pass's form)
   int sync_last_ = 0;                 // exit / count slot of the pass-based sync's result
   bool enc_fast_ = false;             // submit_invert's DCT (wait_invert re-encodes after finish_sync)
+  // output bytes per input byte of the codec's last invert batch (0: none yet): the next batch's
+  // first D2H copy is sized from it instead of from the input sizes alone (VF_JPEG_FETCH_LEARN=0:
+  // the fixed rule), so content that shrinks when re-encoded does not drag twice its output over PCIe
+  double out_ratio_ = 0;
+  uint64_t in_bytes_ = 0;
   TaskPool pool_{4};
   double prep_ms_[3] = {0, 0, 0};  // VF_JPEG_TRACE: prepare_decode's parse / descriptor loop / staging
   std::vector<uint64_t> ekey_;     // prepare_encode's last batch shape (n, settings, sizes, offsets)

@@ -1136,12 +1136,25 @@ int Codec::submit_invert(const uint8_t *const *jpegs, const size_t *jsizes, int 
   const auto t1 = clk::now();
   std::vector<int> ws((size_t)n), hs((size_t)n);
   std::vector<uint64_t> offs((size_t)n);
+  // the first D2H copy's size: an inverted frame re-encoded at the input's quality codes to about
+  // the input's size (+25 % + 8 KB per frame, the rule before any batch); after the codec's first
+  // batch, its measured output/input ratio + 6 % + 1 KB per frame (q95 input re-encoded at q85
+  // halves: the fixed rule then copied 2.4x the output).  Short guesses take finish_fetch's
+  // second copy.
+  static const bool learn = [] {
+    const char *v = std::getenv("VF_JPEG_FETCH_LEARN");
+    return !(v && v[0] == '0');
+  }();
+  const double ratio = learn ? out_ratio_ : 0.0;
   uint64_t guess = 0;
+  in_bytes_ = 0;
   for (int f = 0; f < n; ++f) {
     ws[(size_t)f] = dfr_[(size_t)f].g.w;
     hs[(size_t)f] = dfr_[(size_t)f].g.h;
     offs[(size_t)f] = dfr_[(size_t)f].out_off;
-    guess += align_up(jsizes[f] + jsizes[f] / 4 + 8192, 64);  // an inverted frame codes to about its input's size
+    in_bytes_ += jsizes[f];
+    guess += ratio > 0 ? align_up((uint64_t)((double)jsizes[f] * ratio * 1.06) + 1024, 64)
+                       : align_up(jsizes[f] + jsizes[f] / 4 + 8192, 64);
   }
   const bool fast = (flags & kFlagFastDct) != 0;
   if ((rc = prepare_encode(ws.data(), hs.data(), offs.data(), n, quality, subsamp, fast, err))) return rc;
@@ -1201,6 +1214,7 @@ int Codec::wait_invert(size_t *total, std::string *err) {
   }
   if (rc) return rc;
   if ((rc = finish_fetch(err))) return rc;
+  if (in_bytes_) out_ratio_ = (double)out_total_ / (double)in_bytes_;
   waited_ = true;
   *total = (size_t)out_total_;
   if (std::getenv("VF_JPEG_TRACE"))

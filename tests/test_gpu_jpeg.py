@@ -546,6 +546,25 @@ def test_bench_operating_points_on_the_auto_path(tj, monkeypatch, kind):
     assert [bytes(g) for g in tj.invert_batch_result(t2)] == want[::-1]
 
 
+def test_fetch_sized_from_the_previous_batch(tj):
+    """The first D2H copy of a batch's outputs is sized from the codec's previous batch (output
+    bytes per input byte): batches that shrink when re-encoded (q95 noise at q85), that keep
+    their size (q85 scenes) and that grow (q40 scenes at q85), in turns on one codec, so the
+    learned size falls short (the second copy) and overshoots; bit-exact every time, through the
+    worker's form and the synchronous call."""
+    from vfilter.synthetic import synthetic_noisy_scene, synthetic_scene
+    shrink = [J.encode(synthetic_noisy_scene(s, 240, 320), 95) for s in range(4)]
+    keep = [J.encode(synthetic_scene(s, 240, 320), 85) for s in range(4)]
+    grow = [J.encode(synthetic_scene(s, 240, 320), 40) for s in range(4)]
+    sizes = {k: sum(len(J.invert_jpeg(j)) for j in b) / sum(len(j) for j in b)
+             for k, b in (("shrink", shrink), ("keep", keep), ("grow", grow))}
+    assert sizes["shrink"] < 0.8 < sizes["keep"] < 1.2 < sizes["grow"], sizes
+    for batch in (shrink, keep, shrink, grow, keep, grow, shrink):
+        want = [J.invert_jpeg(j) for j in batch]
+        assert [bytes(g) for g in tj.invert_batch_result(tj.invert_batch_submit(batch))] == want
+        assert tj.invert_batch(batch) == want
+
+
 @pytest.mark.parametrize("hw", [(512, 512), (480, 640)])
 def test_reference_deployment_operating_points(tj, monkeypatch, hw):
     """the reference app's own frames -- webcam_app.py:17,97-111 crops to 512 x 512
