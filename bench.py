@@ -75,8 +75,9 @@ def parse():
     ap.add_argument("--no-sizes", action="store_true", help="skip the 480p / 1080p / 4K kernel leg")
     ap.add_argument("--no-sweep", action="store_true", help="skip the configs[4] 256..4096-frame resident sweep")
     ap.add_argument("--no-per-frame", action="store_true", help="skip the one-frame-per-call drop-in leg")
-    ap.add_argument("--dist-reps", type=int, default=3,
-                    help="repetitions of each JPEG distributor leg (median reported, min/max in the detail)")
+    ap.add_argument("--dist-reps", type=int, default=5,
+                    help="repetitions of each JPEG distributor leg (median reported, min/max in the detail; "
+                         "the small-frame legs swing 0.8-1.2x run to run, profiles/r06_small_legs_spread.txt)")
     ap.add_argument("--cpu-procs", type=int, default=16,
                     help="processes of the multi-process CPU baseline (capped by the CPU affinity; 0 = skip)")
     ap.add_argument("--probe", action="store_true", help=argparse.SUPPRESS)  # child under rocprofv3
