@@ -88,6 +88,7 @@ def test_headline_with_failed_legs():
 
 R06_RUNS = [("profiles/r06_bench_detail_end.json", "profiles/r06_bench_end.json"),
             ("profiles/r06_bench_detail_prefetch.json", "profiles/r06_bench_prefetch.json"),
+            ("profiles/r06_bench_detail_reps5.json", "profiles/r06_bench_reps5.json"),
             ("profiles/r06_bench_detail_confirm.json", "profiles/r06_bench_confirm.json"),
             ("profiles/r06_bench_n2_rehearsal_1card_detail.json", "profiles/r06_bench_n2_rehearsal_1card.json"),
             ("profiles/r06_bench_n4_rehearsal_1card_detail.json", "profiles/r06_bench_n4_rehearsal_1card.json")]
